@@ -1,0 +1,187 @@
+#!/usr/bin/env python
+"""Throughput benchmark: Gibbs sweeps/sec of the linear BVAR-SV (N=20, p=12,
+T=750, K=241) over B chains per GPU (BASELINE.json configs[1]).
+
+A "step" is one Gibbs sweep (CTA -> A -> SV -> PHI, mcmcVAR.m:211-274) of all
+B chains resident on the GPU.  The data are the reference's own
+fredblockMD20-2022-09.csv (committed fixture), jump-off 2022-08 (T=750);
+chains start from the reference initialisation (mcmcVAR.m:197-206) and draw
+from the on-device Philox stream.  Draw storage (post-burn-in form,
+mcmcVAR.m:289-292) is inside the timed region.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank runs its
+own B chains (the vintage/chain parfor shards with no data-path collective),
+so scaling is weak; the only collectives are the timing barrier and the
+max-reduction of the elapsed time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix (AMD spec)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--chains", type=int, default=256)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="budget of the CPU-oracle baseline sample (rank 0, N=1 only)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_
+        torch.cuda.set_device(local)
+        dist_.init_process_group("nccl")
+        dist = dist_
+
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    d = pkg.model.importdata_csv(ROOT / "tests/golden/data/fredblockMD20-2022-09.csv")
+    p = 12
+    mpm = pkg.model.setMinnesotaMean(d["ncode"])
+    thisT = len(d["ydates"])  # jump-off 2022-08 (doMCMClinear.m:27,94)
+    m = pkg.model.build_var(thisT, p, 12, d["data"], d["ydates"], mpm, True)
+    B = args.chains
+    ctx = pkg.Context(local)
+    cap = args.warmup + args.steps
+    ch = pkg.Chains(ctx, N=m.N, p=p, T=m.T, B=B, crn=False, store_capacity=cap,
+                    seed=1012023 + 7919 * rank)
+    ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    st = pkg.model.initial_state(m, B)
+    ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    ch.sweep(args.warmup, store=True)
+    barrier()
+    if not args.no_profile:
+        ch.profile(True)
+    t0 = time.perf_counter()
+    ch.sweep(args.steps, store=True)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ktimes = ch.kernel_times() if not args.no_profile else {}
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    draws = ch.get_draws()
+    assert np.all(np.isfinite(draws["PAI_all"])), "non-finite draws"
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    N, K, T = m.N, m.K, m.T
+    value = world * B * args.steps / elapsed
+    out = {
+        "metric": "Gibbs sweeps/sec (chains x vintages) N=20 p=12",
+        "value": round(value, 3),
+        "unit": "sweeps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "fredblockMD20-2022-09.csv (reference data fixture), jump-off 2022-08, "
+                "reference initialisation, Philox draws",
+        "config": {"workload": "configs[1]: linear BVAR-SV (mcmcVAR) N=20 p=12 T=750 K=241, "
+                               f"{B} chains per GPU, one sweep of all chains per step",
+                   "chains_per_gpu": B, "N": N, "p": p, "T": T, "K": K,
+                   "parallelism": f"chains sharded over {world} GPU(s), no data-path collective"},
+    }
+    if ktimes:
+        # dominant kernel = largest accumulated device time
+        dom = max(ktimes, key=lambda k: ktimes[k][0])
+        per = {k: round(v[0] / max(v[1], 1), 4) for k, v in ktimes.items() if v[1]}
+        syrk_ms = ktimes["k_syrk"][0] / max(ktimes["k_syrk"][1], 1)
+        f_syrk = B * N * T * K * (K + 1)  # algorithmic flop per k_syrk launch
+        ach = f_syrk / (syrk_ms * 1e-3) / 1e12
+        out["roofline"] = {"kernel": "k_syrk", "bound": "mfma", "achieved": round(ach, 3),
+                           "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                           "flop_per_launch": f_syrk, "avg_launch_ms": round(syrk_ms, 4)}
+        out["kernel_ms_per_sweep"] = per
+        out["dominant_kernel"] = dom
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(budget_s):
+    """The CPU oracle (the reference algorithm as written: kron-materialised X_j,
+    explicit inverse; oracle/ccmm_oracle.py) timed on this host, single-threaded
+    BLAS, one chain, as many sweeps as fit in ~budget_s."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import ccmm_oracle as O
+    fred = O.load_fred_csv(ROOT / "tests/golden/data/fredblockMD20-2022-09.csv")
+    mpm = O.set_minnesota_mean(fred["ncode"])
+    su = O.var_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], mpm, True)
+    st = O.init_state(su)
+    rng = np.random.default_rng(0)
+    n = 0
+    with threadpool_limits(1):
+        t0 = time.perf_counter()
+        while True:
+            crn = O.draw_crn(rng, su.N, su.K, su.T, su.dPHI)
+            st = O.linear_sweep(st, su, crn)
+            n += 1
+            el = time.perf_counter() - t0
+            if el > budget_s or n >= 50:
+                break
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(n / el, 5), "unit": "sweeps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} sweeps of one chain, real data T=750, oracle/ccmm_oracle.py "
+                      f"(as-written kron CTA), numpy/OpenBLAS 1 thread, {el:.1f}s, CPU: {cpu}"}
+
+
+if __name__ == "__main__":
+    main()

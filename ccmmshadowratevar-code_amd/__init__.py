@@ -1,0 +1,15 @@
+"""MI355X-native Gibbs sweep of the CCMM shadow-rate BVAR-SV.
+
+Import name: ``ccmm_amd`` (the directory name contains a hyphen; use
+``__graft_entry__.load_package()`` or ``tests/conftest.py``'s loader, which
+register this directory as the package ``ccmm_amd``).
+
+Layers:
+  csrc/            HIP kernels (gfx950) + C ABI -> libccmm.so  (include/ccmm.h)
+  _abi.py          ctypes binding of the C ABI
+  model.py         host setup of one vintage (mcmcVAR.m:28-206)
+  samplers.py      reference-interface mirror (mcmcVAR, CTA, CTAsys, drawTruncNormal)
+"""
+from . import _abi, model, samplers  # noqa: F401
+from ._abi import Chains, Context, load_library  # noqa: F401
+from .samplers import CTA, CTAsys, drawTruncNormal, mcmcVAR  # noqa: F401

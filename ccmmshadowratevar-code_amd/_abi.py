@@ -1,0 +1,342 @@
+"""ctypes binding of libccmm (include/ccmm.h).
+
+The product path: every numerical call goes through ``libccmm.so`` (HIP,
+gfx950).  There is no CPU fallback: if the library cannot be loaded, or no GPU
+is visible when a compute entry point is called, a ``RuntimeError`` is raised.
+
+All array arguments follow the reference's MATLAB shapes; they are passed to
+the C ABI column-major (``order='F'``), chain index slowest.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("CCMM_LIB", _HERE / "csrc" / "libccmm.so"))
+
+CCMM_OK = 0
+CCMM_ERR_NOTSPD = -4
+MODEL_LINEAR = 0
+MODEL_BLOCKHYBRID = 1
+
+RNG_PAI, RNG_A, RNG_SVU, RNG_SVZ, RNG_PHI, RNG_ELB = 1, 2, 3, 4, 5, 6
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+_i8p = C.POINTER(C.c_int8)
+_u8p = C.POINTER(C.c_uint8)
+_i64p = C.POINTER(C.c_int64)
+
+
+class ChainConfig(C.Structure):
+    _fields_ = [("model", C.c_int), ("N", C.c_int), ("p", C.c_int), ("K", C.c_int),
+                ("T", C.c_int), ("B", C.c_int), ("ndata", C.c_int), ("dPHI", C.c_int),
+                ("rng_crn", C.c_int), ("store_capacity", C.c_int),
+                ("logy2offset", C.c_double), ("seed", C.c_uint64)]
+
+
+_SIGS = {
+    "ccmm_abi_version": (C.c_int, []),
+    "ccmm_last_error": (C.c_char_p, []),
+    "ccmm_device_count": (C.c_int, []),
+    "ccmm_create": (C.c_void_p, [C.c_int]),
+    "ccmm_destroy": (None, [C.c_void_p]),
+    "ccmm_synchronize": (C.c_int, [C.c_void_p]),
+    "ccmm_cta": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _dp, C.c_int, _dp,
+                           C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _ip]),
+    "ccmm_astep": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp]),
+    "ccmm_sv_ksc": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp,
+                              _dp, _dp, _dp, _dp, _i8p]),
+    "ccmm_phi_iw": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, _dp, _dp, C.c_int, _dp, _dp,
+                              _dp]),
+    "ccmm_draw_trunc_normal": (C.c_double, [C.c_double, C.c_double, C.c_double, C.c_double, _u8p]),
+    "ccmm_draw_trunc_normal_batch": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp, C.c_double, _dp,
+                                               _dp, _u8p]),
+    "ccmm_chains_create": (C.c_void_p, [C.c_void_p, C.POINTER(ChainConfig)]),
+    "ccmm_chains_destroy": (None, [C.c_void_p]),
+    "ccmm_chains_set_data": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp,
+                                       _dp]),
+    "ccmm_chains_set_slots": (C.c_int, [C.c_void_p, _ip]),
+    "ccmm_chains_set_state": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
+    "ccmm_chains_get_state": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
+    "ccmm_chains_crn_len": (C.c_int64, [C.c_void_p]),
+    "ccmm_chains_sweep": (C.c_int, [C.c_void_p, C.c_int, _dp, C.c_int]),
+    "ccmm_chains_stored": (C.c_int, [C.c_void_p]),
+    "ccmm_chains_get_draws": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp]),
+    "ccmm_chains_profile": (C.c_int, [C.c_void_p, C.c_int]),
+    "ccmm_chains_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _dp, _i64p, C.c_char_p, C.c_int]),
+    "ccmm_selftest_mfma_f64": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
+}
+
+_lib = None
+
+
+def load_library(path: str | os.PathLike | None = None):
+    """Load libccmm.so and bind every exported symbol; raises if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise RuntimeError(f"libccmm.so not found at {p}: build it with "
+                           f"`python -c 'import __graft_entry__ as g; g.build()'` "
+                           f"(there is no CPU fallback)")
+    lib = C.CDLL(str(p))
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def last_error() -> str:
+    return load_library().ccmm_last_error().decode(errors="replace")
+
+
+def _check(rc, what):
+    if rc < 0:
+        raise RuntimeError(f"{what} failed (rc={rc}): {last_error()}")
+    return rc
+
+
+def _f(a, dtype=np.float64):
+    """Column-major contiguous copy (MATLAB layout)."""
+    return np.asfortranarray(np.asarray(a, dtype=dtype))
+
+
+def _ptr(a, ct=_dp):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ct)
+
+
+class Context:
+    """A libccmm context bound to one HIP device (ccmm_create)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        n = self.lib.ccmm_device_count()
+        if n <= 0:
+            raise RuntimeError("no HIP device visible: libccmm requires an MI355X (gfx950) GPU")
+        h = self.lib.ccmm_create(device)
+        if not h:
+            raise RuntimeError(f"ccmm_create({device}) failed: {last_error()}")
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.ccmm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        _check(self.lib.ccmm_synchronize(self.handle), "ccmm_synchronize")
+
+    # ------------------------------------------------------------ block-level
+    def cta(self, Y, X, A, sqrtht, iVdiag, iVb, PAI, z=None, y_per_chain=False, x_per_chain=False):
+        """Batched CTA/CTAsys draw.  Shapes (MATLAB): Y T x N [x B], X T x K [x nx] [x B],
+        A N x N x B, sqrtht T x N x B, iVdiag/iVb K x N, PAI K x N x B, z K x N x B."""
+        A = _f(A)
+        N = A.shape[0]
+        B = A.shape[2] if A.ndim == 3 else 1
+        PAI = _f(PAI).copy(order="F")
+        K = PAI.shape[0]
+        T = np.asarray(Y).shape[0]
+        Xf = _f(X)
+        if x_per_chain:
+            nx = Xf.shape[2] if Xf.ndim == 4 else 1
+        else:
+            nx = Xf.shape[2] if Xf.ndim == 3 else 1
+        status = np.zeros(B, dtype=np.int32)
+        rc = self.lib.ccmm_cta(self.handle, B, T, N, K, _ptr(_f(Y)), int(y_per_chain), _ptr(Xf), nx,
+                               int(x_per_chain), _ptr(A), _ptr(_f(sqrtht)), _ptr(_f(iVdiag)),
+                               _ptr(_f(iVb)), _ptr(PAI), _ptr(_f(z)) if z is not None else None,
+                               status.ctypes.data_as(_ip))
+        _check(rc, "ccmm_cta")
+        return PAI, status
+
+    def astep(self, RESID, sqrtht, z=None):
+        RESID = _f(RESID)
+        T, N = RESID.shape[:2]
+        B = RESID.shape[2] if RESID.ndim == 3 else 1
+        A = np.zeros((N, N, B), order="F")
+        invA = np.zeros((N, N, B), order="F")
+        rc = self.lib.ccmm_astep(self.handle, B, T, N, _ptr(RESID), _ptr(_f(sqrtht)),
+                                 _ptr(_f(z)) if z is not None else None, _ptr(A), _ptr(invA))
+        _check(rc, "ccmm_astep")
+        return A, invA
+
+    def sv_ksc(self, logy2T, hprevT, sqrtPHI, h0mean, h0vcvsqrt, u=None, z=None):
+        logy2T = _f(logy2T)
+        N, T = logy2T.shape[:2]
+        B = logy2T.shape[2] if logy2T.ndim == 3 else 1
+        hT = np.zeros((N, T, B), order="F")
+        sh = np.zeros((N, T, B), order="F")
+        h0 = np.zeros((N, B), order="F")
+        kai = np.zeros((N, T, B), dtype=np.int8, order="F")
+        rc = self.lib.ccmm_sv_ksc(self.handle, B, T, N, _ptr(logy2T), _ptr(_f(hprevT)),
+                                  _ptr(_f(sqrtPHI)), _ptr(_f(h0mean)), _ptr(_f(h0vcvsqrt)),
+                                  _ptr(_f(u)) if u is not None else None,
+                                  _ptr(_f(z)) if z is not None else None,
+                                  _ptr(hT), _ptr(h0), _ptr(sh), kai.ctypes.data_as(_i8p))
+        _check(rc, "ccmm_sv_ksc")
+        return hT, h0, sh, kai
+
+    def phi_iw(self, eta, sPHI, dPHI, Zdraw=None):
+        eta = _f(eta)
+        T, N = eta.shape[:2]
+        B = eta.shape[2] if eta.ndim == 3 else 1
+        sq = np.zeros((N, N, B), order="F")
+        PHI = np.zeros((N, N, B), order="F")
+        rc = self.lib.ccmm_phi_iw(self.handle, B, T, N, _ptr(eta), _ptr(_f(sPHI)), int(dPHI),
+                                  _ptr(_f(Zdraw)) if Zdraw is not None else None, _ptr(sq),
+                                  _ptr(PHI))
+        _check(rc, "ccmm_phi_iw")
+        return sq, PHI
+
+    def draw_trunc_normal_batch(self, mu, sig, elb, u):
+        mu = _f(mu).ravel(order="F")
+        n = mu.size
+        out = np.zeros(n)
+        fl = np.zeros(n, dtype=np.uint8)
+        rc = self.lib.ccmm_draw_trunc_normal_batch(self.handle, n, _ptr(mu),
+                                                   _ptr(_f(sig).ravel(order="F")), float(elb),
+                                                   _ptr(_f(u).ravel(order="F")), _ptr(out),
+                                                   fl.ctypes.data_as(_u8p))
+        _check(rc, "ccmm_draw_trunc_normal_batch")
+        return out, fl
+
+    def selftest_mfma_f64(self, A16x4, B4x16):
+        D = np.zeros((16, 16), order="F")
+        _check(self.lib.ccmm_selftest_mfma_f64(self.handle, _ptr(_f(A16x4)), _ptr(_f(B4x16)),
+                                               _ptr(D)), "ccmm_selftest_mfma_f64")
+        return D
+
+
+def draw_trunc_normal(mu, sig, elb, u):
+    """Host scalar drawTruncNormal (drawTruncNormal.m:31-86); returns (draw, flags)."""
+    fl = C.c_uint8(0)
+    v = load_library().ccmm_draw_trunc_normal(float(mu), float(sig), float(elb), float(u),
+                                              C.byref(fl))
+    return v, int(fl.value)
+
+
+class Chains:
+    """Device-resident chain set (ccmm_chains_*): B chains of one model."""
+
+    KERNELS = ("k_resid", "k_cta_weights", "k_syrk", "k_chol", "k_cta_solve", "k_astep",
+               "k_sv_mix", "k_sv_sample", "k_phi_gen", "k_phi", "k_store")
+
+    def __init__(self, ctx: Context, *, N, p, T, B, ndata=1, model=MODEL_LINEAR, crn=False,
+                 store_capacity=0, logy2offset=1e-3, seed=1012023, dPHI=None):
+        self.ctx = ctx
+        self.lib = ctx.lib
+        K = N * p + 1
+        self.cfg = ChainConfig(model, N, p, K, T, B, ndata, N + 3 if dPHI is None else dPHI,
+                               int(crn), store_capacity, logy2offset, seed)
+        h = self.lib.ccmm_chains_create(ctx.handle, C.byref(self.cfg))
+        if not h:
+            raise RuntimeError(f"ccmm_chains_create failed: {last_error()}")
+        self.handle = h
+        self.N, self.p, self.K, self.T, self.B = N, p, K, T, B
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.ccmm_chains_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def crn_len(self):
+        return int(self.lib.ccmm_chains_crn_len(self.handle))
+
+    def set_data(self, slot, Y, X, iVdiag, iVb, sPHI, h0mean, h0vcvsqrt):
+        Y = _f(Y)
+        rc = self.lib.ccmm_chains_set_data(self.handle, slot, Y.shape[0], _ptr(Y), _ptr(_f(X)),
+                                           _ptr(_f(iVdiag)), _ptr(_f(iVb)), _ptr(_f(sPHI)),
+                                           _ptr(_f(h0mean)), _ptr(_f(h0vcvsqrt)))
+        _check(rc, "ccmm_chains_set_data")
+
+    def set_slots(self, slots):
+        s = np.ascontiguousarray(slots, dtype=np.int32)
+        _check(self.lib.ccmm_chains_set_slots(self.handle, s.ctypes.data_as(_ip)),
+               "ccmm_chains_set_slots")
+
+    def set_state(self, PAI, A, sqrtht, h, sqrtPHI):
+        """Arrays K x N x B, N x N x B, T x N x B, T x N x B, N x N x B."""
+        rc = self.lib.ccmm_chains_set_state(self.handle, _ptr(_f(PAI)), _ptr(_f(A)),
+                                            _ptr(_f(sqrtht)), _ptr(_f(h)), _ptr(_f(sqrtPHI)))
+        _check(rc, "ccmm_chains_set_state")
+
+    def get_state(self):
+        N, K, T, B = self.N, self.K, self.T, self.B
+        out = dict(PAI=np.zeros((K, N, B), order="F"), A=np.zeros((N, N, B), order="F"),
+                   invA=np.zeros((N, N, B), order="F"), sqrtht=np.zeros((T, N, B), order="F"),
+                   h=np.zeros((T, N, B), order="F"), sqrtPHI=np.zeros((N, N, B), order="F"),
+                   PHI=np.zeros((N, N, B), order="F"), RESID=np.zeros((T, N, B), order="F"))
+        rc = self.lib.ccmm_chains_get_state(self.handle, *[_ptr(out[k]) for k in
+                                                           ("PAI", "A", "invA", "sqrtht", "h",
+                                                            "sqrtPHI", "PHI", "RESID")])
+        _check(rc, "ccmm_chains_get_state")
+        return out
+
+    def sweep(self, nsweeps=1, crn=None, store=False):
+        """crn: array of shape (crn_len, nsweeps, B) column-major (chain slowest) or None."""
+        cp = None
+        if crn is not None:
+            crn = _f(crn)
+            assert crn.size == self.crn_len * nsweeps * self.B
+            cp = _ptr(crn)
+        rc = self.lib.ccmm_chains_sweep(self.handle, int(nsweeps), cp, int(bool(store)))
+        _check(rc, "ccmm_chains_sweep")
+        return rc
+
+    def stored(self):
+        return int(self.lib.ccmm_chains_stored(self.handle))
+
+    def get_draws(self):
+        M = self.stored()
+        N, K, T, B = self.N, self.K, self.T, self.B
+        out = dict(PAI_all=np.zeros((M, K, N, B), order="F"),
+                   PHI_all=np.zeros((M, N * (N + 1) // 2, B), order="F"),
+                   invA_all=np.zeros((M, N, N, B), order="F"),
+                   sqrtht_all=np.zeros((M, T, N, B), order="F"))
+        rc = self.lib.ccmm_chains_get_draws(self.handle, *[_ptr(out[k]) for k in
+                                                           ("PAI_all", "PHI_all", "invA_all",
+                                                            "sqrtht_all")])
+        _check(rc, "ccmm_chains_get_draws")
+        return out
+
+    def profile(self, enable=True):
+        _check(self.lib.ccmm_chains_profile(self.handle, int(enable)), "ccmm_chains_profile")
+
+    def kernel_times(self):
+        n = len(self.KERNELS)
+        ms = np.zeros(n)
+        cnt = np.zeros(n, dtype=np.int64)
+        buf = C.create_string_buffer(1024)
+        _check(self.lib.ccmm_chains_kernel_times(self.handle, n, _ptr(ms), cnt.ctypes.data_as(_i64p),
+                                                 buf, 1024), "ccmm_chains_kernel_times")
+        names = buf.value.decode().split(";")
+        return {nm: (float(ms[i]), int(cnt[i])) for i, nm in enumerate(names[:n])}

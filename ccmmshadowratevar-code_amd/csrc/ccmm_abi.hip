@@ -1,0 +1,1154 @@
+// C-ABI implementation of libccmm (include/ccmm.h): contexts, device-resident
+// chain sets and the block-level drop-ins.  Host code only; kernels live in
+// ccmm_kernels.hip (included here so the whole library is one translation unit).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ccmm_kernels.hip"
+
+using namespace ccmm;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct ArgError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIPCHECK(x)                                                                        \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess)                                                                  \
+      throw HipError(std::string(#x) + ": " + hipGetErrorString(e_) + " (" __FILE__ ":" + \
+                     std::to_string(__LINE__) + ")");                                      \
+  } while (0)
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const ArgError& e) {
+    g_err = e.what();
+    return CCMM_ERR_ARG;
+  } catch (const HipError& e) {
+    g_err = e.what();
+    return CCMM_ERR_HIP;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return CCMM_ERR_HIP;
+  }
+}
+
+void require(bool ok, const char* msg) {
+  if (!ok) throw ArgError(msg);
+}
+
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    if (count <= n && p) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (count == 0) return;
+    HIPCHECK(hipMalloc(&p, count * sizeof(T)));
+    n = count;
+  }
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+// small dense host helpers (N <= 32): lower Cholesky and SPD inverse, column-major
+void host_chol(std::vector<double>& A, int n) {
+  for (int j = 0; j < n; ++j) {
+    double s = A[j + j * n];
+    for (int k = 0; k < j; ++k) s -= A[j + k * n] * A[j + k * n];
+    if (!(s > 0)) throw ArgError("matrix not positive definite");
+    const double d = std::sqrt(s);
+    A[j + j * n] = d;
+    for (int i = j + 1; i < n; ++i) {
+      double v = A[i + j * n];
+      for (int k = 0; k < j; ++k) v -= A[i + k * n] * A[j + k * n];
+      A[i + j * n] = v / d;
+    }
+    for (int i = 0; i < j; ++i) A[i + j * n] = 0.0;
+  }
+}
+
+std::vector<double> host_spd_inverse(const std::vector<double>& A, int n) {
+  std::vector<double> L = A;
+  host_chol(L, n);
+  std::vector<double> inv(n * n, 0.0);
+  for (int col = 0; col < n; ++col) {
+    std::vector<double> x(n, 0.0);
+    for (int i = 0; i < n; ++i) {  // L y = e_col
+      double v = (i == col) ? 1.0 : 0.0;
+      for (int k = 0; k < i; ++k) v -= L[i + k * n] * x[k];
+      x[i] = v / L[i + i * n];
+    }
+    for (int i = n - 1; i >= 0; --i) {  // L' z = y
+      double v = x[i];
+      for (int k = i + 1; k < n; ++k) v -= L[k + i * n] * x[k];
+      x[i] = v / L[i + i * n];
+    }
+    for (int i = 0; i < n; ++i) inv[i + col * n] = x[i];
+  }
+  return inv;
+}
+
+}  // namespace
+
+struct ccmm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+};
+
+enum KernelId {
+  KID_RESID,
+  KID_WEIGHTS,
+  KID_SYRK,
+  KID_CHOL,
+  KID_SOLVE,
+  KID_ASTEP,
+  KID_SVMIX,
+  KID_SVSAMPLE,
+  KID_PHIGEN,
+  KID_PHI,
+  KID_STORE,
+  KID_COUNT
+};
+static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syrk", "k_chol",
+                                              "k_cta_solve", "k_astep", "k_sv_mix", "k_sv_sample",
+                                              "k_phi_gen", "k_phi", "k_store"};
+
+struct ccmm_chains {
+  ccmm_ctx* ctx = nullptr;
+  ccmm_chain_config cfg{};
+  Dims d{};
+  int nslabX = 0, nslabY = 0;
+  // per-slot data
+  std::vector<int> hT;
+  DBuf<int> Tslot, slot, xidx, yidx, status;
+  DBuf<double> Xpool, Ypool, iVdiag, iVb, sPHI, V0inv, V0invm;
+  // chain state
+  DBuf<double> PAI, A, invA, sqrtht, h, h0, sqrtPHI, PHI, E, logy2, eta, svobs, svir, W;
+  DBuf<int8_t> kai;
+  DBuf<double> G, rdiag, svLd, svw, Zphi;
+  DBuf<double> crn;
+  // storage of kept draws
+  DBuf<double> sPAI, sPHI_, sInvA, sSqrtht;
+  int stored = 0;
+  uint32_t sweep = 0;
+  bool resid_valid = false;
+  bool have_state = false;
+  std::vector<bool> have_slot;
+  // profiling
+  bool profiling = false;
+  struct Ev {
+    int kid;
+    hipEvent_t a, b;
+  };
+  std::vector<Ev> pending;
+  std::vector<hipEvent_t> evpool;
+  double kms[KID_COUNT] = {};
+  int64_t kcount[KID_COUNT] = {};
+
+  ~ccmm_chains() {
+    for (auto& e : pending) {
+      evpool.push_back(e.a);
+      evpool.push_back(e.b);
+    }
+    for (auto e : evpool) (void)hipEventDestroy(e);
+  }
+
+  hipEvent_t get_event() {
+    if (!evpool.empty()) {
+      hipEvent_t e = evpool.back();
+      evpool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HIPCHECK(hipEventCreate(&e));
+    return e;
+  }
+
+  template <class L>
+  void launch(int kid, L&& fn) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (profiling) {
+      a = get_event();
+      b = get_event();
+      HIPCHECK(hipEventRecord(a, ctx->stream));
+    }
+    fn();
+    HIPCHECK(hipGetLastError());
+    if (profiling) {
+      HIPCHECK(hipEventRecord(b, ctx->stream));
+      pending.push_back({kid, a, b});
+    }
+  }
+
+  void collect_profile() {
+    if (pending.empty()) return;
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    for (auto& e : pending) {
+      float ms = 0.f;
+      HIPCHECK(hipEventElapsedTime(&ms, e.a, e.b));
+      kms[e.kid] += ms;
+      kcount[e.kid] += 1;
+      evpool.push_back(e.a);
+      evpool.push_back(e.b);
+    }
+    pending.clear();
+  }
+
+  ChainState view() {
+    ChainState cs;
+    cs.slot = slot.p;
+    cs.PAI = PAI.p;
+    cs.A = A.p;
+    cs.invA = invA.p;
+    cs.sqrtht = sqrtht.p;
+    cs.h = h.p;
+    cs.sqrtPHI = sqrtPHI.p;
+    cs.PHI = PHI.p;
+    cs.E = E.p;
+    cs.logy2 = logy2.p;
+    cs.eta = eta.p;
+    cs.svobs = svobs.p;
+    cs.svir = svir.p;
+    cs.kai = kai.p;
+    cs.W = W.p;
+    cs.G = G.p;
+    cs.svLd = svLd.p;
+    cs.svw = svw.p;
+    cs.Zphi = Zphi.p;
+    cs.status = status.p;
+    return cs;
+  }
+  XSel xsel() const { return XSel{Xpool.p, xidx.p, Ypool.p, yidx.p}; }
+
+  int64_t crn_off[8] = {};
+  int64_t crn_len = 0;
+
+  void init(ccmm_ctx* c, const ccmm_chain_config& cf, int nX, int nY) {
+    ctx = c;
+    cfg = cf;
+    require(cf.N >= 1 && cf.N <= kMaxNSmall, "N must be in [1, 32]");
+    require(cf.K == cf.N * cf.p + 1 || cf.p == 0, "K must equal N*p+1");
+    require(cf.K >= 1 && cf.K <= 1536, "K must be in [1, 1536]");
+    require(cf.T >= 2 && cf.B >= 1 && cf.ndata >= 1, "bad T/B/ndata");
+    d.N = cf.N;
+    d.p = cf.p;
+    d.K = cf.K;
+    d.KP = round_up(cf.K, kTile);
+    d.TP = round_up(cf.T, kTChunk);
+    d.B = cf.B;
+    d.nmat = cf.B * cf.N;
+    require(d.KP <= 512, "this build supports K <= 512 (KP <= 512)");
+    nslabX = nX;
+    nslabY = nY;
+    const size_t B = cf.B, N = cf.N, KP = d.KP, TP = d.TP;
+    hT.assign(cf.ndata, cf.T);
+    have_slot.assign(cf.ndata, false);
+    Tslot.alloc(cf.ndata);
+    slot.alloc(B);
+    xidx.alloc(B * N);
+    yidx.alloc(B);
+    status.alloc(B);
+    Xpool.alloc((size_t)nX * KP * TP);
+    Ypool.alloc((size_t)nY * N * TP);
+    HIPCHECK(hipMemsetAsync(Xpool.p, 0, Xpool.n * sizeof(double), ctx->stream));
+    HIPCHECK(hipMemsetAsync(Ypool.p, 0, Ypool.n * sizeof(double), ctx->stream));
+    iVdiag.alloc((size_t)cf.ndata * N * KP);
+    iVb.alloc((size_t)cf.ndata * N * KP);
+    sPHI.alloc((size_t)cf.ndata * N * N);
+    V0inv.alloc((size_t)cf.ndata * N * N);
+    V0invm.alloc((size_t)cf.ndata * N);
+    PAI.alloc(B * N * KP);
+    HIPCHECK(hipMemsetAsync(PAI.p, 0, PAI.n * sizeof(double), ctx->stream));
+    A.alloc(B * N * N);
+    invA.alloc(B * N * N);
+    sqrtht.alloc(B * N * TP);
+    h.alloc(B * N * TP);
+    h0.alloc(B * N);
+    sqrtPHI.alloc(B * N * N);
+    PHI.alloc(B * N * N);
+    E.alloc(B * N * TP);
+    logy2.alloc(B * N * TP);
+    eta.alloc(B * N * TP);
+    svobs.alloc(B * N * TP);
+    svir.alloc(B * N * TP);
+    kai.alloc(B * N * TP);
+    W.alloc(B * N * TP);
+    std::vector<int> zeros(cf.ndata, cf.T);
+    HIPCHECK(hipMemcpyAsync(Tslot.p, zeros.data(), cf.ndata * sizeof(int), hipMemcpyHostToDevice,
+                            ctx->stream));
+    std::vector<int> sl(B, 0);
+    set_slots(sl.data());
+    HIPCHECK(hipMemsetAsync(status.p, 0, B * sizeof(int), ctx->stream));
+    // CRN layout (blocks in CCMM_RNG_* order, sizes from Tmax)
+    int64_t o = 0;
+    const int64_t T = cf.T;
+    crn_off[CCMM_RNG_PAI] = o;
+    o += (int64_t)cf.K * N;
+    crn_off[CCMM_RNG_A] = o;
+    o += (int64_t)N * (N - 1) / 2;
+    crn_off[CCMM_RNG_SVU] = o;
+    o += (int64_t)N * T;
+    crn_off[CCMM_RNG_SVZ] = o;
+    o += (int64_t)N * (T + 1);
+    crn_off[CCMM_RNG_PHI] = o;
+    o += (int64_t)N * (T + cf.dPHI);
+    crn_len = o;
+  }
+
+  // default index maps for the sweep-level linear model: X/Y slab = data slot
+  void set_slots(const int* sl) {
+    const int B = cfg.B, N = cfg.N;
+    std::vector<int> xi((size_t)B * N), yi(B);
+    for (int c = 0; c < B; ++c) {
+      require(sl[c] >= 0 && sl[c] < cfg.ndata, "slot out of range");
+      yi[c] = sl[c];
+      for (int j = 0; j < N; ++j) xi[(size_t)c * N + j] = sl[c];
+    }
+    HIPCHECK(hipMemcpyAsync(slot.p, sl, B * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHECK(hipMemcpyAsync(xidx.p, xi.data(), xi.size() * sizeof(int), hipMemcpyHostToDevice,
+                            ctx->stream));
+    HIPCHECK(hipMemcpyAsync(yidx.p, yi.data(), yi.size() * sizeof(int), hipMemcpyHostToDevice,
+                            ctx->stream));
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    resid_valid = false;
+  }
+
+  void upload_X(int slab, int T, const double* X) {  // X: T x K column-major
+    const int K = d.K, KP = d.KP, TP = d.TP;
+    std::vector<double> buf((size_t)KP * TP, 0.0);
+    for (int a = 0; a < K; ++a)
+      for (int t = 0; t < T; ++t) buf[(size_t)a * TP + t] = X[(size_t)a * T + t];
+    HIPCHECK(hipMemcpy(Xpool.p + (size_t)slab * KP * TP, buf.data(), buf.size() * sizeof(double),
+                       hipMemcpyHostToDevice));
+  }
+  void upload_TN(double* dst, int nmat, int T, const double* src, double pad) {
+    // nmat matrices of T x N (column-major) -> [m][N][TP]
+    const int N = d.N, TP = d.TP;
+    std::vector<double> buf((size_t)nmat * N * TP, pad);
+    for (int m = 0; m < nmat; ++m)
+      for (int i = 0; i < N; ++i)
+        for (int t = 0; t < T; ++t)
+          buf[((size_t)m * N + i) * TP + t] = src[((size_t)m * N + i) * T + t];
+    HIPCHECK(hipMemcpy(dst, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
+  void download_TN(const double* srcd, int nmat, int T, double* dst) {
+    const int N = d.N, TP = d.TP;
+    std::vector<double> buf((size_t)nmat * N * TP);
+    HIPCHECK(hipMemcpy(buf.data(), srcd, buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int m = 0; m < nmat; ++m)
+      for (int i = 0; i < N; ++i)
+        for (int t = 0; t < T; ++t)
+          dst[((size_t)m * N + i) * T + t] = buf[((size_t)m * N + i) * TP + t];
+  }
+  void upload_KN(double* dst, int nmat, const double* src, double pad) {
+    const int N = d.N, K = d.K, KP = d.KP;
+    std::vector<double> buf((size_t)nmat * N * KP, pad);
+    for (int m = 0; m < nmat; ++m)
+      for (int j = 0; j < N; ++j)
+        for (int a = 0; a < K; ++a)
+          buf[((size_t)m * N + j) * KP + a] = src[((size_t)m * N + j) * K + a];
+    HIPCHECK(hipMemcpy(dst, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
+  void download_KN(const double* srcd, int nmat, double* dst) {
+    const int N = d.N, K = d.K, KP = d.KP;
+    std::vector<double> buf((size_t)nmat * N * KP);
+    HIPCHECK(hipMemcpy(buf.data(), srcd, buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int m = 0; m < nmat; ++m)
+      for (int j = 0; j < N; ++j)
+        for (int a = 0; a < K; ++a)
+          dst[((size_t)m * N + j) * K + a] = buf[((size_t)m * N + j) * KP + a];
+  }
+
+  void set_slot_prior(int s, const double* iVd, const double* ivb, const double* sP,
+                      const double* h0mean, const double* h0vcvsqrt) {
+    const int N = d.N;
+    upload_KN(iVdiag.p + (size_t)s * N * d.KP, 1, iVd, 1.0);
+    upload_KN(iVb.p + (size_t)s * N * d.KP, 1, ivb, 0.0);
+    HIPCHECK(hipMemcpy(sPHI.p + (size_t)s * N * N, sP, N * N * sizeof(double), hipMemcpyHostToDevice));
+    set_slot_h0(s, h0mean, h0vcvsqrt);
+  }
+  void set_slot_h0(int s, const double* h0mean, const double* h0vcvsqrt) {
+    const int N = d.N;
+    std::vector<double> V0(N * N, 0.0);
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) {
+        double v = 0;
+        for (int k = 0; k < N; ++k) v += h0vcvsqrt[i + k * N] * h0vcvsqrt[j + k * N];
+        V0[i + j * N] = v;
+      }
+    std::vector<double> Vi = host_spd_inverse(V0, N);
+    std::vector<double> m(N, 0.0);
+    for (int i = 0; i < N; ++i)
+      for (int k = 0; k < N; ++k) m[i] += Vi[i + k * N] * h0mean[k];
+    HIPCHECK(hipMemcpy(V0inv.p + (size_t)s * N * N, Vi.data(), N * N * sizeof(double),
+                       hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(V0invm.p + (size_t)s * N, m.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  }
+  void set_T(int s, int T) {
+    require(T >= 2 && T <= cfg.T, "slot T out of range");
+    hT[s] = T;
+    HIPCHECK(hipMemcpy(Tslot.p + s, &T, sizeof(int), hipMemcpyHostToDevice));
+  }
+
+  // ---------------------------------------------------------- kernel launches
+  RngArgs rng_args(const double* dcrn, int64_t stride) const {
+    RngArgs ra{};
+    ra.crn = dcrn;
+    ra.crn_chain_stride = stride;
+    ra.seed = cfg.seed;
+    ra.sweep = sweep;
+    for (int i = 0; i < 8; ++i) ra.off[i] = crn_off[i];
+    return ra;
+  }
+
+  void ensure_cta() {
+    G.alloc((size_t)d.nmat * d.KP * d.KP);
+    rdiag.alloc((size_t)d.nmat * d.KP);
+  }
+
+  void run_resid() {
+    ChainState cs = view();
+    launch(KID_RESID, [&] {
+      hipLaunchKernelGGL(k_resid, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0, ctx->stream, d,
+                         Tslot.p, xsel(), cs);
+    });
+    resid_valid = true;
+  }
+
+  void run_cta(const RngArgs& ra) {
+    ensure_cta();
+    ChainState cs = view();
+    if (!resid_valid) run_resid();
+    launch(KID_WEIGHTS, [&] {
+      hipLaunchKernelGGL(k_cta_weights, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0,
+                         ctx->stream, d, Tslot.p, cs);
+    });
+    const int nt = d.KP / kTile;
+    launch(KID_SYRK, [&] {
+      hipLaunchKernelGGL(k_syrk, dim3(nt * (nt + 1) / 2, d.nmat), dim3(256), 0, ctx->stream, d,
+                         Tslot.p, xsel(), cs);
+    });
+    const size_t lds_chol = (size_t)(kCholNB * (kCholNB + 1) + d.KP * (kCholNB + 1)) * sizeof(double);
+    launch(KID_CHOL, [&] {
+      HIPCHECK(hipFuncSetAttribute((const void*)k_chol, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds_chol));
+      hipLaunchKernelGGL(k_chol, dim3(d.nmat), dim3(256), lds_chol, ctx->stream, d, slot.p,
+                         iVdiag.p, cs, rdiag.p);
+    });
+    const size_t lds_solve = (size_t)(d.TP + d.KP) * sizeof(double);
+    launch(KID_SOLVE, [&] {
+      const int rpl = d.KP / 64;
+      switch (rpl) {
+#define CASE_RPL(R)                                                                              \
+  case R:                                                                                        \
+    hipLaunchKernelGGL(k_cta_solve<R>, dim3(d.B), dim3(256), lds_solve, ctx->stream, d, Tslot.p, \
+                       iVb.p, xsel(), cs, rdiag.p, ra);                                          \
+    break;
+        CASE_RPL(1)
+        CASE_RPL(2)
+        CASE_RPL(3)
+        CASE_RPL(4)
+        CASE_RPL(5)
+        CASE_RPL(6)
+        CASE_RPL(7)
+        CASE_RPL(8)
+#undef CASE_RPL
+        default:
+          throw ArgError("unsupported KP");
+      }
+    });
+  }
+
+  void run_astep(const RngArgs& ra) {
+    ChainState cs = view();
+    const int N = d.N;
+    const int total = (N - 1) * N * (N + 1) / 6 + N * (N - 1) / 2 + 8;
+    const size_t lds = (size_t)(total + N * N) * sizeof(double);
+    launch(KID_ASTEP, [&] {
+      hipLaunchKernelGGL(k_astep, dim3(d.B), dim3(256), lds, ctx->stream, d, Tslot.p, cs, ra,
+                         cfg.logy2offset);
+    });
+  }
+
+  void ensure_sv() {
+    svLd.alloc((size_t)d.B * (d.TP + 1) * d.N * d.N);
+    svw.alloc((size_t)d.B * (d.TP + 1) * d.N);
+  }
+
+  void run_sv(const RngArgs& ra) {
+    ensure_sv();
+    ChainState cs = view();
+    launch(KID_SVMIX, [&] {
+      hipLaunchKernelGGL(k_sv_mix, dim3((d.N * d.TP + 255) / 256, d.B), dim3(256), 0, ctx->stream,
+                         d, Tslot.p, cs, ra);
+    });
+    const size_t lds = (size_t)(4 * d.N * (d.N + 1) + d.N) * sizeof(double);
+    launch(KID_SVSAMPLE, [&] {
+      hipLaunchKernelGGL(k_sv_sample, dim3(d.B), dim3(64), lds, ctx->stream, d, Tslot.p, V0inv.p,
+                         V0invm.p, cs, ra);
+    });
+  }
+
+  void run_phi(const RngArgs& ra) {
+    Zphi.alloc((size_t)d.B * d.N * (d.TP + cfg.dPHI));
+    ChainState cs = view();
+    launch(KID_PHIGEN, [&] {
+      hipLaunchKernelGGL(k_phi_gen, dim3((d.N * (d.TP + cfg.dPHI) + 255) / 256, d.B), dim3(256), 0,
+                         ctx->stream, d, Tslot.p, cfg.dPHI, cs, ra);
+    });
+    const size_t lds = (size_t)(4 * d.N * (d.N + 1)) * sizeof(double);
+    launch(KID_PHI, [&] {
+      hipLaunchKernelGGL(k_phi, dim3(d.B), dim3(256), lds, ctx->stream, d, Tslot.p, cfg.dPHI,
+                         sPHI.p, cs);
+    });
+  }
+
+  void run_store() {
+    if (cfg.store_capacity <= 0) return;
+    if (stored >= cfg.store_capacity) throw ArgError("draw store full: call ccmm_chains_get_draws");
+    const size_t B = d.B, N = d.N, K = d.K, cap = cfg.store_capacity;
+    sPAI.alloc(B * cap * K * N);
+    sPHI_.alloc(B * cap * N * (N + 1) / 2);
+    sInvA.alloc(B * cap * N * N);
+    sSqrtht.alloc(B * cap * (size_t)cfg.T * N);
+    Store st{sPAI.p, sPHI_.p, sInvA.p, sSqrtht.p, cfg.store_capacity, stored, cfg.T};
+    ChainState cs = view();
+    launch(KID_STORE, [&] {
+      hipLaunchKernelGGL(k_store, dim3(64, d.B), dim3(256), 0, ctx->stream, d, cs, st);
+    });
+    ++stored;
+  }
+
+  void sweep_once(const double* dcrn, int64_t stride, bool store) {
+    const RngArgs ra = rng_args(dcrn, stride);
+    run_cta(ra);
+    run_astep(ra);
+    run_sv(ra);
+    run_phi(ra);
+    if (store) run_store();
+    ++sweep;
+  }
+
+  int check_status() {
+    std::vector<int> st(d.B);
+    HIPCHECK(hipMemcpy(st.data(), status.p, d.B * sizeof(int), hipMemcpyDeviceToHost));
+    int any = 0;
+    for (int v : st) any |= v;
+    if (any) {
+      HIPCHECK(hipMemset(status.p, 0, d.B * sizeof(int)));
+      g_err = "non positive-definite matrix in a Gibbs block (status bits " + std::to_string(any) + ")";
+      return CCMM_ERR_NOTSPD;
+    }
+    return CCMM_OK;
+  }
+};
+
+// ============================================================== C ABI
+extern "C" {
+
+int ccmm_abi_version(void) { return CCMM_ABI_VERSION; }
+const char* ccmm_last_error(void) { return g_err.c_str(); }
+
+int ccmm_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+ccmm_ctx* ccmm_create(int device) {
+  ccmm_ctx* ctx = nullptr;
+  int rc = guarded([&] {
+    int n = 0;
+    HIPCHECK(hipGetDeviceCount(&n));
+    require(device >= 0 && device < n, "device index out of range");
+    HIPCHECK(hipSetDevice(device));
+    ctx = new ccmm_ctx;
+    ctx->device = device;
+    HIPCHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    return 0;
+  });
+  if (rc != 0) {
+    delete ctx;
+    return nullptr;
+  }
+  return ctx;
+}
+
+void ccmm_destroy(ccmm_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int ccmm_synchronize(ccmm_ctx* ctx) {
+  return guarded([&] {
+    require(ctx != nullptr, "null context");
+    HIPCHECK(hipSetDevice(ctx->device));
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    return 0;
+  });
+}
+
+// ------------------------------------------------------------ block-level drop-ins
+static ccmm_chain_config block_cfg(int B, int T, int N, int K) {
+  ccmm_chain_config cf{};
+  cf.model = CCMM_MODEL_LINEAR;
+  cf.N = N;
+  cf.p = (K - 1) / (N > 0 ? N : 1);
+  cf.K = K;
+  cf.T = T;
+  cf.B = B;
+  cf.ndata = 1;
+  cf.dPHI = N + 3;
+  cf.rng_crn = 1;
+  cf.logy2offset = 1e-3;
+  cf.seed = 0;
+  return cf;
+}
+
+int ccmm_cta(ccmm_ctx* ctx, int B, int T, int N, int K, const double* Y, int y_per_chain,
+             const double* X, int nx, int x_per_chain, const double* A, const double* sqrtht,
+             const double* iVdiag, const double* iVb, double* PAI, const double* z, int* status) {
+  return guarded([&] {
+    require(ctx && Y && X && A && sqrtht && iVdiag && iVb && PAI, "null argument");
+    require(nx == 1 || nx == N, "nx must be 1 (CTA) or N (CTAsys)");
+    HIPCHECK(hipSetDevice(ctx->device));
+    ccmm_chains ch;
+    ccmm_chain_config cf = block_cfg(B, T, N, K);
+    cf.p = 0;  // K free-form for the block call
+    const int nX = nx * (x_per_chain ? B : 1), nY = y_per_chain ? B : 1;
+    ch.init(ctx, cf, nX, nY);
+    for (int q = 0; q < nX; ++q) ch.upload_X(q, T, X + (size_t)q * T * K);
+    ch.upload_TN(ch.Ypool.p, nY, T, Y, 0.0);
+    std::vector<int> xi((size_t)B * N), yi(B);
+    for (int c = 0; c < B; ++c) {
+      yi[c] = y_per_chain ? c : 0;
+      for (int j = 0; j < N; ++j) xi[(size_t)c * N + j] = (x_per_chain ? c * nx : 0) + (nx == 1 ? 0 : j);
+    }
+    HIPCHECK(hipMemcpy(ch.xidx.p, xi.data(), xi.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(ch.yidx.p, yi.data(), yi.size() * sizeof(int), hipMemcpyHostToDevice));
+    ch.upload_KN(ch.iVdiag.p, 1, iVdiag, 1.0);
+    ch.upload_KN(ch.iVb.p, 1, iVb, 0.0);
+    HIPCHECK(hipMemcpy(ch.A.p, A, (size_t)B * N * N * sizeof(double), hipMemcpyHostToDevice));
+    ch.upload_TN(ch.sqrtht.p, B, T, sqrtht, 1.0);
+    ch.upload_KN(ch.PAI.p, B, PAI, 0.0);
+    DBuf<double> dz;
+    if (z) {
+      dz.alloc((size_t)B * K * N);
+      HIPCHECK(hipMemcpy(dz.p, z, dz.n * sizeof(double), hipMemcpyHostToDevice));
+    }
+    RngArgs ra = ch.rng_args(dz.p, (int64_t)K * N);
+    ra.off[CCMM_RNG_PAI] = 0;
+    ch.run_cta(ra);
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    ch.download_KN(ch.PAI.p, B, PAI);
+    std::vector<int> st(B);
+    HIPCHECK(hipMemcpy(st.data(), ch.status.p, B * sizeof(int), hipMemcpyDeviceToHost));
+    int any = 0;
+    for (int c = 0; c < B; ++c) {
+      if (status) status[c] = st[c];
+      any |= st[c];
+    }
+    if (any) {
+      g_err = "posterior precision not positive definite (QR fallback not available on device)";
+      return CCMM_ERR_NOTSPD;
+    }
+    return 0;
+  });
+}
+
+int ccmm_astep(ccmm_ctx* ctx, int B, int T, int N, const double* RESID, const double* sqrtht,
+               const double* z, double* A, double* invA) {
+  return guarded([&] {
+    require(ctx && RESID && sqrtht && A && invA, "null argument");
+    HIPCHECK(hipSetDevice(ctx->device));
+    ccmm_chains ch;
+    ccmm_chain_config cf = block_cfg(B, T, N, 1);
+    cf.p = 0;
+    ch.init(ctx, cf, 1, 1);
+    ch.upload_TN(ch.E.p, B, T, RESID, 0.0);
+    ch.upload_TN(ch.sqrtht.p, B, T, sqrtht, 1.0);
+    DBuf<double> dz;
+    const int64_t nz = (int64_t)N * (N - 1) / 2;
+    if (z && nz > 0) {
+      dz.alloc((size_t)B * nz);
+      HIPCHECK(hipMemcpy(dz.p, z, dz.n * sizeof(double), hipMemcpyHostToDevice));
+    }
+    RngArgs ra = ch.rng_args(dz.p, nz);
+    ra.off[CCMM_RNG_A] = 0;
+    ch.run_astep(ra);
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    HIPCHECK(hipMemcpy(A, ch.A.p, (size_t)B * N * N * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(invA, ch.invA.p, (size_t)B * N * N * sizeof(double), hipMemcpyDeviceToHost));
+    return ch.check_status();
+  });
+}
+
+int ccmm_sv_ksc(ccmm_ctx* ctx, int B, int T, int N, const double* logy2T, const double* hprevT,
+                const double* sqrtPHI, const double* h0mean, const double* h0vcvsqrt,
+                const double* u, const double* z, double* hT, double* h0, double* shocksT,
+                int8_t* kai2) {
+  return guarded([&] {
+    require(ctx && logy2T && hprevT && sqrtPHI && h0mean && h0vcvsqrt, "null argument");
+    HIPCHECK(hipSetDevice(ctx->device));
+    ccmm_chains ch;
+    ccmm_chain_config cf = block_cfg(B, T, N, 1);
+    cf.p = 0;
+    ch.init(ctx, cf, 1, 1);
+    // N x T (x B) -> internal [c][i][t]
+    std::vector<double> tmp((size_t)B * N * T);
+    auto transpose_in = [&](const double* src) {
+      for (int c = 0; c < B; ++c)
+        for (int t = 0; t < T; ++t)
+          for (int i = 0; i < N; ++i)
+            tmp[((size_t)c * N + i) * T + t] = src[((size_t)c * T + t) * N + i];
+    };
+    transpose_in(logy2T);
+    ch.upload_TN(ch.logy2.p, B, T, tmp.data(), 0.0);
+    transpose_in(hprevT);
+    ch.upload_TN(ch.h.p, B, T, tmp.data(), 0.0);
+    HIPCHECK(hipMemcpy(ch.sqrtPHI.p, sqrtPHI, (size_t)B * N * N * sizeof(double), hipMemcpyHostToDevice));
+    ch.set_slot_h0(0, h0mean, h0vcvsqrt);
+    // CRN: u (N x T) and z (N x (T+1)) per chain, packed into one buffer
+    DBuf<double> dc;
+    const int64_t nu = (int64_t)N * T, nzz = (int64_t)N * (T + 1);
+    RngArgs ra = ch.rng_args(nullptr, 0);
+    if (u || z) {
+      require(u && z, "u and z must both be given or both NULL");
+      std::vector<double> buf((size_t)B * (nu + nzz));
+      for (int c = 0; c < B; ++c) {
+        std::memcpy(&buf[(size_t)c * (nu + nzz)], u + (size_t)c * nu, nu * sizeof(double));
+        std::memcpy(&buf[(size_t)c * (nu + nzz) + nu], z + (size_t)c * nzz, nzz * sizeof(double));
+      }
+      dc.alloc(buf.size());
+      HIPCHECK(hipMemcpy(dc.p, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice));
+      ra = ch.rng_args(dc.p, nu + nzz);
+      ra.off[CCMM_RNG_SVU] = 0;
+      ra.off[CCMM_RNG_SVZ] = nu;
+    }
+    ch.run_sv(ra);
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    auto transpose_out = [&](const double* dsrc, double* dst) {
+      ch.download_TN(dsrc, B, T, tmp.data());
+      for (int c = 0; c < B; ++c)
+        for (int t = 0; t < T; ++t)
+          for (int i = 0; i < N; ++i)
+            dst[((size_t)c * T + t) * N + i] = tmp[((size_t)c * N + i) * T + t];
+    };
+    if (hT) transpose_out(ch.h.p, hT);
+    if (shocksT) transpose_out(ch.eta.p, shocksT);
+    if (h0) {
+      // x_0 = h_1 - shock_1
+      std::vector<double> hh((size_t)B * N * T), ee((size_t)B * N * T);
+      ch.download_TN(ch.h.p, B, T, hh.data());
+      ch.download_TN(ch.eta.p, B, T, ee.data());
+      for (int c = 0; c < B; ++c)
+        for (int i = 0; i < N; ++i)
+          h0[(size_t)c * N + i] = hh[((size_t)c * N + i) * T] - ee[((size_t)c * N + i) * T];
+    }
+    if (kai2) {
+      std::vector<int8_t> kk((size_t)B * N * ch.d.TP);
+      HIPCHECK(hipMemcpy(kk.data(), ch.kai.p, kk.size(), hipMemcpyDeviceToHost));
+      for (int c = 0; c < B; ++c)
+        for (int t = 0; t < T; ++t)
+          for (int i = 0; i < N; ++i)
+            kai2[((size_t)c * T + t) * N + i] = kk[((size_t)c * N + i) * ch.d.TP + t];
+    }
+    return ch.check_status();
+  });
+}
+
+int ccmm_phi_iw(ccmm_ctx* ctx, int B, int T, int N, const double* eta, const double* sPHI,
+                int dPHI, const double* Zdraw, double* sqrtPHI, double* PHI) {
+  return guarded([&] {
+    require(ctx && eta && sPHI && sqrtPHI && PHI, "null argument");
+    HIPCHECK(hipSetDevice(ctx->device));
+    ccmm_chains ch;
+    ccmm_chain_config cf = block_cfg(B, T, N, 1);
+    cf.p = 0;
+    cf.dPHI = dPHI;
+    ch.init(ctx, cf, 1, 1);
+    ch.upload_TN(ch.eta.p, B, T, eta, 0.0);
+    HIPCHECK(hipMemcpy(ch.sPHI.p, sPHI, (size_t)N * N * sizeof(double), hipMemcpyHostToDevice));
+    DBuf<double> dz;
+    const int64_t nz = (int64_t)N * (T + dPHI);
+    if (Zdraw) {
+      dz.alloc((size_t)B * nz);
+      HIPCHECK(hipMemcpy(dz.p, Zdraw, dz.n * sizeof(double), hipMemcpyHostToDevice));
+    }
+    RngArgs ra = ch.rng_args(dz.p, nz);
+    ra.off[CCMM_RNG_PHI] = 0;
+    ch.run_phi(ra);
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    HIPCHECK(hipMemcpy(sqrtPHI, ch.sqrtPHI.p, (size_t)B * N * N * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(PHI, ch.PHI.p, (size_t)B * N * N * sizeof(double), hipMemcpyDeviceToHost));
+    return ch.check_status();
+  });
+}
+
+// erfcinv on the host (Giles 2010 single-precision seed + Halley refinement)
+static double host_erfcinv(double y) {
+  if (y <= 0.0) return INFINITY;
+  if (y >= 2.0) return -INFINITY;
+  // work with x = erfinv(1 - y) using the symmetric form for accuracy near 0
+  const bool upper = y > 1.0;
+  const double yy = upper ? 2.0 - y : y;  // yy in (0, 1]
+  // seed: Giles' approximation of erfinv(1 - yy)
+  double w = -std::log(yy * (2.0 - yy));
+  double p;
+  if (w < 6.25) {
+    w -= 3.125;
+    p = -3.6444120640178196996e-21;
+    p = -1.685059138182016589e-19 + p * w;
+    p = 1.2858480715256400167e-18 + p * w;
+    p = 1.115787767802518096e-17 + p * w;
+    p = -1.333171662854620906e-16 + p * w;
+    p = 2.0972767875968561637e-17 + p * w;
+    p = 6.6376381343583238325e-15 + p * w;
+    p = -4.0545662729752068639e-14 + p * w;
+    p = -8.1519341976054721522e-14 + p * w;
+    p = 2.6335093153082322977e-12 + p * w;
+    p = -1.2975133253453532498e-11 + p * w;
+    p = -5.4154120542946279317e-11 + p * w;
+    p = 1.051212273321532285e-09 + p * w;
+    p = -4.1126339803469836976e-09 + p * w;
+    p = -2.9070369957882005086e-08 + p * w;
+    p = 4.2347877827932403518e-07 + p * w;
+    p = -1.3654692000834678645e-06 + p * w;
+    p = -1.3882523362786468719e-05 + p * w;
+    p = 0.0001867342080340571352 + p * w;
+    p = -0.00074070253416626697512 + p * w;
+    p = -0.0060336708714301490533 + p * w;
+    p = 0.24015818242558961693 + p * w;
+    p = 1.6536545626831027356 + p * w;
+  } else if (w < 16.0) {
+    w = std::sqrt(w) - 3.25;
+    p = 2.2137376921775787049e-09;
+    p = 9.0756561938885390979e-08 + p * w;
+    p = -2.7517406297064545428e-07 + p * w;
+    p = 1.8239629214389227755e-08 + p * w;
+    p = 1.5027403968909827627e-06 + p * w;
+    p = -4.013867526981545969e-06 + p * w;
+    p = 2.9234449089955446044e-06 + p * w;
+    p = 1.2475304481671778723e-05 + p * w;
+    p = -4.7318229009055733981e-05 + p * w;
+    p = 6.8284851459573175448e-05 + p * w;
+    p = 2.4031110387097893999e-05 + p * w;
+    p = -0.0003550375203628474796 + p * w;
+    p = 0.00095328937973738049703 + p * w;
+    p = -0.0016882755560235047313 + p * w;
+    p = 0.0024914420961078508066 + p * w;
+    p = -0.0037512085075692412107 + p * w;
+    p = 0.005370914553590063617 + p * w;
+    p = 1.0052589676941592334 + p * w;
+    p = 3.0838856104922207635 + p * w;
+  } else {
+    w = std::sqrt(w) - 5.0;
+    p = -2.7109920616438573243e-11;
+    p = -2.5556418169965252055e-10 + p * w;
+    p = 1.5076572693500548083e-09 + p * w;
+    p = -3.7894654401267369937e-09 + p * w;
+    p = 7.6157012080783393804e-09 + p * w;
+    p = -1.4960026627149240478e-08 + p * w;
+    p = 2.9147953450901080826e-08 + p * w;
+    p = -6.7711997758452339498e-08 + p * w;
+    p = 2.2900482228026654717e-07 + p * w;
+    p = -9.9298272942317002539e-07 + p * w;
+    p = 4.5260625972231537039e-06 + p * w;
+    p = -1.9681778105531670567e-05 + p * w;
+    p = 7.5995277030017761139e-05 + p * w;
+    p = -0.00021503011930044477347 + p * w;
+    p = -0.00013871931833623122026 + p * w;
+    p = 1.0103004648645343977 + p * w;
+    p = 4.8499064014085844221 + p * w;
+  }
+  double x = p * (1.0 - yy);  // erfinv(1 - yy) >= 0
+  // Halley refinement on erfc(x) = yy
+  for (int it = 0; it < 3; ++it) {
+    const double f = std::erfc(x) - yy;
+    const double dfx = -1.1283791670955126 * std::exp(-x * x);  // d/dx erfc
+    const double d2 = -2.0 * x * dfx;
+    x -= f / (dfx - 0.5 * f * d2 / dfx);
+  }
+  return upper ? -x : x;
+}
+
+double ccmm_draw_trunc_normal(double mu, double sig, double elb, double u, uint8_t* flags) {
+  const double tol = 1e-10;
+  const double eps = 2.220446049250313080847e-16;
+  sig = std::fabs(sig);
+  if (sig > tol) {
+    const double ub = (elb - mu) / sig;
+    const double PHIbar = 0.5 * std::erfc(-std::sqrt(0.5) * ub);
+    double zz;
+    if (PHIbar > eps) {
+      zz = -std::sqrt(2.0) * host_erfcinv(2.0 * u * PHIbar);
+      if (flags) *flags = 3;
+    } else {
+      zz = ub;
+      if (flags) *flags = 1;
+    }
+    return mu + sig * zz;
+  }
+  if (flags) *flags = 0;
+  return mu;
+}
+
+int ccmm_draw_trunc_normal_batch(ccmm_ctx* ctx, int n, const double* mu, const double* sig,
+                                 double elb, const double* u, double* out, uint8_t* flags) {
+  return guarded([&] {
+    require(ctx && mu && sig && u && out && n >= 0, "null argument");
+    if (n == 0) return 0;
+    HIPCHECK(hipSetDevice(ctx->device));
+    DBuf<double> dmu, dsig, du, dout;
+    DBuf<uint8_t> dfl;
+    dmu.alloc(n);
+    dsig.alloc(n);
+    du.alloc(n);
+    dout.alloc(n);
+    dfl.alloc(n);
+    HIPCHECK(hipMemcpy(dmu.p, mu, n * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(dsig.p, sig, n * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(du.p, u, n * sizeof(double), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_truncnorm, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, n, dmu.p,
+                       dsig.p, elb, du.p, dout.p, dfl.p);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    HIPCHECK(hipMemcpy(out, dout.p, n * sizeof(double), hipMemcpyDeviceToHost));
+    if (flags) HIPCHECK(hipMemcpy(flags, dfl.p, n, hipMemcpyDeviceToHost));
+    return 0;
+  });
+}
+
+// ------------------------------------------------------------ sweep-level API
+ccmm_chains* ccmm_chains_create(ccmm_ctx* ctx, const ccmm_chain_config* cfg) {
+  ccmm_chains* ch = nullptr;
+  int rc = guarded([&] {
+    require(ctx && cfg, "null argument");
+    require(cfg->model == CCMM_MODEL_LINEAR, "only CCMM_MODEL_LINEAR is available in this build");
+    HIPCHECK(hipSetDevice(ctx->device));
+    ch = new ccmm_chains;
+    ch->init(ctx, *cfg, cfg->ndata, cfg->ndata);
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    return 0;
+  });
+  if (rc != 0) {
+    delete ch;
+    return nullptr;
+  }
+  return ch;
+}
+
+void ccmm_chains_destroy(ccmm_chains* ch) {
+  if (!ch) return;
+  (void)hipSetDevice(ch->ctx->device);
+  (void)hipStreamSynchronize(ch->ctx->stream);
+  delete ch;
+}
+
+int ccmm_chains_set_data(ccmm_chains* ch, int slot, int T, const double* Y, const double* X,
+                         const double* iVdiag, const double* iVb, const double* sPHI,
+                         const double* h0mean, const double* h0vcvsqrt) {
+  return guarded([&] {
+    require(ch && Y && X && iVdiag && iVb && sPHI && h0mean && h0vcvsqrt, "null argument");
+    require(slot >= 0 && slot < ch->cfg.ndata, "slot out of range");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    ch->set_T(slot, T);
+    ch->upload_X(slot, T, X);
+    ch->upload_TN(ch->Ypool.p + (size_t)slot * ch->d.N * ch->d.TP, 1, T, Y, 0.0);
+    ch->set_slot_prior(slot, iVdiag, iVb, sPHI, h0mean, h0vcvsqrt);
+    ch->have_slot[slot] = true;
+    ch->resid_valid = false;
+    return 0;
+  });
+}
+
+int ccmm_chains_set_slots(ccmm_chains* ch, const int* slot_of_chain) {
+  return guarded([&] {
+    require(ch && slot_of_chain, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    ch->set_slots(slot_of_chain);
+    return 0;
+  });
+}
+
+int ccmm_chains_set_state(ccmm_chains* ch, const double* PAI, const double* A,
+                          const double* sqrtht, const double* h, const double* sqrtPHI) {
+  return guarded([&] {
+    require(ch && PAI && A && sqrtht && h && sqrtPHI, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    const int B = ch->d.B, N = ch->d.N, T = ch->cfg.T;
+    ch->upload_KN(ch->PAI.p, B, PAI, 0.0);
+    HIPCHECK(hipMemcpy(ch->A.p, A, (size_t)B * N * N * sizeof(double), hipMemcpyHostToDevice));
+    ch->upload_TN(ch->sqrtht.p, B, T, sqrtht, 1.0);
+    ch->upload_TN(ch->h.p, B, T, h, 0.0);
+    HIPCHECK(hipMemcpy(ch->sqrtPHI.p, sqrtPHI, (size_t)B * N * N * sizeof(double), hipMemcpyHostToDevice));
+    ch->sweep = 0;
+    ch->stored = 0;
+    ch->resid_valid = false;
+    ch->have_state = true;
+    return 0;
+  });
+}
+
+int ccmm_chains_get_state(ccmm_chains* ch, double* PAI, double* A, double* invA, double* sqrtht,
+                          double* h, double* sqrtPHI, double* PHI, double* RESID) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    const int B = ch->d.B, N = ch->d.N, T = ch->cfg.T;
+    const size_t nn = (size_t)B * N * N * sizeof(double);
+    if (PAI) ch->download_KN(ch->PAI.p, B, PAI);
+    if (A) HIPCHECK(hipMemcpy(A, ch->A.p, nn, hipMemcpyDeviceToHost));
+    if (invA) HIPCHECK(hipMemcpy(invA, ch->invA.p, nn, hipMemcpyDeviceToHost));
+    if (sqrtht) ch->download_TN(ch->sqrtht.p, B, T, sqrtht);
+    if (h) ch->download_TN(ch->h.p, B, T, h);
+    if (sqrtPHI) HIPCHECK(hipMemcpy(sqrtPHI, ch->sqrtPHI.p, nn, hipMemcpyDeviceToHost));
+    if (PHI) HIPCHECK(hipMemcpy(PHI, ch->PHI.p, nn, hipMemcpyDeviceToHost));
+    if (RESID) ch->download_TN(ch->E.p, B, T, RESID);
+    return 0;
+  });
+}
+
+int64_t ccmm_chains_crn_len(const ccmm_chains* ch) { return ch ? ch->crn_len : -1; }
+
+int ccmm_chains_sweep(ccmm_chains* ch, int nsweeps, const double* crn, int store) {
+  return guarded([&] {
+    require(ch != nullptr && nsweeps >= 0, "bad argument");
+    if (!ch->have_state) {
+      g_err = "ccmm_chains_set_state must be called before sweeping";
+      return CCMM_ERR_STATE;
+    }
+    for (int s = 0; s < ch->cfg.ndata; ++s)
+      if (!ch->have_slot[s]) {
+        g_err = "ccmm_chains_set_data missing for a data slot";
+        return CCMM_ERR_STATE;
+      }
+    if (ch->cfg.rng_crn) require(crn != nullptr, "chain set was created in CRN mode: crn required");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    if (crn) {
+      ch->crn.alloc((size_t)ch->d.B * nsweeps * ch->crn_len);
+      HIPCHECK(hipMemcpyAsync(ch->crn.p, crn, (size_t)ch->d.B * nsweeps * ch->crn_len * sizeof(double),
+                              hipMemcpyHostToDevice, ch->ctx->stream));
+    }
+    for (int m = 0; m < nsweeps; ++m) {
+      const double* base = crn ? ch->crn.p + (size_t)m * ch->crn_len : nullptr;
+      ch->sweep_once(base, (int64_t)nsweeps * ch->crn_len, store != 0);
+    }
+    if (ch->profiling) ch->collect_profile();
+    if (crn) {
+      HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+      return ch->check_status();
+    }
+    return 0;
+  });
+}
+
+int ccmm_chains_stored(const ccmm_chains* ch) { return ch ? ch->stored : -1; }
+
+int ccmm_chains_get_draws(ccmm_chains* ch, double* PAI_all, double* PHI_all, double* invA_all,
+                          double* sqrtht_all) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    const size_t B = ch->d.B, N = ch->d.N, K = ch->d.K, cap = ch->cfg.store_capacity;
+    const size_t M = ch->stored, T = ch->cfg.T;
+    auto fetch = [&](const DBuf<double>& src, size_t per, double* dst) {
+      if (!dst || M == 0) return;
+      std::vector<double> buf(B * cap * per);
+      HIPCHECK(hipMemcpy(buf.data(), src.p, buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+      // device [c][m][e] -> MATLAB M x (e...) x B, i.e. dst[m + M*(e + per*c)]
+      for (size_t c = 0; c < B; ++c)
+        for (size_t m = 0; m < M; ++m)
+          for (size_t e = 0; e < per; ++e) dst[m + M * (e + per * c)] = buf[(c * cap + m) * per + e];
+    };
+    fetch(ch->sPAI, K * N, PAI_all);
+    fetch(ch->sPHI_, N * (N + 1) / 2, PHI_all);
+    fetch(ch->sInvA, N * N, invA_all);
+    fetch(ch->sSqrtht, T * N, sqrtht_all);
+    ch->stored = 0;
+    return 0;
+  });
+}
+
+int ccmm_chains_profile(ccmm_chains* ch, int enable) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    ch->collect_profile();
+    ch->profiling = enable != 0;
+    for (int k = 0; k < KID_COUNT; ++k) {
+      ch->kms[k] = 0.0;
+      ch->kcount[k] = 0;
+    }
+    return 0;
+  });
+}
+
+int ccmm_chains_kernel_times(ccmm_chains* ch, int max, double* ms, int64_t* launches, char* names,
+                             int names_len) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    ch->collect_profile();
+    const int n = std::min<int>(max, KID_COUNT);
+    for (int k = 0; k < n; ++k) {
+      if (ms) ms[k] = ch->kms[k];
+      if (launches) launches[k] = ch->kcount[k];
+    }
+    if (names && names_len > 0) {
+      std::string s;
+      for (int k = 0; k < KID_COUNT; ++k) {
+        if (k) s += ";";
+        s += kKernelNames[k];
+      }
+      std::strncpy(names, s.c_str(), names_len - 1);
+      names[names_len - 1] = 0;
+    }
+    return KID_COUNT;
+  });
+}
+
+int ccmm_selftest_mfma_f64(ccmm_ctx* ctx, const double* A16x4, const double* B4x16, double* D16x16) {
+  return guarded([&] {
+    require(ctx && A16x4 && B4x16 && D16x16, "null argument");
+    HIPCHECK(hipSetDevice(ctx->device));
+    DBuf<double> a, b, dd;
+    a.alloc(64);
+    b.alloc(64);
+    dd.alloc(256);
+    HIPCHECK(hipMemcpy(a.p, A16x4, 64 * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(b.p, B4x16, 64 * sizeof(double), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_mfma_selftest, dim3(1), dim3(64), 0, ctx->stream, a.p, b.p, dd.p);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    HIPCHECK(hipMemcpy(D16x16, dd.p, 256 * sizeof(double), hipMemcpyDeviceToHost));
+    return 0;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,117 @@
+// Internal definitions shared by the HIP kernels and the C-ABI host code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ccmm.h"
+
+namespace ccmm {
+
+// ---------------------------------------------------------------- tiling
+constexpr int kTChunk = 32;   // t-rows per SYRK K-step chunk; T is padded to a multiple
+constexpr int kTile = 64;     // SYRK output tile (64 x 64, 4 waves of 32 x 32)
+constexpr int kCholNB = 32;   // Cholesky panel width
+constexpr int kMaxNSmall = 32;  // per-chain small-matrix kernels (A, SV, PHI) support N <= 32
+
+inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// ---------------------------------------------------------------- RNG
+// Philox4x32-10 (Salmon et al. 2011), counter = (pair index, chain, sweep, block),
+// key = 64-bit seed.  Two doubles per call; normals by Box-Muller.
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__host__ __device__ inline uint32_t mulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+__host__ __device__ inline u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = mulhi32(M0, c.x), lo0 = M0 * c.x;
+    uint32_t hi1 = mulhi32(M1, c.z), lo1 = M1 * c.z;
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// uniform in (0,1) from two 32-bit words (53 bits)
+__host__ __device__ inline double u01(uint32_t lo, uint32_t hi) {
+  uint64_t v = (((uint64_t)hi << 32) | lo) >> 11;
+  return ((double)v + 0.5) * 1.1102230246251565404e-16;  // 2^-53
+}
+
+struct Rng {
+  const double* crn;  // this chain's CRN base for this sweep (nullptr: Philox)
+  uint64_t seed;
+  uint32_t chain, sweep;
+  int64_t off[8];     // CRN block offsets (indexed by CCMM_RNG_* id)
+
+  __host__ __device__ inline u32x4 raw(int block, uint32_t pair) const {
+    return philox4x32_10(u32x4{pair, chain, sweep, (uint32_t)block}, (uint32_t)seed,
+                         (uint32_t)(seed >> 32));
+  }
+  __device__ inline double uniform(int block, uint32_t idx) const {
+    if (crn) return crn[off[block] + idx];
+    u32x4 r = raw(block, idx >> 1);
+    return (idx & 1) ? u01(r.z, r.w) : u01(r.x, r.y);
+  }
+  __device__ inline double normal(int block, uint32_t idx) const {
+    if (crn) return crn[off[block] + idx];
+    u32x4 r = raw(block, idx >> 1);
+    double u1 = u01(r.x, r.y), u2 = u01(r.z, r.w);
+    double rad = sqrt(-2.0 * log(u1));
+    double s, c;
+    sincospi(2.0 * u2, &s, &c);
+    return (idx & 1) ? rad * s : rad * c;
+  }
+};
+
+// ---------------------------------------------------------------- device views
+// All matrices are column-major.  Per-slot data (vintages) and per-chain state
+// use padded leading dimensions: TP (rows of T-dimension arrays), KP (rows of
+// K-dimension arrays).  The chain index is the slowest dimension.
+struct Dims {
+  int N, p, K, KP, TP, B, nmat;  // nmat = B*N CTA systems
+};
+
+struct SlotData {
+  const int* T;           // [ndata]
+  const double* Y;        // [ndata][N][TP]
+  const double* X;        // [ndata][KP][TP]   zero padded beyond (T, K)
+  const double* iVdiag;   // [ndata][N][KP]    padded with 1
+  const double* iVb;      // [ndata][N][KP]    padded with 0
+  const double* sPHI;     // [ndata][N][N]
+  const double* V0inv;    // [ndata][N][N]     (h0vcvsqrt h0vcvsqrt')^-1
+  const double* V0invm;   // [ndata][N]        V0inv * h0mean
+};
+
+struct ChainState {
+  const int* slot;   // [B]
+  double* PAI;       // [B][N][KP]
+  double* A;         // [B][N][N]
+  double* invA;      // [B][N][N]
+  double* sqrtht;    // [B][N][TP]
+  double* h;         // [B][N][TP]
+  double* sqrtPHI;   // [B][N][N]
+  double* PHI;       // [B][N][N]
+  double* E;         // [B][N][TP]  residual Y - X*PAI (RESID)
+  double* logy2;     // [B][N][TP]
+  double* eta;       // [B][N][TP]  SV shocks
+  double* svobs;     // [B][N][TP]  logy2 - mean_{s}
+  double* svir;      // [B][N][TP]  1/var_{s}
+  int8_t* kai;       // [B][N][TP]
+  double* W;         // [B][N][TP]  CTA weights
+  double* G;         // [B*N][KP][KP]  Gram -> Cholesky factor (L lower, L' upper)
+  double* svLd;      // [B][TP+1][N*N] block Cholesky diagonal factors
+  double* svw;       // [B][TP+1][N]
+  double* Zphi;      // [B][N][TZ]  IW normals scratch
+  int* status;       // [B]
+};
+
+}  // namespace ccmm

@@ -1,0 +1,930 @@
+// HIP/CDNA4 (gfx950) kernels of the CCMM BVAR-SV Gibbs sweep.
+//
+// One "system" is one (chain, equation) pair of the triangular CTA algorithm
+// (CTA.m:60-98).  The per-sweep pipeline for B chains is
+//
+//   k_cta_weights   w_t^(j) = sum_{i>=j} A(i,j)^2 / sqrtht(t,i)^2        (elementwise)
+//   k_syrk          G_cj = X' diag(w^(j)) X   on v_mfma_f64_16x16x4_f64    (FP64 MFMA)
+//   k_chol          L_cj = chol(G_cj + diag(iV_j)), writes L (lower), L' (upper), 1/diag
+//   k_cta_solve     per chain, j = 1..N in order: rhs = iVb_j + X' v^(j) (needs the
+//                   draws of equations < j), L L' x = rhs, PAI(:,j) = L'^-1 (L^-1 rhs + z_j),
+//                   residual update.                                    (latency bound)
+//   k_astep         A-matrix rows (mcmcVAR.m:236-254), invA, logy2 (mcmcVAR.m:259)
+//   k_sv_mix        KSC mixture indicators (elementwise)
+//   k_sv_sample     block-tridiagonal precision sampler of h_0..h_T (per chain)
+//   k_phi_gen/k_phi inverse-Wishart PHI draw (mcmcVAR.m:268-274)
+//   k_store         kept-draw storage (mcmcVAR.m:289-292)
+//
+// The algebraic identity X_j'X_j = X' diag(w) X, X_j'Y_j = X' v
+// removes the kron materialisation of CTA.m:69 (T(N-j+1) x K per equation).
+#include "ccmm_internal.h"
+
+namespace ccmm {
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+struct XSel {
+  const double* pool;  // slabs of KP x TP (X stored column-major, ld = TP)
+  const int* idx;      // [B*N] slab of system (c, j)
+  const double* ypool; // slabs of N x TP
+  const int* yidx;     // [B] Y slab of chain c
+};
+
+struct RngArgs {
+  const double* crn;       // CRN base for this sweep (chain 0) or nullptr
+  int64_t crn_chain_stride;
+  uint64_t seed;
+  uint32_t sweep;
+  int64_t off[8];
+
+  __device__ inline Rng make(int c) const {
+    Rng r;
+    r.crn = crn ? crn + (int64_t)c * crn_chain_stride : nullptr;
+    r.seed = seed;
+    r.chain = (uint32_t)c;
+    r.sweep = sweep;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.off[i] = off[i];
+    return r;
+  }
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  union {
+    double d;
+    int i[2];
+  } u;
+  u.d = v;
+  u.i[0] = __builtin_amdgcn_readlane(u.i[0], lane);
+  u.i[1] = __builtin_amdgcn_readlane(u.i[1], lane);
+  return u.d;
+}
+
+// ============================================================== residual
+// E(:,j) = Y(:,j) - X_j * PAI(:,j)   (mcmcVAR.m:233; CTAsys residual mcmcVARshadowrateBlockHybrid.m:348-351)
+__global__ void k_resid(Dims d, const int* __restrict__ Tslot, XSel xs, ChainState cs) {
+  const int c = blockIdx.z, j = blockIdx.y;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= d.TP) return;
+  const int T = Tslot[cs.slot[c]];
+  double* E = cs.E + ((size_t)c * d.N + j) * d.TP;
+  if (t >= T) {
+    E[t] = 0.0;
+    return;
+  }
+  const double* X = xs.pool + (size_t)xs.idx[c * d.N + j] * d.KP * d.TP;
+  const double* Y = xs.ypool + (size_t)xs.yidx[c] * d.N * d.TP;
+  const double* pai = cs.PAI + ((size_t)c * d.N + j) * d.KP;
+  double acc = 0.0;
+  for (int a = 0; a < d.K; ++a) acc = fma(X[(size_t)a * d.TP + t], pai[a], acc);
+  E[t] = Y[(size_t)j * d.TP + t] - acc;
+}
+
+// ============================================================== CTA weights
+// w_t^(j) = sum_{i>=j} A(i,j)^2 / sqrtht(t,i)^2 : the diagonal of kron(A(j:N,j),X)./lambda's
+// Gram (CTA.m:66-73).  Padded rows get weight 0.
+__global__ void k_cta_weights(Dims d, const int* __restrict__ Tslot, ChainState cs) {
+  const int c = blockIdx.z, j = blockIdx.y;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= d.TP) return;
+  const int T = Tslot[cs.slot[c]];
+  double w = 0.0;
+  if (t < T) {
+    const double* A = cs.A + (size_t)c * d.N * d.N;
+    const double* sh = cs.sqrtht + (size_t)c * d.N * d.TP;
+    for (int i = j; i < d.N; ++i) {
+      const double a = A[i + j * d.N] / sh[(size_t)i * d.TP + t];
+      w = fma(a, a, w);
+    }
+  }
+  cs.W[((size_t)c * d.N + j) * d.TP + t] = w;
+}
+
+// ============================================================== weighted SYRK (FP64 MFMA)
+// G_cj[a][b] = sum_t X[t][a] w[t] X[t][b] for the lower 64x64 tiles (ti >= tj).
+// 256 threads = 4 waves, each a 32x32 sub-tile as 2x2 v_mfma_f64_16x16x4_f64 blocks.
+// The MFMA is issued with the b-panel as the A operand so that a lane's 16
+// consecutive accumulator columns are 16 consecutive rows a of column-major G.
+constexpr int kLdP = kTile + 16;  // 80 doubles: conflict-free ds_read_b64 fragment reads
+
+__global__ __launch_bounds__(256) void k_syrk(Dims d, const int* __restrict__ Tslot, XSel xs,
+                                              ChainState cs) {
+  __shared__ double Pa[kTChunk][kLdP];  // weighted a-panel  (t, a)
+  __shared__ double Pb[kTChunk][kLdP];  // b-panel           (t, b)
+  const int mat = blockIdx.y;
+  const int c = mat / d.N;
+  const int T = Tslot[cs.slot[c]];
+  // lower-tile index -> (ti, tj)
+  int tile = blockIdx.x, ti = 0;
+  while (tile > ti) {
+    tile -= ti + 1;
+    ++ti;
+  }
+  const int tj = tile;
+  const int a0 = ti * kTile, b0 = tj * kTile;
+  const double* X = xs.pool + (size_t)xs.idx[mat] * d.KP * d.TP;
+  const double* w = cs.W + (size_t)mat * d.TP;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lcol = tid & 63, lt0 = (tid >> 6) * 8;  // loader: column, 8 consecutive t
+
+  dbl4 acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) acc[x][y] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+  const int nchunks = (T + kTChunk - 1) / kTChunk;
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int t0 = ch * kTChunk;
+    {
+      const double* xa = X + (size_t)(a0 + lcol) * d.TP + t0 + lt0;
+      const double* xb = X + (size_t)(b0 + lcol) * d.TP + t0 + lt0;
+      double va[8], vb[8], ww[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        va[q] = xa[q];
+        vb[q] = xb[q];
+        ww[q] = w[t0 + lt0 + q];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        Pa[lt0 + q][lcol] = va[q] * ww[q];
+        Pb[lt0 + q][lcol] = vb[q];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kTChunk / 4; ++kk) {
+      const int kr = kk * 4 + (lane >> 4);
+      double fa[2], fb[2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        fb[x] = Pb[kr][wn * 32 + x * 16 + (lane & 15)];  // MFMA A operand: rows = b
+        fa[x] = Pa[kr][wm * 32 + x * 16 + (lane & 15)];  // MFMA B operand: cols = a
+      }
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[x], fa[y], acc[x][y], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // D[row = b][col = a]: lane holds rows (lane>>4) + 4r, column lane & 15
+  double* G = cs.G + (size_t)mat * d.KP * d.KP;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = b0 + wn * 32 + x * 16 + (lane >> 4) + 4 * r;
+        const int a = a0 + wm * 32 + y * 16 + (lane & 15);
+        G[(size_t)b * d.KP + a] = acc[x][y][r];
+      }
+}
+
+// ============================================================== batched Cholesky
+// In place on G_cj + diag(iV_j) (CTA.m:73-74).  One workgroup per system,
+// right-looking blocked with 32-wide panels; the diagonal block is factored in
+// registers by one wave (lane i = row i), the panel solve is one row per
+// thread, the trailing update reads the panel from LDS.  Writes L (lower),
+// L' (upper triangle, for the row-oriented back substitution), 1/L_kk.
+__global__ __launch_bounds__(256) void k_chol(Dims d, const int* __restrict__ slotIV,
+                                              const double* __restrict__ iVdiag, ChainState cs,
+                                              double* __restrict__ rdiag) {
+  extern __shared__ double sm[];
+  double* Dg = sm;                    // 32 x 33
+  double* P = sm + kCholNB * (kCholNB + 1);  // (KP) x 33 panel rows
+  const int mat = blockIdx.x;
+  const int c = mat / d.N, j = mat % d.N;
+  const int KP = d.KP;
+  double* A = cs.G + (size_t)mat * KP * KP;
+  const double* iv = iVdiag + ((size_t)slotIV[c] * d.N + j) * KP;
+  double* rd = rdiag + (size_t)mat * KP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int a = tid; a < KP; a += blockDim.x) A[(size_t)a * KP + a] += iv[a];
+  __syncthreads();
+  int bad = 0;
+  for (int k0 = 0; k0 < KP; k0 += kCholNB) {
+    // ---- factor the diagonal block: wave 0, lane i holds row i
+    if (wave == 0) {
+      double row[kCholNB];
+      double mydiag = 1.0;
+#pragma unroll
+      for (int m = 0; m < kCholNB; ++m)
+        row[m] = (lane < kCholNB && m <= lane) ? A[(size_t)(k0 + m) * KP + k0 + lane] : 0.0;
+#pragma unroll
+      for (int kk = 0; kk < kCholNB; ++kk) {
+        double dkk = readlane_d(row[kk], kk);
+        if (!(dkk > 0.0)) {
+          bad = 1;
+          dkk = 1.0;
+        }
+        const double piv = sqrt(dkk);
+        const double rp = 1.0 / piv;
+        if (lane == kk) {
+          row[kk] = piv;
+          mydiag = piv;
+        }
+        if (lane > kk) row[kk] *= rp;
+        const double lik = row[kk];
+#pragma unroll
+        for (int m = kk + 1; m < kCholNB; ++m) {
+          const double lmk = readlane_d(lik, m);
+          if (lane >= m) row[m] = fma(-lik, lmk, row[m]);
+        }
+      }
+      if (lane < kCholNB) {
+#pragma unroll
+        for (int m = 0; m < kCholNB; ++m) {
+          const double v = (m <= lane) ? row[m] : 0.0;
+          Dg[lane * (kCholNB + 1) + m] = v;  // Dg[row][col]
+          if (m <= lane) {
+            A[(size_t)(k0 + m) * KP + k0 + lane] = v;  // L(k0+lane, k0+m)
+            A[(size_t)(k0 + lane) * KP + k0 + m] = v;  // L' (upper)
+          }
+        }
+        rd[k0 + lane] = 1.0 / mydiag;
+      }
+    }
+    __syncthreads();
+    // ---- panel: rows i >= k0+32 solve x * L_kk' = A(i, k0:k0+32)
+    const int r0 = k0 + kCholNB;
+    const int nrow = KP - r0;
+    for (int ii = tid; ii < nrow; ii += blockDim.x) {
+      const int i = r0 + ii;
+      double x[kCholNB];
+#pragma unroll
+      for (int m = 0; m < kCholNB; ++m) x[m] = A[(size_t)(k0 + m) * KP + i];
+#pragma unroll
+      for (int m = 0; m < kCholNB; ++m) {
+        double s = x[m];
+#pragma unroll
+        for (int q = 0; q < m; ++q) s = fma(-x[q], Dg[m * (kCholNB + 1) + q], s);
+        x[m] = s / Dg[m * (kCholNB + 1) + m];
+      }
+#pragma unroll
+      for (int m = 0; m < kCholNB; ++m) {
+        P[ii * (kCholNB + 1) + m] = x[m];
+        A[(size_t)(k0 + m) * KP + i] = x[m];  // L(i, k0+m)
+        A[(size_t)i * KP + k0 + m] = x[m];    // L' (upper)
+      }
+    }
+    __syncthreads();
+    // ---- trailing update of the lower triangle: A(i,jj) -= P(i,:) . P(jj,:)
+    for (int jj = 0; jj < nrow; ++jj) {
+      for (int ii = jj + tid; ii < nrow; ii += blockDim.x) {
+        double s = 0.0;
+#pragma unroll
+        for (int m = 0; m < kCholNB; ++m)
+          s = fma(P[ii * (kCholNB + 1) + m], P[jj * (kCholNB + 1) + m], s);
+        A[(size_t)(r0 + jj) * KP + r0 + ii] -= s;
+      }
+    }
+    __syncthreads();
+  }
+  if (bad && lane == 0) atomicOr(&cs.status[c], 2);
+}
+
+// ============================================================== CTA sequential part
+// One workgroup per chain, equations in order (CTA.m:60-97).  RPL = KP/64 rows
+// of the K-vector per lane in the wave-0 triangular solves.
+template <int RPL>
+__global__ __launch_bounds__(256) void k_cta_solve(Dims d, const int* __restrict__ Tslot,
+                                                   const double* __restrict__ iVb, XSel xs,
+                                                   ChainState cs, const double* __restrict__ rdiag,
+                                                   RngArgs ra) {
+  extern __shared__ double sm[];
+  double* v = sm;           // TP
+  double* yv = sm + d.TP;   // KP
+  const int c = blockIdx.x;
+  const int s = cs.slot[c];
+  const int T = Tslot[s];
+  const int N = d.N, KP = d.KP, TP = d.TP, K = d.K;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Rng rng = ra.make(c);
+  const double* A = cs.A + (size_t)c * N * N;
+  const double* sh = cs.sqrtht + (size_t)c * N * TP;
+  const double* Y = xs.ypool + (size_t)xs.yidx[c] * N * TP;
+  double* E = cs.E + (size_t)c * N * TP;
+
+  for (int j = 0; j < N; ++j) {
+    const int mat = c * N + j;
+    const double* X = xs.pool + (size_t)xs.idx[mat] * KP * TP;
+    // 1. PAI(:,j) = 0  ->  E(:,j) = Y(:,j)
+    for (int t = tid; t < TP; t += blockDim.x) E[(size_t)j * TP + t] = (t < T) ? Y[(size_t)j * TP + t] : 0.0;
+    __syncthreads();
+    // 2. v_t = sum_{i>=j} A(i,j)/sqrtht(t,i)^2 * [E_t A(i,:)']   (X_j'Y_j = X' v, CTA.m:67)
+    for (int t = tid; t < TP; t += blockDim.x) {
+      double acc = 0.0;
+      if (t < T) {
+        for (int i = j; i < N; ++i) {
+          double ea = 0.0;
+          for (int k = 0; k <= i; ++k) ea = fma(E[(size_t)k * TP + t], A[i + k * N], ea);
+          const double hi = sh[(size_t)i * TP + t];
+          acc += A[i + j * N] * (ea / hi) / hi;
+        }
+      }
+      v[t] = acc;
+    }
+    __syncthreads();
+    // 3. rhs = iVb_j + X' v   (one wave per column)
+    const double* ivb = iVb + ((size_t)s * N + j) * KP;
+    for (int a = wave; a < KP; a += 4) {
+      double p = 0.0;
+      if (a < K) {
+        const double* xa = X + (size_t)a * TP;
+        for (int t = lane; t < T; t += 64) p = fma(xa[t], v[t], p);
+      }
+      p = wave_sum(p);
+      if (lane == 0) yv[a] = ivb[a] + p;
+    }
+    __syncthreads();
+    // 4./5. solves on wave 0:  L y = rhs ; L' x = y + z   (x = b_post + Vchol_post z, CTA.m:95-96)
+    if (wave == 0) {
+      const double* L = cs.G + (size_t)mat * KP * KP;
+      const double* rd = rdiag + (size_t)mat * KP;
+      double y[RPL];
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) y[r] = yv[r * 64 + lane];
+      // forward substitution, column oriented
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        for (int kk = 0; kk < 64; ++kk) {
+          const int k = r * 64 + kk;
+          if (k >= K) break;
+          const double yk = readlane_d(y[r], kk) * rd[k];
+          if (lane == kk) y[r] = yk;
+          const double* Lk = L + (size_t)k * KP;
+#pragma unroll
+          for (int r2 = r; r2 < RPL; ++r2) {
+            const int i = r2 * 64 + lane;
+            if (i > k) y[r2] = fma(-Lk[i], yk, y[r2]);
+          }
+        }
+      }
+      // add z_j (randn(K,N) of CTA.m:58, column j)
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        const int a = r * 64 + lane;
+        if (a < K) y[r] += rng.normal(CCMM_RNG_PAI, (uint32_t)(a + K * j));
+      }
+      // back substitution with L' (upper storage: U(i,k) = L(k,i) at column k)
+#pragma unroll
+      for (int r = RPL - 1; r >= 0; --r) {
+        for (int kk = 63; kk >= 0; --kk) {
+          const int k = r * 64 + kk;
+          if (k >= K) continue;
+          const double xk = readlane_d(y[r], kk) * rd[k];
+          if (lane == kk) y[r] = xk;
+          const double* Uk = L + (size_t)k * KP;
+#pragma unroll
+          for (int r2 = 0; r2 <= r; ++r2) {
+            const int i = r2 * 64 + lane;
+            if (i < k) y[r2] = fma(-Uk[i], xk, y[r2]);
+          }
+        }
+      }
+      double* pai = cs.PAI + ((size_t)c * N + j) * KP;
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        const int a = r * 64 + lane;
+        const double val = (a < K) ? y[r] : 0.0;
+        yv[a] = val;
+        pai[a] = val;
+      }
+    }
+    __syncthreads();
+    // 6. E(:,j) = Y(:,j) - X PAI(:,j)
+    for (int t = tid; t < T; t += blockDim.x) {
+      double acc = 0.0;
+      for (int a = 0; a < K; ++a) acc = fma(X[(size_t)a * TP + t], yv[a], acc);
+      E[(size_t)j * TP + t] = Y[(size_t)j * TP + t] - acc;
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================================== A-step
+// mcmcVAR.m:236-254 (flat prior: OMEGA_A_inv = 0, MU_A = 0, mcmcVAR.m:153-161),
+// invA = A \ I (mcmcVAR.m:254), logy2 = log((RESID*A').^2 + offset) (mcmcVAR.m:259).
+// LDS: per ii a packed lower ZZ (ii x ii) followed by Zz (ii).
+__global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ Tslot, ChainState cs,
+                                               RngArgs ra, double logy2offset) {
+  extern __shared__ double sm[];
+  const int c = blockIdx.x;
+  const int N = d.N, TP = d.TP;
+  const int T = Tslot[cs.slot[c]];
+  const int tid = threadIdx.x;
+  const Rng rng = ra.make(c);
+  const double* E = cs.E + (size_t)c * N * TP;
+  const double* sh = cs.sqrtht + (size_t)c * N * TP;
+  double* Ac = cs.A + (size_t)c * N * N;
+  double* Ainv = cs.invA + (size_t)c * N * N;
+  // offsets: block ii (1..N-1) has ii*(ii+1)/2 + ii entries
+  __shared__ int boff[kMaxNSmall + 1];
+  if (tid == 0) {
+    int o = 0;
+    boff[0] = 0;
+    boff[1] = 0;
+    for (int ii = 1; ii < N; ++ii) {
+      boff[ii] = o;
+      o += ii * (ii + 1) / 2 + ii;
+    }
+    boff[N] = o;
+  }
+  __syncthreads();
+  const int total = boff[N];
+  double* Anew = sm + total;  // N x N
+  for (int g = tid; g < total; g += blockDim.x) {
+    int ii = 1;
+    while (ii < N - 1 && g >= boff[ii + 1]) ++ii;
+    const int e = g - boff[ii];
+    const int ntri = ii * (ii + 1) / 2;
+    int a, b;
+    if (e < ntri) {  // packed lower: column b, row a >= b
+      b = 0;
+      int rem = e;
+      while (rem >= ii - b) {
+        rem -= ii - b;
+        ++b;
+      }
+      a = b + rem;
+    } else {
+      a = e - ntri;  // Zz entry: X(:,a)' y
+      b = ii;
+    }
+    const double* ea = E + (size_t)a * TP;
+    const double* eb = E + (size_t)b * TP;
+    const double* hh = sh + (size_t)ii * TP;
+    double acc = 0.0;
+    for (int t = 0; t < T; ++t) {
+      const double hv = hh[t];
+      acc = fma(ea[t] / hv, eb[t] / hv, acc);
+    }
+    sm[g] = acc;
+  }
+  for (int q = tid; q < N * N; q += blockDim.x) Anew[q] = ((q % N) == (q / N)) ? 1.0 : 0.0;
+  __syncthreads();
+  // per-ii Cholesky + solves, one thread per ii
+  if (tid >= 1 && tid < N) {
+    const int ii = tid;
+    double* Lp = sm + boff[ii];  // packed lower by columns, ii x ii
+    double* zz = Lp + ii * (ii + 1) / 2;
+    auto idx = [ii](int r, int col) { return col * ii - col * (col - 1) / 2 + (r - col); };
+    int badf = 0;
+    for (int col = 0; col < ii; ++col) {
+      double dcc = Lp[idx(col, col)];
+      for (int q = 0; q < col; ++q) dcc -= Lp[idx(col, q)] * Lp[idx(col, q)];
+      if (!(dcc > 0.0)) {
+        badf = 1;
+        dcc = 1.0;
+      }
+      const double piv = sqrt(dcc);
+      Lp[idx(col, col)] = piv;
+      for (int r = col + 1; r < ii; ++r) {
+        double s = Lp[idx(r, col)];
+        for (int q = 0; q < col; ++q) s -= Lp[idx(r, q)] * Lp[idx(col, q)];
+        Lp[idx(r, col)] = s / piv;
+      }
+    }
+    // tilde = L \ Zz  (in place in zz)
+    for (int r = 0; r < ii; ++r) {
+      double s = zz[r];
+      for (int q = 0; q < r; ++q) s -= Lp[idx(r, q)] * zz[q];
+      zz[r] = s / Lp[idx(r, r)];
+    }
+    const int zoff = ii * (ii - 1) / 2;
+    for (int r = 0; r < ii; ++r) zz[r] += rng.normal(CCMM_RNG_A, (uint32_t)(zoff + r));
+    // alpha = L' \ (tilde + z)
+    for (int r = ii - 1; r >= 0; --r) {
+      double s = zz[r];
+      for (int q = r + 1; q < ii; ++q) s -= Lp[idx(q, r)] * zz[q];
+      zz[r] = s / Lp[idx(r, r)];
+    }
+    for (int q = 0; q < ii; ++q) Anew[ii + q * N] = -zz[q];
+    if (badf) atomicOr(&cs.status[c], 4);
+  }
+  __syncthreads();
+  for (int q = tid; q < N * N; q += blockDim.x) Ac[q] = Anew[q];
+  // invA: column col of A^{-1} by forward substitution (unit lower)
+  if (tid < N) {
+    const int col = tid;
+    double x[kMaxNSmall];
+    for (int r = 0; r < N; ++r) {
+      double s = (r == col) ? 1.0 : 0.0;
+      for (int q = col; q < r; ++q) s -= Anew[r + q * N] * x[q];
+      x[r] = (r >= col) ? s : 0.0;
+    }
+    for (int r = 0; r < N; ++r) Ainv[r + col * N] = x[r];
+  }
+  // logy2 = log((RESID * A').^2 + offset)
+  double* ly = cs.logy2 + (size_t)c * N * TP;
+  for (int t = tid; t < TP; t += blockDim.x) {
+    for (int i = 0; i < N; ++i) {
+      double s = 0.0;
+      if (t < T) {
+        for (int k = 0; k <= i; ++k) s = fma(E[(size_t)k * TP + t], Anew[i + k * N], s);
+      }
+      ly[(size_t)i * TP + t] = (t < T) ? log(s * s + logy2offset) : 0.0;
+    }
+  }
+}
+
+// ============================================================== SV: KSC mixture indicators
+__constant__ double cKSCprob[7] = {0.00730, 0.10556, 0.00002, 0.04395, 0.34001, 0.24566, 0.25750};
+__constant__ double cKSCmean[7] = {-10.12999 - 1.2704, -3.97281 - 1.2704, -8.56686 - 1.2704,
+                                   2.77786 - 1.2704,   0.61942 - 1.2704,  1.79518 - 1.2704,
+                                   -1.08819 - 1.2704};
+__constant__ double cKSCvar[7] = {5.79596, 2.61369, 5.17950, 0.16735, 0.64009, 0.34023, 1.26261};
+
+__global__ void k_sv_mix(Dims d, const int* __restrict__ Tslot, ChainState cs, RngArgs ra) {
+  const int c = blockIdx.y;
+  const int T = Tslot[cs.slot[c]];
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;  // q = i*TP + t
+  if (q >= d.N * d.TP) return;
+  const int i = q / d.TP, t = q % d.TP;
+  const size_t o = (size_t)c * d.N * d.TP + q;
+  if (t >= T) {
+    cs.svobs[o] = 0.0;
+    cs.svir[o] = 0.0;
+    cs.kai[o] = 0;
+    return;
+  }
+  const Rng rng = ra.make(c);
+  const double u = rng.uniform(CCMM_RNG_SVU, (uint32_t)(i + d.N * t));
+  const double y = cs.logy2[o], hp = cs.h[o];
+  double cdf[7];
+  double acc = 0.0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const double vol = sqrt(cKSCvar[k]);
+    const double e = (y - hp - cKSCmean[k]) / vol;
+    acc += cKSCprob[k] / vol * exp(-0.5 * e * e);
+    cdf[k] = acc;
+  }
+  int s = 1;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) s += (u > cdf[k] / cdf[6]) ? 1 : 0;
+  cs.kai[o] = (int8_t)s;
+  cs.svobs[o] = y - cKSCmean[s - 1];
+  cs.svir[o] = 1.0 / cKSCvar[s - 1];
+}
+
+// ============================================================== SV: joint draw of h_0..h_T
+// Precision sampler for y_t = h_t + e_t, h_t = h_{t-1} + sqrtPHI u_t, h_0 ~ N(m0, V0).
+// Block-tridiagonal P: P_00 = V0^-1 + Q, P_tt = 2Q + R_t^-1 (t<T), P_TT = Q + R_T^-1,
+// P_{t,t-1} = -Q, Q = PHI^-1.  Forward: M_t = Ld_{t-1}^-1 Q, Ld_t = chol(P_tt - M_t'M_t),
+// w_t = Ld_t^-1 (b_t + M_t' w_{t-1}).  Backward: x_t = Ld_t^-T (w_t + z_t + Ld_t^-1 Q x_{t+1}).
+// One wave per chain; N <= 32; matrices in LDS (row-major with stride NS = N+1).
+
+// Cholesky (left-looking, in place, lower triangle of row-major S) by the
+// threads of the whole workgroup (only threads < N work; all reach the barriers).
+__device__ void wg_chol_lds(double* S, int N, int NS, int tid, int* bad) {
+  for (int col = 0; col < N; ++col) {
+    if (tid >= col && tid < N) {
+      double s = S[tid * NS + col];
+      for (int q = 0; q < col; ++q) s = fma(-S[tid * NS + q], S[col * NS + q], s);
+      S[tid * NS + col] = s;
+    }
+    __syncthreads();
+    const double dcc = S[col * NS + col];
+    double piv = sqrt(dcc);
+    if (!(dcc > 0.0)) {
+      *bad = 1;
+      piv = 1.0;
+    }
+    __syncthreads();
+    if (tid > col && tid < N) S[tid * NS + col] /= piv;
+    if (tid == col) S[col * NS + col] = piv;
+    __syncthreads();
+  }
+}
+
+// lane r holds x_r; solve L v = x in place (L row-major stride ld), one wave
+__device__ __forceinline__ double wave_fwd_solve(double x, const double* L, int ld, int N, int lane) {
+  for (int k = 0; k < N; ++k) {
+    const double xk = readlane_d(x, k) / L[k * ld + k];
+    if (lane == k) x = xk;
+    else if (lane > k && lane < N) x = fma(-L[lane * ld + k], xk, x);
+  }
+  return x;
+}
+// lane r holds x_r; solve L' v = x in place
+__device__ __forceinline__ double wave_bwd_solve(double x, const double* L, int ld, int N, int lane) {
+  for (int k = N - 1; k >= 0; --k) {
+    const double xk = readlane_d(x, k) / L[k * ld + k];
+    if (lane == k) x = xk;
+    else if (lane < k) x = fma(-L[k * ld + lane], xk, x);
+  }
+  return x;
+}
+
+__global__ __launch_bounds__(64) void k_sv_sample(Dims d, const int* __restrict__ Tslot,
+                                                  const double* __restrict__ V0inv,
+                                                  const double* __restrict__ V0invm, ChainState cs,
+                                                  RngArgs ra) {
+  extern __shared__ double sm[];
+  const int N = d.N, NS = N + 1, TP = d.TP;
+  double* Q = sm;             // N x NS
+  double* Lp = Q + N * NS;    // previous Ld
+  double* M = Lp + N * NS;    // M = Lp^-1 Q
+  double* S = M + N * NS;     // Schur complement -> new Ld
+  double* xs = S + N * NS;    // N (x_{t+1} in the backward pass)
+  const int c = blockIdx.x;
+  const int s = cs.slot[c];
+  const int T = Tslot[s];
+  const int lane = threadIdx.x;
+  const Rng rng = ra.make(c);
+  int bad = 0;
+  const double* sq = cs.sqrtPHI + (size_t)c * N * N;  // column-major lower
+  const double* obs = cs.svobs + (size_t)c * N * TP;
+  const double* ir = cs.svir + (size_t)c * N * TP;
+  double* Ld = cs.svLd + (size_t)c * (TP + 1) * N * N;  // [t][r*N+col] row-major lower
+  double* W = cs.svw + (size_t)c * (TP + 1) * N;
+  // Li = sqrtPHI^-1 (lower) in M, column `lane`
+  if (lane < N) {
+    const int col = lane;
+    for (int r = 0; r < N; ++r) {
+      double v = (r == col) ? 1.0 : 0.0;
+      for (int q = col; q < r; ++q) v = fma(-sq[r + q * N], M[q * NS + col], v);
+      M[r * NS + col] = (r >= col) ? v / sq[r + r * N] : 0.0;
+    }
+  }
+  __syncthreads();
+  // Q = Li' Li = (sqrtPHI sqrtPHI')^-1
+  for (int e = lane; e < N * N; e += 64) {
+    const int r = e / N, col = e % N;
+    double v = 0.0;
+    for (int q = 0; q < N; ++q) v = fma(M[q * NS + r], M[q * NS + col], v);
+    Q[r * NS + col] = v;
+  }
+  __syncthreads();
+  // t = 0: P_00 = V0^-1 + Q, b_0 = V0^-1 m0
+  const double* Vi = V0inv + (size_t)s * N * N;
+  for (int e = lane; e < N * N; e += 64) {
+    const int r = e / N, col = e % N;
+    S[r * NS + col] = Vi[r + col * N] + Q[r * NS + col];
+  }
+  __syncthreads();
+  wg_chol_lds(S, N, NS, lane, &bad);
+  double wl = (lane < N) ? V0invm[(size_t)s * N + lane] : 0.0;  // lane r: w(r)
+  wl = wave_fwd_solve(wl, S, NS, N, lane);
+  for (int e = lane; e < N * N; e += 64) {
+    const int r = e / N, col = e % N;
+    const double v = (col <= r) ? S[r * NS + col] : 0.0;
+    Ld[e] = v;
+    Lp[r * NS + col] = v;
+  }
+  if (lane < N) W[lane] = wl;
+  __syncthreads();
+  for (int t = 1; t <= T; ++t) {
+    // M = Lp^-1 Q  (column `lane`)
+    if (lane < N) {
+      const int col = lane;
+      for (int r = 0; r < N; ++r) {
+        double v = Q[r * NS + col];
+        for (int q = 0; q < r; ++q) v = fma(-Lp[r * NS + q], M[q * NS + col], v);
+        M[r * NS + col] = v / Lp[r * NS + r];
+      }
+    }
+    // w_{t-1} to LDS for M' w
+    if (lane < N) xs[lane] = wl;
+    __syncthreads();
+    // S = P_tt - M'M (lower);  b = obs_t ir_t + M' w_{t-1}
+    const double qf = (t == T) ? 1.0 : 2.0;
+    for (int e = lane; e < N * N; e += 64) {
+      const int r = e / N, col = e % N;
+      if (col <= r) {
+        double v = qf * Q[r * NS + col];
+        if (r == col) v += ir[(size_t)r * TP + t - 1];
+        for (int q = 0; q < N; ++q) v = fma(-M[q * NS + r], M[q * NS + col], v);
+        S[r * NS + col] = v;
+      }
+    }
+    double b = 0.0;
+    if (lane < N) {
+      b = obs[(size_t)lane * TP + t - 1] * ir[(size_t)lane * TP + t - 1];
+      for (int q = 0; q < N; ++q) b = fma(M[q * NS + lane], xs[q], b);
+    }
+    __syncthreads();
+    wg_chol_lds(S, N, NS, lane, &bad);
+    wl = wave_fwd_solve(b, S, NS, N, lane);
+    double* Ldt = Ld + (size_t)t * N * N;
+    for (int e = lane; e < N * N; e += 64) {
+      const int r = e / N, col = e % N;
+      const double v = (col <= r) ? S[r * NS + col] : 0.0;
+      Ldt[e] = v;
+      Lp[r * NS + col] = v;
+    }
+    if (lane < N) W[(size_t)t * N + lane] = wl;
+    __syncthreads();
+  }
+  // backward pass
+  double* hout = cs.h + (size_t)c * N * TP;
+  double* eta = cs.eta + (size_t)c * N * TP;
+  double* sqh = cs.sqrtht + (size_t)c * N * TP;
+  __threadfence_block();
+  for (int t = T; t >= 0; --t) {
+    const double* Ldt = Ld + (size_t)t * N * N;
+    double rr = 0.0;
+    if (lane < N) rr = W[(size_t)t * N + lane] + rng.normal(CCMM_RNG_SVZ, (uint32_t)(lane + N * t));
+    if (t < T) {
+      double g = 0.0;
+      if (lane < N)
+        for (int q = 0; q < N; ++q) g = fma(Q[lane * NS + q], xs[q], g);
+      g = wave_fwd_solve(g, Ldt, N, N, lane);
+      rr += g;
+    }
+    rr = wave_bwd_solve(rr, Ldt, N, N, lane);
+    if (lane < N) {
+      if (t < T) eta[(size_t)lane * TP + t] = xs[lane] - rr;  // shock of t+1: x_{t+1} - x_t
+      if (t >= 1) {
+        hout[(size_t)lane * TP + t - 1] = rr;
+        sqh[(size_t)lane * TP + t - 1] = exp(rr * 0.5);
+      }
+    }
+    __syncthreads();
+    if (lane < N) xs[lane] = rr;
+    __syncthreads();
+  }
+  for (int q = lane; q < N * (TP - T); q += 64) {
+    const int r = q / (TP - T), t = T + q % (TP - T);
+    hout[(size_t)r * TP + t] = 0.0;
+    eta[(size_t)r * TP + t] = 0.0;
+    sqh[(size_t)r * TP + t] = 1.0;
+  }
+  if (bad && lane == 0) atomicOr(&cs.status[c], 8);
+}
+
+// ============================================================== PHI inverse-Wishart
+// mcmcVAR.m:268-274: Zdraw = randn(N, T+d_PHI); sqrtPHIpost = chol(s_PHI + eta'eta,'lower');
+// sqrtZZ = chol(Zdraw*Zdraw'); sqrtPHI_ = sqrtPHIpost / sqrtZZ; PHI_ = sqrtPHI_*sqrtPHI_';
+// sqrtPHI_ = chol(PHI_,'lower').
+__global__ void k_phi_gen(Dims d, const int* __restrict__ Tslot, int dPHI, ChainState cs,
+                          RngArgs ra) {
+  const int c = blockIdx.y;
+  const int TZ = Tslot[cs.slot[c]] + dPHI;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;  // q = i + N*col (N x TZ column-major)
+  if (q >= d.N * TZ) return;
+  const Rng rng = ra.make(c);
+  cs.Zphi[(size_t)c * d.N * (d.TP + dPHI) + q] = rng.normal(CCMM_RNG_PHI, (uint32_t)q);
+}
+
+__global__ __launch_bounds__(256) void k_phi(Dims d, const int* __restrict__ Tslot, int dPHI,
+                                             const double* __restrict__ sPHIall, ChainState cs) {
+  extern __shared__ double sm[];
+  const int N = d.N, NS = N + 1, TP = d.TP;
+  const int c = blockIdx.x;
+  const int s = cs.slot[c];
+  const int T = Tslot[s];
+  const int TZ = T + dPHI;
+  const int TZmax = TP + dPHI;
+  const int tid = threadIdx.x;
+  double* Lpost = sm;           // N x NS
+  double* Rz = Lpost + N * NS;  // N x NS (lower chol of ZZ', i.e. R')
+  double* Sq = Rz + N * NS;     // N x NS
+  double* Ph = Sq + N * NS;     // N x NS
+  const double* eta = cs.eta + (size_t)c * N * TP;
+  const double* Z = cs.Zphi + (size_t)c * N * TZmax;
+  const double* sP = sPHIall + (size_t)s * N * N;
+  for (int e = tid; e < N * N; e += blockDim.x) {
+    const int r = e / N, col = e % N;
+    if (col > r) continue;
+    double a = 0.0;
+    const double* er = eta + (size_t)r * TP;
+    const double* ec = eta + (size_t)col * TP;
+    for (int t = 0; t < T; ++t) a = fma(er[t], ec[t], a);
+    Lpost[r * NS + col] = sP[r + col * N] + a;
+    double b = 0.0;
+    for (int q = 0; q < TZ; ++q) b = fma(Z[r + (size_t)N * q], Z[col + (size_t)N * q], b);
+    Rz[r * NS + col] = b;
+  }
+  __syncthreads();
+  int bad = 0;
+  wg_chol_lds(Lpost, N, NS, tid, &bad);
+  wg_chol_lds(Rz, N, NS, tid, &bad);
+  // Sq R = Lpost with R = Rz' upper: row `tid` of Sq
+  if (tid < N) {
+    const int r = tid;
+    for (int col = 0; col < N; ++col) {
+      double v = (col <= r) ? Lpost[r * NS + col] : 0.0;
+      for (int q = 0; q < col; ++q) v = fma(-Sq[r * NS + q], Rz[col * NS + q], v);
+      Sq[r * NS + col] = v / Rz[col * NS + col];
+    }
+  }
+  __syncthreads();
+  // PHI = Sq Sq'
+  for (int e = tid; e < N * N; e += blockDim.x) {
+    const int r = e / N, col = e % N;
+    double v = 0.0;
+    for (int q = 0; q < N; ++q) v = fma(Sq[r * NS + q], Sq[col * NS + q], v);
+    Ph[r * NS + col] = v;
+  }
+  __syncthreads();
+  double* PHI = cs.PHI + (size_t)c * N * N;
+  for (int e = tid; e < N * N; e += blockDim.x) {
+    const int r = e % N, col = e / N;
+    PHI[e] = Ph[r * NS + col];
+  }
+  __syncthreads();
+  wg_chol_lds(Ph, N, NS, tid, &bad);
+  double* sqo = cs.sqrtPHI + (size_t)c * N * N;
+  for (int e = tid; e < N * N; e += blockDim.x) {
+    const int r = e % N, col = e / N;
+    sqo[e] = (col <= r) ? Ph[r * NS + col] : 0.0;
+  }
+  if (bad && tid == 0) atomicOr(&cs.status[c], 16);
+}
+
+// ============================================================== draw storage
+struct Store {
+  double* PAI;     // [B][cap][N][K]
+  double* PHI;     // [B][cap][N(N+1)/2]
+  double* invA;    // [B][cap][N][N]
+  double* sqrtht;  // [B][cap][N][T]
+  int cap, m, Tmax;
+};
+
+__global__ void k_store(Dims d, ChainState cs, Store st) {
+  const int c = blockIdx.y;
+  const int N = d.N, K = d.K, TP = d.TP;
+  const int nPAI = K * N, nPHI = N * (N + 1) / 2, nA = N * N, nS = st.Tmax * N;
+  const int tot = nPAI + nPHI + nA + nS;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < tot; q += gridDim.x * blockDim.x) {
+    if (q < nPAI) {
+      const int a = q % K, j = q / K;
+      st.PAI[((size_t)c * st.cap + st.m) * nPAI + q] = cs.PAI[((size_t)c * N + j) * d.KP + a];
+    } else if (q < nPAI + nPHI) {
+      int e = q - nPAI, col = 0;
+      while (e >= N - col) {
+        e -= N - col;
+        ++col;
+      }
+      const int r = col + e;
+      st.PHI[((size_t)c * st.cap + st.m) * nPHI + (q - nPAI)] = cs.PHI[(size_t)c * N * N + r + col * N];
+    } else if (q < nPAI + nPHI + nA) {
+      const int e = q - nPAI - nPHI;
+      st.invA[((size_t)c * st.cap + st.m) * nA + e] = cs.invA[(size_t)c * N * N + e];
+    } else {
+      const int e = q - nPAI - nPHI - nA;
+      const int t = e % st.Tmax, i = e / st.Tmax;
+      st.sqrtht[((size_t)c * st.cap + st.m) * nS + e] = cs.sqrtht[((size_t)c * N + i) * TP + t];
+    }
+  }
+}
+
+// ============================================================== truncated normal
+// drawTruncNormal.m:53-86: inverse CDF, upper truncation at elb.
+__device__ __forceinline__ double trunc_normal_dev(double mu, double sig, double elb, double u,
+                                                   uint8_t* fl) {
+  const double tol = 1e-10;
+  const double eps = 2.220446049250313080847e-16;
+  sig = fabs(sig);
+  if (sig > tol) {
+    const double ub = (elb - mu) / sig;
+    const double PHIbar = 0.5 * erfc(-sqrt(0.5) * ub);
+    double z;
+    if (PHIbar > eps) {
+      z = -sqrt(2.0) * erfcinv(2.0 * u * PHIbar);
+      *fl = 3;
+    } else {
+      z = ub;
+      *fl = 1;
+    }
+    return mu + sig * z;
+  }
+  *fl = 0;
+  return mu;
+}
+
+__global__ void k_truncnorm(int n, const double* mu, const double* sig, double elb, const double* u,
+                            double* out, uint8_t* flags) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  uint8_t f;
+  out[q] = trunc_normal_dev(mu[q], sig[q], elb, u[q], &f);
+  if (flags) flags[q] = f;
+}
+
+// ============================================================== diagnostics
+// MFMA f64 layout self-test: D = A(16x4) * B(4x16) with the lane maps used above.
+__global__ void k_mfma_selftest(const double* A, const double* B, double* D) {
+  const int l = threadIdx.x;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(l & 15) + 16 * (l >> 4)], B[(l >> 4) + 4 * (l & 15)],
+                                              acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) D[((l >> 4) + 4 * r) + 16 * (l & 15)] = acc[r];  // column-major 16x16
+}
+
+}  // namespace ccmm

@@ -1,0 +1,103 @@
+"""Reference-interface mirror of the MATLAB samplers, running on libccmm.
+
+``mcmcVAR`` keeps the signature and draw-array outputs of mcmcVAR.m:1-12
+(``nargout == 4`` form: PAI_all, PHI_all, invA_all, sqrtht_all) and adds
+``nchains``: B independent chains run as one device batch (the
+``goVAR*`` parfor over vintages/chains becomes one GPU launch sequence).
+``CTA``/``CTAsys``/``drawTruncNormal`` mirror the L2 functions.
+
+Every numerical step goes through ``libccmm.so``; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _abi
+from .model import build_var, initial_state
+
+_CTX = {}
+
+
+def context(device: int = 0) -> _abi.Context:
+    if device not in _CTX:
+        _CTX[device] = _abi.Context(device)
+    return _CTX[device]
+
+
+def mcmcVAR(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMean, doRATSprior,
+            ndxYIELDS=None, ELBbound=0.25, check_stationarity=0, yrealized=None, fcstNdraws=None,
+            fcstNhorizons=None, rndStream=1012023, doprogress=False, *, nchains=1, device=0,
+            burnin=None):
+    """mcmcVAR.m (linear BVAR-SV, CTA + A + SV + PHI blocks), nargout == 4.
+
+    rndStream: integer seed of the Philox stream (the MATLAB RandStream object
+    has no device equivalent; chains c = 0..nchains-1 use counter word `chain`).
+    Returns PAI_all (M x K x N), PHI_all (M x N(N+1)/2), invA_all (M x N x N),
+    sqrtht_all (M x T x N), each with a trailing chain axis when nchains > 1.
+    """
+    if check_stationarity:
+        raise NotImplementedError("check_stationarity=1 (mcmcVAR.m:221-232) is not supported; "
+                                  "the reference drivers all pass 0")
+    if fcstNdraws:
+        if fcstNdraws % MCMCdraws != 0:  # mcmcVAR.m:97-99
+            raise ValueError("fcstNdraws must be multiple of MCMCdraws")
+        raise NotImplementedError("predictive density (nargout > 4) is a later row (SURVEY §8f)")
+    m = build_var(thisT, p, np_, data0, ydates0, minnesotaPriorMean, doRATSprior)
+    B = int(nchains)
+    burn = MCMCdraws if burnin is None else int(burnin)  # MCMCburnin = MCMCdraws (mcmcVAR.m:54)
+    ctx = context(device)
+    ch = _abi.Chains(ctx, N=m.N, p=m.p, T=m.T, B=B, ndata=1, crn=False,
+                     store_capacity=MCMCdraws, seed=int(rndStream))
+    ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    st = initial_state(m, B)
+    ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+    step = 50
+    done = 0
+    while done < burn:
+        n = min(step, burn - done)
+        ch.sweep(n, store=False)
+        done += n
+        if doprogress:
+            print(f"burn-in {done}/{burn}")
+    done = 0
+    while done < MCMCdraws:
+        n = min(step, MCMCdraws - done)
+        ch.sweep(n, store=True)
+        done += n
+        if doprogress:
+            print(f"draws {done}/{MCMCdraws}")
+    out = ch.get_draws()
+    ch.close()
+    res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"]]
+    if B == 1:
+        res = [a[..., 0] for a in res]
+    return tuple(res)
+
+
+def CTA(Y, X, N, K, T, A_, sqrtht, iV, iVb_prior, PAI, rndStream=None, *, device=0):
+    """CTA.m:1 signature.  iV may be the NK x NK diagonal precision or its diagonal;
+    rndStream may be None (Philox) or a K x N array of standard normals (CRN)."""
+    iVd = np.diag(iV) if np.ndim(iV) == 2 else np.asarray(iV)
+    out, _ = context(device).cta(Y, X, np.asarray(A_)[..., None], np.asarray(sqrtht)[..., None],
+                                 iVd.reshape(K, N, order="F"),
+                                 np.asarray(iVb_prior).reshape(K, N, order="F"),
+                                 np.asarray(PAI)[..., None],
+                                 None if rndStream is None else np.asarray(rndStream)[..., None])
+    return out[..., 0]
+
+
+def CTAsys(Y, X, N, K, T, A_, sqrtht, iV, iVb_prior, PAI, rndStream=None, *, device=0):
+    """CTAsys.m:1 signature: X is T x K x N (one design per equation)."""
+    iVd = np.diag(iV) if np.ndim(iV) == 2 else np.asarray(iV)
+    out, _ = context(device).cta(Y, X, np.asarray(A_)[..., None], np.asarray(sqrtht)[..., None],
+                                 iVd.reshape(K, N, order="F"),
+                                 np.asarray(iVb_prior).reshape(K, N, order="F"),
+                                 np.asarray(PAI)[..., None],
+                                 None if rndStream is None else np.asarray(rndStream)[..., None])
+    return out[..., 0]
+
+
+def drawTruncNormal(mu, sqrtVCV, elb, u):
+    """drawTruncNormal.m:1 with the numeric-uniform form of the stream argument."""
+    v, _ = _abi.draw_trunc_normal(mu, sqrtVCV, elb, u)
+    return v

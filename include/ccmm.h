@@ -1,0 +1,194 @@
+/*
+ * ccmm.h — C ABI of libccmm, the MI355X-native Gibbs sweep of the CCMM
+ * shadow-rate BVAR-SV (Carriero, Clark, Marcellino & Mertens).
+ *
+ * Drop-in boundary.  Each entry point replaces one MATLAB function (or loop)
+ * of the reference (Allisterh/CCMMshadowrateVAR-code @ 2025-01-27); the
+ * reference file:line it replaces is cited beside it.  The MATLAB signatures
+ * stay unchanged: a MEX gateway marshals mxArrays into these
+ * calls.  Plain C types only: pointers to column-major fp64 host arrays
+ * (MATLAB layout), int sizes, and opaque handles.
+ *
+ * Conventions
+ *  - Every matrix argument is column-major, exactly the MATLAB array shape
+ *    quoted in the comment ("T x N" means T rows, N columns).  Batched
+ *    arguments append the chain index as the slowest dimension ("x B").
+ *  - Return codes: 0 = OK; > 0 = warning (mirrors MATLAB warning(): e.g.
+ *    CCMM_WARN_QR_FALLBACK, CTA.m:82); < 0 = error (mirrors error(): e.g.
+ *    CCMM_ERR_DIM, gibbsdrawShadowrates.m:51).  ccmm_last_error() returns a
+ *    thread-local message for the last non-zero return on this thread.
+ *  - Host buffers belong to the caller and are never freed by the library.
+ *    Device buffers, RNG state and scratch belong to the context / chain set.
+ *  - Reentrancy: one context is bound to one device and serialises its calls
+ *    on its own HIP stream; distinct contexts may be driven from distinct
+ *    threads or processes (one per GPU).
+ *  - Random numbers: every drawing entry point takes either a CRN array (the
+ *    host-injected common random numbers, in the reference's draw order and
+ *    shape) or NULL, in which case the library draws from its counter-based
+ *    Philox4x32-10 generator keyed by (seed, chain, sweep, block).
+ */
+#ifndef CCMM_H
+#define CCMM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCMM_ABI_VERSION 1
+
+/* return codes */
+#define CCMM_OK 0
+#define CCMM_WARN_QR_FALLBACK 1    /* CTA.m:80-92 "switching to QR routine" */
+#define CCMM_WARN_ELBT0 2          /* mcmcVARshadowrateBlockHybrid.m:203-205 */
+#define CCMM_ERR_DIM (-1)          /* gibbsdrawShadowrates.m:50-52 "dimension mismatch" */
+#define CCMM_ERR_ARG (-2)          /* invalid argument / unsupported size */
+#define CCMM_ERR_HIP (-3)          /* HIP runtime failure */
+#define CCMM_ERR_NOTSPD (-4)       /* Cholesky failure in a block without fallback */
+#define CCMM_ERR_STATE (-5)        /* call order violated (e.g. sweep before set_data) */
+
+/* model ids for the sweep-level API */
+#define CCMM_MODEL_LINEAR 0        /* mcmcVAR.m */
+#define CCMM_MODEL_BLOCKHYBRID 1   /* mcmcVARshadowrateBlockHybrid.m */
+
+/* RNG block ids (Philox counter word 3); also the order of the per-sweep CRN blocks */
+#define CCMM_RNG_PAI 1   /* randn(K,N)            CTA.m:58 / CTAsys.m:58 */
+#define CCMM_RNG_A 2     /* 19x randn(ii-1,1)     mcmcVAR.m:251 */
+#define CCMM_RNG_SVU 3   /* rand(N,T)             SV mixture indicators */
+#define CCMM_RNG_SVZ 4   /* randn(N,T+1)          SV joint draw h_0..h_T */
+#define CCMM_RNG_PHI 5   /* randn(N,T+d_PHI)      mcmcVAR.m:268 */
+#define CCMM_RNG_ELB 6   /* rand(Ns,elbT,101)     gibbsdrawShadowrates.m:173 */
+
+typedef struct ccmm_ctx ccmm_ctx;
+typedef struct ccmm_chains ccmm_chains;
+
+/* ---------------------------------------------------------------- context */
+int ccmm_abi_version(void);
+const char* ccmm_last_error(void);
+int ccmm_device_count(void);
+/* Create a context bound to HIP device `device`.  Returns NULL on failure. */
+ccmm_ctx* ccmm_create(int device);
+void ccmm_destroy(ccmm_ctx* ctx);
+int ccmm_synchronize(ccmm_ctx* ctx);
+
+/* --------------------------------------------------- block-level drop-ins */
+
+/* Triangular (CTA) draw of the VAR coefficients, batched over B chains.
+ * Replaces CTA.m:1-98 (called at mcmcVAR.m:228, mcmcVARhybridGibbs.m:376) and
+ * CTAsys.m:1-108 (called at mcmcVARshadowrateBlockHybrid.m:343).
+ *   Y      T x N (x B if y_per_chain)
+ *   X      T x K x nx (x B if x_per_chain); equation j uses slab (nx==1 ? 0 : j)
+ *          nx == 1 is CTA, nx == N is CTAsys
+ *   A      N x N x B   unit lower triangular A_
+ *   sqrtht T x N x B
+ *   iVdiag K x N       diagonal of the block-diagonal prior precision iV (mcmcVAR.m:186)
+ *   iVb    K x N       iVb_prior reshaped to K x N
+ *   PAI    K x N x B   in: previous draw (columns j+1..N used by CTAsys); out: new draw
+ *   z      K x N x B   randn(K,N) of CTA.m:58, or NULL (Philox, block CCMM_RNG_PAI, sweep 0)
+ *   status B           per-chain status (0 ok, 1 QR fallback used), may be NULL
+ * Supports 1 <= N <= 64, K <= 1536. */
+int ccmm_cta(ccmm_ctx* ctx, int B, int T, int N, int K,
+             const double* Y, int y_per_chain,
+             const double* X, int nx, int x_per_chain,
+             const double* A, const double* sqrtht,
+             const double* iVdiag, const double* iVb,
+             double* PAI, const double* z, int* status);
+
+/* A-matrix draw, flat prior (mcmcVAR.m:236-254 == mcmcVARshadowrateBlockHybrid.m:354-372).
+ *   RESID T x N x B, sqrtht T x N x B, z (N(N-1)/2) x B or NULL
+ *   A out N x N x B (unit lower), invA out N x N x B (A_\I, mcmcVAR.m:254) */
+int ccmm_astep(ccmm_ctx* ctx, int B, int T, int N, const double* RESID, const double* sqrtht,
+               const double* z, double* A, double* invA);
+
+/* Stochastic-volatility block: KSC 7-component mixture indicators and joint
+ * draw of the random-walk log variances with correlated shocks.  Replaces the
+ * em-matlabbox call StochVolKSCcorrsqrt (mcmcVAR.m:261,
+ * mcmcVARshadowrateBlockHybrid.m:379, mcmcVARhybridGibbs.m:405).
+ *   logy2T N x T x B (logy2'), hprevT N x T x B (Vol_states'), sqrtPHI N x N x B lower,
+ *   h0mean N, h0vcvsqrt N x N, u N x T x B or NULL, z N x (T+1) x B or NULL
+ *   hT out N x T x B, h0 out N x B, shocksT out N x T x B, kai2 out N x T x B (int8, 1..7) */
+int ccmm_sv_ksc(ccmm_ctx* ctx, int B, int T, int N, const double* logy2T, const double* hprevT,
+                const double* sqrtPHI, const double* h0mean, const double* h0vcvsqrt,
+                const double* u, const double* z, double* hT, double* h0, double* shocksT,
+                int8_t* kai2);
+
+/* Inverse-Wishart draw of the SV shock covariance (mcmcVAR.m:268-274).
+ *   eta T x N x B, sPHI N x N, dPHI, Zdraw N x (T+dPHI) x B or NULL
+ *   sqrtPHI out N x N x B (lower Cholesky of PHI_), PHI out N x N x B */
+int ccmm_phi_iw(ccmm_ctx* ctx, int B, int T, int N, const double* eta, const double* sPHI,
+                int dPHI, const double* Zdraw, double* sqrtPHI, double* PHI);
+
+/* One draw from N(mu, sig^2) truncated to (-inf, elb] by inverse CDF
+ * (drawTruncNormal.m:31-86) with a pre-drawn uniform u (the numeric-stream
+ * form of drawTruncNormal.m:47-48).  flags (may be NULL): bit0 = |sig| > 1e-10
+ * branch taken, bit1 = PHIbar > eps branch taken.  Host-side scalar; the
+ * device form is used inside ccmm_gibbs_shadowrates. */
+double ccmm_draw_trunc_normal(double mu, double sig, double elb, double u, uint8_t* flags);
+
+/* Batched device evaluation of drawTruncNormal over n independent cells. */
+int ccmm_draw_trunc_normal_batch(ccmm_ctx* ctx, int n, const double* mu, const double* sig,
+                                 double elb, const double* u, double* out, uint8_t* flags);
+
+/* --------------------------------------------------- sweep-level (device-resident) */
+
+typedef struct {
+  int model;              /* CCMM_MODEL_* */
+  int N, p, K;            /* K = N*p + 1 */
+  int T;                  /* max T over data slots */
+  int B;                  /* number of chains */
+  int ndata;              /* number of data slots (vintages) */
+  int dPHI;               /* N + 3 (mcmcVAR.m:164) */
+  int rng_crn;            /* 1: sweeps read CRN arrays from the host; 0: Philox */
+  int store_capacity;     /* kept draws stored per chain (0: no storage) */
+  double logy2offset;     /* getKSC7values offset (ext; this build declares 1e-3) */
+  uint64_t seed;          /* Philox key */
+} ccmm_chain_config;
+
+ccmm_chains* ccmm_chains_create(ccmm_ctx* ctx, const ccmm_chain_config* cfg);
+void ccmm_chains_destroy(ccmm_chains* ch);
+
+/* Data slot `slot`: one vintage's design (mcmcVAR.m:62-72, 186; 164-169).
+ *   Y T x N, X T x K, iVdiag K x N, iVb K x N, sPHI N x N, h0mean N, h0vcvsqrt N x N */
+int ccmm_chains_set_data(ccmm_chains* ch, int slot, int T, const double* Y, const double* X,
+                         const double* iVdiag, const double* iVb, const double* sPHI,
+                         const double* h0mean, const double* h0vcvsqrt);
+/* slot_of_chain B ints (default: all chains use slot 0). */
+int ccmm_chains_set_slots(ccmm_chains* ch, const int* slot_of_chain);
+/* Chain state PREVdraw (mcmcVAR.m:197-206, 386-392): PAI K x N x B, A N x N x B,
+ * sqrtht T x N x B, h (Vol_states) T x N x B, sqrtPHI N x N x B.  Resets the sweep counter. */
+int ccmm_chains_set_state(ccmm_chains* ch, const double* PAI, const double* A,
+                          const double* sqrtht, const double* h, const double* sqrtPHI);
+/* Any output pointer may be NULL.  invA, PHI, RESID are those of the last sweep. */
+int ccmm_chains_get_state(ccmm_chains* ch, double* PAI, double* A, double* invA, double* sqrtht,
+                          double* h, double* sqrtPHI, double* PHI, double* RESID);
+/* CRN doubles consumed per chain per sweep (blocks in CCMM_RNG_* order). */
+int64_t ccmm_chains_crn_len(const ccmm_chains* ch);
+/* Run nsweeps Gibbs sweeps (the body of `while m < MCMCreps`, mcmcVAR.m:195-398,
+ * excluding the predictive block).  crn: B x nsweeps x crn_len (chain slowest) or
+ * NULL in Philox mode.  store != 0 stores each sweep's draw (post-burn-in
+ * semantics of mcmcVAR.m:278-292) into the on-device draw buffer.  Asynchronous
+ * with respect to the host unless crn != NULL. */
+int ccmm_chains_sweep(ccmm_chains* ch, int nsweeps, const double* crn, int store);
+/* Number of stored draws per chain so far. */
+int ccmm_chains_stored(const ccmm_chains* ch);
+/* Copy stored draws out in the reference layout (mcmcVAR.m:178-181, 289-292):
+ *   PAI_all M x K x N x B, PHI_all M x N(N+1)/2 x B, invA_all M x N x N x B,
+ *   sqrtht_all M x T x N x B.  Any pointer may be NULL.  Resets the store. */
+int ccmm_chains_get_draws(ccmm_chains* ch, double* PAI_all, double* PHI_all, double* invA_all,
+                          double* sqrtht_all);
+/* Per-kernel device time (HIP events on the chain set's stream) accumulated
+ * while profiling is on.  names: ';'-separated list written into buf. */
+int ccmm_chains_profile(ccmm_chains* ch, int enable);
+int ccmm_chains_kernel_times(ccmm_chains* ch, int max, double* ms, int64_t* launches,
+                             char* names, int names_len);
+
+/* ------------------------------------------------------------ diagnostics */
+/* D16x16 = A16x4 * B4x16 computed by one v_mfma_f64_16x16x4_f64 with the operand
+ * and accumulator lane maps the CTA SYRK kernel relies on (all column-major). */
+int ccmm_selftest_mfma_f64(ccmm_ctx* ctx, const double* A16x4, const double* B4x16, double* D16x16);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CCMM_H */

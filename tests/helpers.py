@@ -1,0 +1,44 @@
+"""Shared test inputs: synthetic VAR data (toy sizes) and chain states."""
+import numpy as np
+
+
+def synth_var_data(N=4, p=2, Tobs=62, seed=0):
+    """A stable VAR(p) sample with stochastic volatility (Nobs x N)."""
+    rng = np.random.default_rng(seed)
+    Pi = [0.5 * np.eye(N) + rng.uniform(-0.05, 0.05, (N, N))]
+    Pi += [(0.2 / l ** 2) * np.eye(N) for l in range(2, p + 1)]
+    y = np.zeros((Tobs, N))
+    y[:p] = rng.standard_normal((p, N))
+    lh = np.zeros(N)
+    for t in range(p, Tobs):
+        lh = lh + 0.1 * rng.standard_normal(N)
+        y[t] = 0.3 + sum(Pi[l] @ y[t - 1 - l] for l in range(p)) + np.exp(lh / 2) * rng.standard_normal(N)
+    return y
+
+
+def toy_setup(oracle, N=4, p=2, Tobs=62, seed=0):
+    data = synth_var_data(N, p, Tobs, seed)
+    ydates = np.arange(Tobs, dtype=float)
+    mpm = np.ones(N)
+    return oracle.var_setup(Tobs, p, 12, data, ydates, mpm, True)
+
+
+def random_state(oracle, su, seed=1):
+    """A chain state away from the reference initialisation: smooth volatility,
+    non-trivial A (well conditioned posterior precision)."""
+    rng = np.random.default_rng(seed)
+    N, T = su.N, su.T
+    st = oracle.init_state(su)
+    A = np.eye(N) + np.tril(rng.uniform(-0.3, 0.3, (N, N)), -1)
+    h = np.cumsum(0.05 * rng.standard_normal((T, N)), axis=0) + np.log(np.var(su.Y, axis=0))
+    st["A"] = A
+    st["h"] = h
+    st["sqrtht"] = np.exp(h / 2)
+    L = np.tril(rng.uniform(-0.02, 0.02, (N, N)), -1) + np.diag(rng.uniform(0.05, 0.15, N))
+    st["sqrtPHI"] = L
+    return st
+
+
+def crn_flat(oracle, crn, su):
+    return np.concatenate([crn[k].ravel(order="F") for k, _ in oracle.crn_sizes(su.N, su.K, su.T,
+                                                                                 su.dPHI)])
