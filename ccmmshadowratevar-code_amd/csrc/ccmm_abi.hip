@@ -10,6 +10,9 @@
 #include <vector>
 
 #include "ccmm_kernels.hip"
+#include "ccmm_sv.hip"
+#include "ccmm_cta_solve.hip"
+#include <cstdlib>
 
 using namespace ccmm;
 
@@ -153,6 +156,9 @@ struct ccmm_chains {
   uint32_t sweep = 0;
   bool resid_valid = false;
   bool have_state = false;
+  // kernel variants (A/B): CCMM_OLD_SOLVE=1 selects the first-generation solve kernel
+  bool use_solve2 = std::getenv("CCMM_OLD_SOLVE") == nullptr;
+  bool use_svfast = std::getenv("CCMM_OLD_SV") == nullptr;
   std::vector<bool> have_slot;
   // profiling
   bool profiling = false;
@@ -456,7 +462,21 @@ struct ccmm_chains {
                          iVdiag.p, cs, rdiag.p);
     });
     const size_t lds_solve = (size_t)(d.TP + d.KP) * sizeof(double);
+    const size_t lds_solve2 =
+        (size_t)(d.TP + 2 * d.KP + 64 * kSolveLd + d.N * d.N) * sizeof(double);
     launch(KID_SOLVE, [&] {
+      if (use_solve2) {
+        if (d.N <= 8)
+          hipLaunchKernelGGL(k_cta_solve2<8>, dim3(d.B), dim3(256), lds_solve2, ctx->stream, d,
+                             Tslot.p, iVb.p, xsel(), cs, rdiag.p, ra);
+        else if (d.N <= 20)
+          hipLaunchKernelGGL(k_cta_solve2<20>, dim3(d.B), dim3(256), lds_solve2, ctx->stream, d,
+                             Tslot.p, iVb.p, xsel(), cs, rdiag.p, ra);
+        else
+          hipLaunchKernelGGL(k_cta_solve2<32>, dim3(d.B), dim3(256), lds_solve2, ctx->stream, d,
+                             Tslot.p, iVb.p, xsel(), cs, rdiag.p, ra);
+        return;
+      }
       const int rpl = d.KP / 64;
       switch (rpl) {
 #define CASE_RPL(R)                                                                              \
@@ -504,8 +524,22 @@ struct ccmm_chains {
     });
     const size_t lds = (size_t)(4 * d.N * (d.N + 1) + d.N) * sizeof(double);
     launch(KID_SVSAMPLE, [&] {
-      hipLaunchKernelGGL(k_sv_sample, dim3(d.B), dim3(64), lds, ctx->stream, d, Tslot.p, V0inv.p,
-                         V0invm.p, cs, ra);
+      switch (use_svfast ? d.N : -1) {
+#define CASE_SVN(NN)                                                                          \
+  case NN:                                                                                    \
+    hipLaunchKernelGGL(k_sv_fast<NN>, dim3(d.B), dim3(64), 0, ctx->stream, d, Tslot.p, V0inv.p, \
+                       V0invm.p, cs, ra);                                                     \
+    break;
+        CASE_SVN(4)
+        CASE_SVN(5)
+        CASE_SVN(6)
+        CASE_SVN(20)
+        CASE_SVN(21)
+#undef CASE_SVN
+        default:
+          hipLaunchKernelGGL(k_sv_sample, dim3(d.B), dim3(64), lds, ctx->stream, d, Tslot.p,
+                             V0inv.p, V0invm.p, cs, ra);
+      }
     });
   }
 
