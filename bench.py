@@ -131,13 +131,19 @@ def main():
         # dominant kernel = largest accumulated device time
         dom = max(ktimes, key=lambda k: ktimes[k][0])
         per = {k: round(v[0] / max(v[1], 1), 4) for k, v in ktimes.items() if v[1]}
-        syrk_ms = ktimes["k_syrk"][0] / max(ktimes["k_syrk"][1], 1)
-        f_syrk = B * N * T * K * (K + 1)  # algorithmic flop per k_syrk launch
-        ach = f_syrk / (syrk_ms * 1e-3) / 1e12
-        out["roofline"] = {"kernel": "k_syrk", "bound": "mfma", "achieved": round(ach, 3),
+        if ktimes.get("k_gram_chol", (0, 0))[1]:
+            # fused weighted SYRK + Cholesky: N*[T*K(K+1) + K^3/3] flop per chain
+            kname = "k_gram_chol"
+            flop = B * N * (T * K * (K + 1) + K ** 3 / 3)
+        else:
+            kname = "k_syrk"
+            flop = B * N * T * K * (K + 1)
+        kms = ktimes[kname][0] / max(ktimes[kname][1], 1)
+        ach = flop / (kms * 1e-3) / 1e12
+        out["roofline"] = {"kernel": kname, "bound": "mfma", "achieved": round(ach, 3),
                            "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                            "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                           "flop_per_launch": f_syrk, "avg_launch_ms": round(syrk_ms, 4)}
+                           "flop_per_launch": int(flop), "avg_launch_ms": round(kms, 4)}
         out["kernel_ms_per_sweep"] = per
         out["dominant_kernel"] = dom
     if world == 1 and not args.no_cpu:

@@ -241,7 +241,7 @@ class Chains:
     """Device-resident chain set (ccmm_chains_*): B chains of one model."""
 
     KERNELS = ("k_resid", "k_cta_weights", "k_syrk", "k_chol", "k_cta_solve", "k_astep",
-               "k_sv_mix", "k_sv_sample", "k_phi_gen", "k_phi", "k_store")
+               "k_sv_mix", "k_sv_sample", "k_phi_gen", "k_phi", "k_store", "k_gram_chol")
 
     def __init__(self, ctx: Context, *, N, p, T, B, ndata=1, model=MODEL_LINEAR, crn=False,
                  store_capacity=0, logy2offset=1e-3, seed=1012023, dPHI=None):

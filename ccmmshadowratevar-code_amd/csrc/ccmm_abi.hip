@@ -12,6 +12,7 @@
 #include "ccmm_kernels.hip"
 #include "ccmm_sv.hip"
 #include "ccmm_cta_solve.hip"
+#include "ccmm_gram_chol.hip"
 #include <cstdlib>
 
 using namespace ccmm;
@@ -130,11 +131,12 @@ enum KernelId {
   KID_PHIGEN,
   KID_PHI,
   KID_STORE,
+  KID_GRAMCHOL,
   KID_COUNT
 };
 static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syrk", "k_chol",
                                               "k_cta_solve", "k_astep", "k_sv_mix", "k_sv_sample",
-                                              "k_phi_gen", "k_phi", "k_store"};
+                                              "k_phi_gen", "k_phi", "k_store", "k_gram_chol"};
 
 struct ccmm_chains {
   ccmm_ctx* ctx = nullptr;
@@ -159,6 +161,9 @@ struct ccmm_chains {
   // kernel variants (A/B): CCMM_OLD_SOLVE=1 selects the first-generation solve kernel
   bool use_solve2 = std::getenv("CCMM_OLD_SOLVE") == nullptr;
   bool use_svfast = std::getenv("CCMM_OLD_SV") == nullptr;
+  bool use_fused = std::getenv("CCMM_OLD_CHOL") == nullptr;
+  // timing-only ablation of k_gram_chol (results invalid): 1 = no SYRK, 2 = no Cholesky
+  int gc_mode = std::getenv("CCMM_GC_MODE") ? std::atoi(std::getenv("CCMM_GC_MODE")) : 0;
   std::vector<bool> have_slot;
   // profiling
   bool profiling = false;
@@ -445,11 +450,34 @@ struct ccmm_chains {
     ensure_cta();
     ChainState cs = view();
     if (!resid_valid) run_resid();
+    const bool fused = use_fused && d.KP <= 256;
     launch(KID_WEIGHTS, [&] {
       hipLaunchKernelGGL(k_cta_weights, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0,
-                         ctx->stream, d, Tslot.p, cs);
+                         ctx->stream, d, Tslot.p, cs, fused ? 1 : 0);
     });
+    if (fused) {
+      const size_t lds = (size_t)std::max(2 * kGcTC * kGcLdz, 17 * 16 * kGcLdp) * sizeof(double);
+      launch(KID_GRAMCHOL, [&] {
+        switch (d.KP / 16) {
+#define CASE_GC(NT)                                                                           \
+  case NT:                                                                                    \
+    HIPCHECK(hipFuncSetAttribute((const void*)k_gram_chol<NT>,                                \
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));      \
+    hipLaunchKernelGGL(k_gram_chol<NT>, dim3(d.nmat), dim3(512), lds, ctx->stream, d, Tslot.p, \
+                       xsel(), cs, iVdiag.p, rdiag.p, gc_mode);                               \
+    break;
+          CASE_GC(4)
+          CASE_GC(8)
+          CASE_GC(12)
+          CASE_GC(16)
+#undef CASE_GC
+          default:
+            throw ArgError("k_gram_chol: unsupported KP");
+        }
+      });
+    }
     const int nt = d.KP / kTile;
+    if (!fused) {
     launch(KID_SYRK, [&] {
       hipLaunchKernelGGL(k_syrk, dim3(nt * (nt + 1) / 2, d.nmat), dim3(256), 0, ctx->stream, d,
                          Tslot.p, xsel(), cs);
@@ -461,6 +489,7 @@ struct ccmm_chains {
       hipLaunchKernelGGL(k_chol, dim3(d.nmat), dim3(256), lds_chol, ctx->stream, d, slot.p,
                          iVdiag.p, cs, rdiag.p);
     });
+    }
     const size_t lds_solve = (size_t)(d.TP + d.KP) * sizeof(double);
     const size_t lds_solve2 =
         (size_t)(d.TP + 2 * d.KP + 64 * kSolveLd + d.N * d.N) * sizeof(double);

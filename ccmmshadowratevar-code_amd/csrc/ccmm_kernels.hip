@@ -89,7 +89,7 @@ __global__ void k_resid(Dims d, const int* __restrict__ Tslot, XSel xs, ChainSta
 // ============================================================== CTA weights
 // w_t^(j) = sum_{i>=j} A(i,j)^2 / sqrtht(t,i)^2 : the diagonal of kron(A(j:N,j),X)./lambda's
 // Gram (CTA.m:66-73).  Padded rows get weight 0.
-__global__ void k_cta_weights(Dims d, const int* __restrict__ Tslot, ChainState cs) {
+__global__ void k_cta_weights(Dims d, const int* __restrict__ Tslot, ChainState cs, int sqrt_form) {
   const int c = blockIdx.z, j = blockIdx.y;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= d.TP) return;
@@ -103,7 +103,7 @@ __global__ void k_cta_weights(Dims d, const int* __restrict__ Tslot, ChainState 
       w = fma(a, a, w);
     }
   }
-  cs.W[((size_t)c * d.N + j) * d.TP + t] = w;
+  cs.W[((size_t)c * d.N + j) * d.TP + t] = sqrt_form ? sqrt(w) : w;
 }
 
 // ============================================================== weighted SYRK (FP64 MFMA)
