@@ -9,7 +9,8 @@ Layers:
   _abi.py          ctypes binding of the C ABI
   model.py         host setup of one vintage (mcmcVAR.m:28-206)
   samplers.py      reference-interface mirror (mcmcVAR, CTA, CTAsys, drawTruncNormal)
+  distributed.py   vintage/chain sharding over GPUs, end-of-run reductions
 """
-from . import _abi, model, samplers  # noqa: F401
+from . import _abi, distributed, model, samplers  # noqa: F401
 from ._abi import Chains, Context, load_library  # noqa: F401
 from .samplers import CTA, CTAsys, drawTruncNormal, mcmcVAR  # noqa: F401

@@ -877,6 +877,19 @@ static double host_erfcinv(double y) {
   // work with x = erfinv(1 - y) using the symmetric form for accuracy near 0
   const bool upper = y > 1.0;
   const double yy = upper ? 2.0 - y : y;  // yy in (0, 1]
+  if (yy < 1e-30) {
+    // deep tail: asymptotic seed erfc(x) ~ exp(-x^2)/(x sqrt(pi)), then Newton on log erfc
+    const double ly = std::log(yy);
+    double x = std::sqrt(-ly);
+    for (int it = 0; it < 4; ++it) x = std::sqrt(-ly - std::log(1.7724538509055159 * x));
+    for (int it = 0; it < 3; ++it) {
+      const double e = std::erfc(x);
+      const double f = std::log(e) - ly;
+      const double df = -1.1283791670955126 * std::exp(-x * x) / e;
+      x -= f / df;
+    }
+    return upper ? -x : x;
+  }
   // seed: Giles' approximation of erfinv(1 - yy)
   double w = -std::log(yy * (2.0 - yy));
   double p;

@@ -1,0 +1,137 @@
+"""Multi-GPU layout of the quasi-real-time batch (goVARshadowrateBlockHybrid.m:258).
+
+The reference runs ``parfor ndxT = 1:Njumpoffs`` with one chain per vintage and
+no communication during sampling.  Here every (vintage, chain) unit is
+independent for all sweeps, so units are sharded over ranks (one process per
+GPU, torch.distributed over RCCL) with no data-path collective:
+
+  * all chains of a vintage stay on one rank (quantiles, CRPS and log scores of
+    that vintage need no cross-rank data, goVARshadowrateBlockHybrid.m:331-456);
+  * vintages are assigned longest-processing-time first with the per-chain
+    sweep cost model of SURVEY.md §8e (CTA grows with T, the ELB step with the
+    censored months of the vintage);
+  * the only collectives run at the end of the run: an all-gather of the
+    per-vintage summaries and an all-reduce of global moments, plus the
+    timing barrier/max of the benchmark.
+"""
+from __future__ import annotations
+
+import heapq
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+
+@dataclass
+class World:
+    rank: int
+    size: int
+    local_rank: int
+
+
+def world_from_env() -> World:
+    return World(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+                 int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def unit_cost(T, K, N, n_cens=0, Nstate=None, Ny=None, passes=101):
+    """Relative per-chain sweep cost of one vintage:
+    F_CTA = N [T K (K+1) + K^3/3] plus the ELB setup n_cens (4/3)(Nstate+Ny)^3
+    and the ELB pass traffic (as flop-equivalents at the fp64/HBM ridge)."""
+    f = N * (T * K * (K + 1) + K ** 3 / 3.0)
+    if n_cens:
+        Nstate = N * 12 if Nstate is None else Nstate
+        Ny = N if Ny is None else Ny
+        f += n_cens * (4.0 / 3.0) * (Nstate + Ny) ** 3
+        f += passes * n_cens * (Nstate + Ny) * 8 * 10.0
+    return float(f)
+
+
+def lpt_assign(costs, world_size):
+    """Longest-processing-time-first assignment of units to ranks.
+    Returns a list (per rank) of unit indices, each sorted ascending."""
+    costs = np.asarray(costs, float)
+    order = np.argsort(-costs, kind="stable")
+    heap = [(0.0, r) for r in range(world_size)]
+    heapq.heapify(heap)
+    out = [[] for _ in range(world_size)]
+    for u in order:
+        load, r = heapq.heappop(heap)
+        out[r].append(int(u))
+        heapq.heappush(heap, (load + costs[u], r))
+    return [sorted(x) for x in out]
+
+
+def shard_range(n, world_size, rank):
+    """Contiguous block of n equal-cost units for `rank` (chains of one vintage)."""
+    base, rem = divmod(n, world_size)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def init(backend=None):
+    """Initialise torch.distributed from the torchrun environment (RCCL on GPU,
+    gloo on CPU).  Returns (dist module or None, World)."""
+    w = world_from_env()
+    if w.size <= 1:
+        return None, w
+    import torch
+    import torch.distributed as dist
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(w.local_rank)
+    if not dist.is_initialized():
+        dist.init_process_group(backend)
+    return dist, w
+
+
+def _device_for(dist):
+    import torch
+    if dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def max_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return float(x)
+    import torch
+    t = torch.tensor([float(x)], dtype=torch.float64, device=_device_for(dist))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(dist, arr):
+    """Global sum of per-rank moment arrays (posterior means / second moments)."""
+    a = np.asarray(arr, np.float64)
+    if dist is None:
+        return a.copy()
+    import torch
+    t = torch.as_tensor(a.copy(), device=_device_for(dist))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy()
+
+
+def logmeanexp_over_ranks(dist, local_logs):
+    """log(mean(exp(x))) over the union of every rank's draws (log scores,
+    goVARshadowrateBlockHybrid.m:437-447): allreduce-MAX then allreduce-SUM."""
+    x = np.asarray(local_logs, np.float64).ravel()
+    m = max_over_ranks(dist, x.max() if x.size else -np.inf)
+    s = allreduce_sum(dist, np.array([np.exp(x - m).sum(), float(x.size)]))
+    return float(m + np.log(s[0] / s[1]))
+
+
+def gather_summaries(dist, local: dict, units_per_rank):
+    """All-gather per-unit summary arrays (same shape per unit) into unit order.
+    local maps unit index -> array."""
+    keys = sorted(local)
+    if dist is None:
+        return {k: np.asarray(local[k]) for k in keys}
+    objs = [None] * dist.get_world_size()
+    dist.all_gather_object(objs, {k: np.asarray(v) for k, v in local.items()})
+    out = {}
+    for d in objs:
+        out.update(d)
+    return dict(sorted(out.items()))

@@ -1,0 +1,74 @@
+"""World-size-2 gloo tests (CPU) of the multi-GPU layer: sharding covers every
+unit exactly once, LPT balances vintage costs, end-of-run reductions are exact."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_lpt_and_shards(pkg):
+    dm = pkg.distributed
+    costs = [dm.unit_cost(T, 241, 20, n_cens=max(0, T - 585) // 2) for T in range(587, 751)]
+    for W in (1, 2, 4, 8):
+        parts = dm.lpt_assign(costs, W)
+        flat = sorted(u for p in parts for u in p)
+        assert flat == list(range(len(costs)))
+        loads = [sum(costs[u] for u in p) for p in parts]
+        assert max(loads) / (sum(loads) / W) < 1.02
+        spans = [dm.shard_range(256, W, r) for r in range(W)]
+        assert spans[0][0] == 0 and spans[-1][1] == 256
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import __graft_entry__
+    dm = __graft_entry__.load_package().distributed
+    dist, w = dm.init("gloo")
+    costs = np.arange(1, 11, dtype=float)
+    mine = dm.lpt_assign(costs, w.size)[w.rank]
+    local = {u: np.full(3, float(u)) for u in mine}
+    allu = dm.gather_summaries(dist, local, None)
+    tot = dm.allreduce_sum(dist, np.array([sum(costs[u] for u in mine), len(mine)]))
+    rng = np.random.default_rng(w.rank)
+    x = rng.normal(size=50)
+    lme = dm.logmeanexp_over_ranks(dist, x)
+    mx = dm.max_over_ranks(dist, float(w.rank))
+    q.put((w.rank, sorted(allu), tot.tolist(), lme, mx))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_reductions():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=100) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    x = np.concatenate([np.random.default_rng(r).normal(size=50) for r in range(2)])
+    want = np.log(np.mean(np.exp(x)))
+    for rank, units, tot, lme, mx in res:
+        assert units == list(range(10))
+        assert tot == [55.0, 10.0]
+        assert abs(lme - want) < 1e-12
+        assert mx == 1.0

@@ -1,0 +1,83 @@
+"""CPU tests of the host side: the C-ABI library loads and exports every symbol
+include/ccmm.h declares; host-only entry points behave; the host model setup
+(ccmm_amd.model, mirror of mcmcVAR.m:28-206) equals the oracle's restatement."""
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, rel_err
+
+
+def header_functions():
+    src = (ROOT / "include" / "ccmm.h").read_text()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ccmm_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol(pkg):
+    lib = pkg.load_library()
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(pkg._abi.exported_symbols())
+
+
+def test_abi_version_and_host_entry_points(pkg):
+    lib = pkg.load_library()
+    assert lib.ccmm_abi_version() == 1
+    # host scalar drawTruncNormal (no GPU needed) matches the oracle's branches
+    v, fl = pkg._abi.draw_trunc_normal(0.7, 1e-12, 0.25, 0.3)
+    assert (v, fl) == (0.7, 0)
+    v, fl = pkg._abi.draw_trunc_normal(60.0, 1.0, 0.25, 0.3)
+    assert fl == 1 and abs(v - 0.25) < 1e-12
+
+
+def test_host_trunc_normal_matches_oracle_golden(pkg):
+    g = np.load(ROOT / "tests" / "golden" / "truncnorm_kat.npz")
+    for i in range(g["mu"].size):
+        v, fl = pkg._abi.draw_trunc_normal(g["mu"][i], g["sig"][i], float(g["elb"]), g["u"][i])
+        assert fl == g["flags"][i]
+        assert abs(v - g["draw"][i]) <= 1e-12 * max(1.0, abs(g["draw"][i]))
+
+
+def test_no_gpu_fails_loudly(pkg):
+    """Without a visible GPU the product path refuses to run (no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU visible")
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        pkg.Context(0)
+
+
+def test_host_setup_matches_oracle(pkg, oracle, fred):
+    mpm = pkg.model.setMinnesotaMean(fred["ncode"])
+    np.testing.assert_array_equal(mpm, oracle.set_minnesota_mean(fred["ncode"]))
+    for thisT in (len(fred["ydates"]), 599):
+        m = pkg.model.build_var(thisT, 12, 12, fred["data"], fred["ydates"], mpm, True)
+        su = oracle.var_setup(thisT, 12, 12, fred["data"], fred["ydates"], mpm, True)
+        assert (m.T, m.K, m.N) == (su.T, su.K, su.N)
+        np.testing.assert_array_equal(m.X, su.X)
+        np.testing.assert_array_equal(m.Y, su.Y)
+        assert rel_err(m.iVdiag, su.iVdiag) < 1e-13
+        assert rel_err(m.iVb, su.iVb, 1e-12) < 1e-13
+        assert rel_err(m.sPHI, su.sPHI, 1.0) < 1e-15
+        np.testing.assert_array_equal(m.Xjumpoff, su.Xjumpoff)
+    st = pkg.model.initial_state(m, 3)
+    so = oracle.init_state(su)
+    assert st["PAI"].shape == (su.K, su.N, 3)
+    assert rel_err(st["sqrtht"][..., 2], so["sqrtht"]) < 1e-14
+
+
+def test_shadow_yield_sets(pkg, oracle, fred):
+    for elb in (0.125, 0.25, 0.5):
+        a = pkg.model.setShadowYields(fred["ncode"], elb)
+        b = oracle.set_shadow_yields(fred["ncode"], elb)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    s, o, _ = pkg.model.setShadowYields(fred["ncode"], 0.25)
+    assert [fred["ncode"][i] for i in s] == ["FEDFUNDS", "TB6MS", "GS1"]
+    assert [fred["ncode"][i] for i in o] == ["GS5", "GS10", "BAA"]
+    assert oracle.elb_t0(fred["data"], s, 0.25, 12) == 585
