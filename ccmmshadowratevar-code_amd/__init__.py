@@ -7,10 +7,13 @@ register this directory as the package ``ccmm_amd``).
 Layers:
   csrc/            HIP kernels (gfx950) + C ABI -> libccmm.so  (include/ccmm.h)
   _abi.py          ctypes binding of the C ABI
-  model.py         host setup of one vintage (mcmcVAR.m:28-206)
-  samplers.py      reference-interface mirror (mcmcVAR, CTA, CTAsys, drawTruncNormal)
+  model.py         host setup of one vintage (mcmcVAR.m:28-206,
+                   mcmcVARshadowrateBlockHybrid.m:30-295)
+  samplers.py      reference-interface mirror (mcmcVAR, mcmcVARshadowrateBlockHybrid,
+                   CTA, CTAsys, drawTruncNormal)
   distributed.py   vintage/chain sharding over GPUs, end-of-run reductions
 """
 from . import _abi, distributed, model, samplers  # noqa: F401
-from ._abi import Chains, Context, load_library  # noqa: F401
-from .samplers import CTA, CTAsys, drawTruncNormal, mcmcVAR  # noqa: F401
+from ._abi import MODEL_BLOCKHYBRID, MODEL_LINEAR, Chains, Context, load_library  # noqa: F401
+from .samplers import (CTA, CTAsys, drawTruncNormal, mcmcVAR,  # noqa: F401
+                       mcmcVARshadowrateBlockHybrid)

@@ -36,7 +36,9 @@ class ChainConfig(C.Structure):
     _fields_ = [("model", C.c_int), ("N", C.c_int), ("p", C.c_int), ("K", C.c_int),
                 ("T", C.c_int), ("B", C.c_int), ("ndata", C.c_int), ("dPHI", C.c_int),
                 ("rng_crn", C.c_int), ("store_capacity", C.c_int),
-                ("logy2offset", C.c_double), ("seed", C.c_uint64)]
+                ("logy2offset", C.c_double), ("seed", C.c_uint64),
+                ("Ns", C.c_int), ("elbTmax", C.c_int), ("elb_gibbsburn", C.c_int),
+                ("elb", C.c_double)]
 
 
 _SIGS = {
@@ -66,7 +68,11 @@ _SIGS = {
     "ccmm_chains_crn_len": (C.c_int64, [C.c_void_p]),
     "ccmm_chains_sweep": (C.c_int, [C.c_void_p, C.c_int, _dp, C.c_int]),
     "ccmm_chains_stored": (C.c_int, [C.c_void_p]),
-    "ccmm_chains_get_draws": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp]),
+    "ccmm_chains_get_draws": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
+    "ccmm_chains_set_elb_model": (C.c_int, [C.c_void_p, _ip, _u8p]),
+    "ccmm_chains_set_elb_slot": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p]),
+    "ccmm_chains_get_shadowrate": (C.c_int, [C.c_void_p, _dp]),
+    "ccmm_chains_get_xy": (C.c_int, [C.c_void_p, _dp, _dp]),
     "ccmm_chains_profile": (C.c_int, [C.c_void_p, C.c_int]),
     "ccmm_chains_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _dp, _i64p, C.c_char_p, C.c_int]),
     "ccmm_selftest_mfma_f64": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
@@ -241,15 +247,19 @@ class Chains:
     """Device-resident chain set (ccmm_chains_*): B chains of one model."""
 
     KERNELS = ("k_resid", "k_cta_weights", "k_syrk", "k_chol", "k_cta_solve", "k_astep",
-               "k_sv_mix", "k_sv_sample", "k_phi_gen", "k_phi", "k_store", "k_gram_chol")
+               "k_sv_mix", "k_sv_sample", "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
+               "k_elb_prep", "k_elb_cond", "k_elb_gibbs", "k_elb_rebuild")
 
     def __init__(self, ctx: Context, *, N, p, T, B, ndata=1, model=MODEL_LINEAR, crn=False,
-                 store_capacity=0, logy2offset=1e-3, seed=1012023, dPHI=None):
+                 store_capacity=0, logy2offset=1e-3, seed=1012023, dPHI=None, Ns=0, elbTmax=0,
+                 elb_gibbsburn=100, elb=0.25):
         self.ctx = ctx
         self.lib = ctx.lib
         K = N * p + 1
         self.cfg = ChainConfig(model, N, p, K, T, B, ndata, N + 3 if dPHI is None else dPHI,
-                               int(crn), store_capacity, logy2offset, seed)
+                               int(crn), store_capacity, logy2offset, seed, Ns, elbTmax,
+                               elb_gibbsburn, elb)
+        self.model, self.Ns, self.elbTmax = model, Ns, elbTmax
         h = self.lib.ccmm_chains_create(ctx.handle, C.byref(self.cfg))
         if not h:
             raise RuntimeError(f"ccmm_chains_create failed: {last_error()}")
@@ -322,11 +332,40 @@ class Chains:
                    PHI_all=np.zeros((M, N * (N + 1) // 2, B), order="F"),
                    invA_all=np.zeros((M, N, N, B), order="F"),
                    sqrtht_all=np.zeros((M, T, N, B), order="F"))
-        rc = self.lib.ccmm_chains_get_draws(self.handle, *[_ptr(out[k]) for k in
+        if self.model == MODEL_BLOCKHYBRID:
+            out["shadowrate_all"] = np.zeros((M, self.Ns, self.elbTmax, B), order="F")
+        rc = self.lib.ccmm_chains_get_draws(self.handle, *[_ptr(out.get(k)) for k in
                                                            ("PAI_all", "PHI_all", "invA_all",
-                                                            "sqrtht_all")])
+                                                            "sqrtht_all", "shadowrate_all")])
         _check(rc, "ccmm_chains_get_draws")
         return out
+
+    # ------------------------------------------------ block-hybrid shadow-rate model
+    def set_elb_model(self, ndxS, actual_block):
+        """ndxS: 0-based shadow-rate variable indices; actual_block: bool N (actualrateBlock)."""
+        nd = np.ascontiguousarray(ndxS, dtype=np.int32)
+        ab = np.ascontiguousarray(np.asarray(actual_block, bool), dtype=np.uint8)
+        _check(self.lib.ccmm_chains_set_elb_model(self.handle, nd.ctypes.data_as(_ip),
+                                                  ab.ctypes.data_as(_u8p)),
+               "ccmm_chains_set_elb_model")
+
+    def set_elb_slot(self, slot, elbT0, sNaN):
+        """sNaN: bool Ns x elbT (elbT = T_slot - elbT0)."""
+        m = np.asfortranarray(np.asarray(sNaN, bool), dtype=np.uint8)
+        _check(self.lib.ccmm_chains_set_elb_slot(self.handle, int(slot), int(elbT0),
+                                                 m.ctypes.data_as(_u8p) if m.size else None),
+               "ccmm_chains_set_elb_slot")
+
+    def get_shadowrate(self):
+        out = np.zeros((self.Ns, self.elbTmax, self.B), order="F")
+        _check(self.lib.ccmm_chains_get_shadowrate(self.handle, _ptr(out)), "ccmm_chains_get_shadowrate")
+        return out
+
+    def get_xy(self):
+        X = np.zeros((self.T, self.K, self.B), order="F")
+        Y = np.zeros((self.T, self.N, self.B), order="F")
+        _check(self.lib.ccmm_chains_get_xy(self.handle, _ptr(X), _ptr(Y)), "ccmm_chains_get_xy")
+        return X, Y
 
     def profile(self, enable=True):
         _check(self.lib.ccmm_chains_profile(self.handle, int(enable)), "ccmm_chains_profile")

@@ -13,6 +13,7 @@
 #include "ccmm_sv.hip"
 #include "ccmm_cta_solve.hip"
 #include "ccmm_gram_chol.hip"
+#include "ccmm_elb.hip"
 #include <cstdlib>
 
 using namespace ccmm;
@@ -132,11 +133,17 @@ enum KernelId {
   KID_PHI,
   KID_STORE,
   KID_GRAMCHOL,
+  KID_ELBPREP,
+  KID_ELBCOND,
+  KID_ELBGIBBS,
+  KID_ELBREBUILD,
   KID_COUNT
 };
 static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syrk", "k_chol",
                                               "k_cta_solve", "k_astep", "k_sv_mix", "k_sv_sample",
-                                              "k_phi_gen", "k_phi", "k_store", "k_gram_chol"};
+                                              "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
+                                              "k_elb_prep", "k_elb_cond", "k_elb_gibbs",
+                                              "k_elb_rebuild"};
 
 struct ccmm_chains {
   ccmm_ctx* ctx = nullptr;
@@ -153,7 +160,17 @@ struct ccmm_chains {
   DBuf<double> G, rdiag, svLd, svw, Zphi;
   DBuf<double> crn;
   // storage of kept draws
-  DBuf<double> sPAI, sPHI_, sInvA, sSqrtht;
+  DBuf<double> sPAI, sPHI_, sInvA, sSqrtht, sShadow;
+  // block-hybrid ELB model (mcmcVARshadowrateBlockHybrid.m): X/Y slabs 0..ndata-1 hold
+  // the vintages' actual data, slabs ndata + c the chain's shadow-rate data
+  bool bh = false;
+  bool have_elb_model = false;
+  std::vector<bool> have_elb_slot;
+  std::vector<int> hNdxS, hElbT0, hElbT;
+  std::vector<uint8_t> hActual;
+  DBuf<int> dNdxS, dElbT0, dElbT, dNcens, dCens;
+  DBuf<uint8_t> dActual, dSNaN;
+  DBuf<double> ePhi, eY0, eYt, eEt, eCond, eScur;
   int stored = 0;
   uint32_t sweep = 0;
   bool resid_valid = false;
@@ -257,6 +274,14 @@ struct ccmm_chains {
   void init(ccmm_ctx* c, const ccmm_chain_config& cf, int nX, int nY) {
     ctx = c;
     cfg = cf;
+    bh = cf.model == CCMM_MODEL_BLOCKHYBRID;
+    if (bh) {
+      require(cf.Ns >= 1 && cf.Ns <= kElbNsMax, "Ns must be in [1, 4]");
+      require(cf.elbTmax >= 0 && cf.elbTmax <= cf.T, "elbTmax must be in [0, T]");
+      require(cf.elb_gibbsburn >= 0, "elb_gibbsburn must be >= 0");
+      require(2 * cf.p * cf.Ns <= kElbColMax, "2 p Ns must be <= 128");
+      require(cf.p >= 1, "p must be >= 1");
+    }
     require(cf.N >= 1 && cf.N <= kMaxNSmall, "N must be in [1, 32]");
     require(cf.K == cf.N * cf.p + 1 || cf.p == 0, "K must equal N*p+1");
     require(cf.K >= 1 && cf.K <= 1536, "K must be in [1, 1536]");
@@ -307,6 +332,7 @@ struct ccmm_chains {
     std::vector<int> zeros(cf.ndata, cf.T);
     HIPCHECK(hipMemcpyAsync(Tslot.p, zeros.data(), cf.ndata * sizeof(int), hipMemcpyHostToDevice,
                             ctx->stream));
+    if (bh) init_elb();
     std::vector<int> sl(B, 0);
     set_slots(sl.data());
     HIPCHECK(hipMemsetAsync(status.p, 0, B * sizeof(int), ctx->stream));
@@ -323,7 +349,122 @@ struct ccmm_chains {
     o += (int64_t)N * (T + 1);
     crn_off[CCMM_RNG_PHI] = o;
     o += (int64_t)N * (T + cf.dPHI);
+    if (bh) {
+      crn_off[CCMM_RNG_ELB] = o;
+      o += (int64_t)cf.Ns * cf.elbTmax * (cf.elb_gibbsburn + 1);
+    }
     crn_len = o;
+  }
+
+  void init_elb() {
+    const size_t B = cfg.B, N = cfg.N, Ns = cfg.Ns, ET = std::max(cfg.elbTmax, 1), nd = cfg.ndata;
+    have_elb_slot.assign(nd, false);
+    hNdxS.assign(Ns, 0);
+    hActual.assign(N, 1);
+    hElbT0.assign(nd, cfg.T);
+    hElbT.assign(nd, 0);
+    dNdxS.alloc(Ns);
+    dActual.alloc(N);
+    dElbT0.alloc(nd);
+    dElbT.alloc(nd);
+    dNcens.alloc(nd);
+    dCens.alloc(nd * ET);
+    dSNaN.alloc(nd * ET * Ns);
+    HIPCHECK(hipMemset(dElbT.p, 0, nd * sizeof(int)));
+    HIPCHECK(hipMemset(dNcens.p, 0, nd * sizeof(int)));
+    HIPCHECK(hipMemset(dSNaN.p, 0, dSNaN.n));
+    ePhi.alloc(B * N * N * cfg.p);
+    eY0.alloc(B * ET * N);
+    eYt.alloc(B * ET * N);
+    eEt.alloc(B * ET * N);
+    eCond.alloc(B * ET * (size_t)elb_cond_stride(cfg.Ns, cfg.p));
+    eScur.alloc(B * ET * Ns);
+    HIPCHECK(hipMemset(eScur.p, 0, eScur.n * sizeof(double)));
+  }
+
+  ElbDev elb_view() const {
+    ElbDev e{};
+    e.Ns = cfg.Ns;
+    e.p = cfg.p;
+    e.elbTmax = std::max(cfg.elbTmax, 1);
+    e.passes = cfg.elb_gibbsburn + 1;
+    e.elb = cfg.elb;
+    e.ndxS = dNdxS.p;
+    e.actual = dActual.p;
+    e.elbT0 = dElbT0.p;
+    e.elbT = dElbT.p;
+    e.sNaN = dSNaN.p;
+    e.ncens = dNcens.p;
+    e.cens = dCens.p;
+    e.Xactual = Xpool.p;
+    e.Phi = ePhi.p;
+    e.Y0 = eY0.p;
+    e.Yt = eYt.p;
+    e.Et = eEt.p;
+    e.cond = eCond.p;
+    e.Scur = eScur.p;
+    e.condStride = elb_cond_stride(cfg.Ns, cfg.p);
+    return e;
+  }
+
+  void set_elb_model(const int* ndxS, const uint8_t* actual) {
+    const int N = cfg.N, Ns = cfg.Ns;
+    for (int a = 0; a < Ns; ++a) {
+      require(ndxS[a] >= 0 && ndxS[a] < N, "ndxS out of range");
+      require(!actual[ndxS[a]], "a shadow-rate variable cannot be in the actual-rate block");
+      if (a) require(ndxS[a] > ndxS[a - 1], "ndxS must be strictly increasing");
+      hNdxS[a] = ndxS[a];
+    }
+    for (int i = 0; i < N; ++i) hActual[i] = actual[i] ? 1 : 0;
+    HIPCHECK(hipMemcpy(dNdxS.p, hNdxS.data(), Ns * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(dActual.p, hActual.data(), N, hipMemcpyHostToDevice));
+    have_elb_model = true;
+    std::vector<int> sl(cfg.B);
+    HIPCHECK(hipMemcpy(sl.data(), slot.p, cfg.B * sizeof(int), hipMemcpyDeviceToHost));
+    set_slots(sl.data());
+  }
+
+  void set_elb_slot(int s, int elbT0, const uint8_t* sNaN) {
+    const int Ns = cfg.Ns, ET = std::max(cfg.elbTmax, 1);
+    const int T = hT[s];
+    require(elbT0 >= 0, "elbT0 must be >= 0");
+    const int elbT = std::max(0, T - elbT0);
+    require(elbT <= cfg.elbTmax, "T - elbT0 exceeds elbTmax");
+    std::vector<uint8_t> m((size_t)ET * Ns, 0);
+    std::vector<int> cl(ET, 0);
+    int nc = 0;
+    for (int t = 0; t < elbT; ++t) {
+      bool any = false;
+      for (int a = 0; a < Ns; ++a) {
+        const uint8_t v = sNaN[a + (size_t)Ns * t] ? 1 : 0;  // Ns x elbT column-major
+        m[(size_t)t * Ns + a] = v;
+        any |= v != 0;
+      }
+      if (any) cl[nc++] = t;
+    }
+    hElbT0[s] = elbT0;
+    hElbT[s] = elbT;
+    HIPCHECK(hipMemcpy(dSNaN.p + (size_t)s * ET * Ns, m.data(), m.size(), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(dCens.p + (size_t)s * ET, cl.data(), ET * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(dNcens.p + s, &nc, sizeof(int), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(dElbT0.p + s, &elbT0, sizeof(int), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(dElbT.p + s, &elbT, sizeof(int), hipMemcpyHostToDevice));
+    have_elb_slot[s] = true;
+  }
+
+  // PREVdraw.X = X0, PREVdraw.Y = Y0 (mcmcVARshadowrateBlockHybrid.m:310-316)
+  void reset_chain_slabs() {
+    if (!bh) return;
+    std::vector<int> sl(cfg.B);
+    HIPCHECK(hipMemcpy(sl.data(), slot.p, cfg.B * sizeof(int), hipMemcpyDeviceToHost));
+    const size_t xs = (size_t)d.KP * d.TP, ys = (size_t)d.N * d.TP;
+    for (int c = 0; c < cfg.B; ++c) {
+      HIPCHECK(hipMemcpyAsync(Xpool.p + (size_t)(cfg.ndata + c) * xs, Xpool.p + (size_t)sl[c] * xs,
+                              xs * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+      HIPCHECK(hipMemcpyAsync(Ypool.p + (size_t)(cfg.ndata + c) * ys, Ypool.p + (size_t)sl[c] * ys,
+                              ys * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
   }
 
   // default index maps for the sweep-level linear model: X/Y slab = data slot
@@ -332,8 +473,14 @@ struct ccmm_chains {
     std::vector<int> xi((size_t)B * N), yi(B);
     for (int c = 0; c < B; ++c) {
       require(sl[c] >= 0 && sl[c] < cfg.ndata, "slot out of range");
-      yi[c] = sl[c];
-      for (int j = 0; j < N; ++j) xi[(size_t)c * N + j] = sl[c];
+      if (bh) {  // CTAsys designs: actual-rate block on the vintage's X, shadow block on the chain's
+        yi[c] = cfg.ndata + c;
+        for (int j = 0; j < N; ++j)
+          xi[(size_t)c * N + j] = hActual[j] ? sl[c] : cfg.ndata + c;
+      } else {
+        yi[c] = sl[c];
+        for (int j = 0; j < N; ++j) xi[(size_t)c * N + j] = sl[c];
+      }
     }
     HIPCHECK(hipMemcpyAsync(slot.p, sl, B * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
     HIPCHECK(hipMemcpyAsync(xidx.p, xi.data(), xi.size() * sizeof(int), hipMemcpyHostToDevice,
@@ -599,7 +746,57 @@ struct ccmm_chains {
     launch(KID_STORE, [&] {
       hipLaunchKernelGGL(k_store, dim3(64, d.B), dim3(256), 0, ctx->stream, d, cs, st);
     });
+    if (bh && cfg.elbTmax > 0) {
+      sShadow.alloc(B * cap * cfg.Ns * cfg.elbTmax);
+      ElbDev e = elb_view();
+      launch(KID_STORE, [&] {
+        hipLaunchKernelGGL(k_elb_store, dim3(d.B), dim3(256), 0, ctx->stream, e, cs, sShadow.p,
+                           cfg.store_capacity, stored);
+      });
+    }
     ++stored;
+  }
+
+  void run_elb(const RngArgs& ra) {
+    if (cfg.elbTmax <= 0) return;
+    ChainState cs = view();
+    ElbDev e = elb_view();
+    const int N = d.N, p = cfg.p, Ns = cfg.Ns, Np = N * p;
+    const size_t lds_prep = (size_t)(N * (Np + 1) + 1 + Np) * sizeof(double);
+    launch(KID_ELBPREP, [&] {
+      HIPCHECK(hipFuncSetAttribute((const void*)k_elb_prep, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds_prep));
+      hipLaunchKernelGGL(k_elb_prep, dim3(d.B), dim3(256), lds_prep, ctx->stream, d, e, xsel(), cs);
+    });
+    const size_t lds_cond =
+        (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns) * sizeof(double);
+    launch(KID_ELBCOND, [&] {
+      hipLaunchKernelGGL(k_elb_cond, dim3(e.elbTmax, d.B), dim3(64), lds_cond, ctx->stream, d, e, cs);
+    });
+    const size_t lds_gibbs = (size_t)e.elbTmax * Ns * sizeof(double);
+    launch(KID_ELBGIBBS, [&] {
+      switch (Ns) {
+#define CASE_NS(NS)                                                                            \
+  case NS:                                                                                     \
+    HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs<NS>,                                 \
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gibbs)); \
+    hipLaunchKernelGGL(k_elb_gibbs<NS>, dim3(d.B), dim3(64), lds_gibbs, ctx->stream, d, e, cs, ra); \
+    break;
+        CASE_NS(1)
+        CASE_NS(2)
+        CASE_NS(3)
+        CASE_NS(4)
+#undef CASE_NS
+        default:
+          throw ArgError("Ns must be in [1, 4]");
+      }
+    });
+    const int nrb = e.elbTmax * Ns * (p + 1);
+    launch(KID_ELBREBUILD, [&] {
+      hipLaunchKernelGGL(k_elb_rebuild, dim3((nrb + 255) / 256, d.B), dim3(256), 0, ctx->stream, d, e,
+                         xsel(), cs, cfg.ndata);
+    });
+    resid_valid = false;  // X, Y changed: RESID is recomputed before the next CTA
   }
 
   void sweep_once(const double* dcrn, int64_t stride, bool store) {
@@ -608,6 +805,7 @@ struct ccmm_chains {
     run_astep(ra);
     run_sv(ra);
     run_phi(ra);
+    if (bh) run_elb(ra);
     if (store) run_store();
     ++sweep;
   }
@@ -1022,10 +1220,11 @@ ccmm_chains* ccmm_chains_create(ccmm_ctx* ctx, const ccmm_chain_config* cfg) {
   ccmm_chains* ch = nullptr;
   int rc = guarded([&] {
     require(ctx && cfg, "null argument");
-    require(cfg->model == CCMM_MODEL_LINEAR, "only CCMM_MODEL_LINEAR is available in this build");
+    require(cfg->model == CCMM_MODEL_LINEAR || cfg->model == CCMM_MODEL_BLOCKHYBRID, "unknown model");
     HIPCHECK(hipSetDevice(ctx->device));
     ch = new ccmm_chains;
-    ch->init(ctx, *cfg, cfg->ndata, cfg->ndata);
+    const int extra = cfg->model == CCMM_MODEL_BLOCKHYBRID ? cfg->B : 0;
+    ch->init(ctx, *cfg, cfg->ndata + extra, cfg->ndata + extra);
     HIPCHECK(hipStreamSynchronize(ctx->stream));
     return 0;
   });
@@ -1082,6 +1281,18 @@ int ccmm_chains_set_state(ccmm_chains* ch, const double* PAI, const double* A,
     ch->upload_TN(ch->sqrtht.p, B, T, sqrtht, 1.0);
     ch->upload_TN(ch->h.p, B, T, h, 0.0);
     HIPCHECK(hipMemcpy(ch->sqrtPHI.p, sqrtPHI, (size_t)B * N * N * sizeof(double), hipMemcpyHostToDevice));
+    if (ch->bh) {
+      if (!ch->have_elb_model) {
+        g_err = "ccmm_chains_set_elb_model must be called before set_state";
+        return CCMM_ERR_STATE;
+      }
+      for (int s = 0; s < ch->cfg.ndata; ++s)
+        if (!ch->have_slot[s]) {
+          g_err = "ccmm_chains_set_data missing for a data slot";
+          return CCMM_ERR_STATE;
+        }
+      ch->reset_chain_slabs();
+    }
     ch->sweep = 0;
     ch->stored = 0;
     ch->resid_valid = false;
@@ -1120,8 +1331,8 @@ int ccmm_chains_sweep(ccmm_chains* ch, int nsweeps, const double* crn, int store
       return CCMM_ERR_STATE;
     }
     for (int s = 0; s < ch->cfg.ndata; ++s)
-      if (!ch->have_slot[s]) {
-        g_err = "ccmm_chains_set_data missing for a data slot";
+      if (!ch->have_slot[s] || (ch->bh && !ch->have_elb_slot[s])) {
+        g_err = "ccmm_chains_set_data / set_elb_slot missing for a data slot";
         return CCMM_ERR_STATE;
       }
     if (ch->cfg.rng_crn) require(crn != nullptr, "chain set was created in CRN mode: crn required");
@@ -1147,7 +1358,7 @@ int ccmm_chains_sweep(ccmm_chains* ch, int nsweeps, const double* crn, int store
 int ccmm_chains_stored(const ccmm_chains* ch) { return ch ? ch->stored : -1; }
 
 int ccmm_chains_get_draws(ccmm_chains* ch, double* PAI_all, double* PHI_all, double* invA_all,
-                          double* sqrtht_all) {
+                          double* sqrtht_all, double* shadowrate_all) {
   return guarded([&] {
     require(ch != nullptr, "null argument");
     HIPCHECK(hipSetDevice(ch->ctx->device));
@@ -1167,7 +1378,75 @@ int ccmm_chains_get_draws(ccmm_chains* ch, double* PAI_all, double* PHI_all, dou
     fetch(ch->sPHI_, N * (N + 1) / 2, PHI_all);
     fetch(ch->sInvA, N * N, invA_all);
     fetch(ch->sSqrtht, T * N, sqrtht_all);
+    if (ch->bh && ch->cfg.elbTmax > 0) fetch(ch->sShadow, (size_t)ch->cfg.Ns * ch->cfg.elbTmax, shadowrate_all);
     ch->stored = 0;
+    return 0;
+  });
+}
+
+int ccmm_chains_set_elb_model(ccmm_chains* ch, const int* ndxS, const uint8_t* actual_block) {
+  return guarded([&] {
+    require(ch && ndxS && actual_block, "null argument");
+    require(ch->bh, "chain set was not created with CCMM_MODEL_BLOCKHYBRID");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    ch->set_elb_model(ndxS, actual_block);
+    return 0;
+  });
+}
+
+int ccmm_chains_set_elb_slot(ccmm_chains* ch, int slot, int elbT0, const uint8_t* sNaN) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    require(ch->bh, "chain set was not created with CCMM_MODEL_BLOCKHYBRID");
+    require(slot >= 0 && slot < ch->cfg.ndata, "slot out of range");
+    require(ch->have_slot[slot], "ccmm_chains_set_data must be called before set_elb_slot");
+    require(sNaN != nullptr || ch->hT[slot] <= elbT0, "null sNaN");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    ch->set_elb_slot(slot, elbT0, sNaN);
+    return 0;
+  });
+}
+
+int ccmm_chains_get_shadowrate(ccmm_chains* ch, double* shadowrate) {
+  return guarded([&] {
+    require(ch && shadowrate, "null argument");
+    require(ch->bh, "chain set was not created with CCMM_MODEL_BLOCKHYBRID");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    if (ch->cfg.elbTmax > 0)
+      HIPCHECK(hipMemcpy(shadowrate, ch->eScur.p,
+                         (size_t)ch->d.B * ch->cfg.Ns * ch->cfg.elbTmax * sizeof(double),
+                         hipMemcpyDeviceToHost));
+    return 0;
+  });
+}
+
+int ccmm_chains_get_xy(ccmm_chains* ch, double* X, double* Y) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    const int B = ch->d.B, N = ch->d.N, K = ch->d.K, KP = ch->d.KP, TP = ch->d.TP, T = ch->cfg.T;
+    std::vector<int> sl(B);
+    HIPCHECK(hipMemcpy(sl.data(), ch->slot.p, B * sizeof(int), hipMemcpyDeviceToHost));
+    std::vector<double> xb((size_t)KP * TP), yb((size_t)N * TP);
+    for (int c = 0; c < B; ++c) {
+      const int xs = ch->bh ? ch->cfg.ndata + c : sl[c];
+      if (X) {
+        HIPCHECK(hipMemcpy(xb.data(), ch->Xpool.p + (size_t)xs * KP * TP, xb.size() * sizeof(double),
+                           hipMemcpyDeviceToHost));
+        for (int a = 0; a < K; ++a)
+          for (int t = 0; t < T; ++t) X[((size_t)c * K + a) * T + t] = xb[(size_t)a * TP + t];
+      }
+      if (Y) {
+        HIPCHECK(hipMemcpy(yb.data(), ch->Ypool.p + (size_t)xs * N * TP, yb.size() * sizeof(double),
+                           hipMemcpyDeviceToHost));
+        for (int i = 0; i < N; ++i)
+          for (int t = 0; t < T; ++t) Y[((size_t)c * N + i) * T + t] = yb[(size_t)i * TP + t];
+      }
+    }
     return 0;
   });
 }

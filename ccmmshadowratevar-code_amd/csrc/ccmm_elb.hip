@@ -1,0 +1,479 @@
+// ELB shadow-rate step of the block-hybrid sampler (mcmcVARshadowrateBlockHybrid.m:395-520,
+// gibbsdrawShadowrates.m, drawTruncNormal.m) for B chains.
+//
+// The reference computes, per censored month t, the smoothing weights J_t and the
+// conditional covariance of the Ns shadow rates S_t by QR of a 260 x 260 matrix
+// (gibbsdrawShadowrates.m:74-145).  They are the moments of the Gaussian
+// S_t | X_t, past, y_{t+1..t+p} in the zero-mean VAR on Ytilde = Y - Y0, which
+// factorises exactly into the prior of y_t given the past and p lag-equation
+// likelihoods of the future months (oracle/elb_fast.py states the algebra):
+//
+//   Ω_t = (Λ_t,SS + Σ_k B_k' Λ_{t+k} B_k)^{-1},   Λ_τ = A' diag(SVol_τ)^-2 A,
+//   Spost_t = Y0_S,t + Ω_t g_t(Ytilde),   B_k = Φ_k[:, S],
+//
+// g linear in Ytilde.  The kernels evaluate the same conditionals in a residual
+// form that never builds Y0 (see k_elb_prep).  Per censored month we store the affine map
+// Spost_t = a_t + Σ G_t[k'][s'] S(s', t ± k') over the censored neighbours, and
+// the sequential Gibbs passes cost 2p Ns^2 multiply-adds per month.
+//
+//   k_elb_prep    per chain: Φ, Yhatactual, base residuals ε_τ (stable form, no Y0 path)
+//   k_elb_cond    per (chain, censored month): Ω_t, a_t, G_t, conditional betas
+//   k_elb_gibbs   per chain: burnin + 1 sequential passes, inverse-CDF truncated normals
+//   k_elb_rebuild per chain: splice the shadow rates into the chain's Y and X (:501-509)
+#pragma once
+#include "ccmm_internal.h"
+
+namespace ccmm {
+
+constexpr int kElbNsMax = 4;
+constexpr int kElbColMax = 128;  // 2 p Ns neighbour columns, two per lane
+
+struct ElbDev {
+  int Ns, p, elbTmax, passes;    // passes = gibbsburn + 1
+  double elb;
+  const int* ndxS;               // [Ns]
+  const uint8_t* actual;         // [N] actualrateBlock
+  const int* elbT0;              // [ndata]
+  const int* elbT;               // [ndata]
+  const uint8_t* sNaN;           // [ndata][elbTmax][Ns]  (t-major)
+  const int* ncens;              // [ndata]
+  const int* cens;               // [ndata][elbTmax] censored months in increasing order
+  const double* Xactual;         // X pool (slot slabs first)
+  // per chain scratch
+  double* Phi;    // [B][N][N*p]   Phi[i][(l-1)N + q] = PAIshadow(1+(l-1)N+q, i)
+  double* Y0;     // [B][elbTmax][N]  scratch: Yb - Yhatactual
+  double* Yt;     // [B][elbTmax][N]  Yb: the chain's Y, censored shadow-rate cells at 0
+  double* Et;     // [B][elbTmax][N]  ε_τ (stable residual form, see k_elb_prep)
+  double* cond;   // [B][elbTmax][condStride]
+  double* Scur;   // [B][elbTmax][Ns] shadow rates (in/out)
+  int condStride;
+};
+
+// condition record per censored month (doubles):
+//   a_t [Ns] | beta1 [Ns][Ns-1] | sqrtOmega1 [Ns] | Ω [Ns][Ns] | G [2p Ns][Ns]
+// G column col = kk*Ns + s': kk < p past lag kk+1, kk >= p future lead kk-p+1.
+__host__ __device__ inline int elb_cond_head(int Ns) { return Ns + Ns * (Ns - 1) + Ns + Ns * Ns; }
+__host__ __device__ inline int elb_cond_stride(int Ns, int p) {
+  return elb_cond_head(Ns) + 2 * p * Ns * Ns;
+}
+
+// ---------------------------------------------------------------- prep (per chain)
+// Stable residual form (oracle/elb_fast.py, gibbsdraw_shadowrates_stable): the
+// reference's Ytilde = Y - Y0 is never formed.  Y0 enters the conditionals only
+// through the lag-equation residuals of its path,
+//   e0_τ = [τ = 0: w_{-1};  τ >= 1: c + Σ_{l=τ+1..p} Φ_l w_{τ-1-l}] + yhat_τ - Σ_{l<=τ} Φ_l yhat_{τ-l}
+// (w_{-1-i} = lag block i of elb.X0), bounded by the data even when the companion
+// matrix is explosive, where the as-written form loses all digits to cancellation.
+//   Yt[τ] = Yb_τ   (the chain's Y with censored shadow-rate cells at 0)
+//   Et[τ] = ε_τ = Yb_τ - Σ_{l<=τ} Φ_l Yb_{τ-l} - e0_τ
+__global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, ChainState cs) {
+  extern __shared__ double sm[];
+  const int c = blockIdx.x;
+  const int s = cs.slot[c];
+  const int N = d.N, KP = d.KP, TP = d.TP, p = e.p, Ns = e.Ns;
+  const int Np = N * p, ldp = Np + 1;
+  const int T0 = e.elbT0[s], T = e.elbT[s];
+  if (T <= 0) return;
+  const int tid = threadIdx.x;
+  const double* PAI = cs.PAI + (size_t)c * N * KP;  // PAI(k, i) at [i*KP + k]
+  double* Phi = e.Phi + (size_t)c * N * Np;
+  double* Z = e.Y0 + (size_t)c * e.elbTmax * N;     // Yb - yhat
+  double* Yt = e.Yt + (size_t)c * e.elbTmax * N;
+  double* Et = e.Et + (size_t)c * e.elbTmax * N;
+  double* sPhi = sm;                 // N x ldp
+  double* X0 = sPhi + N * ldp;       // K: elb.X0 = X(elbT0+1, :)'
+  // Φ = PAIshadow(2:1+Np, :)' with (ndxSHADOWRATELAGS, actualrateBlock) zeroed (:404-407)
+  for (int q = tid; q < N * Np; q += 256) {
+    const int i = q / Np, kp = q % Np;
+    bool zero = false;
+    if (e.actual[i])
+      for (int si = 0; si < Ns; ++si) zero |= (kp % N) == e.ndxS[si];
+    const double v = zero ? 0.0 : PAI[(size_t)i * KP + 1 + kp];
+    Phi[q] = v;
+    sPhi[i * ldp + kp] = v;
+  }
+  const double* Xa = e.Xactual + (size_t)s * KP * TP;        // Xactual(t, k) at [k*TP + t]
+  const double* Yc = xs.ypool + (size_t)xs.yidx[c] * N * TP;  // chain's Y(t, i) at [i*TP + t]
+  for (int k = tid; k < 1 + Np; k += 256) X0[k] = Xa[(size_t)k * TP + T0];
+  const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * Ns;
+  // Yb and Z = Yb - Yhatactual;  Yhatactual(:,t) = (Xactual(elbT0+t, lagmask) * PAIactual)' (:400-403)
+  for (int q = tid; q < T * N; q += 256) {
+    const int t = q / N, i = q % N;
+    double yh = 0.0;
+    if (e.actual[i])
+      for (int l = 0; l < p; ++l)
+        for (int si = 0; si < Ns; ++si) {
+          const int k = 1 + l * N + e.ndxS[si];
+          yh = fma(Xa[(size_t)k * TP + T0 + t], PAI[(size_t)i * KP + k], yh);
+        }
+    double yb = Yc[(size_t)i * TP + T0 + t];
+    for (int si = 0; si < Ns; ++si)
+      if (e.ndxS[si] == i && sN[t * Ns + si]) yb = 0.0;
+    Yt[q] = yb;
+    Z[q] = yb - yh;
+  }
+  // Gibbs start values: the chain's current shadow rates (gibbsdrawShadowrates.m:171)
+  double* Sc = e.Scur + (size_t)c * e.elbTmax * Ns;
+  for (int q = tid; q < T * Ns; q += 256) Sc[q] = Yc[(size_t)e.ndxS[q % Ns] * TP + T0 + q / Ns];
+  __syncthreads();
+  // ε_τ = Z_τ - Σ_{l<=τ} Φ_l Z_{τ-l} - [τ = 0: w_{-1};  τ >= 1: c + Σ_{l>τ} Φ_l w_{τ-1-l}]
+  for (int q = tid; q < T * N; q += 256) {
+    const int t = q / N, i = q % N;
+    const double* ph = sPhi + i * ldp;
+    double v = Z[q];
+    for (int l = 1; l <= p && t - l >= 0; ++l) {
+      const double* zl = Z + (size_t)(t - l) * N;
+      for (int r = 0; r < N; ++r) v = fma(-ph[(l - 1) * N + r], zl[r], v);
+    }
+    if (t == 0) {
+      v -= X0[1 + i];
+    } else {
+      double w = PAI[(size_t)i * KP] * X0[0];
+      for (int l = t + 1; l <= p; ++l) {
+        const double* wl = X0 + 1 + (l - t) * N;
+        for (int r = 0; r < N; ++r) w = fma(ph[(l - 1) * N + r], wl[r], w);
+      }
+      v -= w;
+    }
+    Et[q] = v;
+  }
+}
+
+// ---------------------------------------------------------------- conditionals
+// One wave per (censored month, chain).  Lanes i < N own element i of N-vectors;
+// neighbour columns are spread over lanes; Ns x Ns algebra runs redundantly.
+__device__ inline void elb_small_inverse(const double* M, double* Minv, int n) {
+  double W[kElbNsMax * kElbNsMax];
+  for (int q = 0; q < n * n; ++q) {
+    W[q] = M[q];
+    Minv[q] = 0.0;
+  }
+  for (int x = 0; x < n; ++x) Minv[x * n + x] = 1.0;
+  for (int col = 0; col < n; ++col) {
+    const double ip = 1.0 / W[col * n + col];
+    for (int y = 0; y < n; ++y) {
+      W[col * n + y] *= ip;
+      Minv[col * n + y] *= ip;
+    }
+    for (int x = 0; x < n; ++x) {
+      if (x == col) continue;
+      const double f = W[x * n + col];
+      for (int y = 0; y < n; ++y) {
+        W[x * n + y] -= f * W[col * n + y];
+        Minv[x * n + y] -= f * Minv[col * n + y];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs) {
+  extern __shared__ double sm[];
+  const int c = blockIdx.y;
+  const int s = cs.slot[c];
+  const int ci = blockIdx.x;
+  if (ci >= e.ncens[s]) return;
+  const int N = d.N, p = e.p, Ns = e.Ns, Np = N * p;
+  const int T = e.elbT[s], T0 = e.elbT0[s];
+  const int t = e.cens[(size_t)s * e.elbTmax + ci];
+  const int lane = threadIdx.x;
+  const int ncol = 2 * p * Ns;
+  const double* Phi = e.Phi + (size_t)c * N * Np;
+  const double* Yt = e.Yt + (size_t)c * e.elbTmax * N;
+  const double* Et = e.Et + (size_t)c * e.elbTmax * N;
+  const double* A = cs.A + (size_t)c * N * N;  // column-major A(i,j), unit lower
+  const int kmax = min(p, T - 1 - t);
+  double* Q = sm;                              // (p+1) x Ns x N
+  double* gS = Q + (p + 1) * Ns * N;           // (1 + ncol) x Ns
+  double* Pm = gS + (1 + ncol) * Ns;           // Ns x Ns
+  double* Om = Pm + Ns * Ns;                   // Ns x Ns
+  int S[kElbNsMax];
+  for (int a = 0; a < kElbNsMax; ++a) S[a] = a < Ns ? e.ndxS[a] : 0;
+  // ---- Q_0 = Λ_t[S, :], Q_k = B_k' Λ_{t+k};  Λ = A' diag(1/SVol^2) A
+  for (int k = 0; k <= kmax; ++k) {
+    double w[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
+    if (lane < N) {
+      const int i = lane;
+      const double sv = cs.sqrtht[((size_t)c * N + i) * d.TP + T0 + t + k];
+      const double iv = 1.0 / (sv * sv);
+      for (int a = 0; a < Ns; ++a) {
+        double v = 0.0;
+        if (k == 0) {
+          v = A[i + S[a] * N];
+        } else {
+          for (int j = 0; j <= i; ++j) v = fma(A[i + j * N], Phi[(size_t)j * Np + (k - 1) * N + S[a]], v);
+        }
+        w[a] = v * iv;
+      }
+    }
+    // Q_k[a][j] = Σ_{i >= j} W[i][a] A(i,j)
+    for (int a = 0; a < Ns; ++a) {
+      double v = 0.0;
+      for (int i = 0; i < N; ++i) {
+        const double wi = __shfl(w[a], i);
+        if (lane < N && i >= lane) v = fma(wi, A[i + lane * N], v);
+      }
+      if (lane < N) Q[((size_t)k * Ns + a) * N + lane] = v;
+    }
+  }
+  __syncthreads();
+  // ---- P = Λ_t,SS + Σ_k Q_k B_k
+  if (lane < Ns * Ns) {
+    const int a = lane / Ns, b = lane % Ns;
+    double v = Q[(size_t)a * N + S[b]];
+    for (int k = 1; k <= kmax; ++k) {
+      const double* Qk = Q + ((size_t)k * Ns + a) * N;
+      for (int j = 0; j < N; ++j) v = fma(Qk[j], Phi[(size_t)j * Np + (k - 1) * N + S[b]], v);
+    }
+    Pm[lane] = v;
+  }
+  // ---- base g0 = -Q_0 ε'_t + Σ_k Q_k ε'_{t+k}, ε' = ε with S_t = 0:
+  //      ε'_t = ε_t - E_S Yb_S,t,  ε'_{t+k} = ε_{t+k} + Φ_k[:,S] Yb_S,t
+  {
+    double g0[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
+    if (lane < N) {
+      bool isS = false;
+      for (int a = 0; a < Ns; ++a) isS |= (S[a] == lane);
+      const double et = Et[(size_t)t * N + lane];
+      const double u0 = isS ? Yt[(size_t)t * N + lane] - et : -et;  // -ε'_t
+      for (int a = 0; a < Ns; ++a) g0[a] = Q[(size_t)a * N + lane] * u0;
+      for (int k = 1; k <= kmax; ++k) {
+        double r = Et[(size_t)(t + k) * N + lane];
+        for (int b = 0; b < Ns; ++b)
+          r = fma(Phi[(size_t)lane * Np + (k - 1) * N + S[b]], Yt[(size_t)t * N + S[b]], r);
+        for (int a = 0; a < Ns; ++a) g0[a] = fma(Q[((size_t)k * Ns + a) * N + lane], r, g0[a]);
+      }
+    }
+    for (int a = 0; a < Ns; ++a) {
+      const double tot = wave_sum(g0[a]);
+      if (lane == 0) gS[a] = tot;
+    }
+  }
+  // ---- unit responses, one neighbour column per lane
+  //   past  (s', t-kp): Q_0 Φ_kp[:,s'] - Σ_{k + kp <= p} Q_k Φ_{k+kp}[:,s']
+  //   future(s', t+kp): Q_kp[:,s']     - Σ_{k = kp+1..kmax} Q_k Φ_{k-kp}[:,s']
+  for (int col = lane; col < ncol; col += 64) {
+    const int kk = col / Ns, sp = col % Ns;
+    const int q = S[sp];
+    double g[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
+    if (kk < p) {
+      const int kp = kk + 1;
+      if (t - kp >= 0)
+        for (int a = 0; a < Ns; ++a) {
+          double v = 0.0;
+          for (int j = 0; j < N; ++j) v = fma(Q[(size_t)a * N + j], Phi[(size_t)j * Np + (kp - 1) * N + q], v);
+          for (int k = 1; k <= kmax && k + kp <= p; ++k) {
+            const double* Qk = Q + ((size_t)k * Ns + a) * N;
+            for (int j = 0; j < N; ++j) v = fma(-Qk[j], Phi[(size_t)j * Np + (k + kp - 1) * N + q], v);
+          }
+          g[a] = v;
+        }
+    } else {
+      const int kp = kk - p + 1;
+      if (kp <= kmax)
+        for (int a = 0; a < Ns; ++a) {
+          double v = Q[((size_t)kp * Ns + a) * N + q];
+          for (int k = kp + 1; k <= kmax; ++k) {
+            const double* Qk = Q + ((size_t)k * Ns + a) * N;
+            for (int j = 0; j < N; ++j) v = fma(-Qk[j], Phi[(size_t)j * Np + (k - kp - 1) * N + q], v);
+          }
+          g[a] = v;
+        }
+    }
+    for (int a = 0; a < Ns; ++a) gS[(size_t)(1 + col) * Ns + a] = g[a];
+  }
+  __syncthreads();
+  // ---- Ω = P^-1, a_t = Ω g0, betas (gibbsdrawShadowrates.m:130-145)
+  double* rec = e.cond + ((size_t)c * e.elbTmax + ci) * e.condStride;
+  double* beta = rec + Ns;
+  double* so = beta + Ns * (Ns - 1);
+  double* Orec = so + Ns;
+  double* G = Orec + Ns * Ns;
+  if (lane == 0) {
+    double Pl[kElbNsMax * kElbNsMax], Oi[kElbNsMax * kElbNsMax];
+    for (int q = 0; q < Ns * Ns; ++q) Pl[q] = Pm[q];
+    elb_small_inverse(Pl, Oi, Ns);
+    for (int q = 0; q < Ns * Ns; ++q) {
+      Om[q] = Oi[q];
+      Orec[q] = Oi[q];
+    }
+    for (int a = 0; a < Ns; ++a) {
+      double v = 0.0;
+      for (int b = 0; b < Ns; ++b) v = fma(Oi[a * Ns + b], gS[b], v);
+      rec[a] = v;
+    }
+    // beta1(s,:) = Ω(s,o) Ω(o,o)^-1, sqrtOmega1(s) = sqrt(Ω(s,s) - beta1 Ω(o,s))
+    for (int a = 0; a < Ns; ++a) {
+      if (Ns == 1) {
+        so[0] = sqrt(Oi[0]);
+        break;
+      }
+      int oi[kElbNsMax];
+      int no = 0;
+      for (int b = 0; b < Ns; ++b)
+        if (b != a) oi[no++] = b;
+      double M[kElbNsMax * kElbNsMax], Mi[kElbNsMax * kElbNsMax];
+      for (int x = 0; x < no; ++x)
+        for (int y = 0; y < no; ++y) M[x * no + y] = Oi[oi[x] * Ns + oi[y]];
+      elb_small_inverse(M, Mi, no);
+      double var = Oi[a * Ns + a];
+      for (int y = 0; y < no; ++y) {
+        double b = 0.0;
+        for (int x = 0; x < no; ++x) b = fma(Oi[a * Ns + oi[x]], Mi[x * no + y], b);
+        beta[a * (Ns - 1) + y] = b;
+        var -= b * Oi[oi[y] * Ns + a];
+      }
+      so[a] = sqrt(var);
+    }
+  }
+  __syncthreads();
+  // G = Ω g(unit); zero for uncensored or out-of-window neighbours
+  const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * Ns;
+  for (int col = lane; col < ncol; col += 64) {
+    const int kk = col / Ns, sp = col % Ns;
+    const int tn = (kk < p) ? t - (kk + 1) : t + (kk - p + 1);
+    const bool live = tn >= 0 && tn < T && sN[(size_t)tn * Ns + sp];
+    for (int a = 0; a < Ns; ++a) {
+      double v = 0.0;
+      if (live)
+        for (int b = 0; b < Ns; ++b) v = fma(Om[a * Ns + b], gS[(size_t)(1 + col) * Ns + b], v);
+      G[(size_t)col * Ns + a] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- truncated normal (device)
+// drawTruncNormal.m: z = -sqrt(2) erfcinv(2 u Φbar(ub)), ub = (elb - mu)/sig
+__device__ __forceinline__ double elb_trunc_normal(double mu, double sig, double elb, double u) {
+  const double tol = 1e-10;
+  const double eps = 2.220446049250313080847e-16;
+  sig = fabs(sig);
+  if (sig > tol) {
+    const double ub = (elb - mu) / sig;
+    const double PHIbar = 0.5 * erfc(-0.70710678118654752440 * ub);
+    const double z = (PHIbar > eps) ? -1.41421356237309504880 * erfcinv(2.0 * u * PHIbar) : ub;
+    return mu + sig * z;
+  }
+  return mu;
+}
+
+// ---------------------------------------------------------------- Gibbs passes (per chain)
+// One wave per chain.  Each lane owns neighbour columns lane and lane + 64 of every
+// month's record and prefetches the next month's while the current one is drawn;
+// the draws themselves run redundantly on all lanes (uniform control flow).
+template <int NS>
+__global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState cs, RngArgs ra) {
+  extern __shared__ double sm[];
+  const int c = blockIdx.x;
+  const int s = cs.slot[c];
+  const int p = e.p;
+  const int T = e.elbT[s], nc = e.ncens[s];
+  if (nc == 0) return;
+  const int lane = threadIdx.x;
+  const Rng rng = ra.make(c);
+  const int ncol = 2 * p * NS;
+  const int head = elb_cond_head(NS);
+  double* Sl = sm;  // T x NS (t-major)
+  double* Sc = e.Scur + (size_t)c * e.elbTmax * NS;
+  const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * NS;
+  const int* cl = e.cens + (size_t)s * e.elbTmax;
+  const double* recs = e.cond + (size_t)c * e.elbTmax * e.condStride;
+  for (int q = lane; q < T * NS; q += 64) Sl[q] = Sc[q];
+  __syncthreads();
+  // column geometry of this lane
+  const int c0 = lane, c1 = lane + 64;
+  const bool h0 = c0 < ncol, h1 = c1 < ncol;
+  const int kk0 = c0 / NS, sp0 = c0 % NS, kk1 = c1 / NS, sp1 = c1 % NS;
+  const int off0 = (kk0 < p) ? -(kk0 + 1) : (kk0 - p + 1);
+  const int off1 = (kk1 < p) ? -(kk1 + 1) : (kk1 - p + 1);
+  auto load_rec = [&](int ci, double* hd, double* g0, double* g1) {
+    const double* r = recs + (size_t)ci * e.condStride;
+    for (int q = 0; q < elb_cond_head(NS) - NS * NS; ++q) hd[q] = r[q];
+    for (int a = 0; a < NS; ++a) {
+      g0[a] = h0 ? r[head + c0 * NS + a] : 0.0;
+      g1[a] = h1 ? r[head + c1 * NS + a] : 0.0;
+    }
+  };
+  constexpr int kHd = NS + NS * (NS - 1) + NS;
+  double hd[kHd], g0[NS], g1[NS];
+  double hdn[kHd], g0n[NS], g1n[NS];
+  load_rec(0, hd, g0, g1);
+  for (int n = 0; n < e.passes; ++n) {
+    for (int ci = 0; ci < nc; ++ci) {
+      const int t = cl[ci];
+      // prefetch next month's record (wraps to month 0 of the next pass)
+      const int cn = (ci + 1 < nc) ? ci + 1 : 0;
+      load_rec(cn, hdn, g0n, g1n);
+      double u[NS];
+      for (int a = 0; a < NS; ++a) u[a] = rng.uniform(CCMM_RNG_ELB, (uint32_t)(a + NS * (t + T * n)));
+      // Spost = a_t + Σ G S(neighbours)
+      const int tn0 = t + off0, tn1 = t + off1;
+      const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
+      const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
+      double sp[NS];
+      for (int a = 0; a < NS; ++a) sp[a] = fma(g0[a], v0, g1[a] * v1);
+      for (int a = 0; a < NS; ++a) sp[a] = hd[a] + wave_sum(sp[a]);
+      // conditional draws in index order (gibbsdrawShadowrates.m:206-218)
+      const double* beta = hd + NS;
+      const double* so = beta + NS * (NS - 1);
+      double cur[NS];
+      for (int a = 0; a < NS; ++a) cur[a] = Sl[t * NS + a];
+      for (int a = 0; a < NS; ++a) {
+        if (!sN[t * NS + a]) continue;
+        double mu = sp[a];
+        int y = 0;
+        for (int b = 0; b < NS; ++b) {
+          if (b == a) continue;
+          mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
+          ++y;
+        }
+        cur[a] = elb_trunc_normal(mu, so[a], e.elb, u[a]);
+      }
+      for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
+      for (int q = 0; q < kHd; ++q) hd[q] = hdn[q];
+      for (int a = 0; a < NS; ++a) {
+        g0[a] = g0n[a];
+        g1[a] = g1n[a];
+      }
+    }
+  }
+  __syncthreads();
+  for (int q = lane; q < T * NS; q += 64) Sc[q] = Sl[q];
+}
+
+// ---------------------------------------------------------------- rebuild X, Y (per chain)
+// shadowYdata(p+elbT0+1:end, ndxS) = shadowrate'; X(t, 1+(l-1)N+s) = Y(t-l, s) (:501-509)
+__global__ void k_elb_rebuild(Dims d, ElbDev e, XSel xs, ChainState cs, int xslab0) {
+  const int c = blockIdx.y;
+  const int s = cs.slot[c];
+  const int N = d.N, TP = d.TP, Ns = e.Ns, p = e.p;
+  const int T0 = e.elbT0[s], T = e.elbT[s];
+  double* Y = const_cast<double*>(xs.ypool) + (size_t)xs.yidx[c] * N * TP;
+  double* X = const_cast<double*>(xs.pool) + (size_t)(xslab0 + c) * d.KP * TP;
+  const double* Sc = e.Scur + (size_t)c * e.elbTmax * Ns;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;  // (l in 0..p, si, t)
+  if (q >= T * Ns * (p + 1)) return;
+  const int l = q % (p + 1);
+  const int r = q / (p + 1);
+  const int si = r % Ns, t = r / Ns;
+  const double v = Sc[t * Ns + si];
+  const int var = e.ndxS[si];
+  if (l == 0) {
+    Y[(size_t)var * TP + T0 + t] = v;
+  } else {
+    const int row = T0 + t + l;  // X(row, lag l of var) = Y(row - l, var)
+    if (row < T0 + T) X[(size_t)(1 + (l - 1) * N + var) * TP + row] = v;
+  }
+}
+
+// ---------------------------------------------------------------- draw store
+// shadowrate_all(thisMCMCdraw, :, :) = shadowrate (:542); NaN beyond the vintage's elbT
+__global__ void k_elb_store(ElbDev e, ChainState cs, double* out, int cap, int m) {
+  const int c = blockIdx.x;
+  const int T = e.elbT[cs.slot[c]];
+  const int per = e.Ns * e.elbTmax;
+  const double* Sc = e.Scur + (size_t)c * per;
+  double* o = out + ((size_t)c * cap + m) * per;
+  for (int q = threadIdx.x; q < per; q += blockDim.x) o[q] = (q / e.Ns < T) ? Sc[q] : __builtin_nan("");
+}
+
+}  // namespace ccmm

@@ -115,3 +115,50 @@ def initial_state(m: VARModel, B: int = 1):
     rep = lambda a: np.repeat(a[..., None], B, axis=-1)
     return dict(PAI=rep(PAI), A=rep(np.eye(m.N)), sqrtht=rep(sq), h=rep(2 * np.log(sq)),
                 sqrtPHI=rep(0.01 * np.eye(m.N)))
+
+
+def elbT0_of(data, ndxSHADOWRATE, ELBbound, p):
+    """goVARshadowrateBlockHybrid.m:131-134 / doMCMCshadowrateBlockHybrid.m:97-100:
+    startELB = find(any(data(:,ndxSHADOWRATE) <= ELBbound, 2), 1); elbT0 = startELB - 1 - p."""
+    hit = np.any(np.asarray(data)[:, ndxSHADOWRATE] <= ELBbound, axis=1)
+    if not hit.any():
+        return np.asarray(data).shape[0]  # no ELB observation: empty window
+    return int(np.argmax(hit)) + 1 - 1 - p
+
+
+@dataclass
+class BHModel:
+    """A vintage of the block-hybrid shadow-rate VAR (mcmcVARshadowrateBlockHybrid.m:30-295)."""
+    var: VARModel
+    ndxS: np.ndarray          # ndxSHADOWRATE (0-based)
+    ndxO: np.ndarray          # ndxOTHERYIELDS (0-based)
+    actual_block: np.ndarray  # bool N, actualrateBlock (:80-84: ~ismember(1:N, ndxYIELDS))
+    elbT0: int
+    elbT: int
+    sNaN: np.ndarray          # bool Ns x elbT (:163-171, 192)
+    ELB: float
+    warn_elbT0: bool          # :203-205 warning condition
+
+
+def build_bh(thisT, p, np_, data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS, minnesotaPriorMean,
+             ELBbound, elbT0, doRATSprior=True, actualrateBlock=None) -> BHModel:
+    """Host setup of mcmcVARshadowrateBlockHybrid.m for the 1-based jump-off ``thisT``:
+    the VAR matrices and priors of the actual data (X0, Y0) and the ELB window."""
+    m = build_var(thisT, p, np_, data0, ydates0, minnesotaPriorMean, doRATSprior)
+    N, T = m.N, m.T
+    ndxS = np.asarray(ndxSHADOWRATE, int)
+    ndxO = np.asarray(ndxOTHERYIELDS, int)
+    if actualrateBlock is None:  # goVARshadowrateBlockHybrid.m:93
+        actual = ~np.isin(np.arange(N), np.union1d(ndxS, ndxO))
+    else:
+        actual = np.asarray(actualrateBlock, bool)
+    cens = np.zeros_like(m.data, dtype=bool)
+    cens[:, ndxS] = m.data[:, ndxS] <= ELBbound         # :163-166
+    yNaN = cens[p:, :]
+    elbT = max(0, T - elbT0)
+    if elbT > 0 and np.any(yNaN[:elbT0, ndxS]):
+        raise ValueError("something off about elbT0")   # :199-201
+    warn = elbT > 0 and not np.any(yNaN[elbT0, ndxS])   # :203-205
+    sNaN = yNaN[elbT0:, :][:, ndxS].T if elbT > 0 else np.zeros((ndxS.size, 0), bool)
+    return BHModel(var=m, ndxS=ndxS, ndxO=ndxO, actual_block=actual, elbT0=int(elbT0), elbT=elbT,
+                   sNaN=sNaN, ELB=float(ELBbound), warn_elbT0=bool(warn))

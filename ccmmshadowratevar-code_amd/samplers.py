@@ -4,7 +4,8 @@
 (``nargout == 4`` form: PAI_all, PHI_all, invA_all, sqrtht_all) and adds
 ``nchains``: B independent chains run as one device batch (the
 ``goVAR*`` parfor over vintages/chains becomes one GPU launch sequence).
-``CTA``/``CTAsys``/``drawTruncNormal`` mirror the L2 functions.
+``mcmcVARshadowrateBlockHybrid`` mirrors the block-hybrid shadow-rate sampler
+(outputs 1-6).  ``CTA``/``CTAsys``/``drawTruncNormal`` mirror the L2 functions.
 
 Every numerical step goes through ``libccmm.so``; there is no CPU fallback.
 """
@@ -13,7 +14,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _abi
-from .model import build_var, initial_state
+from .model import build_bh, build_var, initial_state
 
 _CTX = {}
 
@@ -51,7 +52,16 @@ def mcmcVAR(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMean, doRATS
     ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
     st = initial_state(m, B)
     ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
-    step = 50
+    _run_chain_set(ch, burn, MCMCdraws, doprogress)
+    out = ch.get_draws()
+    ch.close()
+    res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"]]
+    if B == 1:
+        res = [a[..., 0] for a in res]
+    return tuple(res)
+
+
+def _run_chain_set(ch, burn, MCMCdraws, doprogress, step=50):
     done = 0
     while done < burn:
         n = min(step, burn - done)
@@ -66,9 +76,55 @@ def mcmcVAR(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMean, doRATS
         done += n
         if doprogress:
             print(f"draws {done}/{MCMCdraws}")
+
+
+def mcmcVARshadowrateBlockHybrid(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateBlock,
+                                 minnesotaPriorMean, doRATSprior, ndxSHADOWRATE, ndxOTHERYIELDS,
+                                 doELBsampling, doELBsampleAlternate, ELBbound, elbT0,
+                                 check_stationarity=0, IRF1scale=None, IRFcumcode=None,
+                                 yrealized=None, fcstNdraws=None, fcstNhorizons=None,
+                                 rndStream=1012023, doprogress=False, *, nchains=1, device=0,
+                                 burnin=None, gibbsburn=100):
+    """mcmcVARshadowrateBlockHybrid.m:1-14, outputs PAI_all, PHI_all, invA_all,
+    sqrtht_all, shadowrate_all (M x Nshadowrates x elbT), missingrate_all (NaN).
+
+    The ELB step is the Gibbs sampler of the ``m < MCMCburnin*.5`` branch
+    (:435-437) at every sweep: the acceptance-sampling branch needs
+    VARTVPSVprecisionsamplerNaN from the absent em-matlabbox toolbox.
+    Indices are 0-based; actualrateBlock is a bool vector of length N."""
+    if check_stationarity:
+        raise NotImplementedError("check_stationarity=1 is not supported; the reference drivers "
+                                  "all pass 0")
+    if not doELBsampling or doELBsampleAlternate:
+        raise NotImplementedError("doELBsampling=false / doELBsampleAlternate=true need the "
+                                  "missing-data sampler VARTVPSVprecisionsamplerNaN (absent "
+                                  "em-matlabbox); out of scope")
+    if fcstNdraws or IRF1scale is not None:
+        raise NotImplementedError("predictive density / IRF outputs are a later row (SURVEY §8f)")
+    bm = build_bh(thisT, p, np_, data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS,
+                  minnesotaPriorMean, ELBbound, elbT0, doRATSprior,
+                  actualrateBlock=actualrateBlock)
+    if bm.warn_elbT0:
+        import warnings
+        warnings.warn("elbT0 + 1 should be a missing obs, but it is not ...")  # :203-205
+    m = bm.var
+    B = int(nchains)
+    burn = MCMCdraws if burnin is None else int(burnin)
+    ch = _abi.Chains(context(device), N=m.N, p=m.p, T=m.T, B=B, ndata=1, crn=False,
+                     store_capacity=MCMCdraws, seed=int(rndStream),
+                     model=_abi.MODEL_BLOCKHYBRID, Ns=len(bm.ndxS), elbTmax=bm.elbT,
+                     elb_gibbsburn=gibbsburn, elb=ELBbound)
+    ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    ch.set_elb_model(bm.ndxS, bm.actual_block)
+    ch.set_elb_slot(0, bm.elbT0, bm.sNaN)
+    st = initial_state(m, B)
+    ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+    _run_chain_set(ch, burn, MCMCdraws, doprogress)
     out = ch.get_draws()
     ch.close()
-    res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"]]
+    sr = out.get("shadowrate_all", np.full((MCMCdraws, len(bm.ndxS), 0, B), np.nan))
+    res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"], sr,
+           np.full((MCMCdraws, len(bm.ndxS), bm.elbT, B), np.nan)]
     if B == 1:
         res = [a[..., 0] for a in res]
     return tuple(res)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define CCMM_ABI_VERSION 1
+#define CCMM_ABI_VERSION 2
 
 /* return codes */
 #define CCMM_OK 0
@@ -123,7 +123,7 @@ int ccmm_phi_iw(ccmm_ctx* ctx, int B, int T, int N, const double* eta, const dou
  * (drawTruncNormal.m:31-86) with a pre-drawn uniform u (the numeric-stream
  * form of drawTruncNormal.m:47-48).  flags (may be NULL): bit0 = |sig| > 1e-10
  * branch taken, bit1 = PHIbar > eps branch taken.  Host-side scalar; the
- * device form is used inside ccmm_gibbs_shadowrates. */
+ * device form runs inside the block-hybrid sweep (k_elb_gibbs). */
 double ccmm_draw_trunc_normal(double mu, double sig, double elb, double u, uint8_t* flags);
 
 /* Batched device evaluation of drawTruncNormal over n independent cells. */
@@ -143,6 +143,11 @@ typedef struct {
   int store_capacity;     /* kept draws stored per chain (0: no storage) */
   double logy2offset;     /* getKSC7values offset (ext; this build declares 1e-3) */
   uint64_t seed;          /* Philox key */
+  /* CCMM_MODEL_BLOCKHYBRID only (ignored otherwise) */
+  int Ns;                 /* number of shadow-rate variables, 1..4 (Nshadowrates) */
+  int elbTmax;            /* max over data slots of elbT = T - elbT0 */
+  int elb_gibbsburn;      /* Gibbs burn-in passes per sweep (gibbsdrawShadowrates call, :436: 100) */
+  double elb;             /* ELBbound */
 } ccmm_chain_config;
 
 ccmm_chains* ccmm_chains_create(ccmm_ctx* ctx, const ccmm_chain_config* cfg);
@@ -172,11 +177,32 @@ int64_t ccmm_chains_crn_len(const ccmm_chains* ch);
 int ccmm_chains_sweep(ccmm_chains* ch, int nsweeps, const double* crn, int store);
 /* Number of stored draws per chain so far. */
 int ccmm_chains_stored(const ccmm_chains* ch);
-/* Copy stored draws out in the reference layout (mcmcVAR.m:178-181, 289-292):
+/* Copy stored draws out in the reference layout (mcmcVAR.m:178-181, 289-292;
+ * mcmcVARshadowrateBlockHybrid.m:284-288, 536-543):
  *   PAI_all M x K x N x B, PHI_all M x N(N+1)/2 x B, invA_all M x N x N x B,
- *   sqrtht_all M x T x N x B.  Any pointer may be NULL.  Resets the store. */
+ *   sqrtht_all M x T x N x B, shadowrate_all M x Ns x elbTmax x B (block-hybrid;
+ *   NaN beyond a vintage's elbT).  Any pointer may be NULL.  Resets the store. */
 int ccmm_chains_get_draws(ccmm_chains* ch, double* PAI_all, double* PHI_all, double* invA_all,
-                          double* sqrtht_all);
+                          double* sqrtht_all, double* shadowrate_all);
+
+/* ---- block-hybrid shadow-rate model (mcmcVARshadowrateBlockHybrid.m) ----
+ * Data slot X/Y (ccmm_chains_set_data) are the vintage's ACTUAL data (X0, Y0,
+ * :310-316); every chain keeps its own shadow-rate copy, reset to the slot's
+ * data by ccmm_chains_set_state.  Equations with actual_block[j] != 0 use the
+ * slot's X (CTAsys design of the actual-rate block), the others the chain's.
+ *
+ * ndxS: Ns strictly increasing 0-based shadow-rate variable indices (ndxSHADOWRATE);
+ * actual_block: N bytes, actualrateBlock (:80-84).  Call before set_state. */
+int ccmm_chains_set_elb_model(ccmm_chains* ch, const int* ndxS, const uint8_t* actual_block);
+/* Per vintage: elbT0 (first VAR row, 0-based, of the ELB window; :176-183) and
+ * sNaN Ns x elbT (column-major, elbT = T_slot - elbT0): nonzero where the shadow
+ * rate is censored (data <= ELB, :163-171).  Call after ccmm_chains_set_data. */
+int ccmm_chains_set_elb_slot(ccmm_chains* ch, int slot, int elbT0, const uint8_t* sNaN);
+/* Current shadow rates, Ns x elbTmax x B (the last sweep's draw). */
+int ccmm_chains_get_shadowrate(ccmm_chains* ch, double* shadowrate);
+/* Current per-chain data: X T x K x B, Y T x N x B (block-hybrid: the chain's
+ * shadow-rate X/Y, PREVdraw.X/Y; linear: the slot's data).  Either may be NULL. */
+int ccmm_chains_get_xy(ccmm_chains* ch, double* X, double* Y);
 /* Per-kernel device time (HIP events on the chain set's stream) accumulated
  * while profiling is on.  names: ';'-separated list written into buf. */
 int ccmm_chains_profile(ccmm_chains* ch, int enable);

@@ -42,3 +42,31 @@ def random_state(oracle, su, seed=1):
 def crn_flat(oracle, crn, su):
     return np.concatenate([crn[k].ravel(order="F") for k, _ in oracle.crn_sizes(su.N, su.K, su.T,
                                                                                  su.dPHI)])
+
+
+def synth_bh_data(N=5, p=2, Tobs=150, elb_window=(80, 120), ndxS=(2, 3), seed=3, elb=0.25):
+    """Toy block-hybrid data: a VAR sample whose shadow-rate variables sit at or
+    below the ELB (mixed censoring across the Ns rates) inside ``elb_window``."""
+    y = synth_var_data(N, p, Tobs, seed)
+    rng = np.random.default_rng(seed + 1)
+    a, b = elb_window
+    for k, s in enumerate(ndxS):
+        y[:a, s] = 2.0 + np.abs(y[:a, s])               # above the ELB before the window
+        y[a:b, s] = elb - rng.uniform(0.01, 0.2, b - a)  # censored
+        if k % 2 == 1:                                   # second rate: a few uncensored months
+            y[a + 5:b:7, s] = elb + rng.uniform(0.05, 0.3, len(range(a + 5, b, 7)))
+        y[b:, s] = elb + 0.5 + np.abs(y[b:, s])
+    return y
+
+
+def toy_bh_setup(bh, N=5, p=2, Tobs=150, ndxS=(2, 3), ndxO=(4,), seed=3, elb=0.25):
+    data = synth_bh_data(N, p, Tobs, ndxS=ndxS, seed=seed, elb=elb)
+    ydates = np.arange(Tobs, dtype=float)
+    hit = np.any(data[:, list(ndxS)] <= elb, axis=1)
+    elbT0 = int(np.argmax(hit)) - p
+    return bh.bh_setup(Tobs, p, 12, data, ydates, np.asarray(ndxS), np.asarray(ndxO), np.ones(N),
+                       elb, elbT0)
+
+
+def bh_crn_flat(bh, crn, bs):
+    return np.concatenate([crn[k].ravel(order="F") for k, _ in bh.bh_crn_sizes(bs)])

@@ -27,7 +27,17 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_host_entry_points(pkg):
     lib = pkg.load_library()
-    assert lib.ccmm_abi_version() == 1
+    assert lib.ccmm_abi_version() == 2
+    # the ChainConfig ctypes mirror has the header's fields in order
+    src = (ROOT / "include" / "ccmm.h").read_text()
+    start = src.index("typedef struct {", src.index("sweep-level")) + len("typedef struct {")
+    body = re.sub(r"/\*.*?\*/", "", src[start:src.index("} ccmm_chain_config;")], flags=re.S)
+    names = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if decl:  # "int N, p, K" -> N, p, K
+            names += [n.strip() for n in decl.split(None, 1)[1].split(",")]
+    assert names == [f[0] for f in pkg._abi.ChainConfig._fields_]
     # host scalar drawTruncNormal (no GPU needed) matches the oracle's branches
     v, fl = pkg._abi.draw_trunc_normal(0.7, 1e-12, 0.25, 0.3)
     assert (v, fl) == (0.7, 0)

@@ -1,0 +1,141 @@
+"""Block-hybrid oracle checks on CPU: the per-month conditional formulation the
+GPU kernels use (oracle/elb_fast.py) reproduces gibbsdrawShadowrates as written
+(QR smoothing weights, gibbsdrawShadowrates.m:74-218), and the host setup of
+mcmcVARshadowrateBlockHybrid.m matches the oracle's."""
+import numpy as np
+import pytest
+
+from helpers import toy_bh_setup
+from conftest import CSV
+
+
+@pytest.fixture(scope="module")
+def bh():
+    from oracle import ccmm_oracle_bh
+    return ccmm_oracle_bh
+
+
+def _elb_inputs(bh, bs, seed):
+    from oracle import ccmm_oracle as O
+    lin = bs.lin
+    rng = np.random.default_rng(seed)
+    st = bh.bh_init_state(bs)
+    A = np.eye(lin.N) + np.tril(rng.uniform(-0.3, 0.3, (lin.N, lin.N)), -1)
+    sqrtht = np.exp(np.cumsum(0.05 * rng.standard_normal((lin.T, lin.N)), axis=0) / 2)
+    C, Psi, SVol, Yhat = bh.elb_state_space(bs, st["PAI"], np.linalg.inv(A), sqrtht)
+    crn = bh.bh_draw_crn(rng, bs)
+    return O, st, C, Psi, SVol, Yhat, crn["uELB"]
+
+
+@pytest.mark.parametrize("burn", [0, 2])
+def test_elb_stable_matches_qr_toy(bh, burn):
+    """The residual form the GPU evaluates (no Y0 path) == the as-written QR form."""
+    from oracle import elb_fast as F
+    bs = toy_bh_setup(bh)
+    O, st, C, Psi, SVol, Yhat, u = _elb_inputs(bh, bs, 5)
+    elbY = st["Y"][bs.elbT0:, :].T
+    a = O.gibbsdraw_shadowrates(elbY, bs.X0, Yhat, bs.ndxSmask, bs.sNaN, bs.lin.p, C, Psi, SVol,
+                                bs.ELB, 1, burn, u)
+    b = F.gibbsdraw_shadowrates_stable(elbY, bs.X0, Yhat, bs.ndxSmask, bs.sNaN, bs.lin.p, C, Psi,
+                                       SVol, bs.ELB, 1, burn, u)
+    assert np.max(np.abs(a - b)) < 1e-10
+
+
+def test_elb_stable_explosive_companion(bh, oracle, fred):
+    """Explosive shadow companion matrix (spectral radius > 1, as posterior draws of
+    PAIshadow can have): Y0 grows geometrically over the 165-month window and the
+    as-written Ytilde = Y - Y0 loses its digits.  The stable form agrees with the
+    as-written one while |Y0| is moderate and stays data-scale afterwards."""
+    from oracle import elb_fast as F
+    ndxS, ndxO, _ = oracle.set_shadow_yields(fred["ncode"], 0.25)
+    mpm = oracle.set_minnesota_mean(fred["ncode"])
+    e0 = oracle.elb_t0(fred["data"], ndxS, 0.25, 12)
+    bs = bh.bh_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], ndxS, ndxO, mpm,
+                     0.25, e0)
+    lin = bs.lin
+    st = bh.bh_init_state(bs)
+    PAI = st["PAI"].copy()
+    for s in bs.ndxS:
+        PAI[1 + s, s] *= 1.3                        # own first lag of the shadow rates
+    C, Psi, SVol, Yhat = bh.elb_state_space(bs, PAI, np.eye(lin.N), st["sqrtht"])
+    rho = np.max(np.abs(np.linalg.eigvals(C)))
+    assert rho > 1.2
+    Y0 = F.y0_path(C, bs.X0, Yhat, lin.N, bs.elbT)
+    big = np.max(np.abs(Y0), axis=0)
+    u = bh.bh_draw_crn(np.random.default_rng(8), bs)["uELB"]
+    elbY = st["Y"][bs.elbT0:, :].T
+    a = oracle.gibbsdraw_shadowrates(elbY, bs.X0, Yhat, bs.ndxSmask, bs.sNaN, 12, C, Psi, SVol,
+                                     0.25, 1, 0, u)[:, :, 0]
+    b = F.gibbsdraw_shadowrates_stable(elbY, bs.X0, Yhat, bs.ndxSmask, bs.sNaN, 12, C, Psi, SVol,
+                                       0.25, 1, 0, u)[:, :, 0]
+    early = big < 1e4
+    assert early.sum() > 20 and big.max() > 1e12
+    assert np.max(np.abs(a - b)[:, early]) < 1e-8
+    assert np.all(np.isfinite(b)) and np.max(np.abs(b)) < 50
+    assert np.all(b[bs.sNaN] <= 0.25 + 1e-12)
+
+
+@pytest.mark.parametrize("burn", [0, 2])
+def test_elb_fast_matches_qr_toy(bh, burn):
+    from oracle import elb_fast as F
+    bs = toy_bh_setup(bh)
+    O, st, C, Psi, SVol, Yhat, u = _elb_inputs(bh, bs, 5)
+    elbY = st["Y"][bs.elbT0:, :].T
+    a = O.gibbsdraw_shadowrates(elbY, bs.X0, Yhat, bs.ndxSmask, bs.sNaN, bs.lin.p, C, Psi, SVol,
+                                bs.ELB, 1, burn, u)
+    b = F.gibbsdraw_shadowrates_fast(elbY, bs.X0, Yhat, bs.ndxSmask, bs.sNaN, bs.lin.p, C, Psi,
+                                     SVol, bs.ELB, 1, burn, u)
+    assert np.max(np.abs(a - b)) < 1e-10
+    assert np.all(a[:, :, 0][bs.sNaN] <= bs.ELB + 1e-12)
+
+
+@pytest.mark.slow
+def test_elb_fast_matches_qr_real(bh, oracle, fred):
+    """Real data (elbT = 165, 109 censored months, 276 cells), 3 burn-in passes."""
+    from oracle import elb_fast as F
+    ndxS, ndxO, _ = oracle.set_shadow_yields(fred["ncode"], 0.25)
+    mpm = oracle.set_minnesota_mean(fred["ncode"])
+    e0 = oracle.elb_t0(fred["data"], ndxS, 0.25, 12)
+    bs = bh.bh_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], ndxS, ndxO, mpm,
+                     0.25, e0)
+    O, st, C, Psi, SVol, Yhat, u = _elb_inputs(bh, bs, 6)
+    elbY = st["Y"][bs.elbT0:, :].T
+    a = O.gibbsdraw_shadowrates(elbY, bs.X0, Yhat, bs.ndxSmask, bs.sNaN, 12, C, Psi, SVol, 0.25, 1,
+                                3, u)
+    b = F.gibbsdraw_shadowrates_fast(elbY, bs.X0, Yhat, bs.ndxSmask, bs.sNaN, 12, C, Psi, SVol,
+                                     0.25, 1, 3, u)
+    assert np.max(np.abs(a - b)) < 1e-8
+
+
+def test_host_bh_setup_matches_oracle(pkg, bh, oracle, fred):
+    ndxS, ndxO, _ = pkg.model.setShadowYields(fred["ncode"], 0.25)
+    mpm = pkg.model.setMinnesotaMean(fred["ncode"])
+    e0 = pkg.model.elbT0_of(fred["data"], ndxS, 0.25, 12)
+    assert e0 == oracle.elb_t0(fred["data"], ndxS, 0.25, 12) == 585
+    bm = pkg.model.build_bh(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], ndxS, ndxO,
+                            mpm, 0.25, e0)
+    bs = bh.bh_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], ndxS, ndxO, mpm,
+                     0.25, e0)
+    assert bm.elbT == bs.elbT == 165
+    np.testing.assert_array_equal(bm.sNaN, bs.sNaN)
+    np.testing.assert_array_equal(bm.actual_block, bs.actualrateBlock)
+    np.testing.assert_array_equal(bm.var.X, bs.Xactual)
+    assert not bm.warn_elbT0
+
+
+def test_bh_sweep_oracle_toy(bh):
+    """One block-hybrid oracle sweep on toy data: censored cells respect the ELB,
+    uncensored cells keep their data, X/Y are rebuilt from the draws."""
+    bs = toy_bh_setup(bh)
+    st = bh.bh_init_state(bs)
+    crn = bh.bh_draw_crn(np.random.default_rng(2), bs)
+    out = bh.bh_sweep(st, bs, crn)
+    S = out["shadowrate"]
+    assert np.all(S[bs.sNaN] <= bs.ELB + 1e-12)
+    Yw = bs.lin.Y[bs.elbT0:, bs.ndxS].T
+    np.testing.assert_array_equal(S[~bs.sNaN], Yw[~bs.sNaN])
+    np.testing.assert_array_equal(out["Y"][bs.elbT0:, bs.ndxS], S.T)
+    p, N = bs.lin.p, bs.lin.N
+    for l in range(1, p + 1):  # X lag columns hold the shadow rates
+        np.testing.assert_array_equal(out["X"][bs.elbT0 + l:, 1 + (l - 1) * N + bs.ndxS],
+                                      out["Y"][bs.elbT0:bs.lin.T - l, bs.ndxS])
