@@ -14,6 +14,7 @@
 #include "ccmm_cta_solve.hip"
 #include "ccmm_gram_chol.hip"
 #include "ccmm_elb.hip"
+#include "ccmm_lag.h"
 #include <cstdlib>
 
 using namespace ccmm;
@@ -137,13 +138,16 @@ enum KernelId {
   KID_ELBCOND,
   KID_ELBGIBBS,
   KID_ELBREBUILD,
+  KID_GRAMLAG,
+  KID_SOLVELAG,
   KID_COUNT
 };
 static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syrk", "k_chol",
                                               "k_cta_solve", "k_astep", "k_sv_mix", "k_sv_sample",
                                               "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
                                               "k_elb_prep", "k_elb_cond", "k_elb_gibbs",
-                                              "k_elb_rebuild"};
+                                              "k_elb_rebuild", "k_gram_chol_lag",
+                                              "k_cta_solve_lag"};
 
 struct ccmm_chains {
   ccmm_ctx* ctx = nullptr;
@@ -182,6 +186,13 @@ struct ccmm_chains {
   // timing-only ablation of k_gram_chol (results invalid): 1 = no SYRK, 2 = no Cholesky
   int gc_mode = std::getenv("CCMM_GC_MODE") ? std::atoi(std::getenv("CCMM_GC_MODE")) : 0;
   std::vector<bool> have_slot;
+  // lag-structured design (ccmm_lag.hip): D slabs parallel to the X slabs
+  bool lag_capable = false;
+  bool use_lag = std::getenv("CCMM_NO_LAG") == nullptr;
+  int lagNT = 0, ldd = 0, drows = 0;
+  std::vector<bool> slot_lag;
+  DBuf<double> Dpool;
+  DBuf<int> dColmap;
   // profiling
   bool profiling = false;
   struct Ev {
@@ -308,6 +319,7 @@ struct ccmm_chains {
     Ypool.alloc((size_t)nY * N * TP);
     HIPCHECK(hipMemsetAsync(Xpool.p, 0, Xpool.n * sizeof(double), ctx->stream));
     HIPCHECK(hipMemsetAsync(Ypool.p, 0, Ypool.n * sizeof(double), ctx->stream));
+    init_lag(nX);
     iVdiag.alloc((size_t)cf.ndata * N * KP);
     iVb.alloc((size_t)cf.ndata * N * KP);
     sPHI.alloc((size_t)cf.ndata * N * N);
@@ -354,6 +366,66 @@ struct ccmm_chains {
       o += (int64_t)cf.Ns * cf.elbTmax * (cf.elb_gibbsburn + 1);
     }
     crn_len = o;
+  }
+
+  // The lag path needs X = [1, lags 1..p of the N variables] (mcmcVAR.m:62-72), a
+  // supported tile count and D + weights resident in one CU's LDS.
+  void init_lag(int nX) {
+    slot_lag.assign(cfg.ndata, false);
+    lag_capable = false;
+    if (cfg.p < 1 || cfg.K != cfg.N * cfg.p + 1) return;
+    const int N = cfg.N;
+    lagNT = (N * cfg.p + 15) / 16;
+    ldd = (N % 2 == 0) ? N + 1 : N + 2;  // odd stride, spare zero column N
+    drows = cfg.T + cfg.p + 4;  // SYRK k-steps read up to row T + p + 2
+    const size_t lds_max = 160 * 1024;
+    if (!lag_supported_nt(lagNT) || N > 32 || 16 * lagNT + 1 > d.KP ||
+        gl_lds_bytes(lagNT, drows, ldd, d.TP) > lds_max ||
+        sl_lds_bytes(lagNT, drows, ldd, d.TP, N) > lds_max)
+      return;
+    lag_capable = true;
+    Dpool.alloc((size_t)nX * drows * ldd);
+    HIPCHECK(hipMemsetAsync(Dpool.p, 0, Dpool.n * sizeof(double), ctx->stream));
+    std::vector<int> cm(16 * lagNT);
+    for (int a = 0; a < 16 * lagNT; ++a) {
+      if (a < N * cfg.p) {
+        const int l = a / N + 1, k = a % N;
+        cm[a] = (cfg.p - l) * ldd + k;
+      } else {
+        cm[a] = N;  // spare zero column of row t
+      }
+    }
+    dColmap.alloc(cm.size());
+    HIPCHECK(hipMemcpy(dColmap.p, cm.data(), cm.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  bool lag_active() const {
+    if (!lag_capable || !use_lag) return false;
+    for (int s = 0; s < cfg.ndata; ++s)
+      if (!slot_lag[s]) return false;
+    return true;
+  }
+  LagSel lagsel() const { return LagSel{Dpool.p, xidx.p, dColmap.p, ldd, drows, cfg.p}; }
+  // D (rows x ldd) of a slot from its X (T x K) and Y (T x N): rows 0..p-1 from the
+  // lags of X's first row, rows p.. = Y.  Exact check that X is that lag design.
+  void try_upload_D(int slot, int T, const double* Y, const double* X) {
+    slot_lag[slot] = false;
+    if (!lag_capable) return;
+    const int N = cfg.N, p = cfg.p, K = cfg.K;
+    std::vector<double> D((size_t)drows * ldd, 0.0);
+    for (int l = 1; l <= p; ++l)
+      for (int k = 0; k < N; ++k) D[(size_t)(p - l) * ldd + k] = X[(size_t)(1 + (l - 1) * N + k) * T];
+    for (int t = 0; t < T; ++t)
+      for (int k = 0; k < N; ++k) D[(size_t)(t + p) * ldd + k] = Y[(size_t)k * T + t];
+    for (int t = 0; t < T; ++t) {
+      if (X[t] != 1.0) return;
+      for (int a = 0; a < K - 1; ++a) {
+        const int l = a / N + 1, k = a % N;
+        if (X[(size_t)(1 + a) * T + t] != D[(size_t)(t + p - l) * ldd + k]) return;
+      }
+    }
+    HIPCHECK(hipMemcpy(Dpool.p + (size_t)slot * drows * ldd, D.data(), D.size() * sizeof(double),
+                       hipMemcpyHostToDevice));
+    slot_lag[slot] = true;
   }
 
   void init_elb() {
@@ -463,6 +535,11 @@ struct ccmm_chains {
                               xs * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
       HIPCHECK(hipMemcpyAsync(Ypool.p + (size_t)(cfg.ndata + c) * ys, Ypool.p + (size_t)sl[c] * ys,
                               ys * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+      if (lag_capable) {
+        const size_t ds = (size_t)drows * ldd;
+        HIPCHECK(hipMemcpyAsync(Dpool.p + (size_t)(cfg.ndata + c) * ds, Dpool.p + (size_t)sl[c] * ds,
+                                ds * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+      }
     }
     HIPCHECK(hipStreamSynchronize(ctx->stream));
   }
@@ -597,6 +674,10 @@ struct ccmm_chains {
     ensure_cta();
     ChainState cs = view();
     if (!resid_valid) run_resid();
+    if (lag_active()) {
+      run_cta_lag(ra, cs);
+      return;
+    }
     const bool fused = use_fused && d.KP <= 256;
     launch(KID_WEIGHTS, [&] {
       hipLaunchKernelGGL(k_cta_weights, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0,
@@ -672,6 +753,24 @@ struct ccmm_chains {
         default:
           throw ArgError("unsupported KP");
       }
+    });
+  }
+
+  // CTA on the lag structure: sqrt weights -> Gram + Cholesky + inverse -> sequential solve
+  void run_cta_lag(const RngArgs& ra, const ChainState& cs) {
+    launch(KID_WEIGHTS, [&] {
+      hipLaunchKernelGGL(k_cta_weights, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0,
+                         ctx->stream, d, Tslot.p, cs, 1);
+    });
+    const LagSel ls = lagsel();
+    const size_t lds_g = gl_lds_bytes(lagNT, drows, ldd, d.TP);
+    const size_t lds_s = sl_lds_bytes(lagNT, drows, ldd, d.TP, d.N);
+    const int nmax = d.N <= 8 ? 8 : (d.N <= 20 ? 20 : 32);
+    launch(KID_GRAMLAG, [&] {
+      HIPCHECK(lag_launch_gram(lagNT, ctx->stream, lds_g, d, Tslot.p, ls, cs, iVdiag.p));
+    });
+    launch(KID_SOLVELAG, [&] {
+      HIPCHECK(lag_launch_solve(lagNT, nmax, ctx->stream, lds_s, d, Tslot.p, iVb.p, xsel(), ls, cs, ra));
     });
   }
 
@@ -794,7 +893,7 @@ struct ccmm_chains {
     const int nrb = e.elbTmax * Ns * (p + 1);
     launch(KID_ELBREBUILD, [&] {
       hipLaunchKernelGGL(k_elb_rebuild, dim3((nrb + 255) / 256, d.B), dim3(256), 0, ctx->stream, d, e,
-                         xsel(), cs, cfg.ndata);
+                         xsel(), cs, cfg.ndata, lag_capable ? Dpool.p : nullptr, ldd, drows);
     });
     resid_valid = false;  // X, Y changed: RESID is recomputed before the next CTA
   }
@@ -1252,6 +1351,7 @@ int ccmm_chains_set_data(ccmm_chains* ch, int slot, int T, const double* Y, cons
     HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
     ch->set_T(slot, T);
     ch->upload_X(slot, T, X);
+    ch->try_upload_D(slot, T, Y, X);
     ch->upload_TN(ch->Ypool.p + (size_t)slot * ch->d.N * ch->d.TP, 1, T, Y, 0.0);
     ch->set_slot_prior(slot, iVdiag, iVb, sPHI, h0mean, h0vcvsqrt);
     ch->have_slot[slot] = true;

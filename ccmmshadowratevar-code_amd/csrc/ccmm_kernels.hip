@@ -21,51 +21,6 @@
 
 namespace ccmm {
 
-typedef double dbl4 __attribute__((ext_vector_type(4)));
-
-struct XSel {
-  const double* pool;  // slabs of KP x TP (X stored column-major, ld = TP)
-  const int* idx;      // [B*N] slab of system (c, j)
-  const double* ypool; // slabs of N x TP
-  const int* yidx;     // [B] Y slab of chain c
-};
-
-struct RngArgs {
-  const double* crn;       // CRN base for this sweep (chain 0) or nullptr
-  int64_t crn_chain_stride;
-  uint64_t seed;
-  uint32_t sweep;
-  int64_t off[8];
-
-  __device__ inline Rng make(int c) const {
-    Rng r;
-    r.crn = crn ? crn + (int64_t)c * crn_chain_stride : nullptr;
-    r.seed = seed;
-    r.chain = (uint32_t)c;
-    r.sweep = sweep;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r.off[i] = off[i];
-    return r;
-  }
-};
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-__device__ __forceinline__ double readlane_d(double v, int lane) {
-  union {
-    double d;
-    int i[2];
-  } u;
-  u.d = v;
-  u.i[0] = __builtin_amdgcn_readlane(u.i[0], lane);
-  u.i[1] = __builtin_amdgcn_readlane(u.i[1], lane);
-  return u.d;
-}
-
 // ============================================================== residual
 // E(:,j) = Y(:,j) - X_j * PAI(:,j)   (mcmcVAR.m:233; CTAsys residual mcmcVARshadowrateBlockHybrid.m:348-351)
 __global__ void k_resid(Dims d, const int* __restrict__ Tslot, XSel xs, ChainState cs) {
