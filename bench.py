@@ -131,7 +131,12 @@ def main():
         # dominant kernel = largest accumulated device time
         dom = max(ktimes, key=lambda k: ktimes[k][0])
         per = {k: round(v[0] / max(v[1], 1), 4) for k, v in ktimes.items() if v[1]}
-        if ktimes.get("k_gram_chol", (0, 0))[1]:
+        if ktimes.get("k_gram_chol_lag", (0, 0))[1]:
+            # lag-structured Gram + Cholesky (+ inverse): N*[T*K(K+1) + K^3/3] flop per chain
+            # (the explicit inverse's K^3/3 is not counted)
+            kname = "k_gram_chol_lag"
+            flop = B * N * (T * K * (K + 1) + K ** 3 / 3)
+        elif ktimes.get("k_gram_chol", (0, 0))[1]:
             # fused weighted SYRK + Cholesky: N*[T*K(K+1) + K^3/3] flop per chain
             kname = "k_gram_chol"
             flop = B * N * (T * K * (K + 1) + K ** 3 / 3)

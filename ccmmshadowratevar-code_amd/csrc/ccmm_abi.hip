@@ -404,7 +404,8 @@ struct ccmm_chains {
       if (!slot_lag[s]) return false;
     return true;
   }
-  LagSel lagsel() const { return LagSel{Dpool.p, xidx.p, dColmap.p, ldd, drows, cfg.p}; }
+  int lag_mode = std::getenv("CCMM_LAG_MODE") ? std::atoi(std::getenv("CCMM_LAG_MODE")) : 0;
+  LagSel lagsel() const { return LagSel{Dpool.p, xidx.p, dColmap.p, ldd, drows, cfg.p, lag_mode}; }
   // D (rows x ldd) of a slot from its X (T x K) and Y (T x N): rows 0..p-1 from the
   // lags of X's first row, rows p.. = Y.  Exact check that X is that lag design.
   void try_upload_D(int slot, int T, const double* Y, const double* X) {

@@ -12,6 +12,9 @@ struct LagSel {
   const int* idx;       // [B*N] D slab of CTA system (c, j)
   const int* colmap;    // [16*NT] offset of lag column a relative to row t (doubles)
   int ldd, rows, p;     // row stride (odd), rows per slab (TP + p), lag order
+  int mode;             // timing-only ablation (CCMM_LAG_MODE, results invalid): gram 1 no SYRK,
+                        // 2 no Cholesky, 4 no inverse; solve 16 no v, 32 no X'v, 64 no Linv
+                        // matvecs, 128 no X x
 };
 
 constexpr int kGlWaves = 8;

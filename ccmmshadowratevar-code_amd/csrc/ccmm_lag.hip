@@ -40,7 +40,7 @@ struct GlArgs {
   const double* iv;    // iVdiag of (slot, j), K-space (0 = intercept), padded with 1
   const int* colmap;
   double* out;
-  int T, ldd;
+  int T, ldd, mode;
   const double* Dl;    // LDS D
   const double* swl;   // LDS sqrt weights
 };
@@ -120,7 +120,7 @@ __device__ __forceinline__ int gram_lag_body(const GlArgs& g, double* sm, int ti
 #pragma unroll
   for (int b = 0; b < NT; ++b) off[b] = g.colmap[16 * b + lr];
   double bs0 = 0.0, bs1 = 0.0, csum = 0.0;
-  const int nks = (g.T + 3) >> 2;
+  const int nks = (g.mode & 1) ? 0 : (g.T + 3) >> 2;
   for (int ks = 0; ks < nks; ++ks) {
     const int t = 4 * ks + lq;
     const double sw = g.swl[t];
@@ -190,7 +190,7 @@ __device__ __forceinline__ int gram_lag_body(const GlArgs& g, double* sm, int ti
   __syncthreads();
 
   // ------------------------------------------------------------ Cholesky of M~
-  for (int p = 0; p < NT; ++p) {
+  for (int p = 0; p < ((g.mode & 2) ? 0 : NT); ++p) {
     double* Dg = Dg0 + (p & 1) * kGlTile;
     double* Pn = Pn0 + (p & 1) * NT * kGlTile;
     double* rd = rdv + (p & 1) * 16;
@@ -206,11 +206,11 @@ __device__ __forceinline__ int gram_lag_body(const GlArgs& g, double* sm, int ti
     }
     __syncthreads();
     // (2) diagonal tile
-    if (W == 0) bad |= gl_factor_tile(Dg, rd, lane);
+    if (W == 0 && !(g.mode & 256)) bad |= gl_factor_tile(Dg, rd, lane);
     __syncthreads();
     // (3) panel: L_ip = G_ip L_pp^-T, one thread per row
     {
-      const int nrows = (NT - 1 - p) * 16;
+      const int nrows = (g.mode & 512) ? 0 : (NT - 1 - p) * 16;
       for (int e = tid; e < nrows; e += 512) {
         const int ti = p + 1 + (e >> 4), rr = e & 15;
         double* P = Pn + ti * kGlTile + rr * kGlLd;
@@ -239,7 +239,7 @@ __device__ __forceinline__ int gram_lag_body(const GlArgs& g, double* sm, int ti
         for (int r = 0; r < 4; ++r) acc[k][r] = src[(lq + 4 * r) * kGlLd + lr];
       }
     }
-    if (p + 1 < NT) {
+    if (p + 1 < NT && !(g.mode & 1024)) {
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         double pf[NT];
@@ -276,7 +276,7 @@ __device__ __forceinline__ int gram_lag_body(const GlArgs& g, double* sm, int ti
   // right-looking solve of L X = I by tile rows: at step p
   //   X_pj = Linv_pp B_pj (j < p), X_pp = Linv_pp;   B_ij -= L_ip X_pj (i > p, j <= p)
   // slot (i, j) holds L_ij until step j, then B_ij, then (after step i) X_ij.
-  for (int p = 0; p < NT; ++p) {
+  for (int p = 0; p < ((g.mode & 4) ? 0 : NT); ++p) {
     double* XD = Dg0 + (p & 1) * kGlTile;          // Linv_pp
     double* LP = Pn0 + (p & 1) * NT * kGlTile;     // L_ip, i > p (slot i)
     double* XR = Pn0 + ((p + 1) & 1) * NT * kGlTile;  // X_pj, j <= p (slot j): other panel buffer
@@ -393,6 +393,7 @@ __global__ __launch_bounds__(512, 1) void k_gram_chol_lag(Dims d, const int* __r
   GlArgs g;
   g.T = Tslot[s];
   g.ldd = ls.ldd;
+  g.mode = ls.mode;
   g.colmap = ls.colmap;
   g.iv = iVdiag + ((size_t)s * d.N + j) * d.KP;
   g.out = cs.G + (size_t)mat * d.KP * d.KP;
@@ -460,7 +461,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
     // ---- (1) v_t (E(:,j) = Y(:,j) stands for PAI(:,j) = 0, CTA.m:63)
     for (int t = tid; t < TP; t += kSlThreads) {
       double acc = 0.0;
-      if (t < T) {
+      if (t < T && !(ls.mode & 16)) {
         double e[NMAX], ih[NMAX];
 #pragma unroll
         for (int k = 0; k < NMAX; ++k) {
@@ -488,7 +489,8 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       const int th = ((T + 1) >> 1);
       const int t0 = h ? th : 0, t1 = h ? T : th;
       double p0 = 0.0, p1 = 0.0;
-      if (a < KL) {
+      if (ls.mode & 32) {
+      } else if (a < KL) {
         const double* col = Dl + cm[a];
         int t = t0;
         for (; t + 1 < t1; t += 2) {
@@ -509,7 +511,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
     }
     __syncthreads();
     // ---- (3) y = Linv rhs: tile-row partials, one (tile, row) per thread pass
-    for (int e = tid; e < NTILE * 16; e += kSlThreads) {
+    for (int e = tid; e < ((ls.mode & 64) ? 0 : NTILE * 16); e += kSlThreads) {
       const int gi = e >> 4, rr = e & 15;
       const int ti = gl_ti(NT, gi), tj = gl_tj(NT, gi);
       const double* Lr = Lo + gi * 256 + rr * 16;
@@ -538,7 +540,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       rl[kx] = xl[kx] + ((kx < K) ? rng.normal(CCMM_RNG_PAI, (uint32_t)(kx + K * j)) : 0.0);
     }
     __syncthreads();
-    for (int e = tid; e < NTILE * 16; e += kSlThreads) {
+    for (int e = tid; e < ((ls.mode & 64) ? 0 : NTILE * 16); e += kSlThreads) {
       const int gi = e >> 4, cc = e & 15;
       const int ti = gl_ti(NT, gi);
       const double* Lc = Lo + gi * 256 + cc;
@@ -574,7 +576,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
     for (int k = tid; k < KP; k += kSlThreads) pai[k] = (k < K) ? xl[k] : 0.0;
     for (int t = tid; t < TP; t += kSlThreads) {
       double o = 0.0;
-      if (t < T) {
+      if (t < T && !(ls.mode & 128)) {
         const double* rowp = Dl + t * ldd;
         double s0 = xl[0], s1 = 0.0, s2 = 0.0, s3 = 0.0;
         int a = 0;
