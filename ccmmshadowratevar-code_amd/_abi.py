@@ -247,7 +247,7 @@ class Chains:
     """Device-resident chain set (ccmm_chains_*): B chains of one model."""
 
     KERNELS = ("k_resid", "k_cta_weights", "k_syrk", "k_chol", "k_cta_solve", "k_astep",
-               "k_sv_mix", "k_sv_sample", "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
+               "k_sv_mix", "k_sv_part", "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
                "k_elb_prep", "k_elb_cond", "k_elb_gibbs", "k_elb_rebuild", "k_gram_chol_lag",
                "k_cta_solve_lag")
 

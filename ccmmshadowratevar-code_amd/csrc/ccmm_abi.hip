@@ -10,11 +10,11 @@
 #include <vector>
 
 #include "ccmm_kernels.hip"
-#include "ccmm_sv.hip"
 #include "ccmm_cta_solve.hip"
 #include "ccmm_gram_chol.hip"
 #include "ccmm_elb.hip"
 #include "ccmm_lag.h"
+#include "ccmm_svpart.h"
 #include <cstdlib>
 
 using namespace ccmm;
@@ -143,7 +143,7 @@ enum KernelId {
   KID_COUNT
 };
 static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syrk", "k_chol",
-                                              "k_cta_solve", "k_astep", "k_sv_mix", "k_sv_sample",
+                                              "k_cta_solve", "k_astep", "k_sv_mix", "k_sv_part",
                                               "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
                                               "k_elb_prep", "k_elb_cond", "k_elb_gibbs",
                                               "k_elb_rebuild", "k_gram_chol_lag",
@@ -161,7 +161,7 @@ struct ccmm_chains {
   // chain state
   DBuf<double> PAI, A, invA, sqrtht, h, h0, sqrtPHI, PHI, E, logy2, eta, svobs, svir, W;
   DBuf<int8_t> kai;
-  DBuf<double> G, rdiag, svLd, svw, Zphi;
+  DBuf<double> G, rdiag, svLd, svw, svSep, svG, Zphi;
   DBuf<double> crn;
   // storage of kept draws
   DBuf<double> sPAI, sPHI_, sInvA, sSqrtht, sShadow;
@@ -181,7 +181,6 @@ struct ccmm_chains {
   bool have_state = false;
   // kernel variants (A/B): CCMM_OLD_SOLVE=1 selects the first-generation solve kernel
   bool use_solve2 = std::getenv("CCMM_OLD_SOLVE") == nullptr;
-  bool use_svfast = std::getenv("CCMM_OLD_SV") == nullptr;
   bool use_fused = std::getenv("CCMM_OLD_CHOL") == nullptr;
   // timing-only ablation of k_gram_chol (results invalid): 1 = no SYRK, 2 = no Cholesky
   int gc_mode = std::getenv("CCMM_GC_MODE") ? std::atoi(std::getenv("CCMM_GC_MODE")) : 0;
@@ -786,9 +785,14 @@ struct ccmm_chains {
     });
   }
 
+  // SV scratch of the partitioned sampler (ccmm_svpart.hip): block factors C_t, w_t,
+  // separator records, fill vectors g_t; matrices padded to the bucket size NN
   void ensure_sv() {
-    svLd.alloc((size_t)d.B * (d.TP + 1) * d.N * d.N);
-    svw.alloc((size_t)d.B * (d.TP + 1) * d.N);
+    const size_t NN = sv_bucket(d.N);
+    svLd.alloc((size_t)d.B * (d.TP + 1) * NN * NN);
+    svw.alloc((size_t)d.B * (d.TP + 1) * NN);
+    svSep.alloc((size_t)d.B * sv_sep_len(d.N));
+    svG.alloc((size_t)d.B * (d.TP + 1) * NN);
   }
 
   void run_sv(const RngArgs& ra) {
@@ -798,24 +802,8 @@ struct ccmm_chains {
       hipLaunchKernelGGL(k_sv_mix, dim3((d.N * d.TP + 255) / 256, d.B), dim3(256), 0, ctx->stream,
                          d, Tslot.p, cs, ra);
     });
-    const size_t lds = (size_t)(4 * d.N * (d.N + 1) + d.N) * sizeof(double);
     launch(KID_SVSAMPLE, [&] {
-      switch (use_svfast ? d.N : -1) {
-#define CASE_SVN(NN)                                                                          \
-  case NN:                                                                                    \
-    hipLaunchKernelGGL(k_sv_fast<NN>, dim3(d.B), dim3(64), 0, ctx->stream, d, Tslot.p, V0inv.p, \
-                       V0invm.p, cs, ra);                                                     \
-    break;
-        CASE_SVN(4)
-        CASE_SVN(5)
-        CASE_SVN(6)
-        CASE_SVN(20)
-        CASE_SVN(21)
-#undef CASE_SVN
-        default:
-          hipLaunchKernelGGL(k_sv_sample, dim3(d.B), dim3(64), lds, ctx->stream, d, Tslot.p,
-                             V0inv.p, V0invm.p, cs, ra);
-      }
+      HIPCHECK(sv_launch_part(d.N, ctx->stream, d, Tslot.p, V0inv.p, V0invm.p, cs, ra, svSep.p, svG.p));
     });
   }
 

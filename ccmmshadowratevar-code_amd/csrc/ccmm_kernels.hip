@@ -11,7 +11,7 @@
 //                   residual update.                                    (latency bound)
 //   k_astep         A-matrix rows (mcmcVAR.m:236-254), invA, logy2 (mcmcVAR.m:259)
 //   k_sv_mix        KSC mixture indicators (elementwise)
-//   k_sv_sample     block-tridiagonal precision sampler of h_0..h_T (per chain)
+//   k_sv_part       partitioned block-tridiagonal sampler of h_0..h_T (ccmm_svpart.hip)
 //   k_phi_gen/k_phi inverse-Wishart PHI draw (mcmcVAR.m:268-274)
 //   k_store         kept-draw storage (mcmcVAR.m:289-292)
 //
@@ -535,13 +535,7 @@ __global__ void k_sv_mix(Dims d, const int* __restrict__ Tslot, ChainState cs, R
   cs.svir[o] = 1.0 / cKSCvar[s - 1];
 }
 
-// ============================================================== SV: joint draw of h_0..h_T
-// Precision sampler for y_t = h_t + e_t, h_t = h_{t-1} + sqrtPHI u_t, h_0 ~ N(m0, V0).
-// Block-tridiagonal P: P_00 = V0^-1 + Q, P_tt = 2Q + R_t^-1 (t<T), P_TT = Q + R_T^-1,
-// P_{t,t-1} = -Q, Q = PHI^-1.  Forward: M_t = Ld_{t-1}^-1 Q, Ld_t = chol(P_tt - M_t'M_t),
-// w_t = Ld_t^-1 (b_t + M_t' w_{t-1}).  Backward: x_t = Ld_t^-T (w_t + z_t + Ld_t^-1 Q x_{t+1}).
-// One wave per chain; N <= 32; matrices in LDS (row-major with stride NS = N+1).
-
+// ============================================================== small SPD helpers (PHI block)
 // Cholesky (left-looking, in place, lower triangle of row-major S) by the
 // threads of the whole workgroup (only threads < N work; all reach the barriers).
 __device__ void wg_chol_lds(double* S, int N, int NS, int tid, int* bad) {
@@ -565,161 +559,6 @@ __device__ void wg_chol_lds(double* S, int N, int NS, int tid, int* bad) {
   }
 }
 
-// lane r holds x_r; solve L v = x in place (L row-major stride ld), one wave
-__device__ __forceinline__ double wave_fwd_solve(double x, const double* L, int ld, int N, int lane) {
-  for (int k = 0; k < N; ++k) {
-    const double xk = readlane_d(x, k) / L[k * ld + k];
-    if (lane == k) x = xk;
-    else if (lane > k && lane < N) x = fma(-L[lane * ld + k], xk, x);
-  }
-  return x;
-}
-// lane r holds x_r; solve L' v = x in place
-__device__ __forceinline__ double wave_bwd_solve(double x, const double* L, int ld, int N, int lane) {
-  for (int k = N - 1; k >= 0; --k) {
-    const double xk = readlane_d(x, k) / L[k * ld + k];
-    if (lane == k) x = xk;
-    else if (lane < k) x = fma(-L[k * ld + lane], xk, x);
-  }
-  return x;
-}
-
-__global__ __launch_bounds__(64) void k_sv_sample(Dims d, const int* __restrict__ Tslot,
-                                                  const double* __restrict__ V0inv,
-                                                  const double* __restrict__ V0invm, ChainState cs,
-                                                  RngArgs ra) {
-  extern __shared__ double sm[];
-  const int N = d.N, NS = N + 1, TP = d.TP;
-  double* Q = sm;             // N x NS
-  double* Lp = Q + N * NS;    // previous Ld
-  double* M = Lp + N * NS;    // M = Lp^-1 Q
-  double* S = M + N * NS;     // Schur complement -> new Ld
-  double* xs = S + N * NS;    // N (x_{t+1} in the backward pass)
-  const int c = blockIdx.x;
-  const int s = cs.slot[c];
-  const int T = Tslot[s];
-  const int lane = threadIdx.x;
-  const Rng rng = ra.make(c);
-  int bad = 0;
-  const double* sq = cs.sqrtPHI + (size_t)c * N * N;  // column-major lower
-  const double* obs = cs.svobs + (size_t)c * N * TP;
-  const double* ir = cs.svir + (size_t)c * N * TP;
-  double* Ld = cs.svLd + (size_t)c * (TP + 1) * N * N;  // [t][r*N+col] row-major lower
-  double* W = cs.svw + (size_t)c * (TP + 1) * N;
-  // Li = sqrtPHI^-1 (lower) in M, column `lane`
-  if (lane < N) {
-    const int col = lane;
-    for (int r = 0; r < N; ++r) {
-      double v = (r == col) ? 1.0 : 0.0;
-      for (int q = col; q < r; ++q) v = fma(-sq[r + q * N], M[q * NS + col], v);
-      M[r * NS + col] = (r >= col) ? v / sq[r + r * N] : 0.0;
-    }
-  }
-  __syncthreads();
-  // Q = Li' Li = (sqrtPHI sqrtPHI')^-1
-  for (int e = lane; e < N * N; e += 64) {
-    const int r = e / N, col = e % N;
-    double v = 0.0;
-    for (int q = 0; q < N; ++q) v = fma(M[q * NS + r], M[q * NS + col], v);
-    Q[r * NS + col] = v;
-  }
-  __syncthreads();
-  // t = 0: P_00 = V0^-1 + Q, b_0 = V0^-1 m0
-  const double* Vi = V0inv + (size_t)s * N * N;
-  for (int e = lane; e < N * N; e += 64) {
-    const int r = e / N, col = e % N;
-    S[r * NS + col] = Vi[r + col * N] + Q[r * NS + col];
-  }
-  __syncthreads();
-  wg_chol_lds(S, N, NS, lane, &bad);
-  double wl = (lane < N) ? V0invm[(size_t)s * N + lane] : 0.0;  // lane r: w(r)
-  wl = wave_fwd_solve(wl, S, NS, N, lane);
-  for (int e = lane; e < N * N; e += 64) {
-    const int r = e / N, col = e % N;
-    const double v = (col <= r) ? S[r * NS + col] : 0.0;
-    Ld[e] = v;
-    Lp[r * NS + col] = v;
-  }
-  if (lane < N) W[lane] = wl;
-  __syncthreads();
-  for (int t = 1; t <= T; ++t) {
-    // M = Lp^-1 Q  (column `lane`)
-    if (lane < N) {
-      const int col = lane;
-      for (int r = 0; r < N; ++r) {
-        double v = Q[r * NS + col];
-        for (int q = 0; q < r; ++q) v = fma(-Lp[r * NS + q], M[q * NS + col], v);
-        M[r * NS + col] = v / Lp[r * NS + r];
-      }
-    }
-    // w_{t-1} to LDS for M' w
-    if (lane < N) xs[lane] = wl;
-    __syncthreads();
-    // S = P_tt - M'M (lower);  b = obs_t ir_t + M' w_{t-1}
-    const double qf = (t == T) ? 1.0 : 2.0;
-    for (int e = lane; e < N * N; e += 64) {
-      const int r = e / N, col = e % N;
-      if (col <= r) {
-        double v = qf * Q[r * NS + col];
-        if (r == col) v += ir[(size_t)r * TP + t - 1];
-        for (int q = 0; q < N; ++q) v = fma(-M[q * NS + r], M[q * NS + col], v);
-        S[r * NS + col] = v;
-      }
-    }
-    double b = 0.0;
-    if (lane < N) {
-      b = obs[(size_t)lane * TP + t - 1] * ir[(size_t)lane * TP + t - 1];
-      for (int q = 0; q < N; ++q) b = fma(M[q * NS + lane], xs[q], b);
-    }
-    __syncthreads();
-    wg_chol_lds(S, N, NS, lane, &bad);
-    wl = wave_fwd_solve(b, S, NS, N, lane);
-    double* Ldt = Ld + (size_t)t * N * N;
-    for (int e = lane; e < N * N; e += 64) {
-      const int r = e / N, col = e % N;
-      const double v = (col <= r) ? S[r * NS + col] : 0.0;
-      Ldt[e] = v;
-      Lp[r * NS + col] = v;
-    }
-    if (lane < N) W[(size_t)t * N + lane] = wl;
-    __syncthreads();
-  }
-  // backward pass
-  double* hout = cs.h + (size_t)c * N * TP;
-  double* eta = cs.eta + (size_t)c * N * TP;
-  double* sqh = cs.sqrtht + (size_t)c * N * TP;
-  __threadfence_block();
-  for (int t = T; t >= 0; --t) {
-    const double* Ldt = Ld + (size_t)t * N * N;
-    double rr = 0.0;
-    if (lane < N) rr = W[(size_t)t * N + lane] + rng.normal(CCMM_RNG_SVZ, (uint32_t)(lane + N * t));
-    if (t < T) {
-      double g = 0.0;
-      if (lane < N)
-        for (int q = 0; q < N; ++q) g = fma(Q[lane * NS + q], xs[q], g);
-      g = wave_fwd_solve(g, Ldt, N, N, lane);
-      rr += g;
-    }
-    rr = wave_bwd_solve(rr, Ldt, N, N, lane);
-    if (lane < N) {
-      if (t < T) eta[(size_t)lane * TP + t] = xs[lane] - rr;  // shock of t+1: x_{t+1} - x_t
-      if (t >= 1) {
-        hout[(size_t)lane * TP + t - 1] = rr;
-        sqh[(size_t)lane * TP + t - 1] = exp(rr * 0.5);
-      }
-    }
-    __syncthreads();
-    if (lane < N) xs[lane] = rr;
-    __syncthreads();
-  }
-  for (int q = lane; q < N * (TP - T); q += 64) {
-    const int r = q / (TP - T), t = T + q % (TP - T);
-    hout[(size_t)r * TP + t] = 0.0;
-    eta[(size_t)r * TP + t] = 0.0;
-    sqh[(size_t)r * TP + t] = 1.0;
-  }
-  if (bad && lane == 0) atomicOr(&cs.status[c], 8);
-}
 
 // ============================================================== PHI inverse-Wishart
 // mcmcVAR.m:268-274: Zdraw = randn(N, T+d_PHI); sqrtPHIpost = chol(s_PHI + eta'eta,'lower');

@@ -1,0 +1,526 @@
+// Partitioned block-tridiagonal sampler of the SV log-variances, the device form of
+// oracle/ccmm_oracle.sv_draw_partitioned (declared convention for the absent
+// em-matlabbox StochVolKSCcorrsqrt, called at mcmcVAR.m:261,
+// mcmcVARshadowrateBlockHybrid.m:379, mcmcVARhybridGibbs.m:405):
+//
+//   x = P^{-1} b + Pi' L^{-T} z,   x = [h_0; ...; h_T],   L = block Cholesky factor of
+//   the posterior precision P in the partitioned order Pi (segment interiors in time
+//   order, then the separators).
+//
+// The time-ordered factor is a Riccati recursion over all T + 1 blocks; here the
+// dependency chain is one segment (~T/16 blocks) plus the separators (<= 15).
+//
+// One workgroup of NW waves per chain:
+//   phase A  wave w eliminates segments w, w + NW, ... (time order inside a segment).
+//            Per block: C_t = chol(D~_t) in row layout (lane i = row i, readlane
+//            broadcasts, rsqrt + 2 Newton steps), w_t = C_t^{-1} b~_t, then
+//            [X1 X2] = C_t^{-1} [-Q  M_{t,left}] with one right-hand column per lane,
+//            and one uniform product pass over X in LDS gives, per lane group,
+//              lanes 0..NN-1      rows of X1'X1 -> successor's Schur complement
+//              lanes NN..2NN-1    columns of X1'X2 -> the next fill coupling
+//              lanes 2NN..3NN-1   rows of X2'X2 -> the left separator's update
+//   phase B  wave 0 eliminates the separators in time order.
+//   phase C  wave 0 back-substitutes the separators; every wave then runs its
+//            segments' fill recursion g (forward) and back substitution (backward),
+//            writing h, sqrtht = exp(h/2) and the shocks h_t - h_{t-1}.
+// Matrices are padded to NN (sv_bucket) with identity blocks; the padded
+// coordinates decouple exactly and draw 0.  The diagonal of each stored C_t holds
+// 1 / C_ii (only reciprocals are used in the substitutions).
+#include "ccmm_svpart.h"
+
+namespace ccmm {
+
+__host__ __device__ inline int sv_nseg(int T) {
+  const int P = (T + 1) / 8;
+  return P < 1 ? 1 : (P > kSvMaxSeg ? kSvMaxSeg : P);
+}
+// block index of separator i (0-based, i < P - 1)
+__host__ __device__ inline int sv_sep(int i, int T, int P) { return ((i + 1) * (T + 1)) / P - 1; }
+
+// per-wave LDS doubles: C (NN x NN+1), X (NN x 2NN+1), w (NN), fill columns, separator rows
+__host__ __device__ constexpr int sv_wave_lds(int NN) { return NN * (NN + 1) + NN * (2 * NN + 1) + NN + 2 * NN * NN; }
+
+template <int NN>
+struct SvRec {
+  static constexpr int DR = 0;              // D(s) - X1'X1 of the left segment's last block
+  static constexpr int DL = NN * NN;        // -sum X2'X2 of the right segment
+  static constexpr int M = 2 * NN * NN;     // M[m*NN + r] = M_{s, s_next}[r][m]
+  static constexpr int BR = 3 * NN * NN;    // b(s) - X1'w of the left segment's last block
+  static constexpr int BL = 3 * NN * NN + NN;  // -sum X2'w of the right segment
+  static constexpr int LEN = 3 * NN * NN + 2 * NN;
+};
+
+// 1/sqrt(d) to full precision: hardware estimate + two Newton steps
+__device__ __forceinline__ double sv_rsqrt(double d) {
+  double r = __builtin_amdgcn_rsq(d);
+  const double hd = 0.5 * d;
+  r = r * fma(-hd * r, r, 1.5);
+  r = r * fma(-hd * r, r, 1.5);
+  return r;
+}
+
+// LDS hand-off between the lanes of one wave: its LDS operations complete in order,
+// so only the compiler has to be kept from moving accesses across this point
+__device__ __forceinline__ void sv_wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Cholesky in row layout: lane i < NN holds row i of the SPD matrix in s[0..i];
+// on return row i of the factor (entries k > i are garbage) and rps = 1/diag (uniform)
+template <int NN>
+__device__ __forceinline__ void sv_chol_rows(double (&s)[NN], double (&rps)[NN], int lane, int& bad) {
+#pragma unroll
+  for (int q = 0; q < NN; ++q) {
+    double dq = readlane_d(s[q], q);
+    if (!(dq > 0.0)) {
+      bad = 1;
+      dq = 1.0;
+    }
+    const double rp = sv_rsqrt(dq);
+    rps[q] = rp;
+    s[q] = (lane == q) ? dq * rp : s[q] * rp;
+#pragma unroll
+    for (int k = q + 1; k < NN; ++k) s[k] = fma(-s[q], readlane_d(s[q], k), s[k]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// L y = b, lane i holds b_i and row i of L (off-diagonal part)
+template <int NN>
+__device__ __forceinline__ double sv_fwd(double b, const double (&s)[NN], const double (&rps)[NN], int lane) {
+#pragma unroll
+  for (int k = 0; k < NN; ++k) {
+    const double yk = readlane_d(b, k) * rps[k];
+    b = (lane == k) ? yk : ((lane > k) ? fma(-s[k], yk, b) : b);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return b;
+}
+
+// L' x = r, lane i holds r_i and column i of L (lc[k] = L[k][i], k > i)
+template <int NN>
+__device__ __forceinline__ double sv_bwd(double r, const double (&lc)[NN], const double (&rps)[NN], int lane) {
+#pragma unroll
+  for (int k = NN - 1; k >= 0; --k) {
+    const double xk = readlane_d(r, k) * rps[k];
+    r = (lane == k) ? xk : ((lane < k) ? fma(-lc[k], xk, r) : r);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return r;
+}
+
+template <int NN, int NW>
+__global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restrict__ Tslot,
+                                                      const double* __restrict__ V0inv,
+                                                      const double* __restrict__ V0invm, ChainState cs,
+                                                      RngArgs ra, double* __restrict__ sepbuf,
+                                                      double* __restrict__ gbuf) {
+  constexpr int CLD = NN + 1, XLD = 2 * NN + 1, NN2 = NN * NN;
+  constexpr bool G3 = 3 * NN <= 64;
+  using R = SvRec<NN>;
+  extern __shared__ double sm[];
+  double* Ql = sm;                                   // NN x NN, Q = PHI^-1 (identity padding)
+  double* xsep = Ql + NN2;                           // kSvMaxSeg x NN separator solutions
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double* myC = xsep + kSvMaxSeg * NN + wave * sv_wave_lds(NN);
+  double* myX = myC + NN * CLD;
+  double* myw = myX + NN * XLD;
+  double* myF = myw + NN;
+  double* myD = myF + NN2;
+  const int n = d.N, TP = d.TP;
+  const int c = blockIdx.x, s = cs.slot[c], T = Tslot[s];
+  const int ln = lane < NN ? lane : 0;
+  const bool real = lane < n;
+  const Rng rng = ra.make(c);
+  const double* sq = cs.sqrtPHI + (size_t)c * n * n;  // column-major lower n x n
+  const double* obs = cs.svobs + (size_t)c * n * TP;
+  const double* irv = cs.svir + (size_t)c * n * TP;
+  double* Cg = cs.svLd + (size_t)c * (TP + 1) * NN2;  // [t][i*NN + k]
+  double* Wg = cs.svw + (size_t)c * (TP + 1) * NN;
+  double* rec = sepbuf + (size_t)c * (kSvMaxSeg - 1) * R::LEN;
+  double* Gb = gbuf + (size_t)c * (TP + 1) * NN;
+  double* hout = cs.h + (size_t)c * n * TP;
+  double* eta = cs.eta + (size_t)c * n * TP;
+  double* sqh = cs.sqrtht + (size_t)c * n * TP;
+  const double* V0 = V0inv + (size_t)s * n * n;
+  const double* V0m = V0invm + (size_t)s * n;
+  int bad = 0;
+
+  // ---------------------------------------------------------------- Q = (sqrtPHI sqrtPHI')^-1
+  if (wave == 0) {
+    double li[NN];  // column `lane` of sqrtPHI^-1
+#pragma unroll
+    for (int r = 0; r < NN; ++r) {
+      double v = (r == lane) ? 1.0 : 0.0;
+      if (r < n && lane < n) {
+#pragma unroll
+        for (int q = 0; q < r; ++q) v = fma(-sq[r + q * n], li[q], v);
+        v = (r >= lane) ? v / sq[r + r * n] : 0.0;
+      }
+      li[r] = v;
+    }
+    if (lane < NN) {
+#pragma unroll
+      for (int r = 0; r < NN; ++r) myX[r * XLD + lane] = li[r];
+    }
+    sv_wave_sync();
+    if (lane < NN) {
+#pragma unroll
+      for (int r = 0; r < NN; ++r) {
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < NN; ++q) v = fma(myX[q * XLD + r], li[q], v);
+        Ql[r * NN + lane] = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  const int P = sv_nseg(T);
+  // original diagonal block D0_t, row ln, entry m (irt = diag(R_t^-1) entry of row ln)
+  auto d0 = [&](int t, int m, double irt) __attribute__((always_inline)) -> double {
+    if (t == 0) {
+      const double v0 = (lane < n && m < n) ? V0[ln + m * n] : (m == ln ? 1.0 : 0.0);
+      return v0 + Ql[ln * NN + m];
+    }
+    return ((t == T) ? 1.0 : 2.0) * Ql[ln * NN + m] + ((m == ln) ? irt : 0.0);
+  };
+  auto ir_at = [&](int t) __attribute__((always_inline)) -> double { return (t >= 1 && real) ? irv[(size_t)ln * TP + t - 1] : 1.0; };
+  auto ob_at = [&](int t) __attribute__((always_inline)) -> double { return (t >= 1 && real) ? obs[(size_t)ln * TP + t - 1] : 0.0; };
+  auto b0 = [&](int t, double irt, double obt) __attribute__((always_inline)) -> double {
+    if (t == 0) return real ? V0m[ln] : 0.0;
+    return real ? obt * irt : 0.0;
+  };
+  auto zdraw = [&](int t) __attribute__((always_inline)) -> double {
+    return real ? rng.normal(CCMM_RNG_SVZ, (uint32_t)(ln + n * t)) : 0.0;
+  };
+  // C_t row (lane < NN) -> LDS and HBM, diagonal as its reciprocal
+  auto store_factor = [&](int t, const double (&sr)[NN], const double (&rps)[NN], double w)
+                          __attribute__((always_inline)) {
+    double* Ct = Cg + (size_t)t * NN2;
+    if (lane < NN) {
+#pragma unroll
+      for (int m = 0; m < NN; ++m) {
+        const double v = (m < lane) ? sr[m] : ((m == lane) ? rps[m] : 0.0);
+        myC[lane * CLD + m] = v;
+        Ct[lane * NN + m] = v;
+      }
+      myw[lane] = w;
+      Wg[(size_t)t * NN + lane] = w;
+    }
+  };
+
+  // ---------------------------------------------------------------- phase A: segments
+  // per-wave LDS: myF[k*NN + r] fill column r of M_{t,left} (right-hand side of lane NN+r),
+  // myD[r*NN + m] the left separator's accumulated -sum X2'X2 (row r)
+  for (int q = wave; q < P; q += NW) {
+    const int first = (q == 0) ? 0 : sv_sep(q - 1, T, P) + 1;
+    const int last = (q == P - 1) ? T : sv_sep(q, T, P) - 1;
+    const bool hasL = q > 0, hasR = q < P - 1;
+    const int rB = lane - NN, rD = G3 ? lane - 2 * NN : lane - NN;  // group B column, group C/D row
+    const bool inB = rB >= 0 && rB < NN, inD = rD >= 0 && rD < NN;
+    double sr[NN];
+    double dbl = 0.0, bcur;
+    {
+      const double irt = ir_at(first), obt = ob_at(first);
+#pragma unroll
+      for (int m = 0; m < NN; ++m) sr[m] = d0(first, m, irt);
+      if (inB) {
+#pragma unroll
+        for (int k = 0; k < NN; ++k) myF[k * NN + rB] = -Ql[k * NN + rB];  // M_{first,left} = -Q
+      }
+      if (inD) {
+#pragma unroll
+        for (int m = 0; m < NN; ++m) myD[rD * NN + m] = 0.0;
+      }
+      bcur = b0(first, irt, obt);
+    }
+    sv_wave_sync();
+    for (int t = first; t <= last; ++t) {
+      const bool hasN = t < T;
+      const double irn = hasN ? ir_at(t + 1) : 1.0, obn = hasN ? ob_at(t + 1) : 0.0;
+      {
+        double rps[NN];
+        sv_chol_rows<NN>(sr, rps, lane, bad);
+        const double w = sv_fwd<NN>(bcur, sr, rps, lane);
+        store_factor(t, sr, rps, w);
+      }
+      sv_wave_sync();
+      // [X1 X2] = C^-1 [-Q  M_{t,left}], one right-hand column per lane (the diagonal
+      // of myC holds 1 / C_kk)
+      {
+        const int rcol = (lane < NN) ? lane : (inB ? rB : 0);
+        const double* rhs = (lane < NN) ? Ql : myF;
+        const double sgn = (lane < NN) ? -1.0 : 1.0;
+        double x[NN];
+#pragma unroll
+        for (int k = 0; k < NN; ++k) {
+          double v = sgn * rhs[k * NN + rcol];
+#pragma unroll
+          for (int m = 0; m < k; ++m) v = fma(-myC[k * CLD + m], x[m], v);
+          x[k] = v * myC[k * CLD + k];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (lane < 2 * NN) {
+#pragma unroll
+          for (int k = 0; k < NN; ++k) myX[k * XLD + lane] = x[k];
+        }
+      }
+      sv_wave_sync();
+      // one uniform product pass: pr[m] = sum_k a[k] X[k][m + boff], a = own column
+      // (lanes < 2NN) or the X2 column of lane - NN (lanes 2NN..3NN-1)
+      const int boff = (lane < 2 * NN) ? 0 : NN;
+      const int acol = (lane < 2 * NN) ? lane : ((lane < 3 * NN) ? lane - NN : NN);
+      double pr[NN];
+#pragma unroll
+      for (int m = 0; m < NN; ++m) pr[m] = 0.0;
+      double wd = 0.0;
+#pragma unroll 1
+      for (int k = 0; k < NN; ++k) {
+        const double* xr = myX + k * XLD;
+        const double ak = xr[acol];
+#pragma unroll
+        for (int m = 0; m < NN; ++m) pr[m] = fma(ak, xr[boff + m], pr[m]);
+        wd = fma(ak, myw[k], wd);
+      }
+      // epilogue, uniform over the lanes (each lane group keeps only its own values):
+      //   lanes 0..NN-1:    successor's D~ row / b~ entry (or the right separator's record)
+      //   lanes NN..2NN-1:  next fill column M_{t+1,left}(:, r) = -(X2'X1)(r, :)'
+      //   lanes 2NN..3NN-1: left separator's -sum X2'X2 row
+      {
+        const bool toR = hasR && t == last;
+        double* rR = rec + (size_t)q * R::LEN;
+        double* rL = rec + (size_t)(q > 0 ? q - 1 : 0) * R::LEN;
+        const double bn = b0(t + 1, irn, obn) - wd;
+#pragma unroll
+        for (int m = 0; m < NN; ++m) {
+          const double dn = d0(t + 1, m, irn) - pr[m];
+          sr[m] = dn;
+          if (toR && lane < NN) rR[R::DR + lane * NN + m] = dn;
+          if (hasL && inB) {
+            if (toR) rL[R::M + m * NN + rB] = -pr[m];
+            myF[m * NN + rB] = -pr[m];
+          }
+          if (G3 && hasL && inD) myD[rD * NN + m] -= pr[m];
+        }
+        bcur = bn;
+        if (toR && lane < NN) rR[R::BR + lane] = bn;
+        if (hasL && inB) dbl -= wd;
+      }
+      if constexpr (!G3) {  // 3 NN > 64: X2'X2 rows on lanes NN..2NN-1 in a second pass
+        if (hasL) {
+#pragma unroll
+          for (int m = 0; m < NN; ++m) pr[m] = 0.0;
+#pragma unroll 1
+          for (int k = 0; k < NN; ++k) {
+            const double* xr = myX + k * XLD;
+            const double ak = xr[acol];
+#pragma unroll
+            for (int m = 0; m < NN; ++m) pr[m] = fma(ak, xr[NN + m], pr[m]);
+          }
+          if (inD) {
+#pragma unroll
+            for (int m = 0; m < NN; ++m) myD[rD * NN + m] -= pr[m];
+          }
+        }
+      }
+      sv_wave_sync();
+    }
+    if (hasL) {
+      double* r = rec + (size_t)(q - 1) * R::LEN;
+      if (inB) r[R::BL + rB] = dbl;
+      if (inD) {
+#pragma unroll
+        for (int m = 0; m < NN; ++m) r[R::DL + rD * NN + m] = myD[rD * NN + m];
+      }
+    }
+    sv_wave_sync();
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- phase B: separators
+  if (wave == 0 && P > 1) {
+    double cg[NN], sr[NN];
+#pragma unroll
+    for (int m = 0; m < NN; ++m) cg[m] = 0.0;
+    double cb = 0.0;
+    for (int i = 0; i < P - 1; ++i) {
+      const int sb = sv_sep(i, T, P);
+      const double* r = rec + (size_t)i * R::LEN;
+#pragma unroll
+      for (int m = 0; m < NN; ++m)
+        sr[m] = (lane < NN) ? r[R::DR + ln * NN + m] + r[R::DL + ln * NN + m] - cg[m] : 0.0;
+      const double bcur = (lane < NN) ? r[R::BR + ln] + r[R::BL + ln] - cb : 0.0;
+      {
+        double rps[NN];
+        sv_chol_rows<NN>(sr, rps, lane, bad);
+        const double w = sv_fwd<NN>(bcur, sr, rps, lane);
+        store_factor(sb, sr, rps, w);
+      }
+      sv_wave_sync();
+      if (i + 1 < P - 1) {
+        // X1 = C^-1 M_{sep i, sep i+1}: column `lane` of M is r[M + lane*NN + k]
+        double x[NN];
+#pragma unroll
+        for (int k = 0; k < NN; ++k) {
+          double v = (lane < NN) ? r[R::M + ln * NN + k] : 0.0;
+#pragma unroll
+          for (int m = 0; m < k; ++m) v = fma(-myC[k * CLD + m], x[m], v);
+          x[k] = v * myC[k * CLD + k];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (lane < NN) {
+#pragma unroll
+          for (int k = 0; k < NN; ++k) myX[k * XLD + lane] = x[k];
+        }
+        sv_wave_sync();
+#pragma unroll
+        for (int m = 0; m < NN; ++m) cg[m] = 0.0;
+        cb = 0.0;
+#pragma unroll 1
+        for (int k = 0; k < NN; ++k) {
+          const double* xr = myX + k * XLD;
+          const double ak = xr[ln];
+#pragma unroll
+          for (int m = 0; m < NN; ++m) cg[m] = fma(ak, xr[m], cg[m]);
+          cb = fma(ak, myw[k], cb);
+        }
+      }
+      sv_wave_sync();
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- phase C: back substitution
+  double qrow[NN];
+#pragma unroll
+  for (int m = 0; m < NN; ++m) qrow[m] = Ql[ln * NN + m];
+  // C_t -> LDS (whole wave), then row / column / reciprocal diagonal per lane
+  auto load_factor = [&](int t, double (&lr)[NN], double (&lc)[NN], double (&rps)[NN])
+                         __attribute__((always_inline)) {
+    const double* Ct = Cg + (size_t)t * NN2;
+    for (int e = lane; e < NN2; e += 64) myC[(e / NN) * CLD + (e % NN)] = Ct[e];
+    sv_wave_sync();
+#pragma unroll
+    for (int m = 0; m < NN; ++m) {
+      lr[m] = myC[ln * CLD + m];
+      lc[m] = myC[m * CLD + ln];
+      rps[m] = myC[m * CLD + m];
+    }
+    sv_wave_sync();
+  };
+  if (wave == 0 && P > 1) {
+    for (int i = P - 2; i >= 0; --i) {
+      const int sb = sv_sep(i, T, P);
+      double lr[NN], lc[NN], rps[NN];
+      load_factor(sb, lr, lc, rps);
+      double rv = (lane < NN) ? Wg[(size_t)sb * NN + ln] + zdraw(sb) : 0.0;
+      if (i + 1 < P - 1) {
+        const double* Mr = rec + (size_t)i * R::LEN + R::M;  // row ln of M: Mr[m*NN + ln]
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < NN; ++m) acc = fma(Mr[m * NN + ln], xsep[(i + 1) * NN + m], acc);
+        rv -= sv_fwd<NN>(acc, lr, rps, lane);
+      }
+      const double x = sv_bwd<NN>(rv, lc, rps, lane);
+      if (lane < NN) xsep[i * NN + lane] = x;
+      if (real) {
+        hout[(size_t)ln * TP + sb - 1] = x;
+        sqh[(size_t)ln * TP + sb - 1] = exp(0.5 * x);
+      }
+      sv_wave_sync();
+    }
+  }
+  __syncthreads();
+  for (int q = wave; q < P; q += NW) {
+    const int first = (q == 0) ? 0 : sv_sep(q - 1, T, P) + 1;
+    const int last = (q == P - 1) ? T : sv_sep(q, T, P) - 1;
+    const bool hasL = q > 0, hasR = q < P - 1;
+    if (hasL) {  // g_first = -Q x_left, g_{t+1} = Q C_t^-T C_t^-1 g_t
+      double g = 0.0;
+#pragma unroll
+      for (int m = 0; m < NN; ++m) g = fma(-qrow[m], xsep[(q - 1) * NN + m], g);
+      for (int t = first; t <= last; ++t) {
+        if (lane < NN) Gb[(size_t)t * NN + lane] = g;
+        if (t < last) {
+          double lr[NN], lc[NN], rps[NN];
+          load_factor(t, lr, lc, rps);
+          double v = sv_fwd<NN>(g, lr, rps, lane);
+          v = sv_bwd<NN>(v, lc, rps, lane);
+          if (lane < NN) myw[lane] = v;
+          sv_wave_sync();
+          g = 0.0;
+#pragma unroll
+          for (int m = 0; m < NN; ++m) g = fma(qrow[m], myw[m], g);
+          sv_wave_sync();
+        }
+      }
+    }
+    // successor of `last`: the right separator (x known) or nothing (t == T)
+    if (hasR && lane < NN) myw[lane] = xsep[q * NN + lane];
+    sv_wave_sync();
+    for (int t = last; t >= first; --t) {
+      double lr[NN], lc[NN], rps[NN];
+      load_factor(t, lr, lc, rps);
+      double acc = 0.0, xn = 0.0;
+      if (t < T) {
+#pragma unroll
+        for (int m = 0; m < NN; ++m) acc = fma(-qrow[m], myw[m], acc);
+        xn = myw[ln];
+      }
+      if (hasL && lane < NN) acc += Gb[(size_t)t * NN + ln];
+      double rv = (lane < NN) ? Wg[(size_t)t * NN + ln] + zdraw(t) : 0.0;
+      rv -= sv_fwd<NN>(acc, lr, rps, lane);
+      const double x = sv_bwd<NN>(rv, lc, rps, lane);
+      if (real) {
+        if (t >= 1) {
+          hout[(size_t)ln * TP + t - 1] = x;
+          sqh[(size_t)ln * TP + t - 1] = exp(0.5 * x);
+        }
+        if (t < T) eta[(size_t)ln * TP + t] = xn - x;          // shock of block t + 1
+        if (t == first && hasL) eta[(size_t)ln * TP + t - 1] = x - xsep[(q - 1) * NN + ln];
+      }
+      sv_wave_sync();
+      if (lane < NN) myw[lane] = x;
+      sv_wave_sync();
+    }
+  }
+  // padding beyond T
+  for (int e = tid; e < n * (TP - T); e += 64 * NW) {
+    const int r = e / (TP - T), t = T + e % (TP - T);
+    hout[(size_t)r * TP + t] = 0.0;
+    eta[(size_t)r * TP + t] = 0.0;
+    sqh[(size_t)r * TP + t] = 1.0;
+  }
+  if (bad && lane == 0) atomicOr(&cs.status[c], 8);
+}
+
+template <int NN, int NW>
+static hipError_t sv_launch_one(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
+                                const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf) {
+  constexpr int CLD = NN + 1, XLD = 2 * NN + 1;
+  const size_t lds = (size_t)(NN * NN + kSvMaxSeg * NN + NW * sv_wave_lds(NN)) * sizeof(double);
+  hipError_t e = hipFuncSetAttribute((const void*)k_sv_part<NN, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_sv_part<NN, NW>), dim3(d.B), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm, cs, ra,
+                     sep, gbuf);
+  return hipGetLastError();
+}
+
+hipError_t sv_launch_part(int N, hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
+                          const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf) {
+  switch (sv_bucket(N)) {
+    case 4: return sv_launch_one<4, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
+    case 8: return sv_launch_one<8, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
+    case 12: return sv_launch_one<12, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
+    case 16: return sv_launch_one<16, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
+    case 20: return sv_launch_one<20, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
+    case 24: return sv_launch_one<24, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
+    case 28: return sv_launch_one<28, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
+    default: return sv_launch_one<32, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
+  }
+}
+
+}  // namespace ccmm

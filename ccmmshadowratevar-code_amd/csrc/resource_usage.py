@@ -5,10 +5,10 @@ import subprocess
 from pathlib import Path
 
 here = Path(__file__).resolve().parent
-out = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
-                      "-shared", "ccmm_abi.hip", "-o", "/tmp/_ccmm_ru.so",
-                      "-Rpass-analysis=kernel-resource-usage"], cwd=here, capture_output=True,
-                     text=True).stderr
+out = "".join(subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
+                              "-c", tu, "-o", "/tmp/_ccmm_ru.o", "-Rpass-analysis=kernel-resource-usage"],
+                             cwd=here, capture_output=True, text=True).stderr
+              for tu in ("ccmm_abi.hip", "ccmm_lag.hip", "ccmm_svpart.hip"))
 rows, cur = [], None
 pats = {"vgpr": r"VGPRs: (\d+)", "agpr": r"AGPRs: (\d+)", "scratch": r"ScratchSize \[bytes/lane\]: (\d+)",
         "lds": r"LDS Size \[bytes/block\]: (\d+)", "occ": r"Occupancy \[waves/SIMD\]: (\d+)"}

@@ -335,38 +335,164 @@ def ksc_indicators(y, hprev, u):
     return (1 + np.sum(u[..., None] > cdf, axis=-1)).astype(np.int8)
 
 
+def sv_separators(T):
+    """Separator blocks of the partitioned SV sampler over the T+1 blocks h_0..h_T.
+
+    P = clamp((T+1) // 8, 1, 16) segments; separator k (k = 1..P-1) is block
+    floor(k (T+1) / P) - 1.  Segment k's interior is the open range between
+    separators k-1 and k (separator 0 = -1, separator P = T+1)."""
+    nb = T + 1
+    P = max(1, min(16, nb // 8))
+    return [(k * nb) // P - 1 for k in range(1, P)]
+
+
+def sv_precision(obs, ir, sqrtPHI, h0mean, h0vcvsqrt):
+    """Blocks of the posterior precision / linear term of x = [h_0; ...; h_T].
+
+    Model: y_t = h_t + mean_{s_t} + eps_t, eps_t ~ N(0, diag(var_{s_t})),
+    h_t = h_{t-1} + sqrtPHI e_t, h_0 ~ N(h0mean, V0), V0 = h0vcvsqrt h0vcvsqrt'.
+    Returns D (T+1 x N x N diagonal blocks), b (T+1 x N), Q = PHI^{-1}; the
+    off-diagonal block between t and t+1 is -Q."""
+    N, T = obs.shape
+    Q = np.linalg.inv(sqrtPHI @ sqrtPHI.T)
+    V0inv = np.linalg.inv(h0vcvsqrt @ h0vcvsqrt.T)
+    D = np.empty((T + 1, N, N))
+    b = np.empty((T + 1, N))
+    D[0] = V0inv + Q
+    b[0] = V0inv @ h0mean
+    for t in range(1, T + 1):
+        D[t] = (Q if t == T else 2 * Q) + np.diag(ir[:, t - 1])
+        b[t] = obs[:, t - 1] * ir[:, t - 1]
+    return D, b, Q
+
+
+def sv_draw_sequential(D, b, Q, z):
+    """x = P^{-1} b + L^{-T} z with L the time-ordered block Cholesky factor
+    (the round-1 declared convention; kept as a cross-check of the moments)."""
+    T1, N = b.shape
+    Ld = np.empty_like(D)
+    w = np.empty_like(b)
+    Ld[0] = np.linalg.cholesky(D[0])
+    w[0] = solve_triangular(Ld[0], b[0], lower=True)
+    Lo = np.empty_like(D)
+    for t in range(1, T1):
+        Lo[t] = -solve_triangular(Ld[t - 1], Q, lower=True).T
+        Ld[t] = np.linalg.cholesky(D[t] - Lo[t] @ Lo[t].T)
+        w[t] = solve_triangular(Ld[t], b[t] - Lo[t] @ w[t - 1], lower=True)
+    x = np.empty_like(b)
+    x[T1 - 1] = solve_triangular(Ld[T1 - 1].T, w[T1 - 1] + z[:, T1 - 1], lower=False)
+    for t in range(T1 - 2, -1, -1):
+        x[t] = solve_triangular(Ld[t].T, w[t] + z[:, t] - Lo[t + 1].T @ x[t + 1], lower=False)
+    return x
+
+
+def sv_draw_partitioned(D, b, Q, z, seps=None):
+    """x = P^{-1} b + Pi' L^{-T} z, L the block Cholesky factor of the precision in
+    the partitioned order Pi: segment interiors (each in time order), then the
+    separators (time order).  z column t belongs to block t.
+
+    Eliminating an interior block t (factor C_t = chol(D~_t), w_t = C_t^{-1} b~_t)
+    touches at most two remaining blocks: its successor nxt (coupling M_{t,nxt} = -Q)
+    and the segment's left separator s (fill coupling M_{t,s}):
+        X1 = C_t^{-1} M_{t,nxt},  X2 = C_t^{-1} M_{t,s}
+        D~_nxt -= X1'X1, b~_nxt -= X1'w;   D~_s -= X2'X2, b~_s -= X2'w
+        M_{s,nxt} = -X2'X1
+    The separators then form a block-tridiagonal system, eliminated in time order.
+    Back substitution: x_t = C_t^{-T}(w_t + z_t - C_t^{-1} sum_nbr M_{t,nbr} x_nbr),
+    where inside a segment g_t = M_{t,s} x_s obeys g_first = -Q x_s,
+    g_{t+1} = Q C_t^{-T} C_t^{-1} g_t."""
+    T1, N = b.shape
+    if seps is None:
+        seps = sv_separators(T1 - 1)
+    bounds = [-1] + list(seps) + [T1]
+    C = np.empty_like(D)
+    w = np.empty_like(b)
+    Dsep = {s: D[s].copy() for s in seps}
+    bsep = {s: b[s].copy() for s in seps}
+    Msep = {}
+    negQ = -Q
+    for k in range(1, len(bounds)):
+        left = bounds[k - 1] if k > 1 else None
+        first = bounds[k - 1] + 1
+        last = bounds[k] - 1
+        Dc, bc = D[first].copy(), b[first].copy()
+        Mfill = negQ if left is not None else None  # M_{t,left}
+        for t in range(first, last + 1):
+            Ct = np.linalg.cholesky(Dc)
+            wt = solve_triangular(Ct, bc, lower=True)
+            C[t], w[t] = Ct, wt
+            nxt = t + 1 if t + 1 < T1 else None
+            X1 = solve_triangular(Ct, negQ, lower=True) if nxt is not None else None
+            if nxt is not None:
+                if t < last:
+                    Dc = D[nxt] - X1.T @ X1
+                    bc = b[nxt] - X1.T @ wt
+                else:
+                    Dsep[nxt] -= X1.T @ X1
+                    bsep[nxt] -= X1.T @ wt
+            if left is not None:
+                X2 = solve_triangular(Ct, Mfill, lower=True)
+                Dsep[left] -= X2.T @ X2
+                bsep[left] -= X2.T @ wt
+                if nxt is not None:
+                    Mln = -X2.T @ X1  # M_{left, nxt}
+                    if t < last:
+                        Mfill = Mln.T
+                    else:
+                        Msep[left] = Mln  # M_{left, right}
+    for i, s in enumerate(seps):
+        Ct = np.linalg.cholesky(Dsep[s])
+        wt = solve_triangular(Ct, bsep[s], lower=True)
+        C[s], w[s] = Ct, wt
+        if i + 1 < len(seps):
+            X1 = solve_triangular(Ct, Msep[s], lower=True)
+            s2 = seps[i + 1]
+            Dsep[s2] -= X1.T @ X1
+            bsep[s2] -= X1.T @ wt
+    x = np.empty_like(b)
+    for i in range(len(seps) - 1, -1, -1):
+        s = seps[i]
+        r = w[s] + z[:, s]
+        if i + 1 < len(seps):
+            r = r - solve_triangular(C[s], Msep[s] @ x[seps[i + 1]], lower=True)
+        x[s] = solve_triangular(C[s].T, r, lower=False)
+    for k in range(1, len(bounds)):
+        left = bounds[k - 1] if k > 1 else None
+        first, last = bounds[k - 1] + 1, bounds[k] - 1
+        g = {}
+        if left is not None:
+            gt = negQ @ x[left]
+            for t in range(first, last + 1):
+                g[t] = gt
+                gt = Q @ solve_triangular(C[t].T, solve_triangular(C[t], gt, lower=True), lower=False)
+        for t in range(last, first - 1, -1):
+            acc = np.zeros(N)
+            if t + 1 < T1:
+                acc = acc + negQ @ x[t + 1]
+            if left is not None:
+                acc = acc + g[t]
+            x[t] = solve_triangular(C[t].T, w[t] + z[:, t] - solve_triangular(C[t], acc, lower=True),
+                                    lower=False)
+    return x
+
+
 def sv_ksc_corrsqrt(y, hprev, sqrtPHI, h0mean, h0vcvsqrt, u, z):
     """Joint draw of log variances with correlated random-walk shocks.
 
     y, hprev: N x T (logy2', Vol_states').  Model: y_t = h_t + mean_{s_t} + eps_t,
     eps_t ~ N(0, diag(var_{s_t})); h_t = h_{t-1} + sqrtPHI e_t; h_0 ~ N(h0mean, V0),
     V0 = h0vcvsqrt h0vcvsqrt'.  Posterior precision of x = [h_0; ...; h_T] is
-    block tridiagonal; x = P^{-1} b + L^{-T} z with P = L L' (block Cholesky).
-    z is N x (T+1), column t for block t.  Returns h (N x T), h0 (N),
-    shocks (N x T, h_t - h_{t-1}), indicators (N x T int8).
+    block tridiagonal; x = P^{-1} b + Pi' L^{-T} z with L the block Cholesky factor
+    in the partitioned order of ``sv_draw_partitioned`` (declared convention: the
+    reference's sampler lives in the absent em-matlabbox).  z is N x (T+1), column t
+    for block t.  Returns h (N x T), h0 (N), shocks (N x T, h_t - h_{t-1}),
+    indicators (N x T int8).
     """
-    N, T = y.shape
     kai = ksc_indicators(y, hprev, u)
     obs = y - KSC_MEAN[kai - 1]
     ir = 1.0 / KSC_VAR[kai - 1]
-    Q = np.linalg.inv(sqrtPHI @ sqrtPHI.T)
-    V0inv = np.linalg.inv(h0vcvsqrt @ h0vcvsqrt.T)
-    # block Cholesky of P
-    Ld = np.empty((T + 1, N, N))
-    Lo = np.empty((T + 1, N, N))  # Lo[t] = L_{t,t-1}
-    w = np.empty((T + 1, N))
-    Ld[0] = np.linalg.cholesky(V0inv + Q)
-    w[0] = solve_triangular(Ld[0], V0inv @ h0mean, lower=True)
-    for t in range(1, T + 1):
-        Ptt = (Q if t == T else 2 * Q) + np.diag(ir[:, t - 1])
-        # L_{t,t-1} = -Q L_{t-1}^{-T}
-        Lo[t] = -solve_triangular(Ld[t - 1], Q, lower=True).T
-        Ld[t] = np.linalg.cholesky(Ptt - Lo[t] @ Lo[t].T)
-        w[t] = solve_triangular(Ld[t], obs[:, t - 1] * ir[:, t - 1] - Lo[t] @ w[t - 1], lower=True)
-    x = np.empty((T + 1, N))
-    x[T] = solve_triangular(Ld[T].T, w[T] + z[:, T], lower=False)
-    for t in range(T - 1, -1, -1):
-        x[t] = solve_triangular(Ld[t].T, w[t] + z[:, t] - Lo[t + 1].T @ x[t + 1], lower=False)
+    D, b, Q = sv_precision(obs, ir, sqrtPHI, h0mean, h0vcvsqrt)
+    x = sv_draw_partitioned(D, b, Q, z)
     h = x[1:].T.copy()
     shocks = (x[1:] - x[:-1]).T.copy()
     return h, x[0].copy(), shocks, kai
