@@ -116,6 +116,8 @@ struct ChainState {
 
 // ---------------------------------------------------------------- shared device helpers
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+// pointer into LDS (address space 3): loads/stores through it are ds_* instructions
+typedef __attribute__((address_space(3))) double lds_f64;
 
 struct XSel {
   const double* pool;  // slabs of KP x TP (X stored column-major, ld = TP)

@@ -66,29 +66,49 @@ __device__ __forceinline__ void sv_wave_sync() {
   asm volatile("" ::: "memory");
 }
 
+// An opaque copy of the lane id: lane masks derived from it are recomputed where they
+// are used instead of being hoisted out of the block loops (dozens of loop-invariant
+// 64-bit masks would otherwise spill the scalar file)
+__device__ __forceinline__ int sv_lane(int lane) {
+  int v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"(lane));
+  return v;
+}
+
+// An offset that the compiler must treat as computed after `dep` is known: the loads of
+// a substitution row are then issued row by row instead of all ~NN^2/2 of them being
+// hoisted to the top of the block (which spills hundreds of registers)
+__device__ __forceinline__ int sv_after(int off, double dep, bool on) {
+  if (on) asm volatile("" : "+v"(off) : "v"(dep));
+  return off;
+}
+
 // Cholesky in row layout: lane i < NN holds row i of the SPD matrix in s[0..i];
-// on return row i of the factor (entries k > i are garbage) and rps = 1/diag (uniform)
+// on return row i of the factor with 1 / C_ii on the diagonal (entries k > i are
+// garbage) and rps = 1/diag (uniform)
 template <int NN>
-__device__ __forceinline__ void sv_chol_rows(double (&s)[NN], double (&rps)[NN], int lane, int& bad) {
+__device__ __forceinline__ void sv_chol_rows(double (&s)[NN], double (&rps)[NN], int lane0, int& bad) {
+  const int lane = sv_lane(lane0);
+  double dmin = 1.0;  // smallest pivot (a non-positive one flags the block; no per-pivot masks)
 #pragma unroll
   for (int q = 0; q < NN; ++q) {
     double dq = readlane_d(s[q], q);
-    if (!(dq > 0.0)) {
-      bad = 1;
-      dq = 1.0;
-    }
+    dmin = fmin(dmin, dq);
+    dq = fmax(dq, 1e-300);
     const double rp = sv_rsqrt(dq);
     rps[q] = rp;
-    s[q] = (lane == q) ? dq * rp : s[q] * rp;
+    s[q] = (lane == q) ? rp : s[q] * rp;
 #pragma unroll
     for (int k = q + 1; k < NN; ++k) s[k] = fma(-s[q], readlane_d(s[q], k), s[k]);
     __builtin_amdgcn_sched_barrier(0);
   }
+  if (!(dmin > 0.0)) bad = 1;
 }
 
 // L y = b, lane i holds b_i and row i of L (off-diagonal part)
 template <int NN>
-__device__ __forceinline__ double sv_fwd(double b, const double (&s)[NN], const double (&rps)[NN], int lane) {
+__device__ __forceinline__ double sv_fwd(double b, const double (&s)[NN], const double (&rps)[NN], int lane0) {
+  const int lane = sv_lane(lane0);
 #pragma unroll
   for (int k = 0; k < NN; ++k) {
     const double yk = readlane_d(b, k) * rps[k];
@@ -100,7 +120,8 @@ __device__ __forceinline__ double sv_fwd(double b, const double (&s)[NN], const 
 
 // L' x = r, lane i holds r_i and column i of L (lc[k] = L[k][i], k > i)
 template <int NN>
-__device__ __forceinline__ double sv_bwd(double r, const double (&lc)[NN], const double (&rps)[NN], int lane) {
+__device__ __forceinline__ double sv_bwd(double r, const double (&lc)[NN], const double (&rps)[NN], int lane0) {
+  const int lane = sv_lane(lane0);
 #pragma unroll
   for (int k = NN - 1; k >= 0; --k) {
     const double xk = readlane_d(r, k) * rps[k];
@@ -120,14 +141,17 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   constexpr bool G3 = 3 * NN <= 64;
   using R = SvRec<NN>;
   extern __shared__ double sm[];
-  double* Ql = sm;                                   // NN x NN, Q = PHI^-1 (identity padding)
-  double* xsep = Ql + NN2;                           // kSvMaxSeg x NN separator solutions
+  // explicit LDS address space: keeps every access a 32-bit ds_* op (generic pointers
+  // captured by the lambdas below would otherwise become 64-bit flat addresses)
+  lds_f64* Ql = (lds_f64*)sm;                        // NN x NN, Q = PHI^-1 (identity padding)
+  lds_f64* Dz = Ql + NN2;                            // NN x NN, D0_0 = V0^-1 + Q
+  lds_f64* xsep = Dz + NN2;                          // kSvMaxSeg x NN separator solutions
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double* myC = xsep + kSvMaxSeg * NN + wave * sv_wave_lds(NN);
-  double* myX = myC + NN * CLD;
-  double* myw = myX + NN * XLD;
-  double* myF = myw + NN;
-  double* myD = myF + NN2;
+  lds_f64* myC = xsep + kSvMaxSeg * NN + wave * sv_wave_lds(NN);
+  lds_f64* myX = myC + NN * CLD;
+  lds_f64* myw = myX + NN * XLD;
+  lds_f64* myF = myw + NN;
+  lds_f64* myD = myF + NN2;
   const int n = d.N, TP = d.TP;
   const int c = blockIdx.x, s = cs.slot[c], T = Tslot[s];
   const int ln = lane < NN ? lane : 0;
@@ -174,17 +198,27 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
         Ql[r * NN + lane] = v;
       }
     }
+    sv_wave_sync();
+    if (lane < NN) {  // D0_0 row `lane` (identity on the padding)
+#pragma unroll
+      for (int m = 0; m < NN; ++m)
+        Dz[lane * NN + m] = ((lane < n && m < n) ? V0[lane + m * n] : (m == lane ? 1.0 : 0.0)) +
+                            Ql[lane * NN + m];
+    }
   }
   __syncthreads();
 
   const int P = sv_nseg(T);
   // original diagonal block D0_t, row ln, entry m (irt = diag(R_t^-1) entry of row ln)
   auto d0 = [&](int t, int m, double irt) __attribute__((always_inline)) -> double {
-    if (t == 0) {
-      const double v0 = (lane < n && m < n) ? V0[ln + m * n] : (m == ln ? 1.0 : 0.0);
-      return v0 + Ql[ln * NN + m];
-    }
-    return ((t == T) ? 1.0 : 2.0) * Ql[ln * NN + m] + ((m == ln) ? irt : 0.0);
+    const int lv = sv_lane(ln);
+    if (t == 0) return Dz[ln * NN + m];
+    return ((t == T) ? 1.0 : 2.0) * Ql[ln * NN + m] + ((m == lv) ? irt : 0.0);
+  };
+  // the same for t >= 1 (no prior block)
+  auto d0n = [&](int t, int m, double irt) __attribute__((always_inline)) -> double {
+    const int lv = sv_lane(ln);
+    return ((t == T) ? 1.0 : 2.0) * Ql[ln * NN + m] + ((m == lv) ? irt : 0.0);
   };
   auto ir_at = [&](int t) __attribute__((always_inline)) -> double { return (t >= 1 && real) ? irv[(size_t)ln * TP + t - 1] : 1.0; };
   auto ob_at = [&](int t) __attribute__((always_inline)) -> double { return (t >= 1 && real) ? obs[(size_t)ln * TP + t - 1] : 0.0; };
@@ -202,9 +236,8 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
     if (lane < NN) {
 #pragma unroll
       for (int m = 0; m < NN; ++m) {
-        const double v = (m < lane) ? sr[m] : ((m == lane) ? rps[m] : 0.0);
-        myC[lane * CLD + m] = v;
-        Ct[lane * NN + m] = v;
+        myC[lane * CLD + m] = sr[m];
+        Ct[lane * NN + m] = sr[m];
       }
       myw[lane] = w;
       Wg[(size_t)t * NN + lane] = w;
@@ -251,16 +284,16 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
       // of myC holds 1 / C_kk)
       {
         const int rcol = (lane < NN) ? lane : (inB ? rB : 0);
-        const double* rhs = (lane < NN) ? Ql : myF;
+        const lds_f64* rhs = (lane < NN) ? Ql : myF;
         const double sgn = (lane < NN) ? -1.0 : 1.0;
         double x[NN];
 #pragma unroll
         for (int k = 0; k < NN; ++k) {
+          const int ro = sv_after(k * CLD, x[k > 0 ? k - 1 : 0], k > 0);
           double v = sgn * rhs[k * NN + rcol];
 #pragma unroll
-          for (int m = 0; m < k; ++m) v = fma(-myC[k * CLD + m], x[m], v);
-          x[k] = v * myC[k * CLD + k];
-          __builtin_amdgcn_sched_barrier(0);
+          for (int m = 0; m < k; ++m) v = fma(-myC[ro + m], x[m], v);
+          x[k] = v * myC[ro + k];
         }
         if (lane < 2 * NN) {
 #pragma unroll
@@ -278,35 +311,30 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
       double wd = 0.0;
 #pragma unroll 1
       for (int k = 0; k < NN; ++k) {
-        const double* xr = myX + k * XLD;
+        const lds_f64* xr = myX + k * XLD;
         const double ak = xr[acol];
 #pragma unroll
         for (int m = 0; m < NN; ++m) pr[m] = fma(ak, xr[boff + m], pr[m]);
         wd = fma(ak, myw[k], wd);
       }
       // epilogue, uniform over the lanes (each lane group keeps only its own values):
-      //   lanes 0..NN-1:    successor's D~ row / b~ entry (or the right separator's record)
+      //   lanes 0..NN-1:    successor's D~ row / b~ entry (after the last block of a
+      //                     segment with a right separator: that separator's record)
       //   lanes NN..2NN-1:  next fill column M_{t+1,left}(:, r) = -(X2'X1)(r, :)'
       //   lanes 2NN..3NN-1: left separator's -sum X2'X2 row
-      {
-        const bool toR = hasR && t == last;
-        double* rR = rec + (size_t)q * R::LEN;
-        double* rL = rec + (size_t)(q > 0 ? q - 1 : 0) * R::LEN;
-        const double bn = b0(t + 1, irn, obn) - wd;
 #pragma unroll
-        for (int m = 0; m < NN; ++m) {
-          const double dn = d0(t + 1, m, irn) - pr[m];
-          sr[m] = dn;
-          if (toR && lane < NN) rR[R::DR + lane * NN + m] = dn;
-          if (hasL && inB) {
-            if (toR) rL[R::M + m * NN + rB] = -pr[m];
-            myF[m * NN + rB] = -pr[m];
-          }
-          if (G3 && hasL && inD) myD[rD * NN + m] -= pr[m];
+      for (int m = 0; m < NN; ++m) sr[m] = d0n(t + 1, m, irn) - pr[m];
+      bcur = (real ? obn * irn : 0.0) - wd;
+      if (hasL) {
+        if (inB) {
+#pragma unroll
+          for (int m = 0; m < NN; ++m) myF[m * NN + rB] = -pr[m];
+          dbl -= wd;
         }
-        bcur = bn;
-        if (toR && lane < NN) rR[R::BR + lane] = bn;
-        if (hasL && inB) dbl -= wd;
+        if (G3 && inD) {
+#pragma unroll
+          for (int m = 0; m < NN; ++m) myD[rD * NN + m] -= pr[m];
+        }
       }
       if constexpr (!G3) {  // 3 NN > 64: X2'X2 rows on lanes NN..2NN-1 in a second pass
         if (hasL) {
@@ -314,7 +342,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
           for (int m = 0; m < NN; ++m) pr[m] = 0.0;
 #pragma unroll 1
           for (int k = 0; k < NN; ++k) {
-            const double* xr = myX + k * XLD;
+            const lds_f64* xr = myX + k * XLD;
             const double ak = xr[acol];
 #pragma unroll
             for (int m = 0; m < NN; ++m) pr[m] = fma(ak, xr[NN + m], pr[m]);
@@ -326,6 +354,19 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
         }
       }
       sv_wave_sync();
+    }
+    sv_wave_sync();
+    if (hasR) {  // the right separator: D(s) - X1'X1, b(s) - X1'w of the last block
+      double* r = rec + (size_t)q * R::LEN;
+      if (lane < NN) {
+#pragma unroll
+        for (int m = 0; m < NN; ++m) r[R::DR + lane * NN + m] = sr[m];
+        r[R::BR + lane] = bcur;
+      }
+      if (hasL && inB) {  // coupling M_{left,right}: rec.M[m*NN + r] = M[r][m]
+        double* rl = rec + (size_t)(q - 1) * R::LEN;
+        for (int m = 0; m < NN; ++m) rl[R::M + m * NN + rB] = myF[m * NN + rB];
+      }
     }
     if (hasL) {
       double* r = rec + (size_t)(q - 1) * R::LEN;
@@ -364,11 +405,11 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
         double x[NN];
 #pragma unroll
         for (int k = 0; k < NN; ++k) {
+          const int ro = sv_after(k * CLD, x[k > 0 ? k - 1 : 0], k > 0);
           double v = (lane < NN) ? r[R::M + ln * NN + k] : 0.0;
 #pragma unroll
-          for (int m = 0; m < k; ++m) v = fma(-myC[k * CLD + m], x[m], v);
-          x[k] = v * myC[k * CLD + k];
-          __builtin_amdgcn_sched_barrier(0);
+          for (int m = 0; m < k; ++m) v = fma(-myC[ro + m], x[m], v);
+          x[k] = v * myC[ro + k];
         }
         if (lane < NN) {
 #pragma unroll
@@ -380,7 +421,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
         cb = 0.0;
 #pragma unroll 1
         for (int k = 0; k < NN; ++k) {
-          const double* xr = myX + k * XLD;
+          const lds_f64* xr = myX + k * XLD;
           const double ak = xr[ln];
 #pragma unroll
           for (int m = 0; m < NN; ++m) cg[m] = fma(ak, xr[m], cg[m]);
@@ -500,7 +541,7 @@ template <int NN, int NW>
 static hipError_t sv_launch_one(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
                                 const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf) {
   constexpr int CLD = NN + 1, XLD = 2 * NN + 1;
-  const size_t lds = (size_t)(NN * NN + kSvMaxSeg * NN + NW * sv_wave_lds(NN)) * sizeof(double);
+  const size_t lds = (size_t)(2 * NN * NN + kSvMaxSeg * NN + NW * sv_wave_lds(NN)) * sizeof(double);
   hipError_t e = hipFuncSetAttribute((const void*)k_sv_part<NN, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
