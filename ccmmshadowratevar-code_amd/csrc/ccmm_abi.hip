@@ -159,7 +159,7 @@ struct ccmm_chains {
   DBuf<int> Tslot, slot, xidx, yidx, status;
   DBuf<double> Xpool, Ypool, iVdiag, iVb, sPHI, V0inv, V0invm;
   // chain state
-  DBuf<double> PAI, A, invA, sqrtht, h, h0, sqrtPHI, PHI, E, logy2, eta, svobs, svir, W;
+  DBuf<double> PAI, A, invA, sqrtht, h, h0, sqrtPHI, PHI, E, logy2, eta, svobs, svir, W, ih2;
   DBuf<int8_t> kai;
   DBuf<double> G, rdiag, svLd, svw, svSep, svG, Zphi;
   DBuf<double> crn;
@@ -269,6 +269,7 @@ struct ccmm_chains {
     cs.svir = svir.p;
     cs.kai = kai.p;
     cs.W = W.p;
+    cs.ih2 = ih2.p;
     cs.G = G.p;
     cs.svLd = svLd.p;
     cs.svw = svw.p;
@@ -340,6 +341,7 @@ struct ccmm_chains {
     svir.alloc(B * N * TP);
     kai.alloc(B * N * TP);
     W.alloc(B * N * TP);
+    ih2.alloc(B * N * TP);
     std::vector<int> zeros(cf.ndata, cf.T);
     HIPCHECK(hipMemcpyAsync(Tslot.p, zeros.data(), cf.ndata * sizeof(int), hipMemcpyHostToDevice,
                             ctx->stream));
@@ -404,6 +406,7 @@ struct ccmm_chains {
     return true;
   }
   int lag_mode = std::getenv("CCMM_LAG_MODE") ? std::atoi(std::getenv("CCMM_LAG_MODE")) : 0;
+  int sv_mode = std::getenv("CCMM_SV_MODE") ? std::atoi(std::getenv("CCMM_SV_MODE")) : 0;
   LagSel lagsel() const { return LagSel{Dpool.p, xidx.p, dColmap.p, ldd, drows, cfg.p, lag_mode}; }
   // D (rows x ldd) of a slot from its X (T x K) and Y (T x N): rows 0..p-1 from the
   // lags of X's first row, rows p.. = Y.  Exact check that X is that lag design.
@@ -803,7 +806,7 @@ struct ccmm_chains {
                          d, Tslot.p, cs, ra);
     });
     launch(KID_SVSAMPLE, [&] {
-      HIPCHECK(sv_launch_part(d.N, ctx->stream, d, Tslot.p, V0inv.p, V0invm.p, cs, ra, svSep.p, svG.p));
+      HIPCHECK(sv_launch_part(d.N, ctx->stream, d, Tslot.p, V0inv.p, V0invm.p, cs, ra, svSep.p, svG.p, sv_mode));
     });
   }
 

@@ -107,6 +107,7 @@ struct ChainState {
   double* svir;      // [B][N][TP]  1/var_{s}
   int8_t* kai;       // [B][N][TP]
   double* W;         // [B][N][TP]  CTA weights
+  double* ih2;       // [B][N][TP]  1 / sqrtht^2 (CTA weights kernel)
   double* G;         // [B*N][KP][KP]  Gram -> Cholesky factor (L lower, L' upper)
   double* svLd;      // [B][TP+1][N*N] block Cholesky diagonal factors
   double* svw;       // [B][TP+1][N]

@@ -59,6 +59,13 @@ __global__ void k_cta_weights(Dims d, const int* __restrict__ Tslot, ChainState 
     }
   }
   cs.W[((size_t)c * d.N + j) * d.TP + t] = sqrt_form ? sqrt(w) : w;
+  // 1 / sqrtht(t, j)^2 for the residual weights of the sequential solve
+  double ihv = 0.0;
+  if (t < T) {
+    const double shv = cs.sqrtht[((size_t)c * d.N + j) * d.TP + t];
+    ihv = 1.0 / (shv * shv);
+  }
+  cs.ih2[((size_t)c * d.N + j) * d.TP + t] = ihv;
 }
 
 // ============================================================== weighted SYRK (FP64 MFMA)

@@ -45,81 +45,89 @@ struct GlArgs {
   const double* swl;   // LDS sqrt weights
 };
 
-// factor a 16 x 16 SPD tile held row-major (ld kGlLd) in LDS by one wave (lanes
-// 0..15 = rows); writes L back (zero upper) and rd = 1 / diag(L)
-__device__ __forceinline__ int gl_factor_tile(double* Dg, double* rd, int lane) {
-  int bad = 0;
+// Per-wave factor + inverse of the SPD 16 x 16 tile Dg (row-major, ld kGlLd, lower
+// triangle read): Ws := L^-1 (lower, row-major, ld kGlLd).  Every wave runs this on
+// the same tile, so no barrier separates the factorisation from its consumers.
+__device__ __forceinline__ double gl_rsqrt(double d) {  // rsq estimate + 2 Newton steps
+  double r = __builtin_amdgcn_rsq(d);
+  const double hd = 0.5 * d;
+  r = r * fma(-hd * r, r, 1.5);
+  r = r * fma(-hd * r, r, 1.5);
+  return r;
+}
+
+__device__ __forceinline__ int gl_factor_inv(const double* Dg, double* Ws, int lane) {
   double row[16];
-  double mydiag = 1.0;
+  double rdiag = 1.0, dmin = 1.0;  // smallest pivot: a non-positive one flags the system
 #pragma unroll
   for (int m = 0; m < 16; ++m) row[m] = (lane < 16 && m <= lane) ? Dg[lane * kGlLd + m] : 0.0;
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) {
     double dkk = readlane_d(row[kk], kk);
-    if (!(dkk > 0.0)) {
-      bad = 1;
-      dkk = 1.0;
-    }
-    const double piv = sqrt(dkk);
-    const double rp = 1.0 / piv;
-    if (lane == kk) {
-      row[kk] = piv;
-      mydiag = piv;
-    }
-    if (lane > kk) row[kk] *= rp;
-    const double lik = row[kk];
+    dmin = fmin(dmin, dkk);
+    const double rp = gl_rsqrt(fmax(dkk, 1e-300));
+    if (lane == kk) rdiag = rp;
+    const double lik = (lane > kk) ? row[kk] * rp : 0.0;
+    row[kk] = lik;
 #pragma unroll
-    for (int m = kk + 1; m < 16; ++m) {
-      const double lmk = readlane_d(lik, m);
-      if (lane >= m) row[m] = fma(-lik, lmk, row[m]);
-    }
+    for (int m = kk + 1; m < 16; ++m) row[m] = fma(-lik, readlane_d(lik, m), row[m]);
   }
+  const int bad = (dmin > 0.0) ? 0 : 1;
+  // L -> Ws, diagonal as its reciprocal
   if (lane < 16) {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) Dg[lane * kGlLd + m] = (m <= lane) ? row[m] : 0.0;
-    rd[lane] = 1.0 / mydiag;
+    for (int m = 0; m < 16; ++m) Ws[lane * kGlLd + m] = (m < lane) ? row[m] : ((m == lane) ? rdiag : 0.0);
   }
+  __builtin_amdgcn_wave_barrier();
+  // lane c < 16: column c of L^-1,  x_i = (delta_ic - sum_{m<i} L_im x_m) / L_ii
+  const int c = lane;
+  double x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    // row i's loads are issued after x[i-1] (opaque dependency): all 120 hoisted to the
+    // top they would spill next to the 120 accumulator registers
+    int ro = i * kGlLd;
+    if (i > 0) asm volatile("" : "+v"(ro) : "v"(x[i - 1]));
+    double s0 = (i == c) ? 1.0 : 0.0, s1 = 0.0;
+#pragma unroll
+    for (int m = 0; m < i; m += 2) {
+      s0 = fma(-Ws[ro + m], x[m], s0);
+      if (m + 1 < i) s1 = fma(-Ws[ro + m + 1], x[m + 1], s1);
+    }
+    x[i] = (i >= c) ? (s0 + s1) * Ws[ro + i] : 0.0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < 16) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Ws[i * kGlLd + c] = x[i];
+  }
+  __builtin_amdgcn_wave_barrier();
   return bad;
 }
 
-// in-place inverse of a lower-triangular 16 x 16 tile in LDS (row-major, ld kGlLd)
-// by one wave: lane c < 16 solves L x = e_c (column c of the inverse)
-__device__ __forceinline__ void gl_invert_tile(double* S, int lane) {
-  double x[16];
-  const int c = lane;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    double s = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-    for (int m = 0; m < i; ++m) s = fma(-S[i * kGlLd + m], x[m], s);
-    x[i] = (i >= c) ? s / S[i * kGlLd + i] : 0.0;
-  }
-  // all lanes have read S (in-order LDS within the wave) before the writes below
-  __builtin_amdgcn_wave_barrier();
-  if (lane < 16) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) S[i * kGlLd + c] = x[i];
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
+// Tile slots: slot gi enumerates the lower tile pairs (ti >= tj) column-major; the
+// slot holds the UPPER tile (tj, ti) of the symmetric/triangular matrix, i.e. the
+// transpose of the lower tile (ti, tj).  In that form every triangular product of the
+// factorisation is a left-multiplication  C = A_lds x acc,  the orientation in which
+// v_mfma_f64_16x16x4f64 takes the accumulator tile directly as its B operand.
+// SYRK of the lag columns for wave W (compile-time tile ownership, so that the operand
+// fragments stay in registers).  Only this loop is specialised per wave: the
+// factorisation below runs one copy of the code for all waves (instruction cache).
 template <int NT, int W>
-__device__ __forceinline__ int gram_lag_body(const GlArgs& g, double* sm, int tid) {
+__device__ __forceinline__ void gl_syrk(const GlArgs& g, dbl4 (&acc)[gl_tpw(NT)], double& bs0, double& bs1,
+                                        double& csum, int lane) {
   constexpr int NTILE = gl_ntile(NT);
   constexpr int TPW = gl_tpw(NT);
-  constexpr int KL = 16 * NT;
-  const int lane = tid & 63, lr = lane & 15, lq = lane >> 4;
-  int bad = 0;
-
-  dbl4 acc[TPW];
+  const int lr = lane & 15, lq = lane >> 4;
 #pragma unroll
   for (int k = 0; k < TPW; ++k) acc[k] = dbl4{0.0, 0.0, 0.0, 0.0};
 
-  // ------------------------------------------------------------ SYRK of the lag columns
   int off[NT];
 #pragma unroll
   for (int b = 0; b < NT; ++b) off[b] = g.colmap[16 * b + lr];
-  double bs0 = 0.0, bs1 = 0.0, csum = 0.0;
+  bs0 = 0.0;
+  bs1 = 0.0;
+  csum = 0.0;
   const int nks = (g.mode & 1) ? 0 : (g.T + 3) >> 2;
   for (int ks = 0; ks < nks; ++ks) {
     const int t = 4 * ks + lq;
@@ -130,11 +138,9 @@ __device__ __forceinline__ int gram_lag_body(const GlArgs& g, double* sm, int ti
     for (int b = 0; b < NT; ++b) frag[b] = row[off[b]] * sw;
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {
-      constexpr int dummy = 0;
-      (void)dummy;
       if (W + kGlWaves * k < NTILE) {
         const int gi = W + kGlWaves * k;
-        acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(frag[gl_ti(NT, gi)], frag[gl_tj(NT, gi)], acc[k],
+        acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(frag[gl_tj(NT, gi)], frag[gl_ti(NT, gi)], acc[k],
                                                       0, 0, 0);
       }
     }
@@ -149,14 +155,32 @@ __device__ __forceinline__ int gram_lag_body(const GlArgs& g, double* sm, int ti
   bs1 += __shfl_xor(bs1, 32);
   csum += __shfl_xor(csum, 16);
   csum += __shfl_xor(csum, 32);
+}
+
+// Factorisation stage for wave W (runtime, wave-uniform): intercept peel, Cholesky,
+// inverse, output.  sti/stj: the (ti, tj) of this wave's slots.
+template <int NT>
+__device__ __forceinline__ int gram_lag_factor(const GlArgs& g, double* sm, int tid, int W,
+                                               dbl4 (&acc)[gl_tpw(NT)], double bs0, double bs1, double csum) {
+  constexpr int NTILE = gl_ntile(NT);
+  constexpr int TPW = gl_tpw(NT);
+  constexpr int KL = 16 * NT;
+  const int lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  int bad = 0;
+  int sti[TPW], stj[TPW];
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    const int gi = W + kGlWaves * k;
+    sti[k] = gi < NTILE ? gl_ti(NT, gi) : 0;
+    stj[k] = gi < NTILE ? gl_tj(NT, gi) : 0;
+  }
   __syncthreads();  // D no longer needed: the LDS is reused below
 
   double* lvec = sm;              // KL   b, then l = b / L00
   double* misc = lvec + KL;       // 8
-  double* rdv = misc + 8;         // 2 x 16 (+ spare)
-  double* Dg0 = rdv + 64;         // 2 tiles (double-buffered by panel parity)
-  double* Pn0 = Dg0 + 2 * kGlTile;  // 2 x NT tiles
-  double* Ws = Pn0 + 2 * NT * kGlTile + W * kGlTile;  // this wave's scratch tile
+  double* Dg = misc + 8;          // diagonal tile of the current panel
+  double* Pn0 = Dg + kGlTile;     // 2 x NT tiles: panel rows; (inverse) U column / Z row
+  double* Ws = Pn0 + 2 * NT * kGlTile + W * kGlTile;  // this wave's L_pp^-1
   double* part = Pn0 + 2 * NT * kGlTile + kGlWaves * kGlTile;  // NTILE x 16
 
   if (lq == 0) {
@@ -169,16 +193,16 @@ __device__ __forceinline__ int gram_lag_body(const GlArgs& g, double* sm, int ti
   if (!(G00 > 0.0)) bad = 1;
   const double L00 = sqrt(G00 > 0.0 ? G00 : 1.0);
   const double rL00 = 1.0 / L00;
-  // + diag(iV~) - l l'
+  // + diag(iV~) - l l'   (slot element (lq + 4r, lr) = row 16 tj + lq + 4r, column 16 ti + lr)
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
     const int gi = W + kGlWaves * k;
     if (gi < NTILE) {
-      const int ti = gl_ti(NT, gi), tj = gl_tj(NT, gi);
-      const double lc = lvec[16 * tj + lr] * rL00;
+      const int ti = sti[k], tj = stj[k];
+      const double lc = lvec[16 * ti + lr] * rL00;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int rowi = 16 * ti + lq + 4 * r;
+        const int rowi = 16 * tj + lq + 4 * r;
         double v = fma(-(lvec[rowi] * rL00), lc, acc[k][r]);
         if (ti == tj && lq + 4 * r == lr) v += g.iv[1 + rowi];
         acc[k][r] = v;
@@ -189,177 +213,175 @@ __device__ __forceinline__ int gram_lag_body(const GlArgs& g, double* sm, int ti
   if (tid < KL) lvec[tid] *= rL00;  // l
   __syncthreads();
 
-  // ------------------------------------------------------------ Cholesky of M~
-  for (int p = 0; p < ((g.mode & 2) ? 0 : NT); ++p) {
-    double* Dg = Dg0 + (p & 1) * kGlTile;
-    double* Pn = Pn0 + (p & 1) * NT * kGlTile;
-    double* rd = rdv + (p & 1) * 16;
-    // (1) column p -> LDS
+  // ------------------------------------------------------------ Cholesky M~ = U'U
+  // LinvB (shared) holds L_pp^-1 of the current panel.  Panel p:
+  //   U_pi = L_pp^-1 G_pi (slots ti = i > p, tj = p) on MFMA;  slot (p,p) := U_pp^-1
+  //   trailing  G_ij -= U_pi' U_pj  (slots ti, tj > p) on MFMA from the LDS panel.
+  // Look-ahead: the owner of slot (p+1, p+1) updates that tile first and factors it
+  // (gl_factor_inv -> LinvB) while the other waves run their trailing updates, so each
+  // panel costs two barriers and one serial 16 x 16 factorisation on one wave.
+  double* LinvB = Dg;
+  const bool do_chol = !(g.mode & 2);
+  if (do_chol) {  // prologue: factor the first diagonal tile
+    bool own = false;
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {
       const int gi = W + kGlWaves * k;
-      if (gi < NTILE && gl_tj(NT, gi) == p) {
-        double* dst = (gl_ti(NT, gi) == p) ? Dg : Pn + gl_ti(NT, gi) * kGlTile;
+      if (gi < NTILE && sti[k] == 0 && stj[k] == 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dst[(lq + 4 * r) * kGlLd + lr] = acc[k][r];
+        for (int r = 0; r < 4; ++r) Ws[(lq + 4 * r) * kGlLd + lr] = acc[k][r];
+        own = true;
       }
     }
-    __syncthreads();
-    // (2) diagonal tile
-    if (W == 0 && !(g.mode & 256)) bad |= gl_factor_tile(Dg, rd, lane);
-    __syncthreads();
-    // (3) panel: L_ip = G_ip L_pp^-T, one thread per row
-    {
-      const int nrows = (g.mode & 512) ? 0 : (NT - 1 - p) * 16;
-      for (int e = tid; e < nrows; e += 512) {
-        const int ti = p + 1 + (e >> 4), rr = e & 15;
-        double* P = Pn + ti * kGlTile + rr * kGlLd;
-        double x[16];
+    __builtin_amdgcn_wave_barrier();
+    if (own && !(g.mode & 256)) bad |= gl_factor_inv(Ws, LinvB, lane);
+  }
+  for (int p = 0; p < (do_chol ? NT : 0); ++p) {
+    __syncthreads();  // LinvB = L_pp^-1 visible; the previous trailing reads of Pn are done
+    double* Pn = Pn0;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) x[m] = P[m];
+    for (int k = 0; k < TPW; ++k) {
+      const int gi = W + kGlWaves * k;
+      if (gi < NTILE && stj[k] == p) {
+        const int ti = sti[k];
+        if (ti == p) {  // U_pp^-1 = (L_pp^-1)': element (lq + 4r, lr) = Linv[lr][lq + 4r]
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
-          double s = x[m];
+          for (int r = 0; r < 4; ++r) acc[k][r] = LinvB[lr * kGlLd + lq + 4 * r];
+        } else {
+          dbl4 cc = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int q = 0; q < m; ++q) s = fma(-x[q], Dg[m * kGlLd + q], s);
-          x[m] = s * rd[m];
+          for (int kk = 0; kk < 4; ++kk)
+            cc = __builtin_amdgcn_mfma_f64_16x16x4f64(LinvB[lr * kGlLd + 4 * kk + lq], acc[k][kk], cc, 0, 0, 0);
+          acc[k] = cc;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Pn[ti * kGlTile + (lq + 4 * r) * kGlLd + lr] = cc[r];
         }
-#pragma unroll
-        for (int m = 0; m < 16; ++m) P[m] = x[m];
       }
     }
-    __syncthreads();
-    // (4) column p back to registers; trailing update on MFMA
-#pragma unroll
-    for (int k = 0; k < TPW; ++k) {
-      const int gi = W + kGlWaves * k;
-      if (gi < NTILE && gl_tj(NT, gi) == p) {
-        const double* src = (gl_ti(NT, gi) == p) ? Dg : Pn + gl_ti(NT, gi) * kGlTile;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[k][r] = src[(lq + 4 * r) * kGlLd + lr];
-      }
-    }
+    __syncthreads();  // panel visible; LinvB free for the next factorisation
     if (p + 1 < NT && !(g.mode & 1024)) {
+      const int q = p + 1;
+      // look-ahead: next diagonal tile first, then its factorisation
+      bool own = false;
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        double pf[NT];
+      for (int k = 0; k < TPW; ++k) {
+        const int gi = W + kGlWaves * k;
+        if (gi < NTILE && sti[k] == q && stj[k] == q) {
 #pragma unroll
-        for (int b = 0; b < NT; ++b) pf[b] = (b > p) ? Pn[b * kGlTile + lr * kGlLd + lq + 4 * kk] : 0.0;
+          for (int kk = 0; kk < 4; ++kk) {
+            const double pq = Pn[q * kGlTile + (4 * kk + lq) * kGlLd + lr];
+            acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(-pq, pq, acc[k], 0, 0, 0);
+          }
 #pragma unroll
-        for (int k = 0; k < TPW; ++k) {
-          const int gi = W + kGlWaves * k;
-          if (gi < NTILE && gl_tj(NT, gi) > p)
-            acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(-pf[gl_ti(NT, gi)], pf[gl_tj(NT, gi)], acc[k], 0,
-                                                          0, 0);
+          for (int r = 0; r < 4; ++r) Ws[(lq + 4 * r) * kGlLd + lr] = acc[k][r];
+          own = true;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (own && !(g.mode & 256)) bad |= gl_factor_inv(Ws, LinvB, lane);
+#pragma unroll
+      for (int k = 0; k < TPW; ++k) {
+        const int gi = W + kGlWaves * k;
+        if (gi < NTILE && stj[k] > p && !(sti[k] == q && stj[k] == q)) {
+          const double* Pa = Pn + stj[k] * kGlTile + lq * kGlLd + lr;
+          const double* Pb = Pn + sti[k] * kGlTile + lq * kGlLd + lr;
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+            acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(-Pa[4 * kk * kGlLd], Pb[4 * kk * kGlLd], acc[k], 0, 0,
+                                                          0);
         }
       }
     }
   }
 
-  __syncthreads();  // the last panel's Dg/Pn reads are done before the buffers are reused
+  __syncthreads();
 
-  // ------------------------------------------------------------ inverse of L~
-  // diagonal tiles in place: slot (p,p) := L_pp^-1
-#pragma unroll
-  for (int k = 0; k < TPW; ++k) {
-    const int gi = W + kGlWaves * k;
-    if (gi < NTILE && gl_ti(NT, gi) == gl_tj(NT, gi)) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Ws[(lq + 4 * r) * kGlLd + lr] = acc[k][r];
-      __builtin_amdgcn_wave_barrier();
-      gl_invert_tile(Ws, lane);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[k][r] = Ws[(lq + 4 * r) * kGlLd + lr];
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-  // right-looking solve of L X = I by tile rows: at step p
-  //   X_pj = Linv_pp B_pj (j < p), X_pp = Linv_pp;   B_ij -= L_ip X_pj (i > p, j <= p)
-  // slot (i, j) holds L_ij until step j, then B_ij, then (after step i) X_ij.
-  for (int p = 0; p < ((g.mode & 4) ? 0 : NT); ++p) {
-    double* XD = Dg0 + (p & 1) * kGlTile;          // Linv_pp
-    double* LP = Pn0 + (p & 1) * NT * kGlTile;     // L_ip, i > p (slot i)
-    double* XR = Pn0 + ((p + 1) & 1) * NT * kGlTile;  // X_pj, j <= p (slot j): other panel buffer
-    // (1) Linv_pp and column p of L -> LDS
+  // ------------------------------------------------------------ Z = U^-1 (= Linv~')
+  // block back substitution from the bottom tile row:  at step p
+  //   Z_pj = U_pp^-1 B_pj (j > p), Z_pp = U_pp^-1;   B_ij -= U_ip Z_pj (i < p, j >= p)
+  // upper tile (a, b) lives in slot (ti = b, tj = a); slot (i, j) holds U_ij until
+  // step j, then B_ij, then (after step i) Z_ij.
+  for (int p = ((g.mode & 4) ? -1 : NT - 1); p >= 0; --p) {
+    double* XD = Dg;                                  // U_pp^-1
+    double* LP = Pn0 + (p & 1) * NT * kGlTile;        // U_ip, i < p (slot i)
+    double* XR = Pn0 + ((p + 1) & 1) * NT * kGlTile;  // Z_pj, j >= p (slot j)
+    // (1) U_pp^-1 and column p of U -> LDS
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {
       const int gi = W + kGlWaves * k;
-      if (gi < NTILE && gl_tj(NT, gi) == p) {
-        double* dst = (gl_ti(NT, gi) == p) ? XD : LP + gl_ti(NT, gi) * kGlTile;
+      if (gi < NTILE && sti[k] == p) {
+        const int tj = stj[k];
+        double* dst = (tj == p) ? XD : LP + tj * kGlTile;
 #pragma unroll
         for (int r = 0; r < 4; ++r) dst[(lq + 4 * r) * kGlLd + lr] = acc[k][r];
       }
     }
     __syncthreads();
-    // (2) row p: X_pj = Linv_pp B_pj (j < p); X_pp -> XR as well
+    // (2) row p: Z_pj = U_pp^-1 B_pj (j > p); Z_pp -> XR as well
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {
       const int gi = W + kGlWaves * k;
-      if (gi < NTILE && gl_ti(NT, gi) == p) {
-        const int tj = gl_tj(NT, gi);
-        if (tj < p) {
+      if (gi < NTILE && stj[k] == p) {
+        const int ti = sti[k];
+        if (ti > p) {
           dbl4 cc = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk)
             cc = __builtin_amdgcn_mfma_f64_16x16x4f64(XD[lr * kGlLd + 4 * kk + lq], acc[k][kk], cc, 0, 0, 0);
           acc[k] = cc;
         }
-        double* dst = XR + tj * kGlTile;
+        double* dst = XR + ti * kGlTile;
 #pragma unroll
         for (int r = 0; r < 4; ++r) dst[(lq + 4 * r) * kGlLd + lr] = acc[k][r];
       }
     }
     __syncthreads();
-    // (3) rows below: B_ij -= L_ip X_pj (j < p);  B_ip = -L_ip Linv_pp
+    // (3) rows above: B_ij -= U_ip Z_pj (j > p);  B_ip = -U_ip Z_pp
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {
       const int gi = W + kGlWaves * k;
-      if (gi < NTILE && gl_ti(NT, gi) > p && gl_tj(NT, gi) <= p) {
-        const int ti = gl_ti(NT, gi), tj = gl_tj(NT, gi);
-        const double* La = LP + ti * kGlTile;
-        const double* Xb = XR + tj * kGlTile;
-        dbl4 cc = (tj == p) ? dbl4{0.0, 0.0, 0.0, 0.0} : acc[k];
+      if (gi < NTILE && stj[k] < p && sti[k] >= p) {
+        const int ti = sti[k], tj = stj[k];
+        const double* Ua = LP + tj * kGlTile;
+        const double* Zb = XR + ti * kGlTile;
+        dbl4 cc = (ti == p) ? dbl4{0.0, 0.0, 0.0, 0.0} : acc[k];
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk)
-          cc = __builtin_amdgcn_mfma_f64_16x16x4f64(-La[lr * kGlLd + 4 * kk + lq], Xb[(4 * kk + lq) * kGlLd + lr],
+          cc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Ua[lr * kGlLd + 4 * kk + lq], Zb[(4 * kk + lq) * kGlLd + lr],
                                                     cc, 0, 0, 0);
         acc[k] = cc;
       }
     }
-    // the next step writes the other XD/LP parity; XR of step p+1 is this LP buffer,
-    // written only after the next step's first barrier
+    // the next step writes XD and the other LP parity after its first barrier; XR of
+    // step p-1 is this LP buffer, written only after that barrier
     __syncthreads();
   }
 
   // ------------------------------------------------------------ intercept column of Linv
-  //   Linv(1+a, 0) = -(Linv~ l)_a / L00: per owned tile, row partial sums over its 16 columns
+  //   Linv(1+a, 0) = -(Linv~ l)_a / L00; slot element (lq+4r, lr) = Linv~(16 ti + lr, 16 tj + lq + 4r)
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
     const int gi = W + kGlWaves * k;
     if (gi < NTILE) {
-      const int tj = gl_tj(NT, gi);
-      const double lc = lvec[16 * tj + lr];
+      const int tj = stj[k];
+      double v = 0.0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double v = acc[k][r] * lc;
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        if (lr == 0) part[gi * 16 + lq + 4 * r] = v;
-      }
+      for (int r = 0; r < 4; ++r) v = fma(acc[k][r], lvec[16 * tj + lq + 4 * r], v);
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lq == 0) part[gi * 16 + lr] = v;
     }
   }
   __syncthreads();
   double* o = g.out;
   if (tid < KL) {
     const int ti = tid >> 4, rr = tid & 15;
-    double s = 0.0;
-    for (int tj = 0; tj <= ti; ++tj) s += part[gl_tile(NT, ti, tj) * 16 + rr];
-    o[NTILE * 256 + 1 + tid] = -s * rL00;
+    double sacc = 0.0;
+    for (int tj = 0; tj <= ti; ++tj) sacc += part[gl_tile(NT, ti, tj) * 16 + rr];
+    o[NTILE * 256 + 1 + tid] = -sacc * rL00;
   }
   if (tid == 0) o[NTILE * 256] = rL00;
-  // ------------------------------------------------------------ Linv~ tiles -> HBM
+  // ------------------------------------------------------------ Linv~ tiles -> HBM in slot layout
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
     const int gi = W + kGlWaves * k;
@@ -401,27 +423,34 @@ __global__ __launch_bounds__(512, 1) void k_gram_chol_lag(Dims d, const int* __r
   g.swl = sm + ls.rows * ls.ldd;
   g.w = nullptr;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int bad = 0;
+  dbl4 acc[gl_tpw(NT)];
+  double bs0, bs1, csum;
   switch (wave) {
-    case 0: bad = gram_lag_body<NT, 0>(g, sm, tid); break;
-    case 1: bad = gram_lag_body<NT, 1>(g, sm, tid); break;
-    case 2: bad = gram_lag_body<NT, 2>(g, sm, tid); break;
-    case 3: bad = gram_lag_body<NT, 3>(g, sm, tid); break;
-    case 4: bad = gram_lag_body<NT, 4>(g, sm, tid); break;
-    case 5: bad = gram_lag_body<NT, 5>(g, sm, tid); break;
-    case 6: bad = gram_lag_body<NT, 6>(g, sm, tid); break;
-    case 7: bad = gram_lag_body<NT, 7>(g, sm, tid); break;
+    case 0: gl_syrk<NT, 0>(g, acc, bs0, bs1, csum, tid & 63); break;
+    case 1: gl_syrk<NT, 1>(g, acc, bs0, bs1, csum, tid & 63); break;
+    case 2: gl_syrk<NT, 2>(g, acc, bs0, bs1, csum, tid & 63); break;
+    case 3: gl_syrk<NT, 3>(g, acc, bs0, bs1, csum, tid & 63); break;
+    case 4: gl_syrk<NT, 4>(g, acc, bs0, bs1, csum, tid & 63); break;
+    case 5: gl_syrk<NT, 5>(g, acc, bs0, bs1, csum, tid & 63); break;
+    case 6: gl_syrk<NT, 6>(g, acc, bs0, bs1, csum, tid & 63); break;
+    case 7: gl_syrk<NT, 7>(g, acc, bs0, bs1, csum, tid & 63); break;
     default: __builtin_unreachable();
   }
+  const int bad = gram_lag_factor<NT>(g, sm, tid, wave, acc, bs0, bs1, csum);
   if (bad && (tid & 63) == 0) atomicOr(&cs.status[c], 2);
 }
 
 // ================================================================== sequential solve
+// The Linv~ tiles of the current equation live in registers in the slot layout of
+// k_gram_chol_lag (wave W holds slots W + 8k; element (lq + 4r, lr) of slot (ti, tj) =
+// Linv~(16 ti + lr, 16 tj + lq + 4r)): one coalesced HBM read per system, issued after
+// the v_t loads so that it overlaps the X'v product.
 template <int NT, int NMAX>
 __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int* __restrict__ Tslot,
                                                               const double* __restrict__ iVb, XSel xs, LagSel ls,
                                                               ChainState cs, RngArgs ra) {
   constexpr int NTILE = gl_ntile(NT);
+  constexpr int TPW = gl_tpw(NT);
   constexpr int KL = 16 * NT;
   extern __shared__ double sm[];
   const int N = d.N, TP = d.TP, K = d.K, KP = d.KP;
@@ -438,13 +467,22 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
   const int c = blockIdx.x;
   const int s = cs.slot[c];
   const int T = Tslot[s];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Rng rng = ra.make(c);
-  const double* sh = cs.sqrtht + (size_t)c * N * TP;
+  const double* ih2 = cs.ih2 + (size_t)c * N * TP;
   const double* Y = xs.ypool + (size_t)xs.yidx[c] * N * TP;
   double* E = cs.E + (size_t)c * N * TP;
   for (int q = tid; q < N * N; q += kSlThreads) Al[q] = cs.A[(size_t)c * N * N + q];
   for (int q = tid; q < KL; q += kSlThreads) cm[q] = ls.colmap[q];
+  // this wave's slots: (ti, tj) per register tile
+  int sti[TPW], stj[TPW];
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    const int gi = wave + kGlWaves * k;
+    sti[k] = gi < NTILE ? gl_ti(NT, gi) : 0;
+    stj[k] = gi < NTILE ? gl_tj(NT, gi) : 0;
+  }
   int cur = -1;
 
   for (int j = 0; j < N; ++j) {
@@ -462,12 +500,12 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
     for (int t = tid; t < TP; t += kSlThreads) {
       double acc = 0.0;
       if (t < T && !(ls.mode & 16)) {
-        double e[NMAX], ih[NMAX];
+        double e[NMAX], w2[NMAX];
 #pragma unroll
         for (int k = 0; k < NMAX; ++k) {
           if (k < N) {
             e[k] = (k == j) ? Y[(size_t)k * TP + t] : E[(size_t)k * TP + t];
-            ih[k] = 1.0 / sh[(size_t)k * TP + t];
+            w2[k] = ih2[(size_t)k * TP + t];
           }
         }
 #pragma unroll
@@ -476,32 +514,47 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
             double ea = 0.0;
 #pragma unroll
             for (int k = 0; k <= i; ++k) ea = fma(e[k], Al[i + k * N], ea);
-            acc += Al[i + j * N] * (ea * ih[i]) * ih[i];
+            acc = fma(Al[i + j * N] * ea, w2[i], acc);
           }
         }
       }
       vl[t] = acc;
     }
     __syncthreads();
+    // Linv~ of this system -> registers (consumed in phases 3-4); issued after the
+    // barrier so that they cannot be hoisted into the v_t loop (register pressure)
+    dbl4 lt[TPW];
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) {
+      const int gi = wave + kGlWaves * k;
+      if (gi < NTILE) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lt[k][r] = Lo[gi * 256 + 64 * r + lane];
+      } else {
+        lt[k] = dbl4{0.0, 0.0, 0.0, 0.0};
+      }
+    }
     // ---- (2) rhs = iVb_j + X' v, two t-halves per column
     {
       const int h = tid >> 8, a = tid & 255;
       const int th = ((T + 1) >> 1);
       const int t0 = h ? th : 0, t1 = h ? T : th;
-      double p0 = 0.0, p1 = 0.0;
+      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
       if (ls.mode & 32) {
       } else if (a < KL) {
         const double* col = Dl + cm[a];
         int t = t0;
-        for (; t + 1 < t1; t += 2) {
+        for (; t + 3 < t1; t += 4) {
           p0 = fma(col[t * ldd], vl[t], p0);
           p1 = fma(col[(t + 1) * ldd], vl[t + 1], p1);
+          p2 = fma(col[(t + 2) * ldd], vl[t + 2], p2);
+          p3 = fma(col[(t + 3) * ldd], vl[t + 3], p3);
         }
-        if (t < t1) p0 = fma(col[t * ldd], vl[t], p0);
+        for (; t < t1; ++t) p0 = fma(col[t * ldd], vl[t], p0);
       } else if (a == KL) {
         for (int t = t0; t < t1; ++t) p0 += vl[t];
       }
-      part[h * 256 + a] = p0 + p1;
+      part[h * 256 + a] = (p0 + p1) + (p2 + p3);
     }
     __syncthreads();
     const double* ivb = iVb + ((size_t)s * N + j) * KP;
@@ -510,20 +563,22 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       rl[kx] = part[tid] + part[256 + tid] + ivb[kx];
     }
     __syncthreads();
-    // ---- (3) y = Linv rhs: tile-row partials, one (tile, row) per thread pass
-    for (int e = tid; e < ((ls.mode & 64) ? 0 : NTILE * 16); e += kSlThreads) {
-      const int gi = e >> 4, rr = e & 15;
-      const int ti = gl_ti(NT, gi), tj = gl_tj(NT, gi);
-      const double* Lr = Lo + gi * 256 + rr * 16;
-      const double* rv = rl + 1 + 16 * tj;
-      double s0 = 0.0, s1 = 0.0;
+    // ---- (3) y = Linv rhs: per slot, row 16 ti + lr of Linv~ against rhs block tj
+    if (!(ls.mode & 64)) {
 #pragma unroll
-      for (int n = 0; n < 16; n += 2) {
-        s0 = fma(Lr[n], rv[n], s0);
-        s1 = fma(Lr[n + 1], rv[n + 1], s1);
+      for (int k = 0; k < TPW; ++k) {
+        const int gi = wave + kGlWaves * k;
+        if (gi < NTILE) {
+          const double* rv = rl + 1 + 16 * stj[k] + lq;
+          double v = lt[k][0] * rv[0];
+          v = fma(lt[k][1], rv[4], v);
+          v = fma(lt[k][2], rv[8], v);
+          v = fma(lt[k][3], rv[12], v);
+          v += __shfl_xor(v, 16);
+          v += __shfl_xor(v, 32);
+          if (lq == 0) tp[gi * 16 + lr] = v;
+        }
       }
-      tp[gi * 16 + rr] = s0 + s1;
-      (void)ti;
     }
     __syncthreads();
     if (tid < KL) {
@@ -540,18 +595,26 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       rl[kx] = xl[kx] + ((kx < K) ? rng.normal(CCMM_RNG_PAI, (uint32_t)(kx + K * j)) : 0.0);
     }
     __syncthreads();
-    for (int e = tid; e < ((ls.mode & 64) ? 0 : NTILE * 16); e += kSlThreads) {
-      const int gi = e >> 4, cc = e & 15;
-      const int ti = gl_ti(NT, gi);
-      const double* Lc = Lo + gi * 256 + cc;
-      const double* cv = rl + 1 + 16 * ti;
-      double s0 = 0.0, s1 = 0.0;
+    if (!(ls.mode & 64)) {
+      // slot contribution to x(16 tj + lq + 4r) = sum_lr lt[r] c(16 ti + lr): four sums over
+      // the 16 lanes of a row group, folded so that lane (lr & 3) == 0 ends with r = lr >> 2
+      const bool b8 = lr & 8, b4 = lr & 4;
 #pragma unroll
-      for (int n = 0; n < 16; n += 2) {
-        s0 = fma(Lc[n * 16], cv[n], s0);
-        s1 = fma(Lc[(n + 1) * 16], cv[n + 1], s1);
+      for (int k = 0; k < TPW; ++k) {
+        const int gi = wave + kGlWaves * k;
+        if (gi < NTILE) {
+          const double cv = rl[1 + 16 * sti[k] + lr];
+          const double v0 = lt[k][0] * cv, v1 = lt[k][1] * cv, v2 = lt[k][2] * cv, v3 = lt[k][3] * cv;
+          double a = b8 ? v2 : v0, b = b8 ? v3 : v1;
+          a += __shfl_xor(b8 ? v0 : v2, 8);
+          b += __shfl_xor(b8 ? v1 : v3, 8);
+          double q = b4 ? b : a;
+          q += __shfl_xor(b4 ? a : b, 4);
+          q += __shfl_xor(q, 2);
+          q += __shfl_xor(q, 1);
+          if ((lr & 3) == 0) tp[gi * 16 + lq + 4 * (lr >> 2)] = q;
+        }
       }
-      tp[gi * 16 + cc] = s0 + s1;
     }
     {  // x_0 = c_0 / L00 + sum_a Linv(1+a,0) c_{1+a}
       double pr = (tid < KL) ? Lv[1 + tid] * rl[1 + tid] : 0.0;

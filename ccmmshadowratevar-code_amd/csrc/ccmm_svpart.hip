@@ -136,7 +136,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
                                                       const double* __restrict__ V0inv,
                                                       const double* __restrict__ V0invm, ChainState cs,
                                                       RngArgs ra, double* __restrict__ sepbuf,
-                                                      double* __restrict__ gbuf) {
+                                                      double* __restrict__ gbuf, int mode) {
   constexpr int CLD = NN + 1, XLD = 2 * NN + 1, NN2 = NN * NN;
   constexpr bool G3 = 3 * NN <= 64;
   using R = SvRec<NN>;
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   // ---------------------------------------------------------------- phase A: segments
   // per-wave LDS: myF[k*NN + r] fill column r of M_{t,left} (right-hand side of lane NN+r),
   // myD[r*NN + m] the left separator's accumulated -sum X2'X2 (row r)
-  for (int q = wave; q < P; q += NW) {
+  for (int q = wave; q < ((mode & 1) ? 0 : P); q += NW) {
     const int first = (q == 0) ? 0 : sv_sep(q - 1, T, P) + 1;
     const int last = (q == P - 1) ? T : sv_sep(q, T, P) - 1;
     const bool hasL = q > 0, hasR = q < P - 1;
@@ -381,7 +381,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   __syncthreads();
 
   // ---------------------------------------------------------------- phase B: separators
-  if (wave == 0 && P > 1) {
+  if (wave == 0 && P > 1 && !(mode & 2)) {
     double cg[NN], sr[NN];
 #pragma unroll
     for (int m = 0; m < NN; ++m) cg[m] = 0.0;
@@ -451,7 +451,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
     }
     sv_wave_sync();
   };
-  if (wave == 0 && P > 1) {
+  if (wave == 0 && P > 1 && !(mode & 4)) {
     for (int i = P - 2; i >= 0; --i) {
       const int sb = sv_sep(i, T, P);
       double lr[NN], lc[NN], rps[NN];
@@ -474,11 +474,11 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
     }
   }
   __syncthreads();
-  for (int q = wave; q < P; q += NW) {
+  for (int q = wave; q < ((mode & 8) ? 0 : P); q += NW) {
     const int first = (q == 0) ? 0 : sv_sep(q - 1, T, P) + 1;
     const int last = (q == P - 1) ? T : sv_sep(q, T, P) - 1;
     const bool hasL = q > 0, hasR = q < P - 1;
-    if (hasL) {  // g_first = -Q x_left, g_{t+1} = Q C_t^-T C_t^-1 g_t
+    if (hasL && !(mode & 16)) {  // g_first = -Q x_left, g_{t+1} = Q C_t^-T C_t^-1 g_t
       double g = 0.0;
 #pragma unroll
       for (int m = 0; m < NN; ++m) g = fma(-qrow[m], xsep[(q - 1) * NN + m], g);
@@ -539,28 +539,29 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
 
 template <int NN, int NW>
 static hipError_t sv_launch_one(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
-                                const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf) {
+                                const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
+                                int mode) {
   constexpr int CLD = NN + 1, XLD = 2 * NN + 1;
   const size_t lds = (size_t)(2 * NN * NN + kSvMaxSeg * NN + NW * sv_wave_lds(NN)) * sizeof(double);
   hipError_t e = hipFuncSetAttribute((const void*)k_sv_part<NN, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_sv_part<NN, NW>), dim3(d.B), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm, cs, ra,
-                     sep, gbuf);
+                     sep, gbuf, mode);
   return hipGetLastError();
 }
 
 hipError_t sv_launch_part(int N, hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
-                          const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf) {
+                          const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf, int mode) {
   switch (sv_bucket(N)) {
-    case 4: return sv_launch_one<4, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
-    case 8: return sv_launch_one<8, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
-    case 12: return sv_launch_one<12, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
-    case 16: return sv_launch_one<16, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
-    case 20: return sv_launch_one<20, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
-    case 24: return sv_launch_one<24, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
-    case 28: return sv_launch_one<28, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
-    default: return sv_launch_one<32, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf);
+    case 4: return sv_launch_one<4, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+    case 8: return sv_launch_one<8, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+    case 12: return sv_launch_one<12, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+    case 16: return sv_launch_one<16, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+    case 20: return sv_launch_one<20, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+    case 24: return sv_launch_one<24, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+    case 28: return sv_launch_one<28, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+    default: return sv_launch_one<32, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
   }
 }
 
