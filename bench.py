@@ -145,10 +145,26 @@ def main():
             flop = B * N * T * K * (K + 1)
         kms = ktimes[kname][0] / max(ktimes[kname][1], 1)
         ach = flop / (kms * 1e-3) / 1e12
+        pmc, pmc_src = load_pmc()
+        traffic = pmc.get(kname, {}).get("hbm_bytes")
         out["roofline"] = {"kernel": kname, "bound": "mfma", "achieved": round(ach, 3),
                            "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                           "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4),
+                           "traffic": None if traffic is None else int(traffic),
+                           "traffic_source": pmc_src if traffic is not None else None,
                            "flop_per_launch": int(flop), "avg_launch_ms": round(kms, 4)}
+        # streamed (HBM-roofline) kernels: algorithmic bytes per launch / launch time
+        # (B_SV = 33*T*N bytes per chain-sweep for the SV block)
+        hb = {}
+        for kn, nbytes in (("k_sv_part", B * 33 * T * N), ("k_sv_mix", B * 33 * T * N)):
+            if ktimes.get(kn, (0, 0))[1]:
+                ms = ktimes[kn][0] / ktimes[kn][1]
+                gbs = nbytes / (ms * 1e-3) / 1e9
+                hb[kn] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": int(nbytes),
+                          "traffic": (None if pmc.get(kn, {}).get("hbm_bytes") is None
+                                      else int(pmc[kn]["hbm_bytes"]))}
+        out["hbm_kernels"] = hb
         out["kernel_ms_per_sweep"] = per
         out["dominant_kernel"] = dom
     if world == 1 and not args.no_cpu:
@@ -156,6 +172,19 @@ def main():
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def load_pmc():
+    """HBM bytes per launch from the newest committed rocprofv3 PMC summary
+    (profiles/*_pmc.json, written by tools/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes over this same bench command)."""
+    files = sorted((ROOT / "profiles").glob("*_pmc.json"))
+    if not files:
+        return {}, None
+    try:
+        return json.loads(files[-1].read_text()), f"profiles/{files[-1].name}"
+    except (OSError, ValueError):
+        return {}, None
 
 
 def cpu_baseline(budget_s):
