@@ -22,6 +22,7 @@ CCMM_OK = 0
 CCMM_ERR_NOTSPD = -4
 MODEL_LINEAR = 0
 MODEL_BLOCKHYBRID = 1
+MODEL_HYBRID = 2  # mcmcVARhybridGibbs.m: K = N*p + 1 + Ns*p
 
 RNG_PAI, RNG_A, RNG_SVU, RNG_SVZ, RNG_PHI, RNG_ELB = 1, 2, 3, 4, 5, 6
 
@@ -256,7 +257,7 @@ class Chains:
                  elb_gibbsburn=100, elb=0.25):
         self.ctx = ctx
         self.lib = ctx.lib
-        K = N * p + 1
+        K = N * p + 1 + (Ns * p if model == MODEL_HYBRID else 0)
         self.cfg = ChainConfig(model, N, p, K, T, B, ndata, N + 3 if dPHI is None else dPHI,
                                int(crn), store_capacity, logy2offset, seed, Ns, elbTmax,
                                elb_gibbsburn, elb)
@@ -333,7 +334,7 @@ class Chains:
                    PHI_all=np.zeros((M, N * (N + 1) // 2, B), order="F"),
                    invA_all=np.zeros((M, N, N, B), order="F"),
                    sqrtht_all=np.zeros((M, T, N, B), order="F"))
-        if self.model == MODEL_BLOCKHYBRID:
+        if self.model in (MODEL_BLOCKHYBRID, MODEL_HYBRID):
             out["shadowrate_all"] = np.zeros((M, self.Ns, self.elbTmax, B), order="F")
         rc = self.lib.ccmm_chains_get_draws(self.handle, *[_ptr(out.get(k)) for k in
                                                            ("PAI_all", "PHI_all", "invA_all",
@@ -342,12 +343,15 @@ class Chains:
         return out
 
     # ------------------------------------------------ block-hybrid shadow-rate model
-    def set_elb_model(self, ndxS, actual_block):
-        """ndxS: 0-based shadow-rate variable indices; actual_block: bool N (actualrateBlock)."""
+    def set_elb_model(self, ndxS, actual_block=None):
+        """ndxS: 0-based shadow-rate variable indices; actual_block: bool N (actualrateBlock;
+        None for the hybrid model)."""
         nd = np.ascontiguousarray(ndxS, dtype=np.int32)
-        ab = np.ascontiguousarray(np.asarray(actual_block, bool), dtype=np.uint8)
-        _check(self.lib.ccmm_chains_set_elb_model(self.handle, nd.ctypes.data_as(_ip),
-                                                  ab.ctypes.data_as(_u8p)),
+        abp = None
+        if actual_block is not None:
+            ab = np.ascontiguousarray(np.asarray(actual_block, bool), dtype=np.uint8)
+            abp = ab.ctypes.data_as(_u8p)
+        _check(self.lib.ccmm_chains_set_elb_model(self.handle, nd.ctypes.data_as(_ip), abp),
                "ccmm_chains_set_elb_model")
 
     def set_elb_slot(self, slot, elbT0, sNaN):

@@ -168,6 +168,9 @@ struct ccmm_chains {
   // block-hybrid ELB model (mcmcVARshadowrateBlockHybrid.m): X/Y slabs 0..ndata-1 hold
   // the vintages' actual data, slabs ndata + c the chain's shadow-rate data
   bool bh = false;
+  // hybrid model (mcmcVARhybridGibbs.m): same chain layout as bh, one design per chain
+  // (CTA, no actual-rate block), trailing columns = censored actual-rate lags
+  bool hybrid = false;
   bool have_elb_model = false;
   std::vector<bool> have_elb_slot;
   std::vector<int> hNdxS, hElbT0, hElbT;
@@ -285,7 +288,8 @@ struct ccmm_chains {
   void init(ccmm_ctx* c, const ccmm_chain_config& cf, int nX, int nY) {
     ctx = c;
     cfg = cf;
-    bh = cf.model == CCMM_MODEL_BLOCKHYBRID;
+    bh = cf.model == CCMM_MODEL_BLOCKHYBRID || cf.model == CCMM_MODEL_HYBRID;
+    hybrid = cf.model == CCMM_MODEL_HYBRID;
     if (bh) {
       require(cf.Ns >= 1 && cf.Ns <= kElbNsMax, "Ns must be in [1, 4]");
       require(cf.elbTmax >= 0 && cf.elbTmax <= cf.T, "elbTmax must be in [0, T]");
@@ -294,7 +298,10 @@ struct ccmm_chains {
       require(cf.p >= 1, "p must be >= 1");
     }
     require(cf.N >= 1 && cf.N <= kMaxNSmall, "N must be in [1, 32]");
-    require(cf.K == cf.N * cf.p + 1 || cf.p == 0, "K must equal N*p+1");
+    if (hybrid)  // [1, lags of the N variables, lags of the Ns actual rates] (mcmcVARhybridGibbs.m:84)
+      require(cf.K == cf.N * cf.p + 1 + cf.Ns * cf.p, "hybrid model: K must equal N*p+1+Ns*p");
+    else
+      require(cf.K == cf.N * cf.p + 1 || cf.p == 0, "K must equal N*p+1");
     require(cf.K >= 1 && cf.K <= 1536, "K must be in [1, 1536]");
     require(cf.T >= 2 && cf.B >= 1 && cf.ndata >= 1, "bad T/B/ndata");
     d.N = cf.N;
@@ -479,6 +486,8 @@ struct ccmm_chains {
     e.cond = eCond.p;
     e.Scur = eScur.p;
     e.condStride = elb_cond_stride(cfg.Ns, cfg.p);
+    e.kshadow = cfg.N * cfg.p + 1;
+    e.K = cfg.K;
     return e;
   }
 
@@ -1311,10 +1320,11 @@ ccmm_chains* ccmm_chains_create(ccmm_ctx* ctx, const ccmm_chain_config* cfg) {
   ccmm_chains* ch = nullptr;
   int rc = guarded([&] {
     require(ctx && cfg, "null argument");
-    require(cfg->model == CCMM_MODEL_LINEAR || cfg->model == CCMM_MODEL_BLOCKHYBRID, "unknown model");
+    require(cfg->model == CCMM_MODEL_LINEAR || cfg->model == CCMM_MODEL_BLOCKHYBRID ||
+                cfg->model == CCMM_MODEL_HYBRID, "unknown model");
     HIPCHECK(hipSetDevice(ctx->device));
     ch = new ccmm_chains;
-    const int extra = cfg->model == CCMM_MODEL_BLOCKHYBRID ? cfg->B : 0;
+    const int extra = cfg->model != CCMM_MODEL_LINEAR ? cfg->B : 0;
     ch->init(ctx, *cfg, cfg->ndata + extra, cfg->ndata + extra);
     HIPCHECK(hipStreamSynchronize(ctx->stream));
     return 0;
@@ -1478,10 +1488,17 @@ int ccmm_chains_get_draws(ccmm_chains* ch, double* PAI_all, double* PHI_all, dou
 
 int ccmm_chains_set_elb_model(ccmm_chains* ch, const int* ndxS, const uint8_t* actual_block) {
   return guarded([&] {
-    require(ch && ndxS && actual_block, "null argument");
-    require(ch->bh, "chain set was not created with CCMM_MODEL_BLOCKHYBRID");
+    require(ch && ndxS, "null argument");
+    require(ch->bh, "chain set was not created with CCMM_MODEL_BLOCKHYBRID / CCMM_MODEL_HYBRID");
+    require(actual_block || ch->hybrid, "null argument");
     HIPCHECK(hipSetDevice(ch->ctx->device));
     HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    std::vector<uint8_t> none(ch->cfg.N, 0);
+    if (ch->hybrid) {
+      for (int i = 0; actual_block && i < ch->cfg.N; ++i)
+        require(!actual_block[i], "hybrid model has no actual-rate block (pass NULL or zeros)");
+      actual_block = none.data();
+    }
     ch->set_elb_model(ndxS, actual_block);
     return 0;
   });

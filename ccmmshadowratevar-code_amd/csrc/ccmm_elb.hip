@@ -47,6 +47,7 @@ struct ElbDev {
   double* cond;   // [B][elbTmax][condStride]
   double* Scur;   // [B][elbTmax][Ns] shadow rates (in/out)
   int condStride;
+  int kshadow, K;  // hybrid model: PAI rows kshadow..K-1 load the actual-rate lags (K > kshadow)
 };
 
 // condition record per censored month (doubles):
@@ -100,6 +101,9 @@ __global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, Cha
   for (int q = tid; q < T * N; q += 256) {
     const int t = q / N, i = q % N;
     double yh = 0.0;
+    // hybrid: Yhatactual = Xffrlags(elbT0+t, :) * PAIactual (mcmcVARhybridGibbs.m:429-431)
+    for (int k = e.kshadow; k < e.K; ++k) yh = fma(Xa[(size_t)k * TP + T0 + t], PAI[(size_t)i * KP + k], yh);
+    // block hybrid: Yhatactual from the actual-rate block's shadow-rate lags (:400-403)
     if (e.actual[i])
       for (int l = 0; l < p; ++l)
         for (int si = 0; si < Ns; ++si) {

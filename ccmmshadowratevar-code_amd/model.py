@@ -162,3 +162,55 @@ def build_bh(thisT, p, np_, data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS, minne
     sNaN = yNaN[elbT0:, :][:, ndxS].T if elbT > 0 else np.zeros((ndxS.size, 0), bool)
     return BHModel(var=m, ndxS=ndxS, ndxO=ndxO, actual_block=actual, elbT0=int(elbT0), elbT=elbT,
                    sNaN=sNaN, ELB=float(ELBbound), warn_elbT0=bool(warn))
+
+
+@dataclass
+class HybridModel:
+    """A vintage of the hybrid shadow-rate VAR (mcmcVARhybridGibbs.m:33-339): the VAR
+    on the shadow-rate data plus the lags of the actual policy rates floored at the ELB."""
+    var: VARModel             # X = [1, lags, Xffrlags] (K = Kshadow + Ns p), priors incl. FFRlags
+    Kshadow: int              # 1 + N p (:90)
+    ndxS: np.ndarray          # ndxSHADOWRATE (0-based)
+    elbT0: int
+    elbT: int
+    sNaN: np.ndarray          # bool Ns x elbT (:206-210)
+    ELB: float
+    warn_elbT0: bool          # :216-218 warning condition
+
+
+def build_hybrid(thisT, p, np_, data0, ydates0, ndxSHADOWRATE, minnesotaPriorMean, ELBbound, elbT0,
+                 doRATSprior=True) -> HybridModel:
+    """Host setup of mcmcVARhybridGibbs.m for the 1-based jump-off ``thisT``."""
+    m = build_var(thisT, p, np_, data0, ydates0, minnesotaPriorMean, doRATSprior)
+    theta = (0.04, 0.25, 100.0, 2.0) if doRATSprior else (0.05, 0.5, 100.0, 2.0)
+    N, T, data = m.N, m.T, m.data
+    Nobs = data.shape[0]
+    ndxS = np.asarray(ndxSHADOWRATE, int)
+    Ns = ndxS.size
+    # Xffrlags: lag l of actual rate s in column (l-1) Ns + s, floored at the ELB (:77-84)
+    Xffr = np.hstack([data[p - l:Nobs - l, ndxS] for l in range(1, p + 1)])
+    Xffr = np.where(Xffr < ELBbound, ELBbound, Xffr)
+    # FFRlags prior (:275-298): Minnesota variance of "variable ndxS(s), lag l" in equation i
+    s2 = (m.ARresid ** 2).sum(axis=0) / (T - 2)
+    lag = np.repeat(np.arange(1, p + 1), Ns).astype(float)
+    var = np.tile(ndxS, p)
+    own = var[None, :] == np.arange(N)[:, None]            # N(eq) x Ns p
+    decay = lag[None, :] ** theta[3]
+    pv = np.where(own, theta[0] / decay, (s2[:, None] / s2[var][None, :]) * theta[0] * theta[1] / decay)
+    iVd = np.vstack([m.iVdiag, 1.0 / pv.T])
+    iVb = np.vstack([m.iVb, np.zeros((Ns * p, N))])        # prior mean 0 (:276)
+    jump = np.concatenate([m.Xjumpoff, np.maximum(np.concatenate(
+        [data[Nobs - l, ndxS] for l in range(1, p + 1)]), ELBbound)])  # :117-121
+    hv = VARModel(N=N, p=p, K=m.K + Ns * p, T=T, Y=m.Y, X=np.hstack([m.X, Xffr]), iVdiag=iVd,
+                  iVb=iVb, sPHI=m.sPHI, dPHI=m.dPHI, Vol_0mean=m.Vol_0mean,
+                  Vol_0vcvsqrt=m.Vol_0vcvsqrt, ARresid=m.ARresid, Xjumpoff=jump, data=data)
+    cens = np.zeros_like(data, dtype=bool)
+    cens[:, ndxS] = data[:, ndxS] <= ELBbound               # :178-187
+    yNaN = cens[p:, :]
+    elbT = max(0, T - elbT0)
+    if elbT > 0 and np.any(yNaN[:elbT0, ndxS]):
+        raise ValueError("something off about elbT0")       # :212-214
+    warn = elbT > 0 and not np.any(yNaN[elbT0, ndxS])       # :216-218
+    sNaN = yNaN[elbT0:, :][:, ndxS].T if elbT > 0 else np.zeros((Ns, 0), bool)
+    return HybridModel(var=hv, Kshadow=m.K, ndxS=ndxS, elbT0=int(elbT0), elbT=elbT, sNaN=sNaN,
+                       ELB=float(ELBbound), warn_elbT0=bool(warn))

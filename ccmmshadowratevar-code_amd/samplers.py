@@ -14,7 +14,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _abi
-from .model import build_bh, build_var, initial_state
+from .model import build_bh, build_hybrid, build_var, initial_state
 
 _CTX = {}
 
@@ -125,6 +125,56 @@ def mcmcVARshadowrateBlockHybrid(thisT, MCMCdraws, p, np_, data0, ydates0, actua
     sr = out.get("shadowrate_all", np.full((MCMCdraws, len(bm.ndxS), 0, B), np.nan))
     res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"], sr,
            np.full((MCMCdraws, len(bm.ndxS), bm.elbT, B), np.nan)]
+    if B == 1:
+        res = [a[..., 0] for a in res]
+    return tuple(res)
+
+
+def mcmcVARhybridGibbs(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateWeight,
+                       minnesotaPriorMean, doRATSprior, ndxSHADOWRATE, ndxOTHERYIELDS, doELBsampling,
+                       doELBsampleAlternate, ELBbound, elbT0, check_stationarity=0, IRF1scale=None,
+                       IRFcumcode=None, yrealized=None, fcstNdraws=None, fcstNhorizons=None,
+                       rndStream=1012023, doprogress=False, *, nchains=1, device=0, burnin=None,
+                       gibbsburn=100):
+    """mcmcVARhybridGibbs.m:1-14, outputs PAI_all (M x K x N, K = 1 + N p + Ns p),
+    PHI_all, invA_all, sqrtht_all, shadowrate_all (M x Nshadowrates x elbT),
+    missingrate_all (NaN: it is the first PS proposal, :486).
+
+    The reference draws the shadow rates by accept-first PS proposals with the Gibbs
+    sampler as fallback (:458-483); the proposal sampler VARTVPSVprecisionsamplerNaN
+    is in the absent em-matlabbox toolbox, so the Gibbs draw serves every sweep.
+    actualrateWeight is unused, as in the reference (:16).  Indices are 0-based."""
+    if check_stationarity:
+        import warnings
+        warnings.warn("no stationarity check for hybrid model")  # :22-24
+    if not doELBsampling or doELBsampleAlternate:
+        raise NotImplementedError("doELBsampling=false / doELBsampleAlternate=true need the "
+                                  "missing-data sampler VARTVPSVprecisionsamplerNaN (absent "
+                                  "em-matlabbox); out of scope")
+    if fcstNdraws or IRF1scale is not None:
+        raise NotImplementedError("predictive density / IRF outputs are a later row (SURVEY §8f)")
+    hm = build_hybrid(thisT, p, np_, data0, ydates0, ndxSHADOWRATE, minnesotaPriorMean, ELBbound,
+                      elbT0, doRATSprior)
+    if hm.warn_elbT0:
+        import warnings
+        warnings.warn("elbT0 + 1 should be a missing obs, but it is not ...")  # :216-218
+    m = hm.var
+    B = int(nchains)
+    burn = MCMCdraws if burnin is None else int(burnin)
+    ch = _abi.Chains(context(device), N=m.N, p=m.p, T=m.T, B=B, ndata=1, crn=False,
+                     store_capacity=MCMCdraws, seed=int(rndStream), model=_abi.MODEL_HYBRID,
+                     Ns=len(hm.ndxS), elbTmax=hm.elbT, elb_gibbsburn=gibbsburn, elb=ELBbound)
+    ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    ch.set_elb_model(hm.ndxS, None)
+    ch.set_elb_slot(0, hm.elbT0, hm.sNaN)
+    st = initial_state(m, B)
+    ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+    _run_chain_set(ch, burn, MCMCdraws, doprogress)
+    out = ch.get_draws()
+    ch.close()
+    sr = out.get("shadowrate_all", np.full((MCMCdraws, len(hm.ndxS), 0, B), np.nan))
+    res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"], sr,
+           np.full((MCMCdraws, len(hm.ndxS), hm.elbT, B), np.nan)]
     if B == 1:
         res = [a[..., 0] for a in res]
     return tuple(res)

@@ -51,6 +51,7 @@ extern "C" {
 /* model ids for the sweep-level API */
 #define CCMM_MODEL_LINEAR 0        /* mcmcVAR.m */
 #define CCMM_MODEL_BLOCKHYBRID 1   /* mcmcVARshadowrateBlockHybrid.m */
+#define CCMM_MODEL_HYBRID 2        /* mcmcVARhybridGibbs.m: K = N*p + 1 + Ns*p, X = [1, lags, Xffrlags] */
 
 /* RNG block ids (Philox counter word 3); also the order of the per-sweep CRN blocks */
 #define CCMM_RNG_PAI 1   /* randn(K,N)            CTA.m:58 / CTAsys.m:58 */
@@ -185,7 +186,14 @@ int ccmm_chains_stored(const ccmm_chains* ch);
 int ccmm_chains_get_draws(ccmm_chains* ch, double* PAI_all, double* PHI_all, double* invA_all,
                           double* sqrtht_all, double* shadowrate_all);
 
-/* ---- block-hybrid shadow-rate model (mcmcVARshadowrateBlockHybrid.m) ----
+/* ---- shadow-rate models: block-hybrid (mcmcVARshadowrateBlockHybrid.m) and
+ *      hybrid (mcmcVARhybridGibbs.m) ----
+ * Hybrid: every equation uses the chain's X = [1, lags of the shadow-rate data,
+ * Xffrlags] (CTA, mcmcVARhybridGibbs.m:376); the trailing Ns*p columns of the
+ * slot X are the actual-rate lags floored at the ELB (:77-84) and stay fixed;
+ * the ELB step adds Yhatactual = Xffrlags * PAI(Kshadow+1:end,:) (:429-431) and
+ * uses PAI(1:Kshadow,:) in the companion matrix (:435-437).  actual_block must be
+ * NULL (or all zero) for the hybrid model.
  * Data slot X/Y (ccmm_chains_set_data) are the vintage's ACTUAL data (X0, Y0,
  * :310-316); every chain keeps its own shadow-rate copy, reset to the slot's
  * data by ccmm_chains_set_state.  Equations with actual_block[j] != 0 use the

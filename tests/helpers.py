@@ -70,3 +70,16 @@ def toy_bh_setup(bh, N=5, p=2, Tobs=150, ndxS=(2, 3), ndxO=(4,), seed=3, elb=0.2
 
 def bh_crn_flat(bh, crn, bs):
     return np.concatenate([crn[k].ravel(order="F") for k, _ in bh.bh_crn_sizes(bs)])
+
+
+def toy_hybrid_setup(hy, N=5, p=2, Tobs=150, ndxS=(2, 3), seed=3, elb=0.25):
+    """Toy hybrid model (mcmcVARhybridGibbs.m) on the block-hybrid toy data."""
+    data = synth_bh_data(N, p, Tobs, ndxS=ndxS, seed=seed, elb=elb)
+    ydates = np.arange(Tobs, dtype=float)
+    hit = np.any(data[:, list(ndxS)] <= elb, axis=1)
+    elbT0 = int(np.argmax(hit)) - p
+    return hy.hybrid_setup(Tobs, p, 12, data, ydates, np.asarray(ndxS), np.ones(N), elb, elbT0)
+
+
+def hybrid_crn_flat(hy, crn, hs):
+    return np.concatenate([crn[k].ravel(order="F") for k, _ in hy.hybrid_crn_sizes(hs)])
