@@ -45,6 +45,9 @@ def parse():
                     help="budget of the CPU-oracle baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--bh-steps", type=int, default=5,
+                    help="timed sweeps of the block-hybrid secondary line (configs[2]); 0 = skip")
+    ap.add_argument("--bh-warmup", type=int, default=2)
     return ap.parse_args()
 
 
@@ -100,6 +103,9 @@ def main():
         elapsed = float(t.item())
     draws = ch.get_draws()
     assert np.all(np.isfinite(draws["PAI_all"])), "non-finite draws"
+    ch.close()
+    # secondary line (configs[2]) runs on every rank: it has its own barrier/max-reduction
+    bh = bench_block_hybrid(pkg, ctx, d, B, args, rank, barrier, dist) if args.bh_steps > 0 else None
 
     if rank != 0:
         if dist is not None:
@@ -167,11 +173,80 @@ def main():
         out["hbm_kernels"] = hb
         out["kernel_ms_per_sweep"] = per
         out["dominant_kernel"] = dom
+    if bh is not None:
+        out["block_hybrid"] = bh
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def bench_block_hybrid(pkg, ctx, d, B, args, rank, barrier, dist):
+    """Secondary line, BASELINE.json configs[2] (doMCMCshadowrateBlockHybrid, ELB = 0.25):
+    B chains of the block-hybrid shadow-rate sweep (CTAsys -> A -> SV -> PHI -> ELB Gibbs
+    with gibbsburn + 1 = 101 passes and inverse-CDF truncated normals -> X/Y rebuild,
+    mcmcVARshadowrateBlockHybrid.m:332-520) at the 2022-08 jump-off: elbT = 165 months,
+    109 censored months / 276 censored cells.  Same timing protocol as the main line."""
+    import time as _t
+    p = 12
+    mpm = pkg.model.setMinnesotaMean(d["ncode"])
+    ndxS, ndxO, _ = pkg.model.setShadowYields(d["ncode"], 0.25)
+    e0 = pkg.model.elbT0_of(d["data"], ndxS, 0.25, p)
+    bm = pkg.model.build_bh(len(d["ydates"]), p, 12, d["data"], d["ydates"], ndxS, ndxO, mpm,
+                            0.25, e0, True)
+    m = bm.var
+    Ns = len(bm.ndxS)
+    ch = pkg.Chains(ctx, N=m.N, p=p, T=m.T, B=B, crn=False,
+                    store_capacity=args.bh_warmup + args.bh_steps, seed=1012023 + 7919 * rank + 1,
+                    model=pkg.MODEL_BLOCKHYBRID, Ns=Ns, elbTmax=bm.elbT, elb_gibbsburn=100,
+                    elb=0.25)
+    ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    ch.set_elb_model(bm.ndxS, bm.actual_block)
+    ch.set_elb_slot(0, bm.elbT0, bm.sNaN)
+    st = pkg.model.initial_state(m, B)
+    ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+    ch.sweep(args.bh_warmup, store=True)
+    barrier()
+    if not args.no_profile:
+        ch.profile(True)
+    t0 = _t.perf_counter()
+    ch.sweep(args.bh_steps, store=True)
+    barrier()
+    el = _t.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{ctx.device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    S = ch.get_shadowrate()
+    assert np.all(np.isfinite(S)), "non-finite shadow rates"
+    world = dist.get_world_size() if dist is not None else 1
+    ncens = int(np.any(bm.sNaN, axis=0).sum())
+    res = {"workload": "configs[2]: block-hybrid shadow-rate BVAR-SV (mcmcVARshadowrateBlockHybrid) "
+                       f"N=20 p=12 T={m.T} ELB=0.25, Ns={Ns}, elbT={bm.elbT}, {ncens} censored "
+                       f"months / {int(bm.sNaN.sum())} cells, ELB Gibbs (101 passes) every sweep, "
+                       f"{B} chains per GPU",
+           "value": round(world * B * args.bh_steps / el, 3), "unit": "sweeps/s",
+           "ms_per_step": round(1e3 * el / args.bh_steps, 4), "steps": args.bh_steps,
+           "warmup": args.bh_warmup}
+    if not args.no_profile:
+        kt = ch.kernel_times()
+        res["kernel_ms_per_sweep"] = {k: round(v[0] / v[1], 4) for k, v in kt.items() if v[1]}
+        # k_elb_gibbs streams each censored month's conditional record (elb_cond_stride
+        # minus the Ns x Ns Omega block: 228 doubles at Ns=3, p=12) once per pass and reads
+        # and writes the chain's Ns x elbT shadow rates once (ccmm_elb.hip k_elb_gibbs)
+        if kt.get("k_elb_gibbs", (0, 0))[1]:
+            rec = Ns + Ns * (Ns - 1) + Ns + 2 * p * Ns * Ns
+            nbytes = B * (101 * ncens * rec * 8 + 2 * 8 * Ns * bm.elbT)
+            ms = kt["k_elb_gibbs"][0] / kt["k_elb_gibbs"][1]
+            gbs = nbytes / (ms * 1e-3) / 1e9
+            res["elb_gibbs"] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                "bytes_per_launch": int(nbytes), "avg_launch_ms": round(ms, 4),
+                                "note": "one wave per chain, 101 sequential passes: latency-bound"}
+    ch.close()
+    return res
 
 
 def load_pmc():

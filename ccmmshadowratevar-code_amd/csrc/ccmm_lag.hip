@@ -56,7 +56,17 @@ __device__ __forceinline__ double gl_rsqrt(double d) {  // rsq estimate + 2 Newt
   return r;
 }
 
-__device__ __forceinline__ int gl_factor_inv(const double* Dg, double* Ws, int lane) {
+// Opaque copy of a per-lane value: the factorisation loops below are inlined into the
+// panel loop, and without this LLVM hoists every lane-dependent constant they derive
+// (the δ_ic of the inverse, per-slot LDS addresses) out of that loop and spills them
+// to scratch, putting a scratch reload on the serial path of every panel step.
+__device__ __forceinline__ int gl_opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+__device__ __forceinline__ int gl_factor_inv(const double* Dg, double* Ws, int lane_in) {
+  const int lane = gl_opaque(lane_in);
   double row[16];
   double rdiag = 1.0, dmin = 1.0;  // smallest pivot: a non-positive one flags the system
 #pragma unroll
@@ -165,7 +175,8 @@ __device__ __forceinline__ int gram_lag_factor(const GlArgs& g, double* sm, int 
   constexpr int NTILE = gl_ntile(NT);
   constexpr int TPW = gl_tpw(NT);
   constexpr int KL = 16 * NT;
-  const int lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int lane = tid & 63, lr0 = lane & 15, lq0 = lane >> 4;
+  const int lr = lr0, lq = lq0;
   int bad = 0;
   int sti[TPW], stj[TPW];
 #pragma unroll
@@ -237,6 +248,7 @@ __device__ __forceinline__ int gram_lag_factor(const GlArgs& g, double* sm, int 
     if (own && !(g.mode & 256)) bad |= gl_factor_inv(Ws, LinvB, lane);
   }
   for (int p = 0; p < (do_chol ? NT : 0); ++p) {
+    const int lr = gl_opaque(lr0), lq = gl_opaque(lq0);  // no hoisted per-slot addresses
     __syncthreads();  // LinvB = L_pp^-1 visible; the previous trailing reads of Pn are done
     double* Pn = Pn0;
 #pragma unroll
@@ -302,6 +314,7 @@ __device__ __forceinline__ int gram_lag_factor(const GlArgs& g, double* sm, int 
   // upper tile (a, b) lives in slot (ti = b, tj = a); slot (i, j) holds U_ij until
   // step j, then B_ij, then (after step i) Z_ij.
   for (int p = ((g.mode & 4) ? -1 : NT - 1); p >= 0; --p) {
+    const int lr = gl_opaque(lr0), lq = gl_opaque(lq0);
     double* XD = Dg;                                  // U_pp^-1
     double* LP = Pn0 + (p & 1) * NT * kGlTile;        // U_ip, i < p (slot i)
     double* XR = Pn0 + ((p + 1) & 1) * NT * kGlTile;  // Z_pj, j >= p (slot j)
@@ -467,7 +480,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
   const int c = blockIdx.x;
   const int s = cs.slot[c];
   const int T = Tslot[s];
-  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int tid = threadIdx.x, lane0 = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Rng rng = ra.make(c);
   const double* ih2 = cs.ih2 + (size_t)c * N * TP;
@@ -486,6 +499,9 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
   int cur = -1;
 
   for (int j = 0; j < N; ++j) {
+    // per-equation opaque lane ids: no lane-derived address is hoisted out of the
+    // equation loop next to the 120 Linv registers (see gl_opaque)
+    const int lane = gl_opaque(lane0), lr = lane & 15, lq = lane >> 4;
     const int mat = c * N + j;
     const int slab = ls.idx[mat];
     const double* Lo = cs.G + (size_t)mat * KP * KP;
