@@ -414,6 +414,8 @@ struct ccmm_chains {
   }
   int lag_mode = std::getenv("CCMM_LAG_MODE") ? std::atoi(std::getenv("CCMM_LAG_MODE")) : 0;
   int sv_mode = std::getenv("CCMM_SV_MODE") ? std::atoi(std::getenv("CCMM_SV_MODE")) : 0;
+  // timing-only ablation of k_elb_gibbs (results invalid): 1 no truncnorm, 2 no uniforms
+  int elb_mode = std::getenv("CCMM_ELB_MODE") ? std::atoi(std::getenv("CCMM_ELB_MODE")) : 0;
   LagSel lagsel() const { return LagSel{Dpool.p, xidx.p, dColmap.p, ldd, drows, cfg.p, lag_mode}; }
   // D (rows x ldd) of a slot from its X (T x K) and Y (T x N): rows 0..p-1 from the
   // lags of X's first row, rows p.. = Y.  Exact check that X is that lag design.
@@ -488,6 +490,7 @@ struct ccmm_chains {
     e.condStride = elb_cond_stride(cfg.Ns, cfg.p);
     e.kshadow = cfg.N * cfg.p + 1;
     e.K = cfg.K;
+    e.mode = elb_mode;
     return e;
   }
 
@@ -873,7 +876,7 @@ struct ccmm_chains {
     launch(KID_ELBCOND, [&] {
       hipLaunchKernelGGL(k_elb_cond, dim3(e.elbTmax, d.B), dim3(64), lds_cond, ctx->stream, d, e, cs);
     });
-    const size_t lds_gibbs = (size_t)e.elbTmax * Ns * sizeof(double);
+    const size_t lds_gibbs = (size_t)2 * e.elbTmax * Ns * sizeof(double);  // S | uniforms
     launch(KID_ELBGIBBS, [&] {
       switch (Ns) {
 #define CASE_NS(NS)                                                                            \

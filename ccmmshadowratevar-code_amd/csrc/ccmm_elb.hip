@@ -48,6 +48,7 @@ struct ElbDev {
   double* Scur;   // [B][elbTmax][Ns] shadow rates (in/out)
   int condStride;
   int kshadow, K;  // hybrid model: PAI rows kshadow..K-1 load the actual-rate lags (K > kshadow)
+  int mode;        // CCMM_ELB_MODE timing ablation (0 in production)
 };
 
 // condition record per censored month (doubles):
@@ -376,7 +377,8 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
   const Rng rng = ra.make(c);
   const int ncol = 2 * p * NS;
   const int head = elb_cond_head(NS);
-  double* Sl = sm;  // T x NS (t-major)
+  double* Sl = sm;           // T x NS (t-major)
+  double* Ul = sm + T * NS;  // this pass's uniforms, T x NS (t-major)
   double* Sc = e.Scur + (size_t)c * e.elbTmax * NS;
   const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * NS;
   const int* cl = e.cens + (size_t)s * e.elbTmax;
@@ -402,13 +404,30 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
   double hdn[kHd], g0n[NS], g1n[NS];
   load_rec(0, hd, g0, g1);
   for (int n = 0; n < e.passes; ++n) {
+    // the pass's uniforms rand(Ns, elbT) (gibbsdrawShadowrates.m:173, page n) are data
+    // independent: all lanes draw them up front (Philox pairs in parallel, or the CRN
+    // page), so no generator sits on the serial month-to-month path below
+    if (rng.crn) {
+      for (int q = lane; q < T * NS; q += 64) Ul[q] = rng.uniform(CCMM_RNG_ELB, (uint32_t)(q + T * NS * n));
+    } else {
+      const uint32_t base = (uint32_t)(T * NS * n);  // even when T * NS is odd: handle by index
+      for (int q = 2 * lane; q < T * NS + 1; q += 128) {
+        // pair (base + q) >> 1 covers idx base+q and its partner; write both when in range
+        const uint32_t i0 = base + (uint32_t)q - ((base + (uint32_t)q) & 1u);
+        const u32x4 r = rng.raw(CCMM_RNG_ELB, i0 >> 1);
+        const int q0 = (int)(i0 - base), q1 = q0 + 1;
+        if (q0 >= 0 && q0 < T * NS) Ul[q0] = u01(r.x, r.y);
+        if (q1 >= 0 && q1 < T * NS) Ul[q1] = u01(r.z, r.w);
+      }
+    }
+    __syncthreads();
     for (int ci = 0; ci < nc; ++ci) {
       const int t = cl[ci];
       // prefetch next month's record (wraps to month 0 of the next pass)
       const int cn = (ci + 1 < nc) ? ci + 1 : 0;
       load_rec(cn, hdn, g0n, g1n);
       double u[NS];
-      for (int a = 0; a < NS; ++a) u[a] = rng.uniform(CCMM_RNG_ELB, (uint32_t)(a + NS * (t + T * n)));
+      for (int a = 0; a < NS; ++a) u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
       // Spost = a_t + Σ G S(neighbours)
       const int tn0 = t + off0, tn1 = t + off1;
       const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
@@ -430,7 +449,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
           mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
           ++y;
         }
-        cur[a] = elb_trunc_normal(mu, so[a], e.elb, u[a]);
+        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a]);
       }
       for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
       for (int q = 0; q < kHd; ++q) hd[q] = hdn[q];
