@@ -24,7 +24,8 @@ MODEL_LINEAR = 0
 MODEL_BLOCKHYBRID = 1
 MODEL_HYBRID = 2  # mcmcVARhybridGibbs.m: K = N*p + 1 + Ns*p
 
-RNG_PAI, RNG_A, RNG_SVU, RNG_SVZ, RNG_PHI, RNG_ELB = 1, 2, 3, 4, 5, 6
+RNG_PAI, RNG_A, RNG_SVU, RNG_SVZ, RNG_PHI, RNG_ELB, RNG_FCST = 1, 2, 3, 4, 5, 6, 7
+CCMM_WARN_MVNCDF = 3
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int)
@@ -76,6 +77,9 @@ _SIGS = {
     "ccmm_chains_get_xy": (C.c_int, [C.c_void_p, _dp, _dp]),
     "ccmm_chains_profile": (C.c_int, [C.c_void_p, C.c_int]),
     "ccmm_chains_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _dp, _i64p, C.c_char_p, C.c_int]),
+    "ccmm_fcst": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp,
+                            _dp, _dp, _dp, _dp, _u8p, C.c_double, _dp, _dp, C.c_uint64,
+                            C.c_int, _dp, _dp, _dp, _dp, _ip]),
     "ccmm_selftest_mfma_f64": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
 }
 
@@ -216,6 +220,40 @@ class Context:
                                   _ptr(PHI))
         _check(rc, "ccmm_phi_iw")
         return sq, PHI
+
+    def fcst(self, PAI, invA, logSV0, sqrtPHI, Xjumpoff, yrealized, ndxYields, ELBbound,
+             fcstNhorizons, Ndraws, svz=None, z=None, seed=0, sweep=0):
+        """Predictive density of one kept draw per chain (mcmcVAR.m:298-381).
+
+        PAI K x N [x B], invA N x N [x B], logSV0 N [x B], sqrtPHI N x N [x B],
+        Xjumpoff K [x B], yrealized N, ndxYields bool N.  CRN: svz N x (H*Nd) [x B]
+        (mcmcVAR.m:302), z N x H x Nd [x B] (:306); None = Philox.
+        Returns fcstY, fcstYcensor (N x H x Nd x B), yhat (N x H x B),
+        scores (4 x Nd x B: logscore, ELB logscore, X logscore, I logscore), status (B).
+        """
+        PAI = _f(PAI)
+        K, N = PAI.shape[:2]
+        B = PAI.shape[2] if PAI.ndim == 3 else 1
+        p = (K - 1) // N
+        if K != N * p + 1:
+            raise ValueError("ccmm_fcst: K must equal N*p + 1 (mcmcVAR.m:108-115)")
+        H, Nd = int(fcstNhorizons), int(Ndraws)
+        fY = np.zeros((N, H, Nd, B), order="F")
+        fYc = np.zeros((N, H, Nd, B), order="F")
+        yhat = np.zeros((N, H, B), order="F")
+        sc = np.zeros((4, Nd, B), order="F")
+        st = np.zeros(B, dtype=np.int32)
+        mask = np.ascontiguousarray(np.asarray(ndxYields, bool).astype(np.uint8))
+        crn = svz is not None
+        rc = self.lib.ccmm_fcst(self.handle, B, N, p, H, Nd, _ptr(PAI), _ptr(_f(invA)),
+                                _ptr(_f(logSV0)), _ptr(_f(sqrtPHI)), _ptr(_f(Xjumpoff)),
+                                _ptr(_f(yrealized)), _ptr(mask, _u8p), float(ELBbound),
+                                _ptr(_f(svz)) if crn else None, _ptr(_f(z)) if crn else None,
+                                int(seed), int(sweep), _ptr(fY), _ptr(fYc), _ptr(yhat),
+                                _ptr(sc), _ptr(st, _ip))
+        if rc != CCMM_WARN_MVNCDF:
+            _check(rc, "ccmm_fcst")
+        return fY, fYc, yhat, sc, st
 
     def draw_trunc_normal_batch(self, mu, sig, elb, u):
         mu = _f(mu).ravel(order="F")

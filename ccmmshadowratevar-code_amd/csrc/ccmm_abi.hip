@@ -13,6 +13,7 @@
 #include "ccmm_cta_solve.hip"
 #include "ccmm_gram_chol.hip"
 #include "ccmm_elb.hip"
+#include "ccmm_fcst.hip"
 #include "ccmm_lag.h"
 #include "ccmm_svpart.h"
 #include <cstdlib>
@@ -1597,6 +1598,111 @@ int ccmm_chains_kernel_times(ccmm_chains* ch, int max, double* ms, int64_t* laun
       names[names_len - 1] = 0;
     }
     return KID_COUNT;
+  });
+}
+
+// Gauss-Legendre nodes/weights by Newton on P_n (host, once); negative half
+static GLNodes make_gl_nodes() {
+  GLNodes g{};
+  const int ns[3] = {6, 12, 20};
+  for (int r = 0; r < 3; ++r) {
+    const int n = ns[r];
+    for (int i = 0; i < n / 2; ++i) {
+      double x = -std::cos(M_PI * (i + 0.75) / (n + 0.5));
+      double dp = 0.0;
+      for (int it = 0; it < 100; ++it) {
+        double p0 = 1.0, p1 = x;
+        for (int k = 2; k <= n; ++k) {
+          const double p2 = ((2.0 * k - 1.0) * x * p1 - (k - 1.0) * p0) / k;
+          p0 = p1;
+          p1 = p2;
+        }
+        dp = n * (x * p1 - p0) / (x * x - 1.0);
+        const double dx = p1 / dp;
+        x -= dx;
+        if (std::fabs(dx) < 1e-17) break;
+      }
+      g.x[r][i] = x;
+      g.w[r][i] = 2.0 / ((1.0 - x * x) * dp * dp);
+    }
+  }
+  return g;
+}
+
+int ccmm_fcst(ccmm_ctx* ctx, int B, int N, int p, int H, int Nd, const double* PAI,
+              const double* invA, const double* logSV0, const double* sqrtPHI,
+              const double* Xjumpoff, const double* yrealized, const uint8_t* ndxYields,
+              double elb, const double* svz, const double* z, uint64_t seed, int sweep,
+              double* fcstY, double* fcstYcensor, double* yhat, double* scores, int* status) {
+  return guarded([&] {
+    require(ctx && PAI && invA && logSV0 && sqrtPHI && Xjumpoff && yrealized && ndxYields &&
+                fcstY && fcstYcensor && yhat && scores,
+            "null argument");
+    require(B > 0 && N > 0 && N <= kFcstMaxN && p > 0 && H > 0 && Nd > 0, "unsupported size");
+    require((svz == nullptr) == (z == nullptr), "svz and z must both be given or both NULL");
+    const int K = N * p + 1;
+    int nwx = 0;
+    for (int i = 0; i < N; ++i) nwx += ndxYields[i] ? 0 : 1;
+    require(nwx > 0 && nwx < N, "need at least one macro series and one yield");
+    HIPCHECK(hipSetDevice(ctx->device));
+    int nw = std::min(Nd + 1, kFcstMaxWaves);
+    while (nw > 1 && fcst_lds_bytes(N, p, K, nw) > 160 * 1024) --nw;
+    const size_t lds = fcst_lds_bytes(N, p, K, nw);
+    require(lds <= 160 * 1024, "forecast state does not fit LDS");
+    static const GLNodes gl = make_gl_nodes();
+    auto up = [&](DBuf<double>& d, const double* h, size_t n) {
+      d.alloc(n);
+      HIPCHECK(hipMemcpyAsync(d.p, h, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    };
+    DBuf<double> dPAI, dinvA, dlog, dsq, dXj, dy, dsvz, dz, dfY, dfYc, dyhat, dsc;
+    DBuf<uint8_t> dmask;
+    DBuf<int> dst;
+    up(dPAI, PAI, (size_t)B * K * N);
+    up(dinvA, invA, (size_t)B * N * N);
+    up(dlog, logSV0, (size_t)B * N);
+    up(dsq, sqrtPHI, (size_t)B * N * N);
+    up(dXj, Xjumpoff, (size_t)B * K);
+    up(dy, yrealized, (size_t)N);
+    if (svz) {
+      up(dsvz, svz, (size_t)B * N * H * Nd);
+      up(dz, z, (size_t)B * N * H * Nd);
+    }
+    dmask.alloc(N);
+    HIPCHECK(hipMemcpyAsync(dmask.p, ndxYields, N, hipMemcpyHostToDevice, ctx->stream));
+    const size_t nout = (size_t)B * N * H * Nd;
+    dfY.alloc(nout);
+    dfYc.alloc(nout);
+    dyhat.alloc((size_t)B * N * H);
+    dsc.alloc((size_t)B * 4 * Nd);
+    dst.alloc(B);
+    HIPCHECK(hipMemsetAsync(dst.p, 0, B * sizeof(int), ctx->stream));
+    FcstArgs a;
+    a.B = B; a.N = N; a.p = p; a.K = K; a.H = H; a.Nd = Nd;
+    a.PAI = dPAI.p; a.invA = dinvA.p; a.logSV0 = dlog.p; a.sqrtPHI = dsq.p; a.Xj = dXj.p;
+    a.yreal = dy.p; a.ndxYields = dmask.p; a.elb = elb;
+    a.svz = svz ? dsvz.p : nullptr;
+    a.z = svz ? dz.p : nullptr;
+    a.seed = seed; a.sweep = (uint32_t)sweep;
+    a.fY = dfY.p; a.fYc = dfYc.p; a.yhat = dyhat.p; a.scores = dsc.p; a.status = dst.p;
+    a.gl = gl;
+    HIPCHECK(hipFuncSetAttribute((const void*)k_fcst, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds));
+    hipLaunchKernelGGL(k_fcst, dim3(B), dim3(64 * nw), lds, ctx->stream, a);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    HIPCHECK(hipMemcpy(fcstY, dfY.p, nout * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(fcstYcensor, dfYc.p, nout * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(yhat, dyhat.p, (size_t)B * N * H * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(scores, dsc.p, (size_t)B * 4 * Nd * sizeof(double), hipMemcpyDeviceToHost));
+    std::vector<int> st(B);
+    HIPCHECK(hipMemcpy(st.data(), dst.p, B * sizeof(int), hipMemcpyDeviceToHost));
+    int rc = 0;
+    for (int c = 0; c < B; ++c) {
+      if (status) status[c] = st[c];
+      if (st[c] & 2) rc = CCMM_WARN_MVNCDF;
+    }
+    if (rc) g_err = "censored log score with >= 3 series at the ELB (mvncdf) is NaN";
+    return rc;
   });
 }
 

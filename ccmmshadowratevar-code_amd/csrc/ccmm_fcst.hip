@@ -1,0 +1,367 @@
+// Predictive density of one kept draw per chain (mcmcVAR.m:298-381,
+// mcmcVARshadowrateBlockHybrid.m:550-669): SV shock paths, the linear companion
+// simulation (ltitr), the censored simulation, the Rao-Blackwellised mean path
+// and the one-step predictive log scores (logscoreGaussian.m,
+// logscoreGaussianCensored.m).
+//
+// One workgroup per chain, one wave per forecast draw nn (plus one wave for the
+// zero-shock mean path).  PAI (K x N) is staged once in LDS and shared by all
+// waves; each wave keeps its lag state as a ring of p blocks of N values in LDS
+// (the companion shift x(1+N+r) <- x(1+r) becomes a head-pointer move), lanes
+// i < N each own one equation's dot product.  Scores run on lane 0 of the wave
+// over an N x N LDS scratch (N <= 32): the work is ~N^3 flop per draw.
+#pragma once
+#include "ccmm_internal.h"
+
+namespace ccmm {
+
+constexpr int kFcstMaxN = 32;
+constexpr int kFcstMaxWaves = 8;
+
+struct GLNodes {  // Gauss-Legendre half rules (negative nodes) for n = 6, 12, 20 (Genz BVN)
+  double x[3][10];
+  double w[3][10];
+};
+
+struct FcstArgs {
+  int B, N, p, K, H, Nd;
+  const double* PAI;      // [B][N][K]   (K x N column-major per chain)
+  const double* invA;     // [B][N][N]
+  const double* logSV0;   // [B][N]
+  const double* sqrtPHI;  // [B][N][N]
+  const double* Xj;       // [B][K]      Xjumpoff
+  const double* yreal;    // [N]         yrealized(:,1)
+  const uint8_t* ndxYields;  // [N]
+  double elb;
+  const double* svz;      // [B][Nd*H][N]  randn(N, H*Nd) per chain, or nullptr (Philox)
+  const double* z;        // [B][Nd][H][N] randn(N, H, Nd) per chain, or nullptr
+  uint64_t seed;
+  uint32_t sweep;
+  double* fY;             // [B][Nd][H][N]
+  double* fYc;            // [B][Nd][H][N]
+  double* yhat;           // [B][H][N]
+  double* scores;         // [B][Nd][4]
+  int* status;            // [B]  bit 1: NaN score (>= 3 censored series)
+  GLNodes gl;
+};
+
+__device__ inline double ncdf(double x) { return 0.5 * erfc(-x * 0.70710678118654752440); }
+
+// Genz (2004) BVNU: P(X > dh, Y > dk), correlation r (Drezner & Wesolowsky 1990 form)
+__device__ double bvnu(double dh, double dk, double r, const GLNodes& gl) {
+  int ng, lg;
+  const double ar = fabs(r);
+  if (ar < 0.3) { ng = 0; lg = 3; }
+  else if (ar < 0.75) { ng = 1; lg = 6; }
+  else { ng = 2; lg = 10; }
+  double h = dh, k = dk, hk = h * k, bvn = 0.0;
+  const double twopi = 6.283185307179586477;
+  if (ar < 0.925) {
+    const double hs = (h * h + k * k) * 0.5, asr = asin(r);
+    for (int i = 0; i < lg; ++i) {
+      double sn = sin(asr * (gl.x[ng][i] + 1.0) * 0.5);
+      bvn += gl.w[ng][i] * exp((sn * hk - hs) / (1.0 - sn * sn));
+      sn = sin(asr * (-gl.x[ng][i] + 1.0) * 0.5);
+      bvn += gl.w[ng][i] * exp((sn * hk - hs) / (1.0 - sn * sn));
+    }
+    return bvn * asr / (2.0 * twopi) + ncdf(-h) * ncdf(-k);
+  }
+  if (r < 0) { k = -k; hk = -hk; }
+  if (ar < 1.0) {
+    const double as = (1.0 - r) * (1.0 + r);
+    double a = sqrt(as);
+    const double bs = (h - k) * (h - k);
+    const double c = (4.0 - hk) / 8.0, d = (12.0 - hk) / 16.0;
+    bvn = a * exp(-(bs / as + hk) * 0.5) *
+          (1.0 - c * (bs - as) * (1.0 - d * bs / 5.0) / 3.0 + c * d * as * as / 5.0);
+    if (hk > -160.0) {
+      const double b = sqrt(bs);
+      bvn -= exp(-hk * 0.5) * sqrt(twopi) * ncdf(-b / a) * b * (1.0 - c * bs * (1.0 - d * bs / 5.0) / 3.0);
+    }
+    a *= 0.5;
+    for (int i = 0; i < lg; ++i) {
+      for (int sgn = -1; sgn <= 1; sgn += 2) {
+        double xs = a * (sgn * gl.x[ng][i] + 1.0);
+        xs *= xs;
+        const double rs = sqrt(1.0 - xs);
+        bvn += a * gl.w[ng][i] *
+               (exp(-bs / (2.0 * xs) - hk / (1.0 + rs)) / rs - exp(-(bs / xs + hk) * 0.5) * (1.0 + c * xs * (1.0 + d * xs)));
+      }
+    }
+    bvn = -bvn / twopi;
+  }
+  if (r > 0) return bvn + ncdf(-fmax(h, k));
+  bvn = -bvn;
+  if (k > h) bvn += ncdf(k) - ncdf(h);
+  return bvn;
+}
+
+// in-place lower Cholesky of an n x n LDS matrix (ld = kFcstMaxN); false if not SPD
+__device__ bool chol_lds(double* M, int n) {
+  for (int j = 0; j < n; ++j) {
+    double s = M[j + j * kFcstMaxN];
+    for (int k = 0; k < j; ++k) s -= M[j + k * kFcstMaxN] * M[j + k * kFcstMaxN];
+    if (!(s > 0.0)) return false;
+    const double dj = sqrt(s);
+    M[j + j * kFcstMaxN] = dj;
+    for (int i = j + 1; i < n; ++i) {
+      double v = M[i + j * kFcstMaxN];
+      for (int k = 0; k < j; ++k) v -= M[i + k * kFcstMaxN] * M[j + k * kFcstMaxN];
+      M[i + j * kFcstMaxN] = v / dj;
+    }
+  }
+  return true;
+}
+
+// Omega = S(rows) S(rows)' for the index list rows[0..n) of S = invA diag(sv) (lower
+// triangular): M = chol(Omega, 'lower') (the chol(sqrtOmega(ndx,:)*sqrtOmega(ndx,:)')
+// of mcmcVAR.m:342,347 and logscoreGaussianCensored.m:54-56)
+__device__ bool gram_rows_chol(const double* invA, const double* sv, const int* rows, int n,
+                               int N, double* M) {
+  for (int a = 0; a < n; ++a)
+    for (int b = 0; b <= a; ++b) {
+      const int ra = rows[a], rb = rows[b];
+      const int kmax = ra < rb ? ra : rb;
+      double s = 0.0;
+      for (int k = 0; k <= kmax; ++k) s += invA[ra + k * N] * invA[rb + k * N] * sv[k] * sv[k];
+      M[a + b * kFcstMaxN] = s;
+      M[b + a * kFcstMaxN] = s;
+    }
+  return chol_lds(M, n);
+}
+
+// logscoreGaussian.m:15-20 with lower-triangular L (ld kFcstMaxN), dev = y - mu (overwritten)
+__device__ double score_gauss(const double* L, int n, double* dev, double logdet) {
+  double ss = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double v = dev[i];
+    for (int k = 0; k < i; ++k) v -= L[i + k * kFcstMaxN] * dev[k];
+    v /= L[i + i * kFcstMaxN];
+    dev[i] = v;
+    ss += v * v;
+  }
+  return -0.5 * (n * 1.8378770664093454836 + logdet + ss);
+}
+
+__device__ double logdet_chol(const double* L, int n) {
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) s += log(L[i + i * kFcstMaxN]);
+  return 2.0 * s;
+}
+
+// logscoreGaussianCensored.m:13-88 as written.  sel[0..n) = the series scored (in
+// order), cens[i] whether series sel[i] may be censored.  Returns NaN (and sets
+// *unsupported) when more than 2 series sit at the ELB (MATLAB mvncdf switches to
+// a randomised quasi-Monte Carlo rule at d >= 4; d = 3 is not restated yet).
+__device__ double score_censored(const double* invA, const double* sv, const double* mu,
+                                 const double* y, const int* sel, const uint8_t* cens, int n,
+                                 int N, double elb, double* M, double* dev, int* order,
+                                 const GLNodes& gl, bool* unsupported) {
+  int noff = 0, nat = 0;
+  for (int i = 0; i < n; ++i)
+    if (!(cens[i] && y[sel[i]] <= elb)) order[noff++] = sel[i];
+  for (int i = 0; i < n; ++i)
+    if (cens[i] && y[sel[i]] <= elb) { order[noff + nat] = sel[i]; ++nat; }
+  if (nat > 2) { *unsupported = true; return NAN; }
+  if (!gram_rows_chol(invA, sv, order, n, N, M)) return NAN;
+  double llf1 = 0.0;
+  double y21[2], yat[2];
+  for (int a = 0; a < nat; ++a) { y21[a] = mu[order[noff + a]]; yat[a] = y[order[noff + a]]; }
+  if (noff > 1) {
+    for (int i = 0; i < noff; ++i) dev[i] = y[order[i]] - mu[order[i]];
+    llf1 = score_gauss(M, noff, dev, logdet_chol(M, noff));  // dev now z1
+    for (int a = 0; a < nat; ++a)
+      for (int k = 0; k < noff; ++k) y21[a] += M[(noff + a) + k * kFcstMaxN] * dev[k];
+  }
+  double llf2;
+  const double l11 = M[noff + noff * kFcstMaxN];
+  if (nat == 1) {
+    llf2 = log(ncdf((yat[0] - y21[0]) / l11));
+  } else {
+    // Sigma22 = L22 L22': sd1 = l11, cov = l11 l21, var2 = l21^2 + l22^2
+    const double l21 = M[(noff + 1) + noff * kFcstMaxN];
+    const double l22 = M[(noff + 1) + (noff + 1) * kFcstMaxN];
+    const double s2 = sqrt(l21 * l21 + l22 * l22);
+    const double rho = l21 / s2;
+    const double h = (yat[0] - y21[0]) / l11, k = (yat[1] - y21[1]) / s2;
+    llf2 = log(bvnu(-h, -k, rho, gl));
+  }
+  return llf1 + llf2;
+}
+
+__global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
+  extern __shared__ double sm[];
+  const int c = blockIdx.x;
+  const int N = a.N, K = a.K, p = a.p, H = a.H, Nd = a.Nd;
+  const int nw = blockDim.x >> 6;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // LDS: PAI K x N | per wave: ring_l[p*N] ring_c[p*N] w[N] sv[N] mu[N] dev[N] order[N] M[32*32]
+  double* sPAI = sm;
+  const int per_wave = 2 * p * N + 5 * N + kFcstMaxN * kFcstMaxN;
+  double* base = sm + (size_t)K * N + (size_t)wave * per_wave;
+  double* ringl = base;
+  double* ringc = ringl + p * N;
+  double* w = ringc + p * N;
+  double* sv1 = w + N;
+  double* mu = sv1 + N;
+  double* dev = mu + N;
+  int* order = (int*)(dev + N);
+  double* M = dev + 2 * N;
+
+  const double* PAIc = a.PAI + (size_t)c * K * N;
+  for (int e = threadIdx.x; e < K * N; e += blockDim.x) sPAI[e] = PAIc[e];
+  const double* Xj = a.Xj + (size_t)c * K;
+  const double* invA = a.invA + (size_t)c * N * N;
+  const double* sqrtPHI = a.sqrtPHI + (size_t)c * N * N;
+  Rng rng;
+  rng.crn = nullptr;
+  rng.seed = a.seed;
+  rng.chain = (uint32_t)c;
+  rng.sweep = a.sweep;
+  const int nsv = N * H * Nd;
+  __syncthreads();
+
+  const int njobs = Nd + 1;  // job Nd = zero-shock mean path
+  const int rounds = (njobs + nw - 1) / nw;
+  for (int r = 0; r < rounds; ++r) {
+    const int job = r * nw + wave;
+    const bool active = job < njobs;
+    const bool mean_path = job == Nd;
+    // ring blocks: slot (head - l) mod p holds lag l+1 (l = 0..p-1)
+    if (active)
+      for (int e = lane; e < p * N; e += 64) {
+        const int l = e / N, j = e - l * N;  // lag l+1 goes to slot (-l) mod p
+        const int slot = (l == 0) ? 0 : p - l;
+        ringl[slot * N + j] = Xj[1 + e];
+        ringc[slot * N + j] = Xj[1 + e];
+      }
+    double logsv = (lane < N) ? a.logSV0[(size_t)c * N + lane] : 0.0;
+    int head = 0;
+    __syncthreads();
+    for (int hh = 0; hh < H; ++hh) {
+      // SV path (mcmcVAR.m:302-312) and structural shock w = sv .* z
+      if (active && !mean_path && lane < N) {
+        double shock = 0.0;
+        const int col = hh + job * H;
+        for (int j = 0; j < N; ++j) {
+          const double zz = a.svz ? a.svz[((size_t)c * H * Nd + col) * N + j]
+                                  : rng.normal(CCMM_RNG_FCST, (uint32_t)(col * N + j));
+          shock += sqrtPHI[lane + j * N] * zz;
+        }
+        logsv += shock;
+        const double sv = exp(logsv * 0.5);
+        const size_t zi = ((size_t)job * H + hh) * N + lane;
+        const double zz = a.z ? a.z[(size_t)c * nsv + zi]
+                              : rng.normal(CCMM_RNG_FCST, (uint32_t)(nsv + zi));
+        w[lane] = sv * zz;
+        if (hh == 0) sv1[lane] = sv;
+      }
+      __syncthreads();
+      double yl = 0.0, yc = 0.0;
+      if (active && lane < N) {
+        double nu = 0.0;
+        if (!mean_path)
+          for (int j = 0; j <= lane; ++j) nu += invA[lane + j * N] * w[j];  // invA unit lower
+        const double* col = sPAI + (size_t)lane * K;
+        double sl = Xj[0] * col[0], sc = sl;  // constant state stays 1 (fcstA(1,1) = 1)
+        for (int l = 0; l < p; ++l) {
+          int slot = head - l;
+          slot += (slot < 0) ? p : 0;
+          const double* rl = ringl + slot * N;
+          const double* rc = ringc + slot * N;
+          const double* pc = col + 1 + l * N;
+          for (int j = 0; j < N; ++j) { sl += pc[j] * rl[j]; sc += pc[j] * rc[j]; }
+        }
+        yl = sl + nu;
+        yc = sc + nu;
+        // censored simulation (mcmcVAR.m:360-366)
+        if (a.ndxYields[lane] && yc < a.elb) yc = a.elb;
+        if (mean_path) {
+          a.yhat[((size_t)c * H + hh) * N + lane] = yl;
+        } else {
+          const size_t o = (((size_t)c * Nd + job) * H + hh) * N + lane;
+          a.fY[o] = yl;
+          a.fYc[o] = yc;
+        }
+      }
+      __syncthreads();
+      head = (head + 1 == p) ? 0 : head + 1;
+      if (active && lane < N) { ringl[head * N + lane] = yl; ringc[head * N + lane] = yc; }
+      __syncthreads();
+    }
+    // one-step predictive log scores (mcmcVAR.m:326-352), lane 0 of the wave
+    if (active && !mean_path && lane == 0) {
+      for (int i = 0; i < N; ++i) {
+        double s = 0.0;
+        for (int k = 0; k < K; ++k) s += sPAI[(size_t)i * K + k] * Xj[k];
+        mu[i] = s;
+      }
+      const double* y = a.yreal;
+      int nx = 0, ni = 0, natelb = 0;
+      for (int i = 0; i < N; ++i) {
+        if (a.ndxYields[i]) { ++ni; natelb += (y[i] <= a.elb); } else ++nx;
+      }
+      double sc[4];
+      bool unsupported = false;
+      // (1) full vector: sqrtOmegaY = invA diag(sv1) is lower triangular, logdet = sum logSV(:,1)
+      {
+        double ld = 0.0;
+        for (int i = 0; i < N; ++i) {
+          M[i + i * kFcstMaxN] = sv1[i];  // unit-diagonal invA times sv
+          for (int r2 = i + 1; r2 < N; ++r2) M[r2 + i * kFcstMaxN] = invA[r2 + i * N] * sv1[i];
+          ld += 2.0 * log(sv1[i]);
+          dev[i] = y[i] - mu[i];
+        }
+        sc[0] = score_gauss(M, N, dev, ld);
+      }
+      uint8_t cens[kFcstMaxN];
+      // (2) censored full vector (ndxYIELDS censorable)
+      if (natelb > 0) {
+        for (int i = 0; i < N; ++i) { order[i] = i; cens[i] = a.ndxYields[i]; }
+        int sel[kFcstMaxN];
+        for (int i = 0; i < N; ++i) sel[i] = i;
+        sc[1] = score_censored(invA, sv1, mu, y, sel, cens, N, N, a.elb, M, dev, order, a.gl,
+                               &unsupported);
+      } else {
+        sc[1] = sc[0];
+      }
+      // (3) macro block
+      {
+        int sel[kFcstMaxN];
+        int q = 0;
+        for (int i = 0; i < N; ++i) if (!a.ndxYields[i]) sel[q++] = i;
+        if (gram_rows_chol(invA, sv1, sel, nx, N, M)) {
+          for (int i = 0; i < nx; ++i) dev[i] = y[sel[i]] - mu[sel[i]];
+          sc[2] = score_gauss(M, nx, dev, logdet_chol(M, nx));
+        } else {
+          sc[2] = NAN;
+        }
+      }
+      // (4) yields block: every yield censorable
+      {
+        int sel[kFcstMaxN];
+        int q = 0;
+        for (int i = 0; i < N; ++i) if (a.ndxYields[i]) { sel[q] = i; cens[q] = 1; ++q; }
+        if (natelb > 0) {
+          sc[3] = score_censored(invA, sv1, mu, y, sel, cens, ni, N, a.elb, M, dev, order, a.gl,
+                                 &unsupported);
+        } else if (gram_rows_chol(invA, sv1, sel, ni, N, M)) {
+          for (int i = 0; i < ni; ++i) dev[i] = y[sel[i]] - mu[sel[i]];
+          sc[3] = score_gauss(M, ni, dev, logdet_chol(M, ni));
+        } else {
+          sc[3] = NAN;
+        }
+      }
+      for (int q = 0; q < 4; ++q) a.scores[((size_t)c * Nd + job) * 4 + q] = sc[q];
+      if (unsupported) atomicOr(&a.status[c], 2);
+    }
+    __syncthreads();
+  }
+}
+
+inline size_t fcst_lds_bytes(int N, int p, int K, int nw) {
+  const size_t per_wave = 2 * (size_t)p * N + 5 * (size_t)N + kFcstMaxN * kFcstMaxN;
+  return ((size_t)K * N + (size_t)nw * per_wave) * sizeof(double);
+}
+
+}  // namespace ccmm

@@ -42,6 +42,7 @@ extern "C" {
 #define CCMM_OK 0
 #define CCMM_WARN_QR_FALLBACK 1    /* CTA.m:80-92 "switching to QR routine" */
 #define CCMM_WARN_ELBT0 2          /* mcmcVARshadowrateBlockHybrid.m:203-205 */
+#define CCMM_WARN_MVNCDF 3         /* censored log score with >= 3 series at the ELB: mvncdf not restated, score NaN */
 #define CCMM_ERR_DIM (-1)          /* gibbsdrawShadowrates.m:50-52 "dimension mismatch" */
 #define CCMM_ERR_ARG (-2)          /* invalid argument / unsupported size */
 #define CCMM_ERR_HIP (-3)          /* HIP runtime failure */
@@ -60,6 +61,7 @@ extern "C" {
 #define CCMM_RNG_SVZ 4   /* randn(N,T+1)          SV joint draw h_0..h_T */
 #define CCMM_RNG_PHI 5   /* randn(N,T+d_PHI)      mcmcVAR.m:268 */
 #define CCMM_RNG_ELB 6   /* rand(Ns,elbT,101)     gibbsdrawShadowrates.m:173 */
+#define CCMM_RNG_FCST 7  /* randn(N,H*Nd) then randn(N,H,Nd)  mcmcVAR.m:302,306 */
 
 typedef struct ccmm_ctx ccmm_ctx;
 typedef struct ccmm_chains ccmm_chains;
@@ -218,6 +220,28 @@ int ccmm_chains_kernel_times(ccmm_chains* ch, int max, double* ms, int64_t* laun
                              char* names, int names_len);
 
 /* ------------------------------------------------------------ diagnostics */
+
+/* Predictive density of one kept draw per chain, batched over B chains.
+ * Replaces the doPredictiveDensity block mcmcVAR.m:298-381 (same simulation in
+ * mcmcVARshadowrateBlockHybrid.m:550-669), including logscoreGaussian.m:15-20 and
+ * logscoreGaussianCensored.m:13-88.  Companion form with K = N*p + 1
+ * (mcmcVAR.m:108-115).
+ *   PAI K x N x B, invA N x N x B, logSV0 N x B (= Vol_states(end,:)', log
+ *   variances), sqrtPHI N x N x B, Xjumpoff K x B, yrealized N (first column),
+ *   ndxYields N (1 = yield, censored at elb), svz N x (H*Nd) x B (mcmcVAR.m:302)
+ *   and z N x H x Nd x B (:306) or both NULL (Philox, block CCMM_RNG_FCST,
+ *   counter sweep = `sweep`).
+ * Outputs: fcstY, fcstYcensor N x H x Nd x B (fcstYdraws / fcstYcensorDraws),
+ *   yhat N x H x B (yhatdraws), scores 4 x Nd x B = (fcstLogscoreDraws,
+ *   fcstLogscoreELBdraws, fcstLogscoreXdraws, fcstLogscoreIdraws).
+ * Returns CCMM_WARN_MVNCDF when some censored score needed mvncdf in >= 3
+ * dimensions (that score is NaN; status[c] bit 1 marks the chain). */
+int ccmm_fcst(ccmm_ctx* ctx, int B, int N, int p, int H, int Nd, const double* PAI,
+              const double* invA, const double* logSV0, const double* sqrtPHI,
+              const double* Xjumpoff, const double* yrealized, const uint8_t* ndxYields,
+              double elb, const double* svz, const double* z, uint64_t seed, int sweep,
+              double* fcstY, double* fcstYcensor, double* yhat, double* scores, int* status);
+
 /* D16x16 = A16x4 * B4x16 computed by one v_mfma_f64_16x16x4_f64 with the operand
  * and accumulator lane maps the CTA SYRK kernel relies on (all column-major). */
 int ccmm_selftest_mfma_f64(ccmm_ctx* ctx, const double* A16x4, const double* B4x16, double* D16x16);

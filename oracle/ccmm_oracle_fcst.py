@@ -1,0 +1,178 @@
+"""Oracle (CPU restatement) of the predictive-density block of the Gibbs sweep —
+TEST INFRASTRUCTURE ONLY (see ccmm_oracle.py).
+
+Follows mcmcVAR.m:298-381 (identical in mcmcVARshadowrateBlockHybrid.m:550-669
+for the linear/censored simulation) for ONE kept draw: SV shock paths, the
+linear companion simulation (ltitr), the one-step predictive log scores
+(logscoreGaussian.m:15-20, logscoreGaussianCensored.m:13-88), the censored
+simulation (:354-372) and the Rao-Blackwellised mean path (:375-379).
+
+PARITY UNPINNED (MATLAB reference, no fixtures).  MATLAB built-ins restated:
+``normcdf`` exactly (erfc); ``mvncdf`` for 2 and 3 censored series by
+independent adaptive quadrature (scipy.integrate.quad) of the conditional
+univariate / bivariate integrals — MATLAB's own trivariate
+tolerance is 1e-8 absolute.  With 4+ censored series MATLAB switches to a
+randomised quasi-Monte Carlo rule that cannot be matched; the score is NaN.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+from scipy import integrate
+from scipy.special import ndtr
+
+LOG2PI = math.log(2.0 * math.pi)
+
+
+def bvn_cdf(h, k, r):
+    """P(Z1 <= h, Z2 <= k) for standard normals with correlation r: the conditional
+    integral  int_{-inf}^{h} phi(x) Phi((k - r x) / sqrt(1 - r^2)) dx, adaptive
+    (positive by construction, also deep in the tails)."""
+    if r == 0.0:
+        return ndtr(h) * ndtr(k)
+    s = math.sqrt(1.0 - r * r)
+    f = lambda x: math.exp(-0.5 * x * x) / math.sqrt(2 * math.pi) * ndtr((k - r * x) / s)
+    pts = [k / r] if -50 < k / r < h else None
+    lo = min(-40.0, h - 40.0)
+    val, _ = integrate.quad(f, lo, h, epsabs=1e-300, epsrel=1e-12, limit=400, points=pts)
+    return val
+
+
+def mvncdf(b, mu, S):
+    """mvncdf(b', mu', S) for dimension 1..3 (MATLAB mvncdf semantics, upper limits)."""
+    d = len(b)
+    x = (np.asarray(b, float) - np.asarray(mu, float))
+    if d == 1:
+        return ndtr(x[0] / math.sqrt(S[0, 0]))
+    if d == 2:
+        s1, s2 = math.sqrt(S[0, 0]), math.sqrt(S[1, 1])
+        return bvn_cdf(x[0] / s1, x[1] / s2, S[0, 1] / (s1 * s2))
+    if d == 3:
+        L = np.linalg.cholesky(S)
+        v2 = L[2, 1] ** 2 + L[2, 2] ** 2
+        s3 = math.sqrt(v2)
+        rho = L[2, 1] / s3
+
+        def inner(z1):
+            h = (x[1] - L[1, 0] * z1) / L[1, 1]
+            k = (x[2] - L[2, 0] * z1) / s3
+            return math.exp(-0.5 * z1 * z1) / math.sqrt(2 * math.pi) * bvn_cdf(h, k, rho)
+
+        val, _ = integrate.quad(inner, -np.inf, x[0] / L[0, 0], epsabs=1e-14, epsrel=1e-12,
+                                limit=400)
+        return val
+    return float("nan")
+
+
+def logscore_gaussian(mu, sqrtOmega, y, logdet=None):
+    """logscoreGaussian.m:15-20 (sqrtOmega lower triangular -> triangular solve)."""
+    if logdet is None:
+        logdet = 2 * np.sum(np.log(np.diag(sqrtOmega)))
+    from scipy.linalg import solve_triangular
+    ydev = solve_triangular(sqrtOmega, y - mu, lower=True)
+    return -0.5 * (len(y) * LOG2PI + logdet + np.sum(ydev ** 2))
+
+
+def logscore_gaussian_censored(mu, sqrtOmega, y, elb, censorable=None):
+    """logscoreGaussianCensored.m:13-88 as written (incl. the NoffELB > 1 test at :58)."""
+    N = len(y)
+    if censorable is None:
+        censorable = np.ones(N, bool)
+    at = (y <= elb) & censorable
+    Nat = int(at.sum())
+    Noff = N - Nat
+    if Nat == 0:
+        raise ValueError("logscoreGaussianCensored.m:33 references undefined muY at NatELB == 0")
+    order = np.concatenate([np.nonzero(~at)[0], np.nonzero(at)[0]])
+    ydev = (y - mu)[order]
+    yAt, muAt = y[at], mu[at]
+    S = sqrtOmega[order, :]
+    L = np.linalg.cholesky(S @ S.T)
+    from scipy.linalg import solve_triangular
+    if Noff > 1:
+        L11 = L[:Noff, :Noff]
+        z1 = solve_triangular(L11, ydev[:Noff], lower=True)
+        llf1 = -0.5 * (Noff * LOG2PI + 2 * np.sum(np.log(np.diag(L11))) + np.sum(z1 ** 2))
+        y21 = muAt + L[Noff:, :Noff] @ z1
+    else:
+        llf1 = 0.0
+        y21 = muAt
+    L22 = L[Noff:, Noff:]
+    if Nat == 1:
+        llf2 = math.log(ndtr((yAt[0] - y21[0]) / L22[0, 0]))
+    else:
+        llf2 = math.log(mvncdf(yAt, y21, L22 @ L22.T))
+    return llf1 + llf2
+
+
+def fcst_draw(PAI, invA, logSV0, sqrtPHI, Xjumpoff, yrealized, ndxYields, elb, svz, z):
+    """One kept draw of mcmcVAR.m:298-381.
+
+    PAI K x N, invA N x N, logSV0 N (Vol_states(end,:)'), sqrtPHI N x N,
+    Xjumpoff K, yrealized N (first column), ndxYields bool N, elb scalar,
+    svz = randn(N, H*Nd) (:302), z = randn(N, H, Nd) (:306).
+    Returns fcstY N x H x Nd, fcstYcensor N x H x Nd, yhat N x H,
+    scores 4 x Nd (fcstLogscore, fcstLogscoreELB, fcstLogscoreX, fcstLogscoreI).
+    """
+    K, N = PAI.shape
+    H, Nd = z.shape[1], z.shape[2]
+    ndxYx = ~ndxYields
+    ndxYi = ndxYields
+    yNatELB = int(np.sum(yrealized[ndxYi] <= elb))
+    svshocks = (sqrtPHI @ svz).reshape(N, H, Nd, order="F")
+    fY = np.empty((N, H, Nd))
+    fYc = np.empty((N, H, Nd))
+    scores = np.empty((4, Nd))
+
+    def step(x, nu):
+        xn = np.empty_like(x)
+        xn[0] = x[0]
+        xn[1:N + 1] = PAI.T @ x + nu
+        xn[N + 1:] = x[1:K - N]
+        return xn
+
+    for nn in range(Nd):
+        logSV = logSV0[:, None] + np.cumsum(svshocks[:, :, nn], axis=1)
+        sv = np.exp(logSV * 0.5)
+        nu = invA @ (sv * z[:, :, nn])
+        # linear simulation (ltitr, :322-323)
+        x = Xjumpoff.copy()
+        for hh in range(H):
+            x = step(x, nu[:, hh])
+            fY[:, hh, nn] = x[1:N + 1]
+        # one-step predictive scores (:326-352)
+        muY = PAI.T @ Xjumpoff
+        sqrtOmegaY = invA * sv[:, 0][None, :]
+        scores[0, nn] = logscore_gaussian(muY, sqrtOmegaY, yrealized, np.sum(logSV[:, 0]))
+        if yNatELB > 0:
+            scores[1, nn] = logscore_gaussian_censored(muY, sqrtOmegaY, yrealized, elb, ndxYields)
+        else:
+            scores[1, nn] = scores[0, nn]
+        Sx = sqrtOmegaY[ndxYx, :]
+        Lx = np.linalg.cholesky(Sx @ Sx.T)
+        scores[2, nn] = logscore_gaussian(muY[ndxYx], Lx, yrealized[ndxYx],
+                                          2 * np.sum(np.log(np.diag(Lx))))
+        Si = sqrtOmegaY[ndxYi, :]
+        Li = np.linalg.cholesky(Si @ Si.T)
+        if yNatELB > 0:
+            scores[3, nn] = logscore_gaussian_censored(muY[ndxYi], Li, yrealized[ndxYi], elb)
+        else:
+            scores[3, nn] = logscore_gaussian(muY[ndxYi], Li, yrealized[ndxYi])
+        # censored simulation (:355-372)
+        x = Xjumpoff.copy()
+        for hh in range(H):
+            x = step(x, nu[:, hh])
+            yd = x[1:N + 1].copy()
+            m = ndxYields & (yd < elb)
+            if m.any():
+                yd[m] = elb
+                x[1:N + 1] = yd
+            fYc[:, hh, nn] = yd
+    # RB mean path (:376-379)
+    yhat = np.empty((N, H))
+    x = Xjumpoff.copy()
+    for hh in range(H):
+        x = step(x, np.zeros(N))
+        yhat[:, hh] = x[1:N + 1]
+    return fY, fYc, yhat, scores

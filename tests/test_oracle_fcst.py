@@ -1,0 +1,66 @@
+"""CPU checks of the predictive-density oracle (oracle/ccmm_oracle_fcst.py):
+mvncdf restatement against scipy's Genz integrator, the censored log score's
+reduction identities, and the simulation's structural properties."""
+import numpy as np
+import pytest
+from scipy import stats
+
+from fcst_cases import fcst_inputs
+
+
+@pytest.fixture(scope="module")
+def F():
+    from oracle import ccmm_oracle_fcst
+    return ccmm_oracle_fcst
+
+
+@pytest.mark.parametrize("r", [-0.95, -0.5, 0.0, 0.2, 0.6, 0.9, 0.97])
+def test_bvn_cdf_vs_scipy(F, r):
+    S = np.array([[1.0, r], [r, 1.0]])
+    for h, k in [(-1.0, 0.5), (0.3, 0.3), (1.5, -2.0), (-2.5, -2.2)]:
+        want = stats.multivariate_normal(mean=[0, 0], cov=S).cdf([h, k])
+        assert abs(F.bvn_cdf(h, k, r) - want) < 1e-7
+
+
+def test_tvn_cdf_vs_scipy(F):
+    rng = np.random.default_rng(0)
+    for _ in range(4):
+        L = np.tril(rng.uniform(-0.8, 0.8, (3, 3))) + np.diag([1.0, 0.6, 0.4])
+        S = L @ L.T
+        b = rng.uniform(-1, 1, 3)
+        mu = rng.uniform(-0.3, 0.3, 3)
+        want = stats.multivariate_normal(mean=mu, cov=S).cdf(b)
+        assert abs(F.mvncdf(b, mu, S) - want) < 2e-5  # scipy is a randomized QMC rule (~1e-5)
+
+
+def test_censored_one_at_elb_is_conditional_normal(F):
+    """One censored series: llf = log N(y_off) + log Phi((y_at - E[y_at|y_off]) / sd)."""
+    rng = np.random.default_rng(1)
+    n = 4
+    S = np.tril(rng.uniform(-0.5, 0.5, (n, n))) + np.eye(n)
+    mu = rng.standard_normal(n)
+    y = mu + rng.standard_normal(n)
+    y[2] = -1.0
+    Om = S @ S.T
+    off = [0, 1, 3]
+    c = Om[2, off] @ np.linalg.solve(Om[np.ix_(off, off)], y[off] - mu[off]) + mu[2]
+    v = Om[2, 2] - Om[2, off] @ np.linalg.solve(Om[np.ix_(off, off)], Om[off, 2])
+    want = stats.multivariate_normal(mu[off], Om[np.ix_(off, off)]).logpdf(y[off]) + \
+        stats.norm.logcdf(y[2], c, np.sqrt(v))  # upper limit = yAtELB (:75)
+    got = F.logscore_gaussian_censored(mu, S, y, -0.5, np.array([False, False, True, False]))
+    assert abs(got - want) < 1e-10
+
+
+def test_fcst_structure(F, oracle, fred):
+    d = fcst_inputs(oracle, fred, B=1, H=12, Nd=3)
+    fY, fYc, yhat, sc = F.fcst_draw(d["PAI"][..., 0], d["invA"][..., 0], d["logSV0"][:, 0],
+                                    d["sqrtPHI"][..., 0], d["Xj"][:, 0], d["ys"][1], d["yields"],
+                                    d["elb"], d["svz"][..., 0], d["z"][..., 0])
+    assert np.all(fYc[d["yields"]] >= d["elb"])
+    # before any censoring binds, the censored path equals the linear path
+    first = np.argmax(np.any(fY[d["yields"]] < d["elb"], axis=0), axis=0)
+    assert np.allclose(fY[:, 0, :][:, first > 0], fYc[:, 0, :][:, first > 0])
+    # the X / I split of the uncensored score: the sum is the joint score when the blocks are
+    # uncorrelated only, so check finiteness and the ELB <= uncensored ordering is not assumed
+    assert np.all(np.isfinite(sc))
+    assert np.allclose(yhat[:, 0], d["PAI"][..., 0].T @ d["Xj"][:, 0])
