@@ -41,7 +41,7 @@ struct FcstArgs {
   double* fYc;            // [B][Nd][H][N]
   double* yhat;           // [B][H][N]
   double* scores;         // [B][Nd][4]
-  int* status;            // [B]  bit 1: NaN score (>= 3 censored series)
+  int* status;            // [B]  bit 1: NaN score (>= 4 censored series)
   GLNodes gl;
 };
 
@@ -94,6 +94,56 @@ __device__ double bvnu(double dh, double dk, double r, const GLNodes& gl) {
   bvn = -bvn;
   if (k > h) bvn += ncdf(k) - ncdf(h);
   return bvn;
+}
+
+// Trivariate normal P(X <= x), X ~ N(0, L L') with L lower 3x3 (ld kFcstMaxN at M):
+// P = int_{-inf}^{x1/L11} phi(z) BVN(h(z), k(z); rho) dz with the conditional
+// bivariate of (X2, X3) | z (Genz BVN inside).  The integrand steps where h or k
+// changes sign, so the outer interval is split there and each segment integrated
+// on panels graded geometrically towards both ends (20-point Gauss-Legendre).
+// MATLAB's mvncdf (trivariate rule, absolute tolerance 1e-8) is the reference.
+__device__ double tvn_cdf(const double* x, const double* M, const GLNodes& gl) {
+  const double l11 = M[0], l21 = M[1], l31 = M[2];
+  const double l22 = M[1 + kFcstMaxN], l32 = M[2 + kFcstMaxN], l33 = M[2 + 2 * kFcstMaxN];
+  const double s3 = sqrt(l32 * l32 + l33 * l33), rho = l32 / s3;
+  const double b = x[0] / l11;
+  const double lo = -10.0;
+  if (b <= lo) return 0.0;
+  double brk[4];
+  int nb = 0;
+  brk[nb++] = lo;
+  double cand[2] = {l21 != 0.0 ? x[1] / l21 : lo, l31 != 0.0 ? x[2] / l31 : lo};
+  if (cand[0] > cand[1]) { const double t = cand[0]; cand[0] = cand[1]; cand[1] = t; }
+  for (int i = 0; i < 2; ++i)
+    if (cand[i] > brk[nb - 1] + 1e-12 && cand[i] < b - 1e-12) brk[nb++] = cand[i];
+  brk[nb++] = b;
+  double total = 0.0;
+  for (int sgm = 0; sgm + 1 < nb; ++sgm) {
+    const double a0 = brk[sgm], a1 = brk[sgm + 1];
+    const double half = 0.5 * (a1 - a0);
+    // panels: widths w0 * 2^j from each end until they meet at the midpoint
+    for (int side = 0; side < 2; ++side) {
+      double pos = 0.0, w = fmin(1e-4, half);
+      while (pos < half) {
+        const double wi = fmin(w, half - pos);
+        const double u0 = pos, u1 = pos + wi;  // distance from this end
+        const double c = 0.5 * (u0 + u1), r = 0.5 * (u1 - u0);
+        double acc = 0.0;
+        for (int i = 0; i < 10; ++i) {
+          for (int sg = -1; sg <= 1; sg += 2) {
+            const double u = c + sg * r * gl.x[2][i];
+            const double z = side == 0 ? a0 + u : a1 - u;
+            const double h = (x[1] - l21 * z) / l22, k = (x[2] - l31 * z) / s3;
+            acc += gl.w[2][i] * exp(-0.5 * z * z) * bvnu(-h, -k, rho, gl);
+          }
+        }
+        total += acc * r * 0.39894228040143267794;
+        pos = u1;
+        w *= 2.0;
+      }
+    }
+  }
+  return total;
 }
 
 // in-place lower Cholesky of an n x n LDS matrix (ld = kFcstMaxN); false if not SPD
@@ -151,8 +201,8 @@ __device__ double logdet_chol(const double* L, int n) {
 
 // logscoreGaussianCensored.m:13-88 as written.  sel[0..n) = the series scored (in
 // order), cens[i] whether series sel[i] may be censored.  Returns NaN (and sets
-// *unsupported) when more than 2 series sit at the ELB (MATLAB mvncdf switches to
-// a randomised quasi-Monte Carlo rule at d >= 4; d = 3 is not restated yet).
+// *unsupported) when more than 3 series sit at the ELB (MATLAB mvncdf switches to
+// a randomised quasi-Monte Carlo rule at d >= 4).
 __device__ double score_censored(const double* invA, const double* sv, const double* mu,
                                  const double* y, const int* sel, const uint8_t* cens, int n,
                                  int N, double elb, double* M, double* dev, int* order,
@@ -162,10 +212,10 @@ __device__ double score_censored(const double* invA, const double* sv, const dou
     if (!(cens[i] && y[sel[i]] <= elb)) order[noff++] = sel[i];
   for (int i = 0; i < n; ++i)
     if (cens[i] && y[sel[i]] <= elb) { order[noff + nat] = sel[i]; ++nat; }
-  if (nat > 2) { *unsupported = true; return NAN; }
+  if (nat > 3) { *unsupported = true; return NAN; }
   if (!gram_rows_chol(invA, sv, order, n, N, M)) return NAN;
   double llf1 = 0.0;
-  double y21[2], yat[2];
+  double y21[3], yat[3];
   for (int a = 0; a < nat; ++a) { y21[a] = mu[order[noff + a]]; yat[a] = y[order[noff + a]]; }
   if (noff > 1) {
     for (int i = 0; i < noff; ++i) dev[i] = y[order[i]] - mu[order[i]];
@@ -177,7 +227,7 @@ __device__ double score_censored(const double* invA, const double* sv, const dou
   const double l11 = M[noff + noff * kFcstMaxN];
   if (nat == 1) {
     llf2 = log(ncdf((yat[0] - y21[0]) / l11));
-  } else {
+  } else if (nat == 2) {
     // Sigma22 = L22 L22': sd1 = l11, cov = l11 l21, var2 = l21^2 + l22^2
     const double l21 = M[(noff + 1) + noff * kFcstMaxN];
     const double l22 = M[(noff + 1) + (noff + 1) * kFcstMaxN];
@@ -185,6 +235,9 @@ __device__ double score_censored(const double* invA, const double* sv, const dou
     const double rho = l21 / s2;
     const double h = (yat[0] - y21[0]) / l11, k = (yat[1] - y21[1]) / s2;
     llf2 = log(bvnu(-h, -k, rho, gl));
+  } else {
+    const double xv[3] = {yat[0] - y21[0], yat[1] - y21[1], yat[2] - y21[2]};
+    llf2 = log(tvn_cdf(xv, M + noff + noff * kFcstMaxN, gl));
   }
   return llf1 + llf2;
 }

@@ -59,8 +59,10 @@ def mvncdf(b, mu, S):
             k = (x[2] - L[2, 0] * z1) / s3
             return math.exp(-0.5 * z1 * z1) / math.sqrt(2 * math.pi) * bvn_cdf(h, k, rho)
 
-        val, _ = integrate.quad(inner, -np.inf, x[0] / L[0, 0], epsabs=1e-14, epsrel=1e-12,
-                                limit=400)
+        pts = [v for v in (x[1] / L[1, 0] if L[1, 0] else None, x[2] / L[2, 0] if L[2, 0] else None)
+               if v is not None and -40 < v < x[0] / L[0, 0]]
+        val, _ = integrate.quad(inner, -40.0, x[0] / L[0, 0], epsabs=1e-300, epsrel=1e-11,
+                                limit=400, points=pts or None)
         return val
     return float("nan")
 

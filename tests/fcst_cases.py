@@ -4,7 +4,7 @@ kept draw (fredblockMD20-2022-09.csv, N=20, p=12, K=241) with yields at the ELB 
 import numpy as np
 
 
-def fcst_inputs(oracle, fred, B=4, H=48, Nd=10, seed=11, nat=(0, 1, 2, 0)):
+def fcst_inputs(oracle, fred, B=4, H=48, Nd=10, seed=11, nat=(0, 1, 2, 3)):
     data = fred["data"]
     N, p = data.shape[1], 12
     K = N * p + 1
@@ -37,7 +37,8 @@ def fcst_inputs(oracle, fred, B=4, H=48, Nd=10, seed=11, nat=(0, 1, 2, 0)):
     for n in nat:
         y = PAI0.T @ Xj + 0.1 * rng.standard_normal(N)
         y[yields] = np.maximum(y[yields], 0.45)
-        y[ndxS[:n]] = 0.25 - rng.uniform(0.0, 0.15, n)
+        at = np.concatenate([ndxS, ndxO])[:n]
+        y[at] = 0.25 - rng.uniform(0.0, 0.15, n)
         ys.append(y)
     return dict(PAI=PAI, invA=invA, logSV0=logSV0, sqrtPHI=sqrtPHI, Xj=Xjs, yields=yields,
                 svz=svz, z=z, ys=ys, H=H, Nd=Nd, elb=0.25)

@@ -4,10 +4,12 @@ logscoreGaussianCensored.m) with common random numbers, on a real-data kept draw
 (N=20, p=12, K=241, H=48, Nd=10, 4 chains).
 
 Tolerances: simulated paths 1e-9 in |Δ| / max(|x|, 1) (48-step recursions in a
-different summation order); log scores 1e-9 absolute + relative (one and two
-censored series: normcdf / Genz BVN against the oracle's adaptive quadrature).
-Three censored series: the reference's mvncdf trivariate rule is not restated on
-the device yet — those scores are NaN with CCMM_WARN_MVNCDF, the rest still match."""
+different summation order); log scores 1e-9 absolute + relative for one and two
+censored series (normcdf / Genz BVN against the oracle's adaptive quadrature),
+1e-8 for three (graded Gauss-Legendre outer integral on the device; MATLAB's own
+trivariate mvncdf tolerance is 1e-8 absolute).  Four or more censored series: MATLAB
+mvncdf is randomised quasi-Monte Carlo — those scores are NaN with
+CCMM_WARN_MVNCDF, the rest still match."""
 import numpy as np
 import pytest
 
@@ -30,7 +32,7 @@ def _oracle(F, d, y, B):
     return [np.stack([o[k] for o in outs], axis=-1) for k in range(4)]
 
 
-@pytest.mark.parametrize("case", [0, 1, 2])
+@pytest.mark.parametrize("case", [0, 1, 2, 3])
 def test_fcst_crn(ctx, oracle, fred, F, case):
     B = 4
     d = fcst_inputs(oracle, fred, B=B)
@@ -44,12 +46,13 @@ def test_fcst_crn(ctx, oracle, fred, F, case):
     assert rel_err(fY, rfY, 1.0) < 1e-9
     assert rel_err(fYc, rfYc, 1.0) < 1e-9
     assert np.array_equal(fYc[d["yields"]] == d["elb"], rfYc[d["yields"]] == d["elb"])  # censoring flags
-    assert rel_err(sc, rsc, 1.0) < 1e-9, (sc - rsc)
+    e = rel_err(sc, rsc, 1.0)
+    assert e < (1e-8 if case == 3 else 1e-9), e
 
 
-def test_fcst_three_at_elb_warns(ctx, oracle, fred, F):
+def test_fcst_four_at_elb_warns(ctx, oracle, fred, F):
     B = 2
-    d = fcst_inputs(oracle, fred, B=B, nat=(3,))
+    d = fcst_inputs(oracle, fred, B=B, nat=(4,))
     y = d["ys"][0]
     fY, fYc, yhat, sc, st = ctx.fcst(d["PAI"], d["invA"], d["logSV0"], d["sqrtPHI"], d["Xj"], y,
                                      d["yields"], d["elb"], d["H"], d["Nd"], d["svz"], d["z"])
