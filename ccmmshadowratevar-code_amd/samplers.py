@@ -39,10 +39,12 @@ def mcmcVAR(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMean, doRATS
     if check_stationarity:
         raise NotImplementedError("check_stationarity=1 (mcmcVAR.m:221-232) is not supported; "
                                   "the reference drivers all pass 0")
-    if fcstNdraws:
+    doPredictiveDensity = bool(fcstNdraws)
+    if doPredictiveDensity:
         if fcstNdraws % MCMCdraws != 0:  # mcmcVAR.m:97-99
             raise ValueError("fcstNdraws must be multiple of MCMCdraws")
-        raise NotImplementedError("predictive density (nargout > 4) is a later row (SURVEY §8f)")
+        if yrealized is None or ndxYIELDS is None or fcstNhorizons is None:
+            raise ValueError("predictive density needs yrealized, ndxYIELDS and fcstNhorizons")
     m = build_var(thisT, p, np_, data0, ydates0, minnesotaPriorMean, doRATSprior)
     B = int(nchains)
     burn = MCMCdraws if burnin is None else int(burnin)  # MCMCburnin = MCMCdraws (mcmcVAR.m:54)
@@ -52,13 +54,55 @@ def mcmcVAR(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMean, doRATS
     ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
     st = initial_state(m, B)
     ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
-    _run_chain_set(ch, burn, MCMCdraws, doprogress)
+    if doPredictiveDensity:
+        fc = _run_with_predictive_density(ctx, ch, m, burn, MCMCdraws, ndxYIELDS, ELBbound,
+                                          yrealized, fcstNdraws, fcstNhorizons, rndStream,
+                                          doprogress)
+    else:
+        _run_chain_set(ch, burn, MCMCdraws, doprogress)
     out = ch.get_draws()
     ch.close()
     res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"]]
+    if doPredictiveDensity:
+        res += fc
     if B == 1:
         res = [a[..., 0] for a in res]
     return tuple(res)
+
+
+def _run_with_predictive_density(ctx, ch, m, burn, MCMCdraws, ndxYIELDS, ELBbound, yrealized,
+                                 fcstNdraws, fcstNhorizons, seed, doprogress):
+    """Kept-draw loop of mcmcVAR.m:278-381 with the predictive density of each kept
+    draw on the device (ccmm_fcst), then the reshapes and means of :400-425.
+    Returns fcstYdraws, fcstYhat, fcstYcensorDraws, fcstYcensorHat, fcstYshadowDraws,
+    fcstYshadowHat, fcstYhatRB, fcstLogscoreDraws, fcstLogscoreELBdraws,
+    fcstLogscoreXdraws, fcstLogscoreIdraws (each with a trailing chain axis)."""
+    N, H, B = m.N, int(fcstNhorizons), ch.B
+    Nd = fcstNdraws // MCMCdraws
+    yields = np.zeros(N, bool)
+    yields[np.asarray(ndxYIELDS, int)] = True
+    y1 = np.asarray(yrealized, float).reshape(N, -1, order="F")[:, 0]
+    Xj = np.repeat(m.Xjumpoff[:, None], B, axis=1)
+    fY = np.empty((N, H, Nd, MCMCdraws, B))
+    fYc = np.empty_like(fY)
+    yhat = np.empty((N, H, MCMCdraws, B))
+    sc = np.empty((4, Nd, MCMCdraws, B))
+    _run_chain_set(ch, burn, 0, doprogress)
+    for d in range(MCMCdraws):
+        ch.sweep(1, store=True)
+        st = ch.get_state()
+        out = ctx.fcst(st["PAI"], st["invA"], st["h"][-1, :, :], st["sqrtPHI"], Xj, y1, yields,
+                       ELBbound, H, Nd, seed=seed, sweep=burn + d)
+        fY[:, :, :, d, :], fYc[:, :, :, d, :], yhat[:, :, d, :], sc[:, :, d, :] = out[:4]
+    fYd = fY.reshape(N, H, fcstNdraws, B, order="F")
+    fYcd = fYc.reshape(N, H, fcstNdraws, B, order="F")
+    fYs = fYd.copy()
+    sh = fYs[yields]
+    sh[sh < ELBbound] = ELBbound  # :407-411
+    fYs[yields] = sh
+    scores = [sc[k].reshape(fcstNdraws, B, order="F") for k in range(4)]
+    return [fYd, fYd.mean(axis=2), fYcd, fYcd.mean(axis=2), fYs, fYs.mean(axis=2),
+            yhat.mean(axis=2)] + scores
 
 
 def _run_chain_set(ch, burn, MCMCdraws, doprogress, step=50):

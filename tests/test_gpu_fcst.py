@@ -87,3 +87,35 @@ def test_fcst_philox(ctx, oracle, fred, F):
     assert np.all((ratio > 0.85) & (ratio < 1.2))
     # draws differ across chains (chain index is part of the Philox counter)
     assert not np.allclose(fY[..., 0], fY[..., 1])
+
+
+def test_mcmcVAR_predictive_density(pkg, oracle, fred, F):
+    """samplers.mcmcVAR with fcstNdraws (nargout 15): kept-draw loop + ccmm_fcst.
+    RNG-free end-to-end check: fcstYhatRB = mean over kept draws of the zero-shock
+    path of each stored PAI draw (mcmcVAR.m:375-379, :400)."""
+    sel = [0, 4, 14, 17]  # two macro series, FEDFUNDS-like and a yield (ndxYIELDS = [2, 3])
+    data = fred["data"][-120:, sel]
+    ydates = fred["ydates"][-120:]
+    mpm = np.ones(len(sel))
+    T0 = len(ydates) - 6
+    yreal = data[T0:T0 + 6].T
+    M, Nd_total, H = 20, 40, 6
+    out = pkg.samplers.mcmcVAR(T0, M, 2, 12, data, ydates, mpm, True, ndxYIELDS=[2, 3],
+                               ELBbound=0.25, yrealized=yreal, fcstNdraws=Nd_total,
+                               fcstNhorizons=H, rndStream=7, burnin=10)
+    assert len(out) == 15
+    PAI_all, fYd, fYhat, fYcd, yhatRB, ls = out[0], out[4], out[5], out[6], out[10], out[11]
+    assert fYd.shape == (4, H, Nd_total) and fYcd.shape == (4, H, Nd_total) and ls.shape == (Nd_total,)
+    assert np.all(fYcd[[2, 3]] >= 0.25) and np.all(np.isfinite(ls))
+    assert np.allclose(fYhat, fYd.mean(axis=2))
+    m = pkg.model.build_var(T0, 2, 12, data, ydates, mpm, True)
+    want = np.zeros((4, H))
+    for d in range(M):
+        P = PAI_all[d]
+        x = m.Xjumpoff.copy()
+        for hh in range(H):
+            yv = P.T @ x
+            x = np.concatenate([[1.0], yv, x[1:1 + 4 * (2 - 1)]])
+            want[:, hh] += yv / M
+    e = rel_err(yhatRB, want, 1.0)
+    assert e < 1e-10, e
