@@ -45,6 +45,7 @@ def parse():
                     help="budget of the CPU-oracle baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-fcst", action="store_true", help="skip the predictive-density line")
     ap.add_argument("--bh-steps", type=int, default=5,
                     help="timed sweeps of the block-hybrid secondary line (configs[2]); 0 = skip")
     ap.add_argument("--bh-warmup", type=int, default=2)
@@ -103,6 +104,7 @@ def main():
         elapsed = float(t.item())
     draws = ch.get_draws()
     assert np.all(np.isfinite(draws["PAI_all"])), "non-finite draws"
+    fc = bench_predictive(ctx, ch, m, d, B) if (rank == 0 and not args.no_fcst) else None
     ch.close()
     # secondary line (configs[2]) runs on every rank: it has its own barrier/max-reduction
     bh = bench_block_hybrid(pkg, ctx, d, B, args, rank, barrier, dist) if args.bh_steps > 0 else None
@@ -175,11 +177,35 @@ def main():
         out["dominant_kernel"] = dom
     if bh is not None:
         out["block_hybrid"] = bh
+    if fc is not None:
+        out["predictive"] = fc
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def bench_predictive(ctx, ch, m, d, B, H=48, Nd=10, reps=3):
+    """Predictive density of one kept draw for every chain (mcmcVAR.m:298-381) through
+    the block-level C-ABI ccmm_fcst (host buffers in and out, so PCIe-inclusive; the
+    kernel time k_fcst is in the rocprofv3 stats).  Not part of a sweep."""
+    st = ch.get_state()
+    yields = np.zeros(m.N, bool)
+    yields[[i for i, c in enumerate(d["ncode"]) if c in
+            ("FEDFUNDS", "TB6MS", "GS1", "GS5", "GS10", "BAA")]] = True
+    y1 = m.data[-1]  # realized values: the jump-off month itself (synthetic stand-in)
+    Xj = np.repeat(m.Xjumpoff[:, None], B, axis=1)
+    args = (st["PAI"], st["invA"], st["h"][-1], st["sqrtPHI"], Xj, y1, yields, 0.25, H, Nd)
+    ctx.fcst(*args, seed=5, sweep=0)  # warm-up
+    t0 = time.perf_counter()
+    for r in range(reps):
+        out = ctx.fcst(*args, seed=5, sweep=r + 1)
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    assert np.all(np.isfinite(out[3][0]))
+    return {"workload": f"ccmm_fcst: {B} chains x {Nd} draws x {H} horizons, linear + censored "
+                        "paths, RB mean, 4 log scores", "ms_per_call": round(ms, 3),
+            "chain_draws_per_s": round(B / (ms * 1e-3), 1), "boundary": "host buffers (PCIe-inclusive)"}
 
 
 def bench_block_hybrid(pkg, ctx, d, B, args, rank, barrier, dist):
