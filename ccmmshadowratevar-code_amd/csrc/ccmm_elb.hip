@@ -434,7 +434,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
       const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
       double sp[NS];
       for (int a = 0; a < NS; ++a) sp[a] = fma(g0[a], v0, g1[a] * v1);
-      for (int a = 0; a < NS; ++a) sp[a] = hd[a] + wave_sum(sp[a]);
+      for (int a = 0; a < NS; ++a) sp[a] = hd[a] + wave_sum_dpp(sp[a]);
       // conditional draws in index order (gibbsdrawShadowrates.m:206-218)
       const double* beta = hd + NS;
       const double* so = beta + NS * (NS - 1);

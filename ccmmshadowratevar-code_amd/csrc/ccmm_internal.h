@@ -163,4 +163,28 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
   return u.d;
 }
 
+// Wave-wide sum returned uniformly, on the DPP path: xor-1 / xor-2 quad permutes, half-row
+// and row mirrors leave every lane holding its 16-lane row sum, then four readlanes add
+// the rows.  No LDS traffic (the __shfl_xor butterfly above is ds_bpermute per step), so
+// it suits latency-bound serial loops.  Summation order differs from wave_sum.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  union {
+    double d;
+    int i[2];
+  } u, r;
+  u.d = v;
+  r.i[0] = __builtin_amdgcn_update_dpp(0, u.i[0], CTRL, 0xF, 0xF, false);
+  r.i[1] = __builtin_amdgcn_update_dpp(0, u.i[1], CTRL, 0xF, 0xF, false);
+  return r.d;
+}
+
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);  // row_half_mirror
+  v += dpp_d<0x140>(v);  // row_mirror
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
 }  // namespace ccmm
