@@ -249,7 +249,7 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
       }
     }
     for (int a = 0; a < Ns; ++a) {
-      const double tot = wave_sum(g0[a]);
+      const double tot = wave_sum_dpp(g0[a]);
       if (lane == 0) gS[a] = tot;
     }
   }

@@ -626,15 +626,15 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
           b += __shfl_xor(b8 ? v1 : v3, 8);
           double q = b4 ? b : a;
           q += __shfl_xor(b4 ? a : b, 4);
-          q += __shfl_xor(q, 2);
-          q += __shfl_xor(q, 1);
+          q += dpp_d<0x4E>(q);  // xor 2 (quad_perm, no LDS round trip)
+          q += dpp_d<0xB1>(q);  // xor 1
           if ((lr & 3) == 0) tp[gi * 16 + lq + 4 * (lr >> 2)] = q;
         }
       }
     }
     {  // x_0 = c_0 / L00 + sum_a Linv(1+a,0) c_{1+a}
       double pr = (tid < KL) ? Lv[1 + tid] * rl[1 + tid] : 0.0;
-      pr = wave_sum(pr);
+      pr = wave_sum_dpp(pr);
       if (lane == 0) red[wave] = pr;
     }
     __syncthreads();
