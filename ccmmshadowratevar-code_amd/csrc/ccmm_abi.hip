@@ -794,10 +794,20 @@ struct ccmm_chains {
     ChainState cs = view();
     const int N = d.N;
     const int total = (N - 1) * N * (N + 1) / 6 + N * (N - 1) / 2 + 8;
-    const size_t lds = (size_t)(total + N * N) * sizeof(double);
+    size_t lds = (size_t)(total + N * N) * sizeof(double);
+    // stage the chain's residuals in LDS when they fit (N = 20, T = 750: 138 KB in all)
+    int es_off = -1;
+    const size_t staged = lds + (size_t)N * d.TP * sizeof(double);
+    if (staged <= 160 * 1024) {
+      es_off = total + N * N;
+      lds = staged;
+      if (lds > 64 * 1024)
+        HIPCHECK(hipFuncSetAttribute((const void*)k_astep,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    }
     launch(KID_ASTEP, [&] {
       hipLaunchKernelGGL(k_astep, dim3(d.B), dim3(256), lds, ctx->stream, d, Tslot.p, cs, ra,
-                         cfg.logy2offset);
+                         cfg.logy2offset, es_off);
     });
   }
 

@@ -381,7 +381,7 @@ __global__ __launch_bounds__(256) void k_cta_solve(Dims d, const int* __restrict
 // invA = A \ I (mcmcVAR.m:254), logy2 = log((RESID*A').^2 + offset) (mcmcVAR.m:259).
 // LDS: per ii a packed lower ZZ (ii x ii) followed by Zz (ii).
 __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ Tslot, ChainState cs,
-                                               RngArgs ra, double logy2offset) {
+                                               RngArgs ra, double logy2offset, int es_off) {
   extern __shared__ double sm[];
   const int c = blockIdx.x;
   const int N = d.N, TP = d.TP;
@@ -404,15 +404,20 @@ __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ T
     }
     boff[N] = o;
   }
+  // es_off >= 0: this chain's residuals E (N x TP) are staged in LDS at sm + es_off
+  if (es_off >= 0)
+    for (int q = tid; q < N * TP; q += blockDim.x) sm[es_off + q] = E[q];
   __syncthreads();
+  const double* Ew = (es_off >= 0) ? sm + es_off : E;
   const int total = boff[N];
   double* Anew = sm + total;  // N x N
-  for (int g = tid; g < total; g += blockDim.x) {
-    int ii = 1;
+  // entry g of block ii: (a, b) of the ii x ii Gram ZZ = E(:,0:ii-1)' diag(1/h_ii^2) E(:,0:ii-1)
+  // (packed lower) or of Zz = E(:,0:ii-1)' diag(1/h_ii^2) E(:,ii)
+  auto entry = [&](int g, int& ii, int& a, int& b) {
+    ii = 1;
     while (ii < N - 1 && g >= boff[ii + 1]) ++ii;
     const int e = g - boff[ii];
     const int ntri = ii * (ii + 1) / 2;
-    int a, b;
     if (e < ntri) {  // packed lower: column b, row a >= b
       b = 0;
       int rem = e;
@@ -425,15 +430,52 @@ __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ T
       a = e - ntri;  // Zz entry: X(:,a)' y
       b = ii;
     }
-    const double* ea = E + (size_t)a * TP;
-    const double* eb = E + (size_t)b * TP;
-    const double* hh = sh + (size_t)ii * TP;
-    double acc = 0.0;
-    for (int t = 0; t < T; ++t) {
-      const double hv = hh[t];
-      acc = fma(ea[t] / hv, eb[t] / hv, acc);
+  };
+  constexpr int kAsTPL = 16;  // t values per lane on the wave-per-entry path (T <= 1024)
+  if (T <= 64 * kAsTPL) {
+    // one wave per entry, lanes over t (coalesced rows of E), 1/h_ii^2 cached in registers
+    // while consecutive entries of this wave stay in the same block ii; DPP reduction
+    const int lane = tid & 63, wave = tid >> 6, nwv = blockDim.x >> 6;
+    double ih[kAsTPL];
+    int cur_ii = -1;
+    for (int g = wave; g < total; g += nwv) {
+      int ii, a, b;
+      entry(g, ii, a, b);
+      if (ii != cur_ii) {
+        cur_ii = ii;
+        const double* hh = sh + (size_t)ii * TP;
+#pragma unroll
+        for (int k = 0; k < kAsTPL; ++k) {
+          const int t = lane + 64 * k;
+          const double hv = (t < T) ? hh[t] : 1.0;
+          ih[k] = (t < T) ? 1.0 / (hv * hv) : 0.0;
+        }
+      }
+      const double* ea = Ew + (size_t)a * TP;
+      const double* eb = Ew + (size_t)b * TP;
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < kAsTPL; ++k) {
+        const int t = lane + 64 * k;
+        if (t < T) acc = fma(ea[t] * eb[t], ih[k], acc);
+      }
+      acc = wave_sum_dpp(acc);
+      if (lane == 0) sm[g] = acc;
     }
-    sm[g] = acc;
+  } else {
+    for (int g = tid; g < total; g += blockDim.x) {
+      int ii, a, b;
+      entry(g, ii, a, b);
+      const double* ea = E + (size_t)a * TP;
+      const double* eb = E + (size_t)b * TP;
+      const double* hh = sh + (size_t)ii * TP;
+      double acc = 0.0;
+      for (int t = 0; t < T; ++t) {
+        const double hv = hh[t];
+        acc = fma(ea[t] / hv, eb[t] / hv, acc);
+      }
+      sm[g] = acc;
+    }
   }
   for (int q = tid; q < N * N; q += blockDim.x) Anew[q] = ((q % N) == (q / N)) ? 1.0 : 0.0;
   __syncthreads();
@@ -495,7 +537,7 @@ __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ T
     for (int i = 0; i < N; ++i) {
       double s = 0.0;
       if (t < T) {
-        for (int k = 0; k <= i; ++k) s = fma(E[(size_t)k * TP + t], Anew[i + k * N], s);
+        for (int k = 0; k <= i; ++k) s = fma(Ew[(size_t)k * TP + t], Anew[i + k * N], s);
       }
       ly[(size_t)i * TP + t] = (t < T) ? log(s * s + logy2offset) : 0.0;
     }
