@@ -251,3 +251,62 @@ def drawTruncNormal(mu, sqrtVCV, elb, u):
     """drawTruncNormal.m:1 with the numeric-uniform form of the stream argument."""
     v, _ = _abi.draw_trunc_normal(mu, sqrtVCV, elb, u)
     return v
+
+
+def _logmeanexp(x, axis=0):
+    """log(mean(exp(x))) with the max shift of goVARshadowrateBlockHybrid.m:438-439."""
+    x = np.asarray(x, float)
+    m = np.max(x, axis=axis, keepdims=True)
+    return np.squeeze(np.log(np.mean(np.exp(x - m), axis=axis, keepdims=True)) + m, axis=axis)
+
+
+def goVAR_batch(data0, ydates0, Tjumpoffs, p, np_, MCMCdraws, fcstNdraws, fcstNhorizons,
+                minnesotaPriorMean, ndxYIELDS, ELBbound=0.25, doRATSprior=True, *, nchains=1,
+                rndStream=1012023, dist=None, device=0, burnin=None, run_vintage=None):
+    """The quasi-real-time OOS loop of goVAR.m:242 / goVARshadowrateBlockHybrid.m:258-517
+    for the linear sampler: every vintage thisT in Tjumpoffs runs mcmcVAR with its
+    predictive density; vintages are sharded over ranks longest-processing-time first
+    (distributed.lpt_assign, no collective while sampling) and the per-vintage results
+    are gathered at the end (one all-gather).
+
+    Per vintage: fcstYmvlogscore{,X,I} = log mean exp over the fcstNdraws x nchains
+    one-step log-score draws (:437-447), fcstYhat (N x H, mean over draws), and the
+    censored ELB log score.  yrealized = the data rows after the jump-off (NaN past the
+    end of the sample).  ``run_vintage(thisT, yrealized, seed)`` replaces the mcmcVAR
+    call (tests use it to drive the sharding on CPU).  Returns a dict on every rank.
+    """
+    from . import distributed as dm
+    data0 = np.asarray(data0, float)
+    Nobs, N = data0.shape
+    K = N * p + 1
+    rank = dist.get_rank() if dist is not None else 0
+    size = dist.get_world_size() if dist is not None else 1
+    Tjumpoffs = [int(t) for t in Tjumpoffs]
+    costs = [dm.unit_cost(t - p, K, N) for t in Tjumpoffs]
+    mine = dm.lpt_assign(costs, size)[rank]
+    H = int(fcstNhorizons)
+    local = {}
+    for v in mine:
+        thisT = Tjumpoffs[v]
+        yreal = np.full((N, H), np.nan)
+        nreal = max(0, min(H, Nobs - thisT))
+        yreal[:, :nreal] = data0[thisT:thisT + nreal].T
+        seed = int(rndStream) + 7919 * v  # per-vintage stream (initRandStreams analogue)
+        if run_vintage is not None:
+            ls, lsELB, lsX, lsI, fYhat = run_vintage(thisT, yreal, seed)
+        else:
+            out = mcmcVAR(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMean,
+                          doRATSprior, ndxYIELDS=ndxYIELDS, ELBbound=ELBbound, yrealized=yreal,
+                          fcstNdraws=fcstNdraws, fcstNhorizons=H, rndStream=seed,
+                          nchains=nchains, device=device, burnin=burnin)
+            fYhat = out[5]
+            ls, lsELB, lsX, lsI = out[11], out[12], out[13], out[14]
+            if nchains > 1:
+                fYhat = fYhat.mean(axis=-1)
+        summ = [_logmeanexp(np.ravel(a)) for a in (ls, lsELB, lsX, lsI)]
+        local[v] = np.concatenate([np.array(summ), np.ravel(fYhat, order="F")])
+    allv = dm.gather_summaries(dist, local, None)
+    S = np.stack([allv[v] for v in range(len(Tjumpoffs))], axis=1)
+    return dict(fcstYmvlogscore=S[0], fcstYmvlogscoreELB=S[1], fcstYmvlogscoreX=S[2],
+                fcstYmvlogscoreI=S[3], fcstYhat=S[4:].reshape(N, H, -1, order="F"),
+                assignment=dm.lpt_assign(costs, size))

@@ -72,3 +72,57 @@ def test_gloo_world2_reductions():
         assert tot == [55.0, 10.0]
         assert abs(lme - want) < 1e-12
         assert mx == 1.0
+
+
+def _fake_vintage(thisT, yreal, seed):
+    """Deterministic stand-in for one vintage's mcmcVAR (CPU): log-score draws and a
+    forecast mean that depend only on (thisT, seed)."""
+    rng = np.random.default_rng(seed)
+    ls = rng.normal(-20.0, 3.0, size=(40, 2))
+    return ls, ls - 0.5, ls / 2, ls / 3, np.full((3, 4), float(thisT))
+
+
+def _govar_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import __graft_entry__
+    pkg = __graft_entry__.load_package()
+    dist, w = pkg.distributed.init("gloo")
+    data = np.arange(60 * 3, dtype=float).reshape(60, 3)
+    res = pkg.samplers.goVAR_batch(data, np.arange(60.0), [40, 45, 50, 55, 58], 2, 12, 10, 40, 4,
+                                   np.ones(3), [2], dist=dist, run_vintage=_fake_vintage)
+    q.put((w.rank, res["fcstYmvlogscore"].tolist(), res["fcstYhat"][0, 0].tolist(),
+           res["assignment"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_govar_batch():
+    """goVAR_batch over 5 vintages on 2 gloo ranks: LPT sharding, per-vintage log mean exp
+    of the log-score draws (goVARshadowrateBlockHybrid.m:437-447), one all-gather; every
+    rank ends with the same, complete per-vintage table equal to the world-1 result."""
+    import __graft_entry__
+    pkg = __graft_entry__.load_package()
+    data = np.arange(60 * 3, dtype=float).reshape(60, 3)
+    ref = pkg.samplers.goVAR_batch(data, np.arange(60.0), [40, 45, 50, 55, 58], 2, 12, 10, 40, 4,
+                                   np.ones(3), [2], run_vintage=_fake_vintage)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_govar_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=100) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for rank, ls, yh, assign in res:
+        assert sorted(assign[0] + assign[1]) == list(range(5)) and assign[0] and assign[1]
+        assert np.allclose(ls, ref["fcstYmvlogscore"], rtol=0, atol=1e-12)
+        assert yh == [40.0, 45.0, 50.0, 55.0, 58.0]
+    x = _fake_vintage(40, None, 1012023)[0]
+    assert abs(ref["fcstYmvlogscore"][0] - np.log(np.mean(np.exp(x)))) < 1e-10

@@ -119,3 +119,16 @@ def test_mcmcVAR_predictive_density(pkg, oracle, fred, F):
             want[:, hh] += yv / M
     e = rel_err(yhatRB, want, 1.0)
     assert e < 1e-10, e
+
+
+def test_goVAR_batch_gpu(pkg, fred):
+    """goVAR_batch (world 1) over two real-data vintages with mcmcVAR + ccmm_fcst:
+    per-vintage log mean exp of the returned log-score draws, fcstYhat per vintage."""
+    sel = [0, 4, 14, 17]
+    data = fred["data"][-140:, sel]
+    ydates = fred["ydates"][-140:]
+    res = pkg.samplers.goVAR_batch(data, ydates, [120, 128], 2, 12, 10, 20, 4, np.ones(4), [2, 3],
+                                   nchains=2, burnin=5)
+    assert res["fcstYmvlogscore"].shape == (2,) and np.all(np.isfinite(res["fcstYmvlogscore"]))
+    assert res["fcstYhat"].shape == (4, 4, 2) and np.all(np.isfinite(res["fcstYhat"]))
+    assert np.all(res["fcstYmvlogscoreX"] > -1e3) and np.all(res["fcstYmvlogscoreI"] > -1e3)
