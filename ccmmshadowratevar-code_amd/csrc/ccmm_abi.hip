@@ -840,10 +840,18 @@ struct ccmm_chains {
       hipLaunchKernelGGL(k_phi_gen, dim3((d.N * (d.TP + cfg.dPHI) + 255) / 256, d.B), dim3(256), 0,
                          ctx->stream, d, Tslot.p, cfg.dPHI, cs, ra);
     });
-    const size_t lds = (size_t)(4 * d.N * (d.N + 1)) * sizeof(double);
+    size_t lds = (size_t)(4 * d.N * (d.N + 1)) * sizeof(double);
+    const size_t staged = lds + (size_t)d.N * (d.TP + 1) * sizeof(double);
+    const int stage_eta = staged <= 160 * 1024 ? 1 : 0;
+    if (stage_eta) {
+      lds = staged;
+      if (lds > 64 * 1024)
+        HIPCHECK(hipFuncSetAttribute((const void*)k_phi, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds));
+    }
     launch(KID_PHI, [&] {
       hipLaunchKernelGGL(k_phi, dim3(d.B), dim3(256), lds, ctx->stream, d, Tslot.p, cfg.dPHI,
-                         sPHI.p, cs);
+                         sPHI.p, cs, stage_eta);
     });
   }
 

@@ -624,7 +624,8 @@ __global__ void k_phi_gen(Dims d, const int* __restrict__ Tslot, int dPHI, Chain
 }
 
 __global__ __launch_bounds__(256) void k_phi(Dims d, const int* __restrict__ Tslot, int dPHI,
-                                             const double* __restrict__ sPHIall, ChainState cs) {
+                                             const double* __restrict__ sPHIall, ChainState cs,
+                                             int stage_eta) {
   extern __shared__ double sm[];
   const int N = d.N, NS = N + 1, TP = d.TP;
   const int c = blockIdx.x;
@@ -640,12 +641,25 @@ __global__ __launch_bounds__(256) void k_phi(Dims d, const int* __restrict__ Tsl
   const double* eta = cs.eta + (size_t)c * N * TP;
   const double* Z = cs.Zphi + (size_t)c * N * TZmax;
   const double* sP = sPHIall + (size_t)s * N * N;
+  // stage_eta: the SV shocks eta (N x T) go to LDS with odd row stride TP + 1, so the
+  // lanes of a wave (different rows r, same t) hit different banks
+  const int lde = stage_eta ? TP + 1 : TP;
+  const double* etaw = eta;
+  if (stage_eta) {
+    double* es = Ph + N * NS;
+    for (int q = tid; q < N * TP; q += blockDim.x) {
+      const int r = q / TP, t = q - r * TP;
+      es[r * lde + t] = eta[q];
+    }
+    __syncthreads();
+    etaw = es;
+  }
   for (int e = tid; e < N * N; e += blockDim.x) {
     const int r = e / N, col = e % N;
     if (col > r) continue;
     double a = 0.0;
-    const double* er = eta + (size_t)r * TP;
-    const double* ec = eta + (size_t)col * TP;
+    const double* er = etaw + (size_t)r * lde;
+    const double* ec = etaw + (size_t)col * lde;
     for (int t = 0; t < T; ++t) a = fma(er[t], ec[t], a);
     Lpost[r * NS + col] = sP[r + col * N] + a;
     double b = 0.0;
