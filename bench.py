@@ -279,7 +279,12 @@ def load_pmc():
     """HBM bytes per launch from the newest committed rocprofv3 PMC summary
     (profiles/*_pmc.json, written by tools/pmc_summary.py from separate
     FETCH_SIZE / WRITE_SIZE passes over this same bench command)."""
-    files = sorted((ROOT / "profiles").glob("*_pmc.json"))
+    import re
+
+    def natural(pth):  # r01_v11 after r01_v9
+        return [int(x) if x.isdigit() else x for x in re.split(r"(\d+)", pth.name)]
+
+    files = sorted((ROOT / "profiles").glob("*_pmc.json"), key=natural)
     if not files:
         return {}, None
     try:
