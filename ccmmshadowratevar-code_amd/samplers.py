@@ -260,9 +260,39 @@ def _logmeanexp(x, axis=0):
     return np.squeeze(np.log(np.mean(np.exp(x - m), axis=axis, keepdims=True)) + m, axis=axis)
 
 
+def realized_values(data0, thisT, fcstNhorizons, ndxSHADOWRATE, ELBbound):
+    """yrealized of one vintage (goVAR.m:252-267 == goVARshadowrateBlockHybrid.m:267-283):
+    the data rows after the 1-based jump-off ``thisT`` (NaN past the end of the sample),
+    with the shadow-rate series floored at the ELB."""
+    data0 = np.asarray(data0, float)
+    Tdata, N = data0.shape
+    H = int(fcstNhorizons)
+    yreal = np.full((N, H), np.nan)
+    nreal = max(0, min(H, Tdata - thisT))
+    yreal[:, :nreal] = data0[thisT:thisT + nreal].T
+    if ELBbound is not None and ndxSHADOWRATE is not None and len(ndxSHADOWRATE):
+        s = np.asarray(ndxSHADOWRATE, int)
+        ys = yreal[s, :]
+        ys[ys < ELBbound] = ELBbound  # NaN compares false: missing months stay NaN
+        yreal[s, :] = ys
+    return yreal
+
+
+def _rank_device(dist, device):
+    """Device of this rank: explicit ``device`` wins; with a process group the rank's
+    LOCAL_RANK (one process per GPU, torchrun layout); else device 0."""
+    if device is not None:
+        return int(device)
+    if dist is not None:
+        from . import distributed as dm
+        return dm.world_from_env().local_rank
+    return 0
+
+
 def goVAR_batch(data0, ydates0, Tjumpoffs, p, np_, MCMCdraws, fcstNdraws, fcstNhorizons,
                 minnesotaPriorMean, ndxYIELDS, ELBbound=0.25, doRATSprior=True, *, nchains=1,
-                rndStream=1012023, dist=None, device=0, burnin=None, run_vintage=None):
+                rndStream=1012023, dist=None, device=None, burnin=None, run_vintage=None,
+                ndxSHADOWRATE=None):
     """The quasi-real-time OOS loop of goVAR.m:242 / goVARshadowrateBlockHybrid.m:258-517
     for the linear sampler: every vintage thisT in Tjumpoffs runs mcmcVAR with its
     predictive density; vintages are sharded over ranks longest-processing-time first
@@ -272,8 +302,10 @@ def goVAR_batch(data0, ydates0, Tjumpoffs, p, np_, MCMCdraws, fcstNdraws, fcstNh
     Per vintage: fcstYmvlogscore{,X,I} = log mean exp over the fcstNdraws x nchains
     one-step log-score draws (:437-447), fcstYhat (N x H, mean over draws), and the
     censored ELB log score.  yrealized = the data rows after the jump-off (NaN past the
-    end of the sample).  ``run_vintage(thisT, yrealized, seed)`` replaces the mcmcVAR
-    call (tests use it to drive the sharding on CPU).  Returns a dict on every rank.
+    end of the sample) with the ``ndxSHADOWRATE`` series floored at the ELB
+    (goVAR.m:262-267; ``realized_values``).  ``run_vintage(thisT, yrealized, seed)``
+    replaces the mcmcVAR call (tests use it to drive the sharding on CPU).  ``device``
+    defaults to the rank's LOCAL_RANK under a process group.  Returns a dict on every rank.
     """
     from . import distributed as dm
     data0 = np.asarray(data0, float)
@@ -281,6 +313,7 @@ def goVAR_batch(data0, ydates0, Tjumpoffs, p, np_, MCMCdraws, fcstNdraws, fcstNh
     K = N * p + 1
     rank = dist.get_rank() if dist is not None else 0
     size = dist.get_world_size() if dist is not None else 1
+    device = _rank_device(dist, device)
     Tjumpoffs = [int(t) for t in Tjumpoffs]
     costs = [dm.unit_cost(t - p, K, N) for t in Tjumpoffs]
     mine = dm.lpt_assign(costs, size)[rank]
@@ -288,9 +321,7 @@ def goVAR_batch(data0, ydates0, Tjumpoffs, p, np_, MCMCdraws, fcstNdraws, fcstNh
     local = {}
     for v in mine:
         thisT = Tjumpoffs[v]
-        yreal = np.full((N, H), np.nan)
-        nreal = max(0, min(H, Nobs - thisT))
-        yreal[:, :nreal] = data0[thisT:thisT + nreal].T
+        yreal = realized_values(data0, thisT, H, ndxSHADOWRATE, ELBbound)
         seed = int(rndStream) + 7919 * v  # per-vintage stream (initRandStreams analogue)
         if run_vintage is not None:
             ls, lsELB, lsX, lsI, fYhat = run_vintage(thisT, yreal, seed)

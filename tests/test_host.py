@@ -91,3 +91,45 @@ def test_shadow_yield_sets(pkg, oracle, fred):
     assert [fred["ncode"][i] for i in s] == ["FEDFUNDS", "TB6MS", "GS1"]
     assert [fred["ncode"][i] for i in o] == ["GS5", "GS10", "BAA"]
     assert oracle.elb_t0(fred["data"], s, 0.25, 12) == 585
+
+
+def test_realized_values_floor_shadow_rates(pkg, fred):
+    """yrealized of a vintage (goVAR.m:252-267): data rows after the jump-off, NaN past
+    the sample end, shadow-rate series floored at the ELB; other series untouched."""
+    s, o, _ = pkg.model.setShadowYields(fred["ncode"], 0.25)
+    data = fred["data"]
+    thisT = len(fred["ydates"]) - 30      # 2020-02: the funds rate goes to the ELB in 2020-04
+    yr = pkg.samplers.realized_values(data, thisT, 48, s, 0.25)
+    assert yr.shape == (data.shape[1], 48)
+    assert np.all(np.isnan(yr[:, 30:])) and np.all(np.isfinite(yr[:, :30]))
+    raw = data[thisT:thisT + 30].T
+    floored = raw[s] < 0.25
+    assert floored.any()
+    np.testing.assert_array_equal(yr[s, :30][floored], 0.25)
+    np.testing.assert_array_equal(yr[s, :30][~floored], raw[s][~floored])
+    others = np.setdiff1d(np.arange(data.shape[1]), s)
+    np.testing.assert_array_equal(yr[others, :30], raw[others])
+
+
+def test_govar_batch_floors_yrealized_and_picks_rank_device(pkg, monkeypatch):
+    """goVAR_batch hands run_vintage the floored yrealized, and a rank under a
+    process group defaults to its LOCAL_RANK device."""
+    data = np.full((60, 3), 1.0)
+    data[:, 2] = 0.1                       # a shadow-rate series below the ELB
+    seen = []
+
+    def run_vintage(thisT, yreal, seed):
+        seen.append(yreal.copy())
+        ls = np.zeros((4, 1))
+        return ls, ls, ls, ls, np.zeros((3, 2))
+
+    pkg.samplers.goVAR_batch(data, np.arange(60.0), [40, 50], 2, 12, 4, 4, 2, np.ones(3), [2],
+                             run_vintage=run_vintage, ndxSHADOWRATE=[2])
+    assert len(seen) == 2
+    for y in seen:
+        np.testing.assert_array_equal(y[2], 0.25)
+        np.testing.assert_array_equal(y[:2], 1.0)
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    assert pkg.samplers._rank_device(object(), None) == 3
+    assert pkg.samplers._rank_device(object(), 1) == 1
+    assert pkg.samplers._rank_device(None, None) == 0
