@@ -71,6 +71,12 @@ _SIGS = {
     "ccmm_chains_sweep": (C.c_int, [C.c_void_p, C.c_int, _dp, C.c_int]),
     "ccmm_chains_stored": (C.c_int, [C.c_void_p]),
     "ccmm_chains_get_draws": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
+    "ccmm_chains_set_rng_ids": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "ccmm_chains_get_status": (C.c_int, [C.c_void_p, _ip]),
+    "ccmm_chains_set_fcst": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, C.c_int]),
+    "ccmm_chains_set_fcst_slot": (C.c_int, [C.c_void_p, C.c_int, _dp]),
+    "ccmm_chains_fcst_stored": (C.c_int, [C.c_void_p]),
+    "ccmm_chains_get_fcst": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp, _dp]),
     "ccmm_chains_set_elb_model": (C.c_int, [C.c_void_p, _ip, _u8p]),
     "ccmm_chains_set_elb_slot": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p]),
     "ccmm_chains_get_shadowrate": (C.c_int, [C.c_void_p, _dp]),
@@ -288,7 +294,7 @@ class Chains:
     KERNELS = ("k_resid", "k_cta_weights", "k_syrk", "k_chol", "k_cta_solve", "k_astep",
                "k_sv_mix", "k_sv_part", "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
                "k_elb_prep", "k_elb_cond", "k_elb_gibbs", "k_elb_rebuild", "k_gram_chol_lag",
-               "k_cta_solve_lag")
+               "k_cta_solve_lag", "k_fcst")
 
     def __init__(self, ctx: Context, *, N, p, T, B, ndata=1, model=MODEL_LINEAR, crn=False,
                  store_capacity=0, logy2offset=1e-3, seed=1012023, dPHI=None, Ns=0, elbTmax=0,
@@ -321,6 +327,33 @@ class Chains:
     def crn_len(self):
         return int(self.lib.ccmm_chains_crn_len(self.handle))
 
+    def crn_layout(self):
+        """Per-sweep CRN record of one chain (ccmm_chains_sweep): name -> (offset, length,
+        kind) in CCMM_RNG_* order, sizes from the set's maximum T / elbT (include/ccmm.h)."""
+        cf = self.cfg
+        N, T = self.N, self.T
+        blocks = [("PAI", self.K * N, "n"), ("A", N * (N - 1) // 2, "n"), ("SVU", N * T, "u"),
+                  ("SVZ", N * (T + 1), "n"), ("PHI", N * (T + cf.dPHI), "n")]
+        if self.model in (MODEL_BLOCKHYBRID, MODEL_HYBRID):
+            blocks.append(("ELB", self.Ns * self.elbTmax * (cf.elb_gibbsburn + 1), "u"))
+        if getattr(self, "fH", 0):
+            blocks.append(("FCST", 2 * N * self.fH * self.fNd, "n"))
+        out, o = {}, 0
+        for name, n, kind in blocks:
+            out[name] = (o, n, kind)
+            o += n
+        assert o == self.crn_len, (o, self.crn_len)
+        return out
+
+    def draw_crn(self, rng, nsweeps=1):
+        """A random CRN array (crn_len, nsweeps, B): normals / uniforms per block."""
+        lay = self.crn_layout()
+        out = np.empty((self.crn_len, nsweeps, self.B), order="F")
+        for o, n, kind in lay.values():
+            shape = (n, nsweeps, self.B)
+            out[o:o + n] = rng.random(shape) if kind == "u" else rng.standard_normal(shape)
+        return out
+
     def set_data(self, slot, Y, X, iVdiag, iVb, sPHI, h0mean, h0vcvsqrt):
         Y = _f(Y)
         rc = self.lib.ccmm_chains_set_data(self.handle, slot, Y.shape[0], _ptr(Y), _ptr(_f(X)),
@@ -332,6 +365,22 @@ class Chains:
         s = np.ascontiguousarray(slots, dtype=np.int32)
         _check(self.lib.ccmm_chains_set_slots(self.handle, s.ctypes.data_as(_ip)),
                "ccmm_chains_set_slots")
+
+    def set_rng_ids(self, ids):
+        """Philox stream id per chain (None: the chain index)."""
+        if ids is None:
+            _check(self.lib.ccmm_chains_set_rng_ids(self.handle, None), "ccmm_chains_set_rng_ids")
+            return
+        a = np.ascontiguousarray(ids, dtype=np.uint32)
+        assert a.size == self.B
+        _check(self.lib.ccmm_chains_set_rng_ids(self.handle, a.ctypes.data_as(C.POINTER(C.c_uint32))),
+               "ccmm_chains_set_rng_ids")
+
+    def get_status(self):
+        st = np.zeros(self.B, dtype=np.int32)
+        _check(self.lib.ccmm_chains_get_status(self.handle, st.ctypes.data_as(_ip)),
+               "ccmm_chains_get_status")
+        return st
 
     def set_state(self, PAI, A, sqrtht, h, sqrtPHI):
         """Arrays K x N x B, N x N x B, T x N x B, T x N x B, N x N x B."""
@@ -378,6 +427,43 @@ class Chains:
                                                            ("PAI_all", "PHI_all", "invA_all",
                                                             "sqrtht_all", "shadowrate_all")])
         _check(rc, "ccmm_chains_get_draws")
+        return out
+
+    # ------------------------------------------------ predictive density (on device)
+    def set_fcst(self, H, Nd, ndxYields, keep_paths=False):
+        """Forecast every stored sweep (ccmm_chains_set_fcst): H horizons, Nd draws per kept
+        draw; ndxYields bool N (ndxYIELDS)."""
+        m = np.ascontiguousarray(np.asarray(ndxYields, bool), dtype=np.uint8)
+        _check(self.lib.ccmm_chains_set_fcst(self.handle, int(H), int(Nd), m.ctypes.data_as(_u8p),
+                                             int(bool(keep_paths))), "ccmm_chains_set_fcst")
+        self.fH, self.fNd, self.fKeep = int(H), int(Nd), bool(keep_paths)
+
+    def set_fcst_slot(self, slot, yrealized):
+        """yrealized(:,1) of data slot ``slot`` (N values, shadow rates floored at the ELB)."""
+        y = _f(np.asarray(yrealized, float).reshape(self.N, -1, order="F")[:, 0])
+        _check(self.lib.ccmm_chains_set_fcst_slot(self.handle, int(slot), _ptr(y)),
+               "ccmm_chains_set_fcst_slot")
+
+    def fcst_stored(self):
+        return int(self.lib.ccmm_chains_fcst_stored(self.handle))
+
+    def get_fcst(self, paths=False):
+        """Forecast records of the kept draws so far (then reset): scores Nd x M x 4 x B,
+        fYsum / fYcsum / yhatsum N x H x B, and with ``paths`` the paths N x H x Nd x M x B."""
+        M = self.fcst_stored()
+        N, H, Nd, B = self.N, self.fH, self.fNd, self.B
+        out = dict(M=M, scores=np.zeros((Nd, M, 4, B), order="F"),
+                   fYsum=np.zeros((N, H, B), order="F"), fYcsum=np.zeros((N, H, B), order="F"),
+                   yhatsum=np.zeros((N, H, B), order="F"))
+        if paths:
+            out["paths"] = np.zeros((N, H, Nd, M, B), order="F")
+            out["paths_censored"] = np.zeros((N, H, Nd, M, B), order="F")
+        rc = self.lib.ccmm_chains_get_fcst(self.handle, _ptr(out["scores"]), _ptr(out["fYsum"]),
+                                           _ptr(out["fYcsum"]), _ptr(out["yhatsum"]),
+                                           _ptr(out.get("paths")), _ptr(out.get("paths_censored")))
+        if rc != CCMM_WARN_MVNCDF:
+            _check(rc, "ccmm_chains_get_fcst")
+        out["warn_mvncdf"] = rc == CCMM_WARN_MVNCDF
         return out
 
     # ------------------------------------------------ block-hybrid shadow-rate model

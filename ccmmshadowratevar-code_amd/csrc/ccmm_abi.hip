@@ -117,6 +117,34 @@ std::vector<double> host_spd_inverse(const std::vector<double>& A, int n) {
 
 }  // namespace
 
+// Gauss-Legendre nodes/weights by Newton on P_n (host, once); negative half
+static GLNodes make_gl_nodes() {
+  GLNodes g{};
+  const int ns[3] = {6, 12, 20};
+  for (int r = 0; r < 3; ++r) {
+    const int n = ns[r];
+    for (int i = 0; i < n / 2; ++i) {
+      double x = -std::cos(M_PI * (i + 0.75) / (n + 0.5));
+      double dp = 0.0;
+      for (int it = 0; it < 100; ++it) {
+        double p0 = 1.0, p1 = x;
+        for (int k = 2; k <= n; ++k) {
+          const double p2 = ((2.0 * k - 1.0) * x * p1 - (k - 1.0) * p0) / k;
+          p0 = p1;
+          p1 = p2;
+        }
+        dp = n * (x * p1 - p0) / (x * x - 1.0);
+        const double dx = p1 / dp;
+        x -= dx;
+        if (std::fabs(dx) < 1e-17) break;
+      }
+      g.x[r][i] = x;
+      g.w[r][i] = 2.0 / ((1.0 - x * x) * dp * dp);
+    }
+  }
+  return g;
+}
+
 struct ccmm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -141,6 +169,7 @@ enum KernelId {
   KID_ELBREBUILD,
   KID_GRAMLAG,
   KID_SOLVELAG,
+  KID_FCST,
   KID_COUNT
 };
 static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syrk", "k_chol",
@@ -148,7 +177,7 @@ static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syr
                                               "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
                                               "k_elb_prep", "k_elb_cond", "k_elb_gibbs",
                                               "k_elb_rebuild", "k_gram_chol_lag",
-                                              "k_cta_solve_lag"};
+                                              "k_cta_solve_lag", "k_fcst"};
 
 struct ccmm_chains {
   ccmm_ctx* ctx = nullptr;
@@ -181,6 +210,17 @@ struct ccmm_chains {
   DBuf<double> ePhi, eY0, eYt, eEt, eCond, eScur;
   int stored = 0;
   uint32_t sweep = 0;
+  // predictive density of every stored sweep (mcmcVAR.m:298-381,
+  // mcmcVARshadowrateBlockHybrid.m:550-669), kept on the device
+  bool have_fcst = false;
+  int fH = 0, fNd = 0, fKeep = 0, fstored = 0, fldXj = 0, fnw = 1;
+  DBuf<uint8_t> fYields;
+  std::vector<bool> have_fcst_slot;
+  DBuf<double> fYreal, fXj, fY, fYc, fYhat, fSc, fYsum, fYcsum, fYhatsum, fScStore, fPaths, fPathsC;
+  DBuf<int> fStatus;
+  // Philox stream ids (counter word 1) per chain; default the chain index
+  bool have_ids = false;
+  DBuf<uint32_t> rngIds;
   bool resid_valid = false;
   bool have_state = false;
   // kernel variants (A/B): CCMM_OLD_SOLVE=1 selects the first-generation solve kernel
@@ -357,7 +397,14 @@ struct ccmm_chains {
     std::vector<int> sl(B, 0);
     set_slots(sl.data());
     HIPCHECK(hipMemsetAsync(status.p, 0, B * sizeof(int), ctx->stream));
-    // CRN layout (blocks in CCMM_RNG_* order, sizes from Tmax)
+    layout_crn();
+  }
+
+  // CRN layout (blocks in CCMM_RNG_* order, sizes from Tmax); the predictive-density
+  // block (mcmcVAR.m:302,306) is appended once ccmm_chains_set_fcst configured it
+  void layout_crn() {
+    const ccmm_chain_config& cf = cfg;
+    const int64_t N = cf.N;
     int64_t o = 0;
     const int64_t T = cf.T;
     crn_off[CCMM_RNG_PAI] = o;
@@ -373,6 +420,10 @@ struct ccmm_chains {
     if (bh) {
       crn_off[CCMM_RNG_ELB] = o;
       o += (int64_t)cf.Ns * cf.elbTmax * (cf.elb_gibbsburn + 1);
+    }
+    if (have_fcst) {
+      crn_off[CCMM_RNG_FCST] = o;
+      o += 2 * N * fH * fNd;
     }
     crn_len = o;
   }
@@ -668,6 +719,7 @@ struct ccmm_chains {
     ra.crn_chain_stride = stride;
     ra.seed = cfg.seed;
     ra.sweep = sweep;
+    ra.ids = have_ids ? rngIds.p : nullptr;
     for (int i = 0; i < 8; ++i) ra.off[i] = crn_off[i];
     return ra;
   }
@@ -921,6 +973,98 @@ struct ccmm_chains {
     resid_valid = false;  // X, Y changed: RESID is recomputed before the next CTA
   }
 
+  void set_fcst(int H, int Nd, const uint8_t* ndxYields, int keep) {
+    const int N = cfg.N, p = cfg.p;
+    require(!hybrid, "predictive density of the hybrid model is not built (block-hybrid and linear only)");
+    require(cfg.p >= 1 && cfg.K == N * p + 1, "predictive density needs K = N*p + 1");
+    require(N <= kFcstMaxN, "predictive density supports N <= 32");
+    require(H >= 1 && Nd >= 1, "H and Nd must be >= 1");
+    require(cfg.store_capacity > 0, "predictive density needs store_capacity > 0 (one record per kept draw)");
+    int nwx = 0;
+    for (int i = 0; i < N; ++i) nwx += ndxYields[i] ? 0 : 1;
+    require(nwx > 0 && nwx < N, "need at least one macro series and one yield");
+    if (bh)
+      for (int i = 0; i < N; ++i)
+        require(!(hActual[i] && ndxYields[i]), "a yield cannot be in the actual-rate block");
+    fH = H;
+    fNd = Nd;
+    fKeep = keep ? 1 : 0;
+    fldXj = cfg.K + N * p;
+    const size_t B = cfg.B, HN = (size_t)H * N, cap = cfg.store_capacity;
+    fYields.alloc(N);
+    HIPCHECK(hipMemcpy(fYields.p, ndxYields, N, hipMemcpyHostToDevice));
+    fYreal.alloc((size_t)cfg.ndata * N);
+    std::vector<double> nan((size_t)cfg.ndata * N, std::nan(""));
+    HIPCHECK(hipMemcpy(fYreal.p, nan.data(), nan.size() * sizeof(double), hipMemcpyHostToDevice));
+    have_fcst_slot.assign(cfg.ndata, false);
+    fXj.alloc(B * fldXj);
+    fY.alloc(B * Nd * HN);
+    fYc.alloc(B * Nd * HN);
+    fYhat.alloc(B * HN);
+    fSc.alloc(B * Nd * 4);
+    fStatus.alloc(B);
+    fYsum.alloc(B * HN);
+    fYcsum.alloc(B * HN);
+    fYhatsum.alloc(B * HN);
+    fScStore.alloc(B * cap * Nd * 4);
+    if (fKeep) {
+      fPaths.alloc(B * cap * Nd * HN);
+      fPathsC.alloc(B * cap * Nd * HN);
+    }
+    int nw = std::min((bh ? Nd : Nd + 1), kFcstMaxWaves);
+    while (nw > 1 && fcst_lds_bytes(N, p, cfg.K, nw) > 160 * 1024) --nw;
+    require(fcst_lds_bytes(N, p, cfg.K, nw) <= 160 * 1024, "forecast state does not fit LDS");
+    fnw = nw;
+    have_fcst = true;
+    reset_fcst();
+    layout_crn();
+  }
+  void reset_fcst() {
+    const size_t HN = (size_t)fH * cfg.N, B = cfg.B;
+    HIPCHECK(hipMemsetAsync(fYsum.p, 0, B * HN * sizeof(double), ctx->stream));
+    HIPCHECK(hipMemsetAsync(fYcsum.p, 0, B * HN * sizeof(double), ctx->stream));
+    HIPCHECK(hipMemsetAsync(fYhatsum.p, 0, B * HN * sizeof(double), ctx->stream));
+    HIPCHECK(hipMemsetAsync(fStatus.p, 0, B * sizeof(int), ctx->stream));
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    fstored = 0;
+  }
+
+  void run_fcst(const RngArgs& ra) {
+    if (fstored >= cfg.store_capacity) throw ArgError("forecast store full: call ccmm_chains_get_fcst");
+    static const GLNodes gl = make_gl_nodes();
+    const int N = d.N, B = d.B, H = fH, Nd = fNd;
+    ChainState cs = view();
+    FcstArgs a{};
+    a.B = B; a.N = N; a.p = cfg.p; a.K = cfg.K; a.H = H; a.Nd = Nd; a.bh = bh ? 1 : 0;
+    a.PAI = PAI.p; a.ldPAI = d.KP; a.invA = invA.p; a.logSV = h.p; a.ldSV = d.TP;
+    a.svT = Tslot.p; a.slot = slot.p; a.sqrtPHI = sqrtPHI.p; a.Xj = fXj.p; a.ldXj = fldXj;
+    a.yreal = fYreal.p; a.ldY = N; a.ndxYields = fYields.p; a.actual = bh ? dActual.p : nullptr;
+    a.elb = cfg.elb;
+    if (ra.crn) {
+      a.svz = ra.crn + ra.off[CCMM_RNG_FCST];
+      a.z = a.svz + (size_t)N * H * Nd;
+      a.crnStride = ra.crn_chain_stride;
+    }
+    a.seed = cfg.seed; a.sweep = ra.sweep; a.ids = ra.ids;
+    a.fY = fY.p; a.fYc = fYc.p; a.yhat = fYhat.p; a.scores = fSc.p; a.status = fStatus.p;
+    a.gl = gl;
+    const size_t lds = fcst_lds_bytes(N, cfg.p, cfg.K, fnw);
+    const XSel xs = xsel();
+    launch(KID_FCST, [&] {
+      hipLaunchKernelGGL(k_fcst_jumpoff, dim3(B), dim3(256), 0, ctx->stream, N, cfg.p, cfg.K, d.TP,
+                         Tslot.p, slot.p, xs.ypool, xs.yidx, fldXj, fXj.p);
+      HIPCHECK(hipFuncSetAttribute((const void*)k_fcst, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds));
+      hipLaunchKernelGGL(k_fcst, dim3(B), dim3(64 * fnw), lds, ctx->stream, a);
+      hipLaunchKernelGGL(k_fcst_accum, dim3(B), dim3(256), 0, ctx->stream, N, H, Nd,
+                         cfg.store_capacity, fstored, fY.p, fYc.p, bh ? nullptr : fYhat.p, fSc.p,
+                         fYsum.p, fYcsum.p, fYhatsum.p, fScStore.p, fKeep ? fPaths.p : nullptr,
+                         fKeep ? fPathsC.p : nullptr);
+    });
+    (void)cs;
+    ++fstored;
+  }
+
   void sweep_once(const double* dcrn, int64_t stride, bool store) {
     const RngArgs ra = rng_args(dcrn, stride);
     run_cta(ra);
@@ -929,6 +1073,7 @@ struct ccmm_chains {
     run_phi(ra);
     if (bh) run_elb(ra);
     if (store) run_store();
+    if (store && have_fcst) run_fcst(ra);
     ++sweep;
   }
 
@@ -1393,6 +1538,34 @@ int ccmm_chains_set_slots(ccmm_chains* ch, const int* slot_of_chain) {
   });
 }
 
+int ccmm_chains_set_rng_ids(ccmm_chains* ch, const uint32_t* ids) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    if (!ids) {
+      ch->have_ids = false;
+      return 0;
+    }
+    ch->rngIds.alloc(ch->cfg.B);
+    HIPCHECK(hipMemcpy(ch->rngIds.p, ids, ch->cfg.B * sizeof(uint32_t), hipMemcpyHostToDevice));
+    ch->have_ids = true;
+    return 0;
+  });
+}
+
+int ccmm_chains_get_status(ccmm_chains* ch, int* status) {
+  return guarded([&] {
+    require(ch && status, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    HIPCHECK(hipMemcpy(status, ch->status.p, ch->cfg.B * sizeof(int), hipMemcpyDeviceToHost));
+    int any = 0;
+    for (int c = 0; c < ch->cfg.B; ++c) any |= status[c];
+    return any ? 1 : 0;
+  });
+}
+
 int ccmm_chains_set_state(ccmm_chains* ch, const double* PAI, const double* A,
                           const double* sqrtht, const double* h, const double* sqrtPHI) {
   return guarded([&] {
@@ -1419,6 +1592,8 @@ int ccmm_chains_set_state(ccmm_chains* ch, const double* PAI, const double* A,
     }
     ch->sweep = 0;
     ch->stored = 0;
+    HIPCHECK(hipMemset(ch->status.p, 0, ch->cfg.B * sizeof(int)));
+    if (ch->have_fcst) ch->reset_fcst();
     ch->resid_valid = false;
     ch->have_state = true;
     return 0;
@@ -1460,6 +1635,12 @@ int ccmm_chains_sweep(ccmm_chains* ch, int nsweeps, const double* crn, int store
         return CCMM_ERR_STATE;
       }
     if (ch->cfg.rng_crn) require(crn != nullptr, "chain set was created in CRN mode: crn required");
+    if (ch->have_fcst && store)
+      for (int s = 0; s < ch->cfg.ndata; ++s)
+        if (!ch->have_fcst_slot[s]) {
+          g_err = "ccmm_chains_set_fcst_slot missing for a data slot";
+          return CCMM_ERR_STATE;
+        }
     HIPCHECK(hipSetDevice(ch->ctx->device));
     if (crn) {
       ch->crn.alloc((size_t)ch->d.B * nsweeps * ch->crn_len);
@@ -1505,6 +1686,79 @@ int ccmm_chains_get_draws(ccmm_chains* ch, double* PAI_all, double* PHI_all, dou
     if (ch->bh && ch->cfg.elbTmax > 0) fetch(ch->sShadow, (size_t)ch->cfg.Ns * ch->cfg.elbTmax, shadowrate_all);
     ch->stored = 0;
     return 0;
+  });
+}
+
+int ccmm_chains_set_fcst(ccmm_chains* ch, int H, int Nd, const uint8_t* ndxYields, int keep_paths) {
+  return guarded([&] {
+    require(ch && ndxYields, "null argument");
+    require(!ch->bh || ch->have_elb_model, "ccmm_chains_set_elb_model must be called before set_fcst");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    ch->set_fcst(H, Nd, ndxYields, keep_paths);
+    return 0;
+  });
+}
+
+int ccmm_chains_set_fcst_slot(ccmm_chains* ch, int slot, const double* yrealized) {
+  return guarded([&] {
+    require(ch && yrealized, "null argument");
+    require(ch->have_fcst, "ccmm_chains_set_fcst must be called first");
+    require(slot >= 0 && slot < ch->cfg.ndata, "slot out of range");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    HIPCHECK(hipMemcpy(ch->fYreal.p + (size_t)slot * ch->cfg.N, yrealized, ch->cfg.N * sizeof(double),
+                       hipMemcpyHostToDevice));
+    ch->have_fcst_slot[slot] = true;
+    return 0;
+  });
+}
+
+int ccmm_chains_fcst_stored(const ccmm_chains* ch) { return ch && ch->have_fcst ? ch->fstored : -1; }
+
+int ccmm_chains_get_fcst(ccmm_chains* ch, double* scores, double* fYsum, double* fYcsum,
+                         double* yhatsum, double* paths, double* paths_censored) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    require(ch->have_fcst, "ccmm_chains_set_fcst was not called");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    const size_t B = ch->cfg.B, N = ch->cfg.N, H = ch->fH, Nd = ch->fNd;
+    const size_t cap = ch->cfg.store_capacity, M = ch->fstored, HN = H * N;
+    if (scores && M) {
+      std::vector<double> buf(B * cap * Nd * 4);
+      HIPCHECK(hipMemcpy(buf.data(), ch->fScStore.p, buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+      // device [c][m][job][k] -> Nd x M x 4 x B
+      for (size_t c = 0; c < B; ++c)
+        for (size_t m = 0; m < M; ++m)
+          for (size_t job = 0; job < Nd; ++job)
+            for (size_t k = 0; k < 4; ++k)
+              scores[job + Nd * (m + M * (k + 4 * c))] = buf[((c * cap + m) * Nd + job) * 4 + k];
+    }
+    auto sums = [&](const DBuf<double>& src, double* dst) {
+      if (dst) HIPCHECK(hipMemcpy(dst, src.p, B * HN * sizeof(double), hipMemcpyDeviceToHost));
+    };
+    sums(ch->fYsum, fYsum);
+    sums(ch->fYcsum, fYcsum);
+    sums(ch->fYhatsum, yhatsum);
+    auto fetch_paths = [&](const DBuf<double>& src, double* dst) {
+      if (!dst || !M) return;
+      require(ch->fKeep != 0, "paths were not kept (keep_paths = 0)");
+      const size_t per = M * Nd * HN;  // N x H x Nd x M per chain: the device order
+      for (size_t c = 0; c < B; ++c)
+        HIPCHECK(hipMemcpy(dst + c * per, src.p + c * cap * Nd * HN, per * sizeof(double),
+                           hipMemcpyDeviceToHost));
+    };
+    fetch_paths(ch->fPaths, paths);
+    fetch_paths(ch->fPathsC, paths_censored);
+    std::vector<int> st(B);
+    HIPCHECK(hipMemcpy(st.data(), ch->fStatus.p, B * sizeof(int), hipMemcpyDeviceToHost));
+    int rc = 0;
+    for (int v : st)
+      if (v & 2) rc = CCMM_WARN_MVNCDF;
+    if (rc) g_err = "censored log score with >= 4 series at the ELB (mvncdf) is NaN";
+    ch->reset_fcst();
+    return rc;
   });
 }
 
@@ -1619,34 +1873,6 @@ int ccmm_chains_kernel_times(ccmm_chains* ch, int max, double* ms, int64_t* laun
   });
 }
 
-// Gauss-Legendre nodes/weights by Newton on P_n (host, once); negative half
-static GLNodes make_gl_nodes() {
-  GLNodes g{};
-  const int ns[3] = {6, 12, 20};
-  for (int r = 0; r < 3; ++r) {
-    const int n = ns[r];
-    for (int i = 0; i < n / 2; ++i) {
-      double x = -std::cos(M_PI * (i + 0.75) / (n + 0.5));
-      double dp = 0.0;
-      for (int it = 0; it < 100; ++it) {
-        double p0 = 1.0, p1 = x;
-        for (int k = 2; k <= n; ++k) {
-          const double p2 = ((2.0 * k - 1.0) * x * p1 - (k - 1.0) * p0) / k;
-          p0 = p1;
-          p1 = p2;
-        }
-        dp = n * (x * p1 - p0) / (x * x - 1.0);
-        const double dx = p1 / dp;
-        x -= dx;
-        if (std::fabs(dx) < 1e-17) break;
-      }
-      g.x[r][i] = x;
-      g.w[r][i] = 2.0 / ((1.0 - x * x) * dp * dp);
-    }
-  }
-  return g;
-}
-
 int ccmm_fcst(ccmm_ctx* ctx, int B, int N, int p, int H, int Nd, const double* PAI,
               const double* invA, const double* logSV0, const double* sqrtPHI,
               const double* Xjumpoff, const double* yrealized, const uint8_t* ndxYields,
@@ -1694,12 +1920,14 @@ int ccmm_fcst(ccmm_ctx* ctx, int B, int N, int p, int H, int Nd, const double* P
     dsc.alloc((size_t)B * 4 * Nd);
     dst.alloc(B);
     HIPCHECK(hipMemsetAsync(dst.p, 0, B * sizeof(int), ctx->stream));
-    FcstArgs a;
-    a.B = B; a.N = N; a.p = p; a.K = K; a.H = H; a.Nd = Nd;
-    a.PAI = dPAI.p; a.invA = dinvA.p; a.logSV0 = dlog.p; a.sqrtPHI = dsq.p; a.Xj = dXj.p;
-    a.yreal = dy.p; a.ndxYields = dmask.p; a.elb = elb;
+    FcstArgs a{};
+    a.B = B; a.N = N; a.p = p; a.K = K; a.H = H; a.Nd = Nd; a.bh = 0;
+    a.PAI = dPAI.p; a.ldPAI = K; a.invA = dinvA.p; a.logSV = dlog.p; a.ldSV = 1;
+    a.svT = nullptr; a.slot = nullptr; a.sqrtPHI = dsq.p; a.Xj = dXj.p; a.ldXj = K;
+    a.yreal = dy.p; a.ldY = 0; a.ndxYields = dmask.p; a.actual = nullptr; a.elb = elb;
     a.svz = svz ? dsvz.p : nullptr;
     a.z = svz ? dz.p : nullptr;
+    a.crnStride = (int64_t)N * H * Nd;
     a.seed = seed; a.sweep = (uint32_t)sweep;
     a.fY = dfY.p; a.fYc = dfYc.p; a.yhat = dyhat.p; a.scores = dsc.p; a.status = dst.p;
     a.gl = gl;

@@ -25,21 +25,31 @@ struct GLNodes {  // Gauss-Legendre half rules (negative nodes) for n = 6, 12, 2
 
 struct FcstArgs {
   int B, N, p, K, H, Nd;
-  const double* PAI;      // [B][N][K]   (K x N column-major per chain)
+  int bh;                 // block-hybrid companion (mcmcVARshadowrateBlockHybrid.m:147-159,566-625)
+  const double* PAI;      // [B][N][ldPAI]  (K x N column-major per chain, ld K or KP)
+  int ldPAI;
   const double* invA;     // [B][N][N]
-  const double* logSV0;   // [B][N]
+  const double* logSV;    // logSV0(c, i) = logSV[(c N + i) ldSV + (svT ? svT[slot c] - 1 : 0)]
+  int ldSV;
+  const int* svT;         // per-slot T (chain set: Vol_states(end,:) of the vintage) or nullptr
+  const int* slot;        // [B] data slot of chain c, or nullptr (slot 0)
   const double* sqrtPHI;  // [B][N][N]
-  const double* Xj;       // [B][K]      Xjumpoff
-  const double* yreal;    // [N]         yrealized(:,1)
+  const double* Xj;       // [B][ldXj] Xjumpoff: K states [1, y(T), .., y(T-p+1)]; block hybrid:
+  int ldXj;               //   then p blocks of N actual-data lags Xj[K + l N + i] (:88-96,511-520)
+  const double* yreal;    // yrealized(:,1) of chain c at yreal + slot(c) * ldY
+  int ldY;
   const uint8_t* ndxYields;  // [N]
+  const uint8_t* actual;     // [N] actualrateBlock (bh) or nullptr
   double elb;
-  const double* svz;      // [B][Nd*H][N]  randn(N, H*Nd) per chain, or nullptr (Philox)
-  const double* z;        // [B][Nd][H][N] randn(N, H, Nd) per chain, or nullptr
+  const double* svz;      // randn(N, H*Nd) of chain c at svz + c * crnStride, or nullptr (Philox)
+  const double* z;        // randn(N, H, Nd) of chain c at z + c * crnStride, or nullptr
+  int64_t crnStride;
   uint64_t seed;
   uint32_t sweep;
-  double* fY;             // [B][Nd][H][N]
-  double* fYc;            // [B][Nd][H][N]
-  double* yhat;           // [B][H][N]
+  const uint32_t* ids;    // Philox stream id of chain c, or nullptr (c)
+  double* fY;             // [B][Nd][H][N]  simulated paths (bh: uncensored)
+  double* fYc;            // [B][Nd][H][N]  censored simulation (bh: yields floored at the ELB)
+  double* yhat;           // [B][H][N]      zero-shock mean path (linear only)
   double* scores;         // [B][Nd][4]
   int* status;            // [B]  bit 1: NaN score (>= 4 censored series)
   GLNodes gl;
@@ -242,6 +252,13 @@ __device__ double score_censored(const double* invA, const double* sv, const dou
   return llf1 + llf2;
 }
 
+// Linear model (mcmcVAR.m:298-381): ring l = the linear simulation, ring c = the
+// censored simulation (yields floored inside the recursion, :354-372), plus the
+// zero-shock mean path.  Block hybrid (mcmcVARshadowrateBlockHybrid.m:566-625): ONE
+// simulation on the Nstates = K + Nyields p state; ring l holds the shadow lags, ring c
+// the same lags with every yield replaced by its actual rate max(y, ELB) (:623, the
+// actual-rate states fcstX0(ndxfcstActual)); the actual-rate equations read ring c (their
+// PAIactual on the yield lags, PAIshadow zero there: :567-574), the others ring l.
 __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   extern __shared__ double sm[];
   const int c = blockIdx.x;
@@ -261,20 +278,30 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   int* order = (int*)(dev + N);
   double* M = dev + 2 * N;
 
-  const double* PAIc = a.PAI + (size_t)c * K * N;
-  for (int e = threadIdx.x; e < K * N; e += blockDim.x) sPAI[e] = PAIc[e];
-  const double* Xj = a.Xj + (size_t)c * K;
+  const int sl = a.slot ? a.slot[c] : 0;
+  const double* PAIc = a.PAI + (size_t)c * a.ldPAI * N;
+  for (int e = threadIdx.x; e < K * N; e += blockDim.x) {
+    const int j = e / K, k = e - j * K;
+    sPAI[e] = PAIc[(size_t)j * a.ldPAI + k];
+  }
+  const double* Xj = a.Xj + (size_t)c * a.ldXj;
   const double* invA = a.invA + (size_t)c * N * N;
   const double* sqrtPHI = a.sqrtPHI + (size_t)c * N * N;
+  const double* y = a.yreal + (size_t)sl * a.ldY;
+  const int tsv = a.svT ? a.svT[sl] - 1 : 0;
+  const double* svz = a.svz ? a.svz + (size_t)c * a.crnStride : nullptr;
+  const double* zc = a.z ? a.z + (size_t)c * a.crnStride : nullptr;
+  const bool isact = a.bh && lane < N && a.actual[lane];
+  const bool isyield = lane < N && a.ndxYields[lane];
   Rng rng;
   rng.crn = nullptr;
   rng.seed = a.seed;
-  rng.chain = (uint32_t)c;
+  rng.chain = a.ids ? a.ids[c] : (uint32_t)c;
   rng.sweep = a.sweep;
   const int nsv = N * H * Nd;
   __syncthreads();
 
-  const int njobs = Nd + 1;  // job Nd = zero-shock mean path
+  const int njobs = a.bh ? Nd : Nd + 1;  // job Nd = zero-shock mean path (linear model)
   const int rounds = (njobs + nw - 1) / nw;
   for (int r = 0; r < rounds; ++r) {
     const int job = r * nw + wave;
@@ -286,9 +313,10 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         const int l = e / N, j = e - l * N;  // lag l+1 goes to slot (-l) mod p
         const int slot = (l == 0) ? 0 : p - l;
         ringl[slot * N + j] = Xj[1 + e];
-        ringc[slot * N + j] = Xj[1 + e];
+        // block hybrid: yields carry their actual-rate lags (Xjumpoff(K+1:end), :93-96)
+        ringc[slot * N + j] = (a.bh && a.ndxYields[j]) ? Xj[K + e] : Xj[1 + e];
       }
-    double logsv = (lane < N) ? a.logSV0[(size_t)c * N + lane] : 0.0;
+    double logsv = (lane < N) ? a.logSV[((size_t)c * N + lane) * a.ldSV + tsv] : 0.0;
     int head = 0;
     __syncthreads();
     for (int hh = 0; hh < H; ++hh) {
@@ -297,15 +325,14 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         double shock = 0.0;
         const int col = hh + job * H;
         for (int j = 0; j < N; ++j) {
-          const double zz = a.svz ? a.svz[((size_t)c * H * Nd + col) * N + j]
-                                  : rng.normal(CCMM_RNG_FCST, (uint32_t)(col * N + j));
+          const double zz = svz ? svz[(size_t)col * N + j]
+                                : rng.normal(CCMM_RNG_FCST, (uint32_t)(col * N + j));
           shock += sqrtPHI[lane + j * N] * zz;
         }
         logsv += shock;
         const double sv = exp(logsv * 0.5);
         const size_t zi = ((size_t)job * H + hh) * N + lane;
-        const double zz = a.z ? a.z[(size_t)c * nsv + zi]
-                              : rng.normal(CCMM_RNG_FCST, (uint32_t)(nsv + zi));
+        const double zz = zc ? zc[zi] : rng.normal(CCMM_RNG_FCST, (uint32_t)(nsv + zi));
         w[lane] = sv * zz;
         if (hh == 0) sv1[lane] = sv;
       }
@@ -316,19 +343,24 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         if (!mean_path)
           for (int j = 0; j <= lane; ++j) nu += invA[lane + j * N] * w[j];  // invA unit lower
         const double* col = sPAI + (size_t)lane * K;
-        double sl = Xj[0] * col[0], sc = sl;  // constant state stays 1 (fcstA(1,1) = 1)
+        double sl2 = Xj[0] * col[0], sc = sl2;  // constant state stays 1 (fcstA(1,1) = 1)
         for (int l = 0; l < p; ++l) {
           int slot = head - l;
           slot += (slot < 0) ? p : 0;
           const double* rl = ringl + slot * N;
           const double* rc = ringc + slot * N;
           const double* pc = col + 1 + l * N;
-          for (int j = 0; j < N; ++j) { sl += pc[j] * rl[j]; sc += pc[j] * rc[j]; }
+          for (int j = 0; j < N; ++j) { sl2 += pc[j] * rl[j]; sc += pc[j] * rc[j]; }
         }
-        yl = sl + nu;
-        yc = sc + nu;
-        // censored simulation (mcmcVAR.m:360-366)
-        if (a.ndxYields[lane] && yc < a.elb) yc = a.elb;
+        if (a.bh) {
+          yl = (isact ? sc : sl2) + nu;               // fcstA * fcstX0 + fcstB * shocks (:615)
+          yc = (isyield && yl < a.elb) ? a.elb : yl;  // actual rate max(shadow, ELB) (:623)
+        } else {
+          yl = sl2 + nu;
+          yc = sc + nu;
+          // censored simulation (mcmcVAR.m:360-366)
+          if (isyield && yc < a.elb) yc = a.elb;
+        }
         if (mean_path) {
           a.yhat[((size_t)c * H + hh) * N + lane] = yl;
         } else {
@@ -342,14 +374,19 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
       if (active && lane < N) { ringl[head * N + lane] = yl; ringc[head * N + lane] = yc; }
       __syncthreads();
     }
-    // one-step predictive log scores (mcmcVAR.m:326-352), lane 0 of the wave
+    // one-step predictive log scores (mcmcVAR.m:326-352; block hybrid :577-608), lane 0
     if (active && !mean_path && lane == 0) {
       for (int i = 0; i < N; ++i) {
+        // muY = fcstA(ndxfcstY, :) * Xjumpoff
+        const bool act = a.bh && a.actual[i];
         double s = 0.0;
-        for (int k = 0; k < K; ++k) s += sPAI[(size_t)i * K + k] * Xj[k];
+        for (int k = 0; k < K; ++k) {
+          double xv = Xj[k];
+          if (act && k > 0 && a.ndxYields[(k - 1) % N]) xv = Xj[K + k - 1];
+          s += sPAI[(size_t)i * K + k] * xv;
+        }
         mu[i] = s;
       }
-      const double* y = a.yreal;
       int nx = 0, ni = 0, natelb = 0;
       for (int i = 0; i < N; ++i) {
         if (a.ndxYields[i]) { ++ni; natelb += (y[i] <= a.elb); } else ++nx;
@@ -368,7 +405,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         sc[0] = score_gauss(M, N, dev, ld);
       }
       uint8_t cens[kFcstMaxN];
-      // (2) censored full vector (ndxYIELDS censorable)
+      // (2) censored full vector (ndxYIELDS censorable); the block-hybrid fcstLogscoreDraws
       if (natelb > 0) {
         for (int i = 0; i < N; ++i) { order[i] = i; cens[i] = a.ndxYields[i]; }
         int sel[kFcstMaxN];
@@ -410,6 +447,63 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
     }
     __syncthreads();
   }
+}
+
+// Xjumpoff of every chain from its resident data (mcmcVAR.m:108-115;
+// mcmcVARshadowrateBlockHybrid.m:511-520): [1, y(T), ..., y(T-p+1)] from the chain's Y
+// slab (block hybrid: the shadow-rate data), then p blocks of N lags of the slot's
+// actual data (the block-hybrid actual-rate states, data(Nobs-(l-1), ndxYIELDS)).
+__global__ void k_fcst_jumpoff(int N, int p, int K, int TP, const int* __restrict__ Tslot,
+                               const int* __restrict__ slot, const double* __restrict__ ypool,
+                               const int* __restrict__ yidx, int ldXj, double* __restrict__ Xj) {
+  const int c = blockIdx.x;
+  const int s = slot[c];
+  const int T = Tslot[s];
+  const double* Ych = ypool + (size_t)yidx[c] * N * TP;
+  const double* Ysl = ypool + (size_t)s * N * TP;
+  for (int e = threadIdx.x; e < ldXj; e += blockDim.x) {
+    double v = 1.0;
+    if (e > 0 && e < K) {
+      const int q = e - 1, l = q / N, i = q - l * N;
+      v = Ych[(size_t)i * TP + T - 1 - l];
+    } else if (e >= K) {
+      const int q = e - K, l = q / N, i = q - l * N;
+      v = Ysl[(size_t)i * TP + T - 1 - l];
+    }
+    Xj[(size_t)c * ldXj + e] = v;
+  }
+}
+
+// Per kept draw: running sums of the paths over the Nd draws (the means of
+// mcmcVAR.m:400-414 / BlockHybrid.m:693-742), the score draws into the store at index m
+// (fcstLogscore*Draws(:, thisMCMCdraw)), and optionally the paths themselves.
+__global__ void k_fcst_accum(int N, int H, int Nd, int cap, int m, const double* __restrict__ fY,
+                             const double* __restrict__ fYc, const double* __restrict__ yhat,
+                             const double* __restrict__ sc, double* __restrict__ sum,
+                             double* __restrict__ sumc, double* __restrict__ sumhat,
+                             double* __restrict__ scStore, double* __restrict__ paths,
+                             double* __restrict__ pathsc) {
+  const int c = blockIdx.x;
+  const size_t HN = (size_t)H * N, per = (size_t)Nd * HN;
+  const double* y = fY + (size_t)c * per;
+  const double* yc = fYc + (size_t)c * per;
+  for (size_t q = threadIdx.x; q < HN; q += blockDim.x) {
+    double a = 0.0, b = 0.0;
+    for (int job = 0; job < Nd; ++job) {
+      a += y[(size_t)job * HN + q];
+      b += yc[(size_t)job * HN + q];
+    }
+    sum[(size_t)c * HN + q] += a;
+    sumc[(size_t)c * HN + q] += b;
+    if (yhat) sumhat[(size_t)c * HN + q] += yhat[(size_t)c * HN + q];
+  }
+  for (int q = threadIdx.x; q < Nd * 4; q += blockDim.x)
+    scStore[((size_t)c * cap + m) * Nd * 4 + q] = sc[(size_t)c * Nd * 4 + q];
+  if (paths)
+    for (size_t q = threadIdx.x; q < per; q += blockDim.x) {
+      paths[((size_t)c * cap + m) * per + q] = y[q];
+      pathsc[((size_t)c * cap + m) * per + q] = yc[q];
+    }
 }
 
 inline size_t fcst_lds_bytes(int N, int p, int K, int nw) {

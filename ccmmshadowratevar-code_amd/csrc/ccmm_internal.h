@@ -133,12 +133,13 @@ struct RngArgs {
   uint64_t seed;
   uint32_t sweep;
   int64_t off[8];
+  const uint32_t* ids;     // Philox stream id of chain c (counter word 1), nullptr: c
 
   __device__ inline Rng make(int c) const {
     Rng r;
     r.crn = crn ? crn + (int64_t)c * crn_chain_stride : nullptr;
     r.seed = seed;
-    r.chain = (uint32_t)c;
+    r.chain = ids ? ids[c] : (uint32_t)c;
     r.sweep = sweep;
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.off[i] = off[i];

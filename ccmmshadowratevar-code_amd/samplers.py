@@ -5,7 +5,8 @@
 ``nchains``: B independent chains run as one device batch (the
 ``goVAR*`` parfor over vintages/chains becomes one GPU launch sequence).
 ``mcmcVARshadowrateBlockHybrid`` mirrors the block-hybrid shadow-rate sampler
-(outputs 1-6).  ``CTA``/``CTAsys``/``drawTruncNormal`` mirror the L2 functions.
+(outputs 1-13: draws and the predictive density).  ``goVARshadowrateBlockHybrid_batch``
+is the quasi-real-time OOS run over all vintages as one device batch per GPU.  ``CTA``/``CTAsys``/``drawTruncNormal`` mirror the L2 functions.
 
 Every numerical step goes through ``libccmm.so``; there is no CPU fallback.
 """
@@ -14,7 +15,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _abi
-from .model import build_bh, build_hybrid, build_var, initial_state
+from .model import build_bh, build_hybrid, build_var, elbT0_of, initial_state
 
 _CTX = {}
 
@@ -55,9 +56,8 @@ def mcmcVAR(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMean, doRATS
     st = initial_state(m, B)
     ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
     if doPredictiveDensity:
-        fc = _run_with_predictive_density(ctx, ch, m, burn, MCMCdraws, ndxYIELDS, ELBbound,
-                                          yrealized, fcstNdraws, fcstNhorizons, rndStream,
-                                          doprogress)
+        fc = _run_with_predictive_density(ch, m, burn, MCMCdraws, ndxYIELDS, ELBbound,
+                                          yrealized, fcstNdraws, fcstNhorizons, doprogress)
     else:
         _run_chain_set(ch, burn, MCMCdraws, doprogress)
     out = ch.get_draws()
@@ -70,39 +70,32 @@ def mcmcVAR(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMean, doRATS
     return tuple(res)
 
 
-def _run_with_predictive_density(ctx, ch, m, burn, MCMCdraws, ndxYIELDS, ELBbound, yrealized,
-                                 fcstNdraws, fcstNhorizons, seed, doprogress):
-    """Kept-draw loop of mcmcVAR.m:278-381 with the predictive density of each kept
-    draw on the device (ccmm_fcst), then the reshapes and means of :400-425.
-    Returns fcstYdraws, fcstYhat, fcstYcensorDraws, fcstYcensorHat, fcstYshadowDraws,
-    fcstYshadowHat, fcstYhatRB, fcstLogscoreDraws, fcstLogscoreELBdraws,
-    fcstLogscoreXdraws, fcstLogscoreIdraws (each with a trailing chain axis)."""
+def _run_with_predictive_density(ch, m, burn, MCMCdraws, ndxYIELDS, ELBbound, yrealized,
+                                 fcstNdraws, fcstNhorizons, doprogress):
+    """Kept-draw loop of mcmcVAR.m:278-381 with the predictive density of each kept draw
+    simulated inside the chain set (ccmm_chains_set_fcst: no host round trip per draw),
+    then the reshapes and means of :400-425.  Returns fcstYdraws, fcstYhat,
+    fcstYcensorDraws, fcstYcensorHat, fcstYshadowDraws, fcstYshadowHat, fcstYhatRB,
+    fcstLogscoreDraws, fcstLogscoreELBdraws, fcstLogscoreXdraws, fcstLogscoreIdraws (each
+    with a trailing chain axis)."""
     N, H, B = m.N, int(fcstNhorizons), ch.B
     Nd = fcstNdraws // MCMCdraws
     yields = np.zeros(N, bool)
     yields[np.asarray(ndxYIELDS, int)] = True
     y1 = np.asarray(yrealized, float).reshape(N, -1, order="F")[:, 0]
-    Xj = np.repeat(m.Xjumpoff[:, None], B, axis=1)
-    fY = np.empty((N, H, Nd, MCMCdraws, B))
-    fYc = np.empty_like(fY)
-    yhat = np.empty((N, H, MCMCdraws, B))
-    sc = np.empty((4, Nd, MCMCdraws, B))
-    _run_chain_set(ch, burn, 0, doprogress)
-    for d in range(MCMCdraws):
-        ch.sweep(1, store=True)
-        st = ch.get_state()
-        out = ctx.fcst(st["PAI"], st["invA"], st["h"][-1, :, :], st["sqrtPHI"], Xj, y1, yields,
-                       ELBbound, H, Nd, seed=seed, sweep=burn + d)
-        fY[:, :, :, d, :], fYc[:, :, :, d, :], yhat[:, :, d, :], sc[:, :, d, :] = out[:4]
-    fYd = fY.reshape(N, H, fcstNdraws, B, order="F")
-    fYcd = fYc.reshape(N, H, fcstNdraws, B, order="F")
+    ch.set_fcst(H, Nd, yields, keep_paths=True)
+    ch.set_fcst_slot(0, y1)
+    _run_chain_set(ch, burn, MCMCdraws, doprogress)
+    fc = ch.get_fcst(paths=True)
+    fYd = fc["paths"].reshape(N, H, fcstNdraws, B, order="F")
+    fYcd = fc["paths_censored"].reshape(N, H, fcstNdraws, B, order="F")
     fYs = fYd.copy()
     sh = fYs[yields]
     sh[sh < ELBbound] = ELBbound  # :407-411
     fYs[yields] = sh
-    scores = [sc[k].reshape(fcstNdraws, B, order="F") for k in range(4)]
+    scores = [fc["scores"][:, :, k, :].reshape(fcstNdraws, B, order="F") for k in range(4)]
     return [fYd, fYd.mean(axis=2), fYcd, fYcd.mean(axis=2), fYs, fYs.mean(axis=2),
-            yhat.mean(axis=2)] + scores
+            fc["yhatsum"] / MCMCdraws] + scores
 
 
 def _run_chain_set(ch, burn, MCMCdraws, doprogress, step=50):
@@ -143,8 +136,14 @@ def mcmcVARshadowrateBlockHybrid(thisT, MCMCdraws, p, np_, data0, ydates0, actua
         raise NotImplementedError("doELBsampling=false / doELBsampleAlternate=true need the "
                                   "missing-data sampler VARTVPSVprecisionsamplerNaN (absent "
                                   "em-matlabbox); out of scope")
-    if fcstNdraws or IRF1scale is not None:
-        raise NotImplementedError("predictive density / IRF outputs are a later row (SURVEY §8f)")
+    if IRF1scale is not None:
+        raise NotImplementedError("IRF outputs (doIRF1) are a later row (SURVEY §8f rank 4)")
+    doPredictiveDensity = bool(fcstNdraws)
+    if doPredictiveDensity:
+        if fcstNdraws % MCMCdraws != 0:  # :123-126
+            raise ValueError("fcstNdraws must be multiple of MCMCdraws")
+        if yrealized is None or fcstNhorizons is None:
+            raise ValueError("predictive density needs yrealized and fcstNhorizons")
     bm = build_bh(thisT, p, np_, data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS,
                   minnesotaPriorMean, ELBbound, elbT0, doRATSprior,
                   actualrateBlock=actualrateBlock)
@@ -163,12 +162,29 @@ def mcmcVARshadowrateBlockHybrid(thisT, MCMCdraws, p, np_, data0, ydates0, actua
     ch.set_elb_slot(0, bm.elbT0, bm.sNaN)
     st = initial_state(m, B)
     ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+    if doPredictiveDensity:
+        N, H = m.N, int(fcstNhorizons)
+        Nd = fcstNdraws // MCMCdraws
+        ndxYIELDS = np.union1d(bm.ndxS, bm.ndxO)                  # :83
+        yields = np.zeros(N, bool)
+        yields[ndxYIELDS] = True
+        ch.set_fcst(H, Nd, yields, keep_paths=True)
+        ch.set_fcst_slot(0, np.asarray(yrealized, float).reshape(N, -1, order="F")[:, 0])
     _run_chain_set(ch, burn, MCMCdraws, doprogress)
+    if doPredictiveDensity:
+        fc = ch.get_fcst(paths=True)
     out = ch.get_draws()
     ch.close()
     sr = out.get("shadowrate_all", np.full((MCMCdraws, len(bm.ndxS), 0, B), np.nan))
     res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"], sr,
            np.full((MCMCdraws, len(bm.ndxS), bm.elbT, B), np.nan)]
+    if doPredictiveDensity:
+        # outputs 7-13 (:692-748): censored draws / mean, uncensored yields (shadow-rate
+        # forecasts) / mean, the three one-step score draws
+        fYd = fc["paths_censored"].reshape(N, H, fcstNdraws, B, order="F")
+        fSd = fc["paths"][yields].reshape(int(yields.sum()), H, fcstNdraws, B, order="F")
+        sc = [fc["scores"][:, :, k, :].reshape(fcstNdraws, B, order="F") for k in (1, 2, 3)]
+        res += [fYd, fYd.mean(axis=2), fSd, fSd.mean(axis=2), sc[0], sc[1], sc[2]]
     if B == 1:
         res = [a[..., 0] for a in res]
     return tuple(res)
@@ -341,3 +357,279 @@ def goVAR_batch(data0, ydates0, Tjumpoffs, p, np_, MCMCdraws, fcstNdraws, fcstNh
     return dict(fcstYmvlogscore=S[0], fcstYmvlogscoreELB=S[1], fcstYmvlogscoreX=S[2],
                 fcstYmvlogscoreI=S[3], fcstYhat=S[4:].reshape(N, H, -1, order="F"),
                 assignment=dm.lpt_assign(costs, size))
+
+
+# ---------------------------------------------------------------------------------------
+# Block-hybrid quasi-real-time OOS batch (goVARshadowrateBlockHybrid.m) on the device
+
+def datenum(y, m, d):
+    """MATLAB datenum of a calendar date (proleptic Gregorian, day 1 = 0000-01-01)."""
+    import datetime
+    return float(datetime.date(y, m, d).toordinal() + 366)
+
+
+def matlab_prctile(x, pct, axis=0):
+    """MATLAB prctile (Statistics Toolbox): sorted values sit at percentiles
+    100 (i - 0.5) / n, linear interpolation between, clamped outside = numpy 'hazen'."""
+    return np.percentile(np.asarray(x, float), pct, axis=axis, method="hazen")
+
+
+def _bh_units(data0, ydates0, Tjumpoffs, p, np_, ndxSHADOWRATE, ndxOTHERYIELDS,
+              minnesotaPriorMean, ELBbound, elbT0, doRATSprior, fcstNhorizons):
+    """Host setup of every vintage (mcmcVARshadowrateBlockHybrid.m:30-295) and its
+    yrealized (goVARshadowrateBlockHybrid.m:267-283)."""
+    out = []
+    for thisT in Tjumpoffs:
+        bm = build_bh(int(thisT), p, np_, data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS,
+                      minnesotaPriorMean, ELBbound, elbT0, doRATSprior)
+        yr = realized_values(data0, int(thisT), fcstNhorizons, ndxSHADOWRATE, ELBbound)
+        out.append((int(thisT), bm, yr))
+    return out
+
+
+def _bh_chain_set(ctx, units, C, *, seed, ids, store_capacity, gibbsburn, ELBbound, ndxYIELDS,
+                  fcstNhorizons=None, Nd=None, keep_paths=False):
+    """One device-resident chain set holding every unit (vintage) as a data slot with C
+    chains each (the parfor over vintages as one batch), reference initialisation per
+    chain (:308-317), predictive density on every stored sweep."""
+    bm0 = units[0][1]
+    N, p = bm0.var.N, bm0.var.p
+    Tmax = max(u[1].var.T for u in units)
+    elbTmax = max(max(u[1].elbT for u in units), 1)
+    B = C * len(units)
+    ch = _abi.Chains(ctx, N=N, p=p, T=Tmax, B=B, ndata=len(units), crn=False,
+                     store_capacity=store_capacity, seed=int(seed), model=_abi.MODEL_BLOCKHYBRID,
+                     Ns=len(bm0.ndxS), elbTmax=elbTmax, elb_gibbsburn=gibbsburn, elb=ELBbound)
+    for s, (_, bm, _) in enumerate(units):
+        m = bm.var
+        ch.set_data(s, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    ch.set_elb_model(bm0.ndxS, bm0.actual_block)
+    yields = np.zeros(N, bool)
+    yields[np.asarray(ndxYIELDS, int)] = True
+    if fcstNhorizons:
+        ch.set_fcst(fcstNhorizons, Nd, yields, keep_paths=keep_paths)
+    slots = np.repeat(np.arange(len(units)), C).astype(np.int32)
+    ch.set_slots(slots)
+    K = bm0.var.K
+    init = dict(PAI=np.zeros((K, N, B), order="F"), A=np.zeros((N, N, B), order="F"),
+                sqrtht=np.ones((Tmax, N, B), order="F"), h=np.zeros((Tmax, N, B), order="F"),
+                sqrtPHI=np.zeros((N, N, B), order="F"))
+    for s, (_, bm, yr) in enumerate(units):
+        ch.set_elb_slot(s, bm.elbT0, bm.sNaN)
+        if fcstNhorizons:
+            ch.set_fcst_slot(s, yr[:, 0])
+        st = initial_state(bm.var, C)
+        T = bm.var.T
+        for k in init:
+            if k in ("sqrtht", "h"):
+                init[k][:T, :, s * C:(s + 1) * C] = st[k]
+            else:
+                init[k][..., s * C:(s + 1) * C] = st[k]
+    ch.set_state(init["PAI"], init["A"], init["sqrtht"], init["h"], init["sqrtPHI"])
+    ch.set_rng_ids(ids)
+    return ch, slots, yields
+
+
+def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS,
+                                     minnesotaPriorMean, *, Tjumpoffs=None, p=12, np_=12,
+                                     MCMCdraws=1000, fcstNdraws=None, fcstNhorizons=48,
+                                     ELBbound=0.25, doRATSprior=True, nchains=1, burnin=None,
+                                     gibbsburn=100, rndStream=1012023, dist=None, device=None,
+                                     chunk=50, max_retries=2, keep_draws=False, progress=False):
+    """The quasi-real-time OOS run of goVARshadowrateBlockHybrid.m:126-517 for the block-
+    hybrid shadow-rate VAR, as ONE device-resident chain set per rank: every vintage
+    thisT in Tjumpoffs (default: ydates > 2008-12, :127) is a data slot of the set with
+    ``nchains`` chains (the parfor over vintages, :258, becomes the batch), vintages are
+    sharded over ranks longest-processing-time first (all chains of a vintage on one
+    rank), and nothing crosses ranks until the end (one all-gather of the per-vintage
+    summaries).
+
+    Per chain: MCMCdraws burn-in + MCMCdraws kept sweeps (mcmcVARshadowrateBlockHybrid.m:
+    56-58); every kept sweep stores the draw and simulates fcstNdraws / MCMCdraws forecast
+    paths on the device (:550-625).  The ELB step is the Gibbs sampler at every sweep (the
+    PS-proposal branch, :438-466, needs the absent em-matlabbox sampler; the reference
+    falls back to the same Gibbs draw).  Philox streams are keyed by the global unit
+    (vintage index * nchains + chain), so results do not depend on the number of ranks.
+
+    Failure recovery (:287-310): chains whose blocks flagged a non-SPD pivot
+    (ccmm_chains_get_status) have their vintage re-run from scratch on fresh streams, up
+    to ``max_retries`` times.
+
+    Returns (every rank) a dict with, per vintage v: fcstYmvlogscore{,X,I} (log mean exp
+    of the fcstNdraws * nchains one-step score draws, :437-447), fcstYhat (N x H x V,
+    censored paths), fcstShadowYhat (Nyields x H x V), fcstYrealized, fcstYhaterror,
+    PAImean / PAIstdev (K x N x V, :376-378), shadowrateVintagesMid / Tails
+    (Tdata x Ns (x 4) x V, median and prctile [5 25 75 95] of the kept shadow rates,
+    :331-334,497-506), plus run statistics."""
+    import time
+    from . import distributed as dm
+    data0 = np.asarray(data0, float)
+    ydates0 = np.asarray(ydates0, float)
+    Tdata, N = data0.shape
+    ndxSHADOWRATE = np.asarray(ndxSHADOWRATE, int)
+    ndxOTHERYIELDS = np.asarray(ndxOTHERYIELDS, int)
+    ndxYIELDS = np.union1d(ndxSHADOWRATE, ndxOTHERYIELDS)
+    if Tjumpoffs is None:
+        Tjumpoffs = np.flatnonzero(ydates0 > datenum(2008, 12, 1)) + 1   # 1-based (:127)
+    Tjumpoffs = [int(t) for t in Tjumpoffs]
+    if fcstNdraws is None:
+        fcstNdraws = 10 * MCMCdraws                                      # :38
+    if fcstNdraws % MCMCdraws:
+        raise ValueError("fcstNdraws must be multiple of MCMCdraws")     # :123-126
+    Nd = fcstNdraws // MCMCdraws
+    burn = MCMCdraws if burnin is None else int(burnin)
+    C = int(nchains)
+    H = int(fcstNhorizons)
+    # ELB window start, global over vintages (:131-134)
+    elbT0 = elbT0_of(data0, ndxSHADOWRATE, ELBbound, p)
+    startELB = elbT0 + 1 + p                                            # 1-based month
+    rank = dist.get_rank() if dist is not None else 0
+    size = dist.get_world_size() if dist is not None else 1
+    device = _rank_device(dist, device)
+    K = N * p + 1
+    costs = [dm.unit_cost(t - p, K, N, n_cens=max(0, t - startELB + 1)) * C for t in Tjumpoffs]
+    assignment = dm.lpt_assign(costs, size)
+    mine = assignment[rank]
+    t0 = time.perf_counter()
+    units = _bh_units(data0, ydates0, [Tjumpoffs[v] for v in mine], p, np_, ndxSHADOWRATE,
+                      ndxOTHERYIELDS, minnesotaPriorMean, ELBbound, elbT0, doRATSprior, H) if mine else []
+    t_setup = time.perf_counter() - t0
+    ctx = context(device)
+    Ns = ndxSHADOWRATE.size
+    chunk = max(1, min(int(chunk), MCMCdraws))
+
+    def run(vidx, attempt):
+        """Run the vintages vidx (indices into `mine`); returns per-vintage results and
+        the list of vintages whose chains were flagged."""
+        us = [units[i] for i in vidx]
+        ids = np.array([(mine[i] * C + c) + attempt * 1_000_003 for i in vidx for c in range(C)],
+                       dtype=np.uint32)
+        ch, slots, yields = _bh_chain_set(ctx, us, C, seed=rndStream, ids=ids,
+                                          store_capacity=chunk, gibbsburn=gibbsburn,
+                                          ELBbound=ELBbound, ndxYIELDS=ndxYIELDS,
+                                          fcstNhorizons=H, Nd=Nd)
+        B = ch.B
+        done = 0
+        while done < burn:
+            n = min(chunk, burn - done)
+            ch.sweep(n, store=False)
+            done += n
+            if progress:
+                print(f"[rank {rank}] burn-in {done}/{burn}", flush=True)
+        scores = np.empty((Nd, MCMCdraws, 4, B))
+        fYsum = np.zeros((N, H, B))
+        fYcsum = np.zeros((N, H, B))
+        Psum = np.zeros((K, N, B))
+        P2sum = np.zeros((K, N, B))
+        elbTmax = ch.elbTmax
+        shadow = np.empty((MCMCdraws, Ns, elbTmax, B)) if elbTmax else None
+        PAIdraws = np.empty((MCMCdraws, K, N, B)) if keep_draws else None
+        done = 0
+        while done < MCMCdraws:
+            n = min(chunk, MCMCdraws - done)
+            ch.sweep(n, store=True)
+            fc = ch.get_fcst()
+            dr = ch.get_draws()
+            scores[:, done:done + n] = fc["scores"]
+            fYsum += fc["fYsum"]
+            fYcsum += fc["fYcsum"]
+            P = dr["PAI_all"]
+            Psum += P.sum(axis=0)
+            P2sum += (P * P).sum(axis=0)
+            if shadow is not None:
+                shadow[done:done + n] = dr["shadowrate_all"]
+            if PAIdraws is not None:
+                PAIdraws[done:done + n] = P
+            done += n
+            if progress:
+                print(f"[rank {rank}] kept {done}/{MCMCdraws}", flush=True)
+        status = ch.get_status()
+        ch.close()
+        res, failed = {}, []
+        for k, i in enumerate(vidx):
+            cs = slice(k * C, (k + 1) * C)
+            if np.any(status[cs] != 0):
+                failed.append(i)
+                continue
+            thisT, bm, yr = units[i]
+            nk = MCMCdraws * C
+            r = dict(thisT=thisT, yrealized=yr,
+                     logscore=_logmeanexp(scores[:, :, 1, cs].ravel()),
+                     logscoreX=_logmeanexp(scores[:, :, 2, cs].ravel()),
+                     logscoreI=_logmeanexp(scores[:, :, 3, cs].ravel()),
+                     fcstYhat=fYcsum[:, :, cs].sum(axis=2) / (nk * Nd),
+                     fcstShadowYhat=fYsum[ndxYIELDS][:, :, cs].sum(axis=2) / (nk * Nd),
+                     PAImean=Psum[:, :, cs].sum(axis=2) / nk)
+            var = P2sum[:, :, cs].sum(axis=2) / nk - r["PAImean"] ** 2
+            r["PAIstdev"] = np.sqrt(np.maximum(var, 0.0))               # std(.,1,1): 1/n
+            if shadow is not None and bm.elbT > 0:
+                # shadowrate_all permuted to (Nobs, Ns, draws) (:329-334)
+                sr = shadow[:, :, :bm.elbT, cs].transpose(2, 1, 0, 3).reshape(bm.elbT, Ns, -1)
+                r["shadowrateMid"] = np.median(sr, axis=2)
+                r["shadowrateTails"] = np.moveaxis(matlab_prctile(sr, [5, 25, 75, 95], axis=2), 0, 2)
+            if PAIdraws is not None:
+                r["PAI_all"] = PAIdraws[..., cs]
+            res[mine[i]] = r
+        return res, failed
+
+    t1 = time.perf_counter()
+    local, retries = {}, []
+    todo = list(range(len(mine)))
+    attempt = 0
+    while todo:
+        res, failed = run(todo, attempt)
+        local.update(res)
+        if failed:
+            retries.append([mine[i] for i in failed])
+        if not failed or attempt >= max_retries:
+            todo = []
+            for i in failed:                       # give up: NaN summaries for the unit
+                local[mine[i]] = None
+        else:
+            todo = failed
+        attempt += 1
+    ctx.synchronize()
+    t_run = time.perf_counter() - t1
+    # ---- end of run: one all-gather of the per-vintage summaries
+    allv = dict(local)
+    if dist is not None:
+        objs = [None] * size
+        dist.all_gather_object(objs, local)
+        for d_ in objs:
+            allv.update(d_)
+    V = len(Tjumpoffs)
+    Ny = ndxYIELDS.size
+    out = dict(Tjumpoffs=np.array(Tjumpoffs), assignment=assignment,
+               fcstYmvlogscore=np.full(V, np.nan), fcstYmvlogscoreX=np.full(V, np.nan),
+               fcstYmvlogscoreI=np.full(V, np.nan), fcstYhat=np.full((N, H, V), np.nan),
+               fcstShadowYhat=np.full((Ny, H, V), np.nan), fcstYrealized=np.full((N, H, V), np.nan),
+               PAImean=np.full((K, N, V), np.nan), PAIstdev=np.full((K, N, V), np.nan),
+               shadowrateVintagesMid=np.full((Tdata, Ns, V), np.nan),
+               shadowrateVintagesTails=np.full((Tdata, Ns, 4, V), np.nan))
+    if keep_draws:
+        out["PAI_all"] = {}
+    jumpoff = p + elbT0                                                  # :497
+    for v in range(V):
+        r = allv.get(v)
+        if r is None:
+            continue
+        out["fcstYmvlogscore"][v] = r["logscore"]
+        out["fcstYmvlogscoreX"][v] = r["logscoreX"]
+        out["fcstYmvlogscoreI"][v] = r["logscoreI"]
+        out["fcstYhat"][..., v] = r["fcstYhat"]
+        out["fcstShadowYhat"][..., v] = r["fcstShadowYhat"]
+        out["fcstYrealized"][..., v] = r["yrealized"]
+        out["PAImean"][..., v] = r["PAImean"]
+        out["PAIstdev"][..., v] = r["PAIstdev"]
+        if "shadowrateMid" in r:
+            thisT = r["thisT"]
+            out["shadowrateVintagesMid"][jumpoff:thisT, :, v] = r["shadowrateMid"]
+            out["shadowrateVintagesTails"][jumpoff:thisT, :, :, v] = r["shadowrateTails"]
+        if keep_draws and "PAI_all" in r:
+            out["PAI_all"][v] = r["PAI_all"]
+    out["fcstYhaterror"] = out["fcstYrealized"] - out["fcstYhat"]
+    n_units = len(mine) * C
+    out["stats"] = dict(rank=rank, world=size, device=device, vintages_local=len(mine),
+                        units_local=n_units, sweeps_local=n_units * (burn + MCMCdraws),
+                        setup_s=t_setup, run_s=t_run, retries=retries)
+    return out

@@ -42,7 +42,7 @@ extern "C" {
 #define CCMM_OK 0
 #define CCMM_WARN_QR_FALLBACK 1    /* CTA.m:80-92 "switching to QR routine" */
 #define CCMM_WARN_ELBT0 2          /* mcmcVARshadowrateBlockHybrid.m:203-205 */
-#define CCMM_WARN_MVNCDF 3         /* censored log score with >= 3 series at the ELB: mvncdf not restated, score NaN */
+#define CCMM_WARN_MVNCDF 3         /* censored log score with >= 4 series at the ELB: MATLAB mvncdf is randomised QMC there, score NaN */
 #define CCMM_ERR_DIM (-1)          /* gibbsdrawShadowrates.m:50-52 "dimension mismatch" */
 #define CCMM_ERR_ARG (-2)          /* invalid argument / unsupported size */
 #define CCMM_ERR_HIP (-3)          /* HIP runtime failure */
@@ -167,6 +167,16 @@ int ccmm_chains_set_slots(ccmm_chains* ch, const int* slot_of_chain);
  * sqrtht T x N x B, h (Vol_states) T x N x B, sqrtPHI N x N x B.  Resets the sweep counter. */
 int ccmm_chains_set_state(ccmm_chains* ch, const double* PAI, const double* A,
                           const double* sqrtht, const double* h, const double* sqrtPHI);
+/* Philox stream id of every chain (counter word 1; B values; NULL restores the default,
+ * the chain index).  A batch driver keys chains by their global (vintage, chain) unit so
+ * draws do not depend on how units are sharded over GPUs or packed into chain sets. */
+int ccmm_chains_set_rng_ids(ccmm_chains* ch, const uint32_t* ids);
+/* Per-chain status word since set_state (B ints, OR of: 2 CTA Cholesky, 4 A-step
+ * Cholesky, 8 SV sampler, 16 PHI Cholesky found a non-positive pivot; the block
+ * then continued with a unit pivot, so the chain's draws are invalid).  Returns 1 if any
+ * chain is flagged, 0 otherwise; the batch driver re-runs flagged units
+ * (goVARshadowrateBlockHybrid.m:287-310). */
+int ccmm_chains_get_status(ccmm_chains* ch, int* status);
 /* Any output pointer may be NULL.  invA, PHI, RESID are those of the last sweep. */
 int ccmm_chains_get_state(ccmm_chains* ch, double* PAI, double* A, double* invA, double* sqrtht,
                           double* h, double* sqrtPHI, double* PHI, double* RESID);
@@ -187,6 +197,40 @@ int ccmm_chains_stored(const ccmm_chains* ch);
  *   NaN beyond a vintage's elbT).  Any pointer may be NULL.  Resets the store. */
 int ccmm_chains_get_draws(ccmm_chains* ch, double* PAI_all, double* PHI_all, double* invA_all,
                           double* sqrtht_all, double* shadowrate_all);
+
+/* ---- predictive density inside the chain set (post-burn-in block of
+ *      mcmcVAR.m:298-381 and mcmcVARshadowrateBlockHybrid.m:550-669) ----
+ * Once configured, every stored sweep (ccmm_chains_sweep with store != 0) also
+ * simulates Nd forecast paths of H horizons per chain from the chain's draw, without
+ * leaving the device: Xjumpoff from the chain's resident data (block hybrid: shadow-rate
+ * lags plus the vintage's actual-rate lags, :511-520), SV paths, the companion recursion
+ * (linear: ltitr + censored simulation + zero-shock mean path; block hybrid: one
+ * simulation on the K + Nyields p states with the actual rates max(shadow, ELB), :615-623)
+ * and the one-step log scores (logscoreGaussian.m, logscoreGaussianCensored.m).
+ * CRN mode appends randn(N, H*Nd) and randn(N, H, Nd) (block CCMM_RNG_FCST) to every
+ * sweep's CRN record.  Linear and block-hybrid models, N <= 32.
+ *   ndxYields N bytes (ndxYIELDS), keep_paths != 0 keeps every path for quantiles/CRPS.
+ * Call after set_elb_model (block hybrid) and before sweeping. */
+int ccmm_chains_set_fcst(ccmm_chains* ch, int H, int Nd, const uint8_t* ndxYields, int keep_paths);
+/* yrealized(:,1) of data slot `slot` (N values; goVARshadowrateBlockHybrid.m:267-283,
+ * shadow rates floored at the ELB by the caller). */
+int ccmm_chains_set_fcst_slot(ccmm_chains* ch, int slot, const double* yrealized);
+/* Kept draws with a forecast record so far (-1: not configured). */
+int ccmm_chains_fcst_stored(const ccmm_chains* ch);
+/* Copy out and reset the forecast records of the M kept draws so far:
+ *   scores   Nd x M x 4 x B: (:,:,k,c) reshaped to fcstNdraws x 1 is, for k = 0..3,
+ *            fcstLogscoreDraws (uncensored Gaussian), fcstLogscoreELBdraws (censored; the
+ *            block-hybrid fcstLogscoreDraws, :588-593), fcstLogscoreXdraws, fcstLogscoreIdraws
+ *   fYsum    N x H x B  sum over the M x Nd paths (linear fcstYdraws; block hybrid the
+ *            uncensored fcstShadowrateDraws)
+ *   fYcsum   N x H x B  sum of the censored paths (linear fcstYcensorDraws; block hybrid
+ *            fcstYdraws with the yields floored at the ELB, :697-700)
+ *   yhatsum  N x H x B  sum of the zero-shock mean paths (linear yhatdraws; zero for bh)
+ *   paths, paths_censored  N x H x Nd x M x B (only with keep_paths)
+ * Any pointer may be NULL.  Returns CCMM_WARN_MVNCDF when some censored score needed
+ * mvncdf in >= 4 dimensions (that score is NaN). */
+int ccmm_chains_get_fcst(ccmm_chains* ch, double* scores, double* fYsum, double* fYcsum,
+                         double* yhatsum, double* paths, double* paths_censored);
 
 /* ---- shadow-rate models: block-hybrid (mcmcVARshadowrateBlockHybrid.m) and
  *      hybrid (mcmcVARhybridGibbs.m) ----

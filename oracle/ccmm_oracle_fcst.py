@@ -178,3 +178,83 @@ def fcst_draw(PAI, invA, logSV0, sqrtPHI, Xjumpoff, yrealized, ndxYields, elb, s
         x = step(x, np.zeros(N))
         yhat[:, hh] = x[1:N + 1]
     return fY, fYc, yhat, scores
+
+
+def bh_jumpoff(Y, data, p, ndxYIELDS):
+    """Xjumpoff of mcmcVARshadowrateBlockHybrid.m:511-520 (Nstates = K + Nyields p):
+    [1, Y(end), ..., Y(end-p+1)] of the (shadow-rate) Y, then the actual data's yields
+    data(Nobs-(l-1), ndxYIELDS) for l = 1..p."""
+    T, N = Y.shape
+    ny = np.flatnonzero(ndxYIELDS)
+    x = [np.ones(1)] + [Y[T - l] for l in range(1, p + 1)]
+    x += [data[data.shape[0] - l, ny] for l in range(1, p + 1)]
+    return np.concatenate(x)
+
+
+def fcst_draw_bh(PAI, invA, logSV0, sqrtPHI, Xjumpoff, yrealized, ndxYields, actualrateBlock,
+                 elb, svz, z):
+    """One kept draw of mcmcVARshadowrateBlockHybrid.m:550-625 as written: the dense
+    companion fcstA on Nstates = K + Nyields p states (:147-159) with PAIshadow / PAIactual
+    (:566-574), the simulation with the actual-rate states max(shadow, ELB) (:611-625),
+    and the one-step scores (:577-608).
+
+    Xjumpoff: Nstates (bh_jumpoff).  Returns fcstY N x H x Nd (uncensored: the yields are
+    floored afterwards, :696-700) and scores 3 x Nd = (fcstLogscoreDraws,
+    fcstLogscoreXdraws, fcstLogscoreIdraws)."""
+    K, N = PAI.shape
+    p = (K - 1) // N
+    H, Nd = z.shape[1], z.shape[2]
+    ndxYields = np.asarray(ndxYields, bool)
+    actual = np.asarray(actualrateBlock, bool)
+    ny = np.flatnonzero(ndxYields)
+    Nyields = ny.size
+    Nstates = K + Nyields * p
+    ndxYIELDLAGS = np.concatenate([[False], np.tile(ndxYields, p)])
+    fcstA = np.zeros((Nstates, Nstates))
+    fcstA[0, 0] = 1.0
+    fcstA[1 + N:K, 1:K - N] = np.eye(N * (p - 1))
+    fcstA[K + Nyields:, K:K + Nyields * (p - 1)] = np.eye(Nyields * (p - 1))
+    ndxfcstActual = K + np.arange(Nyields)
+    ndxfcstShadow = 1 + ny
+    ndxfcstY = 1 + np.arange(N)
+    fcstB = np.zeros((Nstates, N))
+    fcstB[ndxfcstY, :] = np.eye(N)
+    PAIactual = PAI[ndxYIELDLAGS, :].copy()
+    PAIactual[:, ~actual] = 0.0
+    PAIshadow = PAI.copy()
+    PAIshadow[np.ix_(ndxYIELDLAGS, actual)] = 0.0
+    fcstA[np.ix_(ndxfcstY, np.arange(K))] = PAIshadow.T
+    fcstA[np.ix_(ndxfcstY, np.arange(K, Nstates))] = PAIactual.T
+    logSVshocks = (sqrtPHI @ svz).reshape(N, H, Nd, order="F")
+    logSV = logSV0[:, None, None] + np.cumsum(logSVshocks, axis=1)
+    fcstSVdraws = np.exp(logSV * 0.5)
+    nushocks = fcstSVdraws * z
+    ndxYx = ~ndxYields
+    yNatELB = int(np.sum(yrealized[ndxYields] <= elb))
+    fY = np.empty((N, H, Nd))
+    scores = np.empty((3, Nd))
+    for nn in range(Nd):
+        muY = (fcstA @ Xjumpoff)[ndxfcstY]
+        sqrtOmegaY = invA @ np.diag(fcstSVdraws[:, 0, nn])
+        if yNatELB > 0:
+            scores[0, nn] = logscore_gaussian_censored(muY, sqrtOmegaY, yrealized, elb, ndxYields)
+        else:
+            scores[0, nn] = logscore_gaussian(muY, sqrtOmegaY, yrealized, np.sum(logSV[:, 0, nn]))
+        Sx = sqrtOmegaY[ndxYx, :]
+        Lx = np.linalg.cholesky(Sx @ Sx.T)
+        scores[1, nn] = logscore_gaussian(muY[ndxYx], Lx, yrealized[ndxYx],
+                                          2 * np.sum(np.log(np.diag(Lx))))
+        Si = sqrtOmegaY[ndxYields, :]
+        Li = np.linalg.cholesky(Si @ Si.T)
+        if yNatELB > 0:
+            scores[2, nn] = logscore_gaussian_censored(muY[ndxYields], Li, yrealized[ndxYields], elb)
+        else:
+            scores[2, nn] = logscore_gaussian(muY[ndxYields], Li, yrealized[ndxYields])
+        x = Xjumpoff.copy()
+        theseShocks = invA @ nushocks[:, :, nn]
+        for hh in range(H):
+            xd = fcstA @ x + fcstB @ theseShocks[:, hh]
+            fY[:, hh, nn] = xd[ndxfcstY]
+            x = xd
+            x[ndxfcstActual] = np.maximum(x[ndxfcstShadow], elb)
+    return fY, scores

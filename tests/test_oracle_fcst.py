@@ -64,3 +64,60 @@ def test_fcst_structure(F, oracle, fred):
     # uncorrelated only, so check finiteness and the ELB <= uncensored ordering is not assumed
     assert np.all(np.isfinite(sc))
     assert np.allclose(yhat[:, 0], d["PAI"][..., 0].T @ d["Xj"][:, 0])
+
+
+def test_bh_forecast_reduces_to_linear(F, oracle, fred):
+    """With no actual-rate block the block-hybrid companion (K + Nyields p states) is the
+    linear one: paths equal fcst_draw's, scores equal its ELB / X / I scores."""
+    d = fcst_inputs(oracle, fred, B=1, H=6, Nd=3)
+    N, p = 20, 12
+    y = d["ys"][2]
+    args = (d["PAI"][..., 0], d["invA"][..., 0], d["logSV0"][:, 0], d["sqrtPHI"][..., 0])
+    fY, fYc, yhat, sc = F.fcst_draw(*args, d["Xj"][:, 0], y, d["yields"], 0.25,
+                                    d["svz"][..., 0], d["z"][..., 0])
+    ny = int(d["yields"].sum())
+    Xj = np.concatenate([d["Xj"][:, 0], np.full(ny * p, 0.123)])  # actual lags: unused here
+    bY, bsc = F.fcst_draw_bh(*args, Xj, y, d["yields"], np.zeros(N, bool), 0.25,
+                             d["svz"][..., 0], d["z"][..., 0])
+    np.testing.assert_allclose(bY, fY, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(bsc, sc[1:], rtol=1e-12, atol=1e-12)
+
+
+def test_bh_forecast_actual_rates(F, oracle, fred):
+    """The actual-rate equations read the ELB-floored yields (fcstX0(ndxfcstActual) =
+    max(shadow, ELB), mcmcVARshadowrateBlockHybrid.m:623); an independent lag-ring
+    restatement of the same recursion agrees with the dense-companion oracle."""
+    d = fcst_inputs(oracle, fred, B=1, H=8, Nd=2)
+    N, p, elb = 20, 12, 0.25
+    K = N * p + 1
+    yields = d["yields"]
+    actual = ~yields
+    PAI, invA = d["PAI"][..., 0].copy(), d["invA"][..., 0]
+    PAI[0, yields] -= 0.6                          # push the yields below the ELB
+    rng = np.random.default_rng(3)
+    ny = np.flatnonzero(yields)
+    act_lags = rng.uniform(0.0, 0.3, (p, ny.size))
+    Xj = np.concatenate([d["Xj"][:, 0], act_lags.ravel()])
+    y = d["ys"][0]
+    fY, sc = F.fcst_draw_bh(PAI, invA, d["logSV0"][:, 0], d["sqrtPHI"][..., 0], Xj, y, yields,
+                            actual, elb, d["svz"][..., 0], d["z"][..., 0])
+    assert (fY[yields] < elb).any()                # the floor binds somewhere
+    H, Nd = 8, 2
+    svs = (d["sqrtPHI"][..., 0] @ d["svz"][..., 0]).reshape(N, H, Nd, order="F")
+    for nn in range(Nd):
+        sv = np.exp(0.5 * (d["logSV0"][:, 0][:, None] + np.cumsum(svs[:, :, nn], axis=1)))
+        nu = invA @ (sv * d["z"][..., 0][:, :, nn])
+        shadow = [Xj[1 + l * N:1 + (l + 1) * N].copy() for l in range(p)]
+        mixed = [s.copy() for s in shadow]
+        for l in range(p):
+            mixed[l][ny] = act_lags[l]
+        for hh in range(H):
+            xs = np.concatenate([[1.0]] + shadow)
+            xm = np.concatenate([[1.0]] + mixed)
+            yv = np.where(actual, PAI.T @ xm, PAI.T @ xs) + nu[:, hh]
+            np.testing.assert_allclose(fY[:, hh, nn], yv, rtol=1e-11, atol=1e-11)
+            shadow = [yv.copy()] + shadow[:-1]
+            ym = yv.copy()
+            ym[yields] = np.maximum(ym[yields], elb)
+            mixed = [ym] + mixed[:-1]
+    assert np.all(np.isfinite(sc))
