@@ -41,14 +41,21 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--chains", type=int, default=256)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0,
-                    help="budget of the CPU-oracle baseline sample (rank 0, N=1 only)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="budget per process of each CPU-oracle baseline line (rank 0, N=1 only)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-fcst", action="store_true", help="skip the predictive-density line")
-    ap.add_argument("--bh-steps", type=int, default=5,
-                    help="timed sweeps of the block-hybrid secondary line (configs[2]); 0 = skip")
-    ap.add_argument("--bh-warmup", type=int, default=2)
+    ap.add_argument("--bh-steps", type=int, default=3,
+                    help="timed sweeps of the block-hybrid secondary lines (configs[2]); 0 = skip")
+    ap.add_argument("--bh-warmup", type=int, default=1)
+    ap.add_argument("--bh-chains", default="256,1024,4096",
+                    help="chains per GPU of the block-hybrid lines (comma list)")
+    ap.add_argument("--oos-steps", type=int, default=3,
+                    help="timed kept sweeps (with forecasts) of the OOS line (configs[3]); 0 = skip")
+    ap.add_argument("--oos-chains", default="1,8", help="chains per vintage of the OOS lines")
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help="parallel single-thread CPU baseline processes (0: min(16, cpus))")
     return ap.parse_args()
 
 
@@ -64,6 +71,11 @@ def main():
         torch.cuda.set_device(local)
         dist_.init_process_group("nccl")
         dist = dist_
+
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        # before the GPU is initialised: the baseline runs in spawned single-thread processes
+        cpu = cpu_baseline(args.cpu_seconds, args.cpu_workers)
 
     import __graft_entry__ as ge
     pkg = ge.load_package()
@@ -106,8 +118,15 @@ def main():
     assert np.all(np.isfinite(draws["PAI_all"])), "non-finite draws"
     fc = bench_predictive(ctx, ch, m, d, B) if (rank == 0 and not args.no_fcst) else None
     ch.close()
-    # secondary line (configs[2]) runs on every rank: it has its own barrier/max-reduction
-    bh = bench_block_hybrid(pkg, ctx, d, B, args, rank, barrier, dist) if args.bh_steps > 0 else None
+    # secondary lines (configs[2], configs[3]) run on every rank: own barrier/max-reduction
+    bh = None
+    if args.bh_steps > 0:
+        bh = [bench_block_hybrid(pkg, ctx, d, int(b), args, rank, barrier, dist)
+              for b in args.bh_chains.split(",") if b.strip()]
+    oos = None
+    if args.oos_steps > 0:
+        oos = [bench_oos(pkg, ctx, d, int(c), args, rank, barrier, dist)
+               for c in args.oos_chains.split(",") if c.strip()]
 
     if rank != 0:
         if dist is not None:
@@ -177,10 +196,12 @@ def main():
         out["dominant_kernel"] = dom
     if bh is not None:
         out["block_hybrid"] = bh
+    if oos is not None:
+        out["oos"] = oos
     if fc is not None:
         out["predictive"] = fc
-    if world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -206,6 +227,76 @@ def bench_predictive(ctx, ch, m, d, B, H=48, Nd=10, reps=3):
     return {"workload": f"ccmm_fcst: {B} chains x {Nd} draws x {H} horizons, linear + censored "
                         "paths, RB mean, 4 log scores", "ms_per_call": round(ms, 3),
             "chain_draws_per_s": round(B / (ms * 1e-3), 1), "boundary": "host buffers (PCIe-inclusive)"}
+
+
+def bench_oos(pkg, ctx, d, C, args, rank, barrier, dist, H=48, Nd=10):
+    """BASELINE.json configs[3] (goVARshadowrateBlockHybrid quasi-real-time OOS): all 164
+    vintages (jump-offs after 2008-12: T = 587..750, elbT = 2..165) x C chains as ONE
+    device-resident chain set per GPU (vintages sharded over ranks longest-processing-time
+    first), ELB Gibbs (101 passes) every sweep.  Timed: kept sweeps, each storing the draw
+    and simulating the predictive density on the device (10 draws x 48 horizons per kept
+    draw and chain, mcmcVARshadowrateBlockHybrid.m:550-625) plus the one-step log scores;
+    then plain (burn-in) sweeps.  value = units x sweeps / time summed over ranks (fixed
+    total work: strong scaling).  The projected OOS wall time is 1000 burn-in + 1000 kept
+    sweeps per unit at these rates."""
+    import time as _t
+    p = 12
+    S = pkg.samplers
+    ndxS, ndxO, ndxY = pkg.model.setShadowYields(d["ncode"], 0.25)
+    mpm = pkg.model.setMinnesotaMean(d["ncode"])
+    Tj = [int(t) for t in (np.flatnonzero(d["ydates"] > S.datenum(2008, 12, 1)) + 1)]
+    world = dist.get_world_size() if dist is not None else 1
+    N, K = d["data"].shape[1], d["data"].shape[1] * p + 1
+    e0 = pkg.model.elbT0_of(d["data"], ndxS, 0.25, p)
+    costs = [pkg.distributed.unit_cost(t - p, K, N, n_cens=max(0, t - (e0 + 1 + p) + 1)) for t in Tj]
+    mine = pkg.distributed.lpt_assign(costs, world)[rank]
+    units = S._bh_units(d["data"], d["ydates"], [Tj[v] for v in mine], p, 12, ndxS, ndxO, mpm,
+                        0.25, e0, True, H)
+    ids = np.array([v * C + c for v in mine for c in range(C)], dtype=np.uint32)
+    steps = args.oos_steps
+    ch, _, _ = S._bh_chain_set(ctx, units, C, seed=1012023, ids=ids, store_capacity=steps + 1,
+                                gibbsburn=100, ELBbound=0.25, ndxYIELDS=ndxY, fcstNhorizons=H, Nd=Nd)
+    ch.sweep(1, store=True)                       # warm-up (also the forecast path)
+    ch.get_fcst()
+    ch.get_draws()
+    barrier()
+    if not args.no_profile:
+        ch.profile(True)
+    t0 = _t.perf_counter()
+    ch.sweep(steps, store=True)
+    barrier()
+    el_kept = _t.perf_counter() - t0
+    kt = ch.kernel_times() if not args.no_profile else {}
+    fc = ch.get_fcst()
+    assert np.all(np.isfinite(fc["fYsum"])), "non-finite forecasts"
+    ch.profile(False)
+    t0 = _t.perf_counter()
+    ch.sweep(steps, store=False)
+    barrier()
+    el_burn = _t.perf_counter() - t0
+    st = ch.get_status()
+    ch.close()
+    if dist is not None:
+        import torch
+        tt = torch.tensor([el_kept, el_burn], dtype=torch.float64, device=f"cuda:{ctx.device}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el_kept, el_burn = (float(x) for x in tt.tolist())
+    units_total = len(Tj) * C
+    kept = units_total * steps / el_kept
+    burn = units_total * steps / el_burn
+    res = {"workload": f"configs[3]: goVARshadowrateBlockHybrid OOS, {len(Tj)} vintages x {C} "
+                       f"chain(s) = {units_total} units (T = 587..750, elbT = 2..165), one "
+                       f"device-resident chain set per GPU, vintages LPT-sharded over {world} "
+                       f"GPU(s)",
+           "value": round(kept, 3), "unit": "sweeps/s (kept sweeps incl. predictive density)",
+           "burnin_sweeps_per_s": round(burn, 3), "ms_per_kept_step": round(1e3 * el_kept / steps, 3),
+           "ms_per_burnin_step": round(1e3 * el_burn / steps, 3), "steps": steps,
+           "forecast": f"{Nd} draws x {H} horizons per kept draw and chain + 4 one-step scores",
+           "projected_full_run_s": round(1000 * units_total / burn + 1000 * units_total / kept, 1),
+           "flagged_units": int(np.count_nonzero(st)), "scaling": "strong"}
+    if kt:
+        res["kernel_ms_per_sweep"] = {k: round(v[0] / v[1], 4) for k, v in kt.items() if v[1]}
+    return res
 
 
 def bench_block_hybrid(pkg, ctx, d, B, args, rank, barrier, dist):
@@ -293,28 +384,71 @@ def load_pmc():
         return {}, None
 
 
-def cpu_baseline(budget_s):
-    """The CPU oracle (the reference algorithm as written: kron-materialised X_j,
-    explicit inverse; oracle/ccmm_oracle.py) timed on this host, single-threaded
-    BLAS, one chain, as many sweeps as fit in ~budget_s."""
+def _cpu_worker(kind, budget_s, seed, q):
+    """One single-threaded oracle process (parfor worker): as many sweeps of one chain as
+    fit in budget_s.  kind: linear-kron | linear-syrk | blockhybrid."""
+    import sys as _s
+    _s.path.insert(0, str(ROOT))
     from threadpoolctl import threadpool_limits
 
     from oracle import ccmm_oracle as O
     fred = O.load_fred_csv(ROOT / "tests/golden/data/fredblockMD20-2022-09.csv")
     mpm = O.set_minnesota_mean(fred["ncode"])
-    su = O.var_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], mpm, True)
-    st = O.init_state(su)
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(seed)
     n = 0
     with threadpool_limits(1):
+        if kind == "blockhybrid":
+            from oracle import ccmm_oracle_bh as BH
+            ndxS, ndxO, _ = O.set_shadow_yields(fred["ncode"], 0.25)
+            e0 = O.elb_t0(fred["data"], ndxS, 0.25, 12)
+            bs = BH.bh_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], ndxS, ndxO,
+                             mpm, 0.25, e0)
+            st = BH.bh_init_state(bs)
+            step = lambda st: BH.bh_sweep(st, bs, BH.bh_draw_crn(rng, bs), elb_impl="qr")
+        else:
+            su = O.var_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], mpm, True)
+            st = O.init_state(su)
+            form = kind.split("-")[1]
+            step = lambda st: O.linear_sweep(st, su, O.draw_crn(rng, su.N, su.K, su.T, su.dPHI),
+                                             cta_form=form)
         t0 = time.perf_counter()
         while True:
-            crn = O.draw_crn(rng, su.N, su.K, su.T, su.dPHI)
-            st = O.linear_sweep(st, su, crn)
+            st = step(st)
             n += 1
             el = time.perf_counter() - t0
-            if el > budget_s or n >= 50:
+            if el > budget_s:
                 break
+    q.put((n, el))
+
+
+def _cpu_line(kind, budget_s, workers, sample):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_cpu_worker, args=(kind, budget_s, 1000 + w, q)) for w in range(workers)]
+    for p_ in ps:
+        p_.start()
+    res = [q.get(timeout=budget_s * 20 + 300) for _ in ps]
+    for p_ in ps:
+        p_.join(timeout=60)
+    value = sum(n / el for n, el in res)
+    nsw = sum(n for n, _ in res)
+    return {"value": round(value, 4), "unit": "sweeps/s", "cores": workers, "kind": "port",
+            "sample": f"{nsw} sweeps: {workers} single-thread processes (parfor-style, one chain "
+                      f"each) x ~{budget_s:.0f} s, {sample}"}
+
+
+def cpu_baseline(budget_s, workers=0):
+    """The reference algorithm restated on the host (oracle/; MATLAB cannot run here),
+    parfor-style: `workers` single-thread processes, one chain each, real data T = 750.
+    Three lines: the linear sampler as written (kron-materialised X_j,
+    explicit inverse: CTA.m:69-78), the linear sampler in the algorithmic weighted-SYRK
+    form, and the block-hybrid sampler as written (QR smoothing weights,
+    gibbsdrawShadowrates.m:74-127, 101 Gibbs passes).  The first is the reported
+    ``cpu_baseline``; the others ride along."""
+    import os
+    if workers <= 0:
+        workers = min(16, os.cpu_count() or 1)   # the GPU box's CPU share for one GPU
     cpu = platform.processor() or platform.machine()
     try:
         with open("/proc/cpuinfo") as fh:
@@ -324,9 +458,27 @@ def cpu_baseline(budget_s):
                     break
     except OSError:
         pass
-    return {"value": round(n / el, 5), "unit": "sweeps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} sweeps of one chain, real data T=750, oracle/ccmm_oracle.py "
-                      f"(as-written kron CTA), numpy/OpenBLAS 1 thread, {el:.1f}s, CPU: {cpu}"}
+    blas = "unknown"
+    try:
+        from threadpoolctl import threadpool_info
+        info = [i for i in threadpool_info() if i.get("user_api") == "blas"]
+        if info:
+            blas = f"{info[0].get('internal_api')} {info[0].get('version')}"
+    except Exception:
+        pass
+    env = f"numpy/scipy, BLAS {blas} (1 thread per process), CPU {cpu}, {os.cpu_count()} " \
+          f"logical CPUs visible"
+    lin = _cpu_line("linear-kron", budget_s, workers,
+                    "oracle/ccmm_oracle.py linear sweep as written (kron CTA, explicit inverse), " + env)
+    lin["lines"] = {
+        "linear_syrk": _cpu_line("linear-syrk", budget_s, workers,
+                                 "linear sweep, algorithmic CTA (weighted SYRK + Cholesky + "
+                                 "triangular solves), " + env),
+        "blockhybrid": _cpu_line("blockhybrid", budget_s, workers,
+                                 "block-hybrid sweep as written (CTAsys kron form, ELB Gibbs with "
+                                 "QR smoothing weights, 101 passes), " + env),
+    }
+    return lin
 
 
 if __name__ == "__main__":

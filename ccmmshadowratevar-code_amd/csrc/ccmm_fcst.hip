@@ -110,14 +110,17 @@ __device__ double bvnu(double dh, double dk, double r, const GLNodes& gl) {
 // P = int_{-inf}^{x1/L11} phi(z) BVN(h(z), k(z); rho) dz with the conditional
 // bivariate of (X2, X3) | z (Genz BVN inside).  The integrand steps where h or k
 // changes sign, so the outer interval is split there and each segment integrated
-// on panels graded geometrically towards both ends (20-point Gauss-Legendre).
+// on panels graded geometrically towards both ends (20-point Gauss-Legendre):
+// panel j of a side spans [w0 (2^j - 1), min(w0 (2^(j+1) - 1), half)] from that end.
 // MATLAB's mvncdf (trivariate rule, absolute tolerance 1e-8) is the reference.
-__device__ double tvn_cdf(const double* x, const double* M, const GLNodes& gl) {
+// Called by all 64 lanes of a wave with identical arguments: the (segment, side, panel,
+// node) evaluations are spread over the lanes and summed with one wave reduction.
+__device__ double tvn_cdf(const double* x, const double* M, const GLNodes& gl, int lane) {
   const double l11 = M[0], l21 = M[1], l31 = M[2];
   const double l22 = M[1 + kFcstMaxN], l32 = M[2 + kFcstMaxN], l33 = M[2 + 2 * kFcstMaxN];
   const double s3 = sqrt(l32 * l32 + l33 * l33), rho = l32 / s3;
   const double b = x[0] / l11;
-  const double lo = -10.0;
+  const double lo = -10.0, w0 = 1e-4;
   if (b <= lo) return 0.0;
   double brk[4];
   int nb = 0;
@@ -127,33 +130,42 @@ __device__ double tvn_cdf(const double* x, const double* M, const GLNodes& gl) {
   for (int i = 0; i < 2; ++i)
     if (cand[i] > brk[nb - 1] + 1e-12 && cand[i] < b - 1e-12) brk[nb++] = cand[i];
   brk[nb++] = b;
-  double total = 0.0;
+  // panels per side of each segment
+  int npan[3];
+  int total = 0;
   for (int sgm = 0; sgm + 1 < nb; ++sgm) {
+    const double half = 0.5 * (brk[sgm + 1] - brk[sgm]);
+    int n = 0;
+    double pos = 0.0, w = fmin(w0, half);
+    while (pos < half) {
+      pos += fmin(w, half - pos);
+      w *= 2.0;
+      ++n;
+    }
+    npan[sgm] = n;
+    total += 2 * n * 20;
+  }
+  double acc = 0.0;
+  for (int q = lane; q < total; q += 64) {
+    int rem = q, sgm = 0;
+    while (rem >= 2 * npan[sgm] * 20) { rem -= 2 * npan[sgm] * 20; ++sgm; }
+    const int side = rem / (npan[sgm] * 20);
+    rem -= side * npan[sgm] * 20;
+    const int j = rem / 20, node = rem - j * 20;
     const double a0 = brk[sgm], a1 = brk[sgm + 1];
     const double half = 0.5 * (a1 - a0);
-    // panels: widths w0 * 2^j from each end until they meet at the midpoint
-    for (int side = 0; side < 2; ++side) {
-      double pos = 0.0, w = fmin(1e-4, half);
-      while (pos < half) {
-        const double wi = fmin(w, half - pos);
-        const double u0 = pos, u1 = pos + wi;  // distance from this end
-        const double c = 0.5 * (u0 + u1), r = 0.5 * (u1 - u0);
-        double acc = 0.0;
-        for (int i = 0; i < 10; ++i) {
-          for (int sg = -1; sg <= 1; sg += 2) {
-            const double u = c + sg * r * gl.x[2][i];
-            const double z = side == 0 ? a0 + u : a1 - u;
-            const double h = (x[1] - l21 * z) / l22, k = (x[2] - l31 * z) / s3;
-            acc += gl.w[2][i] * exp(-0.5 * z * z) * bvnu(-h, -k, rho, gl);
-          }
-        }
-        total += acc * r * 0.39894228040143267794;
-        pos = u1;
-        w *= 2.0;
-      }
-    }
+    const double wj = fmin(w0, half) * exp2((double)j);
+    const double u0 = (j == 0) ? 0.0 : fmin(w0, half) * (exp2((double)j) - 1.0);
+    const double u1 = fmin(u0 + wj, half);
+    const double c = 0.5 * (u0 + u1), r = 0.5 * (u1 - u0);
+    const int i = node >> 1;
+    const double sg = (node & 1) ? 1.0 : -1.0;
+    const double u = c + sg * r * gl.x[2][i];
+    const double z = side == 0 ? a0 + u : a1 - u;
+    const double h = (x[1] - l21 * z) / l22, k = (x[2] - l31 * z) / s3;
+    acc += gl.w[2][i] * exp(-0.5 * z * z) * bvnu(-h, -k, rho, gl) * r;
   }
-  return total;
+  return wave_sum(acc) * 0.39894228040143267794;
 }
 
 // in-place lower Cholesky of an n x n LDS matrix (ld = kFcstMaxN); false if not SPD
@@ -216,7 +228,7 @@ __device__ double logdet_chol(const double* L, int n) {
 __device__ double score_censored(const double* invA, const double* sv, const double* mu,
                                  const double* y, const int* sel, const uint8_t* cens, int n,
                                  int N, double elb, double* M, double* dev, int* order,
-                                 const GLNodes& gl, bool* unsupported) {
+                                 const GLNodes& gl, bool* unsupported, int lane) {
   int noff = 0, nat = 0;
   for (int i = 0; i < n; ++i)
     if (!(cens[i] && y[sel[i]] <= elb)) order[noff++] = sel[i];
@@ -247,7 +259,7 @@ __device__ double score_censored(const double* invA, const double* sv, const dou
     llf2 = log(bvnu(-h, -k, rho, gl));
   } else {
     const double xv[3] = {yat[0] - y21[0], yat[1] - y21[1], yat[2] - y21[2]};
-    llf2 = log(tvn_cdf(xv, M + noff + noff * kFcstMaxN, gl));
+    llf2 = log(tvn_cdf(xv, M + noff + noff * kFcstMaxN, gl, lane));
   }
   return llf1 + llf2;
 }
@@ -374,8 +386,10 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
       if (active && lane < N) { ringl[head * N + lane] = yl; ringc[head * N + lane] = yc; }
       __syncthreads();
     }
-    // one-step predictive log scores (mcmcVAR.m:326-352; block hybrid :577-608), lane 0
-    if (active && !mean_path && lane == 0) {
+    // one-step predictive log scores (mcmcVAR.m:326-352; block hybrid :577-608): every lane
+    // of the wave runs the same scalar algebra (uniform control flow, identical LDS
+    // writes); the trivariate mvncdf quadrature spreads its nodes over the lanes
+    if (active && !mean_path) {
       for (int i = 0; i < N; ++i) {
         // muY = fcstA(ndxfcstY, :) * Xjumpoff
         const bool act = a.bh && a.actual[i];
@@ -411,7 +425,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         int sel[kFcstMaxN];
         for (int i = 0; i < N; ++i) sel[i] = i;
         sc[1] = score_censored(invA, sv1, mu, y, sel, cens, N, N, a.elb, M, dev, order, a.gl,
-                               &unsupported);
+                               &unsupported, lane);
       } else {
         sc[1] = sc[0];
       }
@@ -434,7 +448,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         for (int i = 0; i < N; ++i) if (a.ndxYields[i]) { sel[q] = i; cens[q] = 1; ++q; }
         if (natelb > 0) {
           sc[3] = score_censored(invA, sv1, mu, y, sel, cens, ni, N, a.elb, M, dev, order, a.gl,
-                                 &unsupported);
+                                 &unsupported, lane);
         } else if (gram_rows_chol(invA, sv1, sel, ni, N, M)) {
           for (int i = 0; i < ni; ++i) dev[i] = y[sel[i]] - mu[sel[i]];
           sc[3] = score_gauss(M, ni, dev, logdet_chol(M, ni));
@@ -442,8 +456,10 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
           sc[3] = NAN;
         }
       }
-      for (int q = 0; q < 4; ++q) a.scores[((size_t)c * Nd + job) * 4 + q] = sc[q];
-      if (unsupported) atomicOr(&a.status[c], 2);
+      if (lane == 0) {
+        for (int q = 0; q < 4; ++q) a.scores[((size_t)c * Nd + job) * 4 + q] = sc[q];
+        if (unsupported) atomicOr(&a.status[c], 2);
+      }
     }
     __syncthreads();
   }

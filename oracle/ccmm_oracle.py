@@ -273,6 +273,26 @@ def cta_sys(Y, XX, N, K, T, A, sqrtht, iVdiag, iVb, PAI, z, return_sd=False):
     return PAI, status
 
 
+def cta_syrk(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z):
+    """CTA.m:57-98 in the algorithmic form the device uses: per equation
+    the weighted Gram X' diag(w) X + diag(iV_j) (no kron materialisation), Cholesky and
+    two triangular solves.  Equal to ``cta`` in exact arithmetic; the second CPU baseline
+    line of bench.py."""
+    PAI = np.array(PAI, dtype=float, copy=True)
+    ih2 = 1.0 / sqrtht ** 2
+    for j in range(N):
+        PAI[:, j] = 0.0
+        E = Y - X @ PAI
+        w = ih2[:, j:] @ (A[j:, j] ** 2)
+        v = ((E @ A[j:, :].T) * ih2[:, j:]) @ A[j:, j]
+        G = X.T @ (X * w[:, None])
+        G[np.diag_indices(K)] += iVdiag[:, j]
+        L = np.linalg.cholesky(G)
+        y = solve_triangular(L, iVb[:, j] + X.T @ v, lower=True)
+        PAI[:, j] = solve_triangular(L.T, y + z[:, j], lower=False)
+    return PAI, 0
+
+
 def cta_post_moments_syrk(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, j):
     """Algebraic (weighted-SYRK) form of equation j's posterior precision and rhs,
     used only by tests to cross-check the kron form (SURVEY.md §3.4 identity)."""
@@ -518,10 +538,12 @@ def vech_lower(M):
 # --------------------------------------------------------------------------
 # One linear BVAR-SV sweep (mcmcVAR.m:211-274)
 # --------------------------------------------------------------------------
-def linear_sweep(st, su: Setup, crn):
+def linear_sweep(st, su: Setup, crn, cta_form="kron"):
+    """cta_form: "kron" = CTA.m as written; "syrk" = the algorithmic form (cta_syrk)."""
     N, K, T = su.N, su.K, su.T
-    PAI, status = cta(su.Y, su.X, N, K, st["A"], st["sqrtht"], su.iVdiag, su.iVb, st["PAI"],
-                      crn["zPAI"])
+    f = cta if cta_form == "kron" else cta_syrk
+    PAI, status = f(su.Y, su.X, N, K, st["A"], st["sqrtht"], su.iVdiag, su.iVb, st["PAI"],
+                    crn["zPAI"])
     RESID = su.Y - su.X @ PAI
     A, invA = a_step(RESID, st["sqrtht"], crn["zA"])
     logy2 = np.log((RESID @ A.T) ** 2 + su.logy2offset)
