@@ -294,7 +294,7 @@ class Chains:
     KERNELS = ("k_resid", "k_cta_weights", "k_syrk", "k_chol", "k_cta_solve", "k_astep",
                "k_sv_mix", "k_sv_part", "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
                "k_elb_prep", "k_elb_cond", "k_elb_gibbs", "k_elb_rebuild", "k_gram_chol_lag",
-               "k_cta_solve_lag", "k_fcst")
+               "k_cta_solve_lag", "k_fcst", "k_gram_big", "k_chol_big", "k_cta_solve_big")
 
     def __init__(self, ctx: Context, *, N, p, T, B, ndata=1, model=MODEL_LINEAR, crn=False,
                  store_capacity=0, logy2offset=1e-3, seed=1012023, dPHI=None, Ns=0, elbTmax=0,

@@ -16,6 +16,7 @@
 #include "ccmm_fcst.hip"
 #include "ccmm_lag.h"
 #include "ccmm_svpart.h"
+#include "ccmm_big.h"
 #include <cstdlib>
 
 using namespace ccmm;
@@ -71,6 +72,10 @@ struct DBuf {
     if (count == 0) return;
     HIPCHECK(hipMalloc(&p, count * sizeof(T)));
     n = count;
+    // debug: CCMM_POISON=1 fills new allocations with 0xFF bytes (NaN doubles) to expose
+    // reads of never-written device memory
+    static const bool poison = std::getenv("CCMM_POISON") != nullptr;
+    if (poison) HIPCHECK(hipMemset(p, 0xFF, count * sizeof(T)));
   }
   ~DBuf() {
     if (p) (void)hipFree(p);
@@ -170,6 +175,9 @@ enum KernelId {
   KID_GRAMLAG,
   KID_SOLVELAG,
   KID_FCST,
+  KID_GRAMBIG,
+  KID_CHOLBIG,
+  KID_SOLVEBIG,
   KID_COUNT
 };
 static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syrk", "k_chol",
@@ -177,7 +185,8 @@ static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syr
                                               "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
                                               "k_elb_prep", "k_elb_cond", "k_elb_gibbs",
                                               "k_elb_rebuild", "k_gram_chol_lag",
-                                              "k_cta_solve_lag", "k_fcst"};
+                                              "k_cta_solve_lag", "k_fcst",
+                                              "k_gram_big", "k_chol_big", "k_cta_solve_big"};
 
 struct ccmm_chains {
   ccmm_ctx* ctx = nullptr;
@@ -236,6 +245,11 @@ struct ccmm_chains {
   std::vector<bool> slot_lag;
   DBuf<double> Dpool;
   DBuf<int> dColmap;
+  // large-system CTA (ccmm_big.hip): K > 512 or N > 32, or CCMM_FORCE_BIG=1
+  bool big = false;
+  int nGroups = 0;
+  DBuf<int4> bigGroups;
+  DBuf<double> Ubuf;
   // profiling
   bool profiling = false;
   struct Ev {
@@ -338,7 +352,7 @@ struct ccmm_chains {
       require(2 * cf.p * cf.Ns <= kElbColMax, "2 p Ns must be <= 128");
       require(cf.p >= 1, "p must be >= 1");
     }
-    require(cf.N >= 1 && cf.N <= kMaxNSmall, "N must be in [1, 32]");
+    require(cf.N >= 1 && cf.N <= kBigMaxN, "N must be in [1, 128]");
     if (hybrid)  // [1, lags of the N variables, lags of the Ns actual rates] (mcmcVARhybridGibbs.m:84)
       require(cf.K == cf.N * cf.p + 1 + cf.Ns * cf.p, "hybrid model: K must equal N*p+1+Ns*p");
     else
@@ -352,7 +366,8 @@ struct ccmm_chains {
     d.TP = round_up(cf.T, kTChunk);
     d.B = cf.B;
     d.nmat = cf.B * cf.N;
-    require(d.KP <= 512, "this build supports K <= 512 (KP <= 512)");
+    require(d.KP <= kBigMaxKP, "this build supports K <= 1536");
+    big = d.KP > 512 || cf.N > kMaxNSmall || std::getenv("CCMM_FORCE_BIG") != nullptr;
     nslabX = nX;
     nslabY = nY;
     const size_t B = cf.B, N = cf.N, KP = d.KP, TP = d.TP;
@@ -629,10 +644,35 @@ struct ccmm_chains {
     HIPCHECK(hipMemcpyAsync(slot.p, sl, B * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
     HIPCHECK(hipMemcpyAsync(xidx.p, xi.data(), xi.size() * sizeof(int), hipMemcpyHostToDevice,
                             ctx->stream));
+    build_groups(xi);
     HIPCHECK(hipMemcpyAsync(yidx.p, yi.data(), yi.size() * sizeof(int), hipMemcpyHostToDevice,
                             ctx->stream));
     HIPCHECK(hipStreamSynchronize(ctx->stream));
     resid_valid = false;
+  }
+
+  // systems of a chain that share one X slab, four per Gram workgroup (ccmm_big.hip)
+  void build_groups(const std::vector<int>& xi) {
+    const int B = cfg.B, N = cfg.N;
+    if (big) {
+      std::vector<int4> g;
+      for (int c = 0; c < B; ++c) {
+        std::vector<bool> done(N, false);
+        for (int j = 0; j < N; ++j) {
+          if (done[j]) continue;
+          int m[4] = {-1, -1, -1, -1}, n = 0;
+          for (int q = j; q < N && n < 4; ++q)
+            if (!done[q] && xi[(size_t)c * N + q] == xi[(size_t)c * N + j]) {
+              m[n++] = c * N + q;
+              done[q] = true;
+            }
+          g.push_back(int4{m[0], m[1], m[2], m[3]});
+        }
+      }
+      nGroups = (int)g.size();
+      bigGroups.alloc(g.size());
+      HIPCHECK(hipMemcpy(bigGroups.p, g.data(), g.size() * sizeof(int4), hipMemcpyHostToDevice));
+    }
   }
 
   void upload_X(int slab, int T, const double* X) {  // X: T x K column-major
@@ -742,6 +782,10 @@ struct ccmm_chains {
     ensure_cta();
     ChainState cs = view();
     if (!resid_valid) run_resid();
+    if (big) {
+      run_cta_big(ra, cs);
+      return;
+    }
     if (lag_active()) {
       run_cta_lag(ra, cs);
       return;
@@ -824,6 +868,35 @@ struct ccmm_chains {
     });
   }
 
+  // large-N blocks (N > 32; ccmm_big.hip)
+  void run_astep_big(const RngArgs&) { throw ArgError("A-step for N > 32 not built yet"); }
+  void run_sv_big(const RngArgs&) { throw ArgError("SV block for N > 32 not built yet"); }
+  void run_phi_big(const RngArgs&) { throw ArgError("PHI block for N > 32 not built yet"); }
+  void run_elb_big(const RngArgs&) { throw ArgError("ELB step for N > 32 not built yet"); }
+
+  // CTA for large systems (ccmm_big.hip): weights -> multi-equation MFMA Gram -> per-system
+  // blocked Cholesky -> per-chain sequential solve
+  int big_mask = std::getenv("CCMM_BIG_MASK") ? std::atoi(std::getenv("CCMM_BIG_MASK")) : 7;
+  void run_cta_big(const RngArgs& ra, const ChainState& cs) {
+    Ubuf.alloc((size_t)d.B * d.N * d.TP);
+    launch(KID_WEIGHTS, [&] {
+      hipLaunchKernelGGL(k_cta_weights, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0,
+                         ctx->stream, d, Tslot.p, cs, 0);
+    });
+    launch(KID_GRAMBIG, [&] {
+      HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
+                              nGroups, rdiag.p, ra, Ubuf.p, 1 & big_mask));
+    });
+    launch(KID_CHOLBIG, [&] {
+      HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
+                              nGroups, rdiag.p, ra, Ubuf.p, 2 & big_mask));
+    });
+    launch(KID_SOLVEBIG, [&] {
+      HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
+                              nGroups, rdiag.p, ra, Ubuf.p, 4 & big_mask));
+    });
+  }
+
   // CTA on the lag structure: sqrt weights -> Gram + Cholesky + inverse -> sequential solve
   void run_cta_lag(const RngArgs& ra, const ChainState& cs) {
     launch(KID_WEIGHTS, [&] {
@@ -843,6 +916,10 @@ struct ccmm_chains {
   }
 
   void run_astep(const RngArgs& ra) {
+    if (d.N > kMaxNSmall) {
+      run_astep_big(ra);
+      return;
+    }
     ChainState cs = view();
     const int N = d.N;
     const int total = (N - 1) * N * (N + 1) / 6 + N * (N - 1) / 2 + 8;
@@ -874,6 +951,10 @@ struct ccmm_chains {
   }
 
   void run_sv(const RngArgs& ra) {
+    if (d.N > kMaxNSmall) {
+      run_sv_big(ra);
+      return;
+    }
     ensure_sv();
     ChainState cs = view();
     launch(KID_SVMIX, [&] {
@@ -886,6 +967,10 @@ struct ccmm_chains {
   }
 
   void run_phi(const RngArgs& ra) {
+    if (d.N > kMaxNSmall) {
+      run_phi_big(ra);
+      return;
+    }
     Zphi.alloc((size_t)d.B * d.N * (d.TP + cfg.dPHI));
     ChainState cs = view();
     launch(KID_PHIGEN, [&] {
@@ -932,6 +1017,10 @@ struct ccmm_chains {
   }
 
   void run_elb(const RngArgs& ra) {
+    if (d.N > kMaxNSmall) {
+      run_elb_big(ra);
+      return;
+    }
     if (cfg.elbTmax <= 0) return;
     ChainState cs = view();
     ElbDev e = elb_view();
@@ -1112,7 +1201,10 @@ ccmm_ctx* ccmm_create(int device) {
     HIPCHECK(hipSetDevice(device));
     ctx = new ccmm_ctx;
     ctx->device = device;
-    HIPCHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    // a BLOCKING stream: host uploads use hipMemcpy on the null stream, and a pageable
+    // host-to-device copy may return before its DMA has landed; only a stream that
+    // synchronises with the null stream orders the kernels after it
+    HIPCHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault));
     return 0;
   });
   if (rc != 0) {
@@ -1176,6 +1268,7 @@ int ccmm_cta(ccmm_ctx* ctx, int B, int T, int N, int K, const double* Y, int y_p
     }
     HIPCHECK(hipMemcpy(ch.xidx.p, xi.data(), xi.size() * sizeof(int), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(ch.yidx.p, yi.data(), yi.size() * sizeof(int), hipMemcpyHostToDevice));
+    ch.build_groups(xi);
     ch.upload_KN(ch.iVdiag.p, 1, iVdiag, 1.0);
     ch.upload_KN(ch.iVb.p, 1, iVb, 0.0);
     HIPCHECK(hipMemcpy(ch.A.p, A, (size_t)B * N * N * sizeof(double), hipMemcpyHostToDevice));
