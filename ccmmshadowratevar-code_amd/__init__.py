@@ -13,7 +13,7 @@ Layers:
                    CTA, CTAsys, drawTruncNormal)
   distributed.py   vintage/chain sharding over GPUs, end-of-run reductions
 """
-from . import _abi, distributed, model, samplers  # noqa: F401
+from . import _abi, distributed, model, samplers, synthetic  # noqa: F401
 from ._abi import MODEL_BLOCKHYBRID, MODEL_HYBRID, MODEL_LINEAR, Chains, Context, load_library  # noqa: F401
 from .samplers import (CTA, CTAsys, drawTruncNormal, mcmcVAR,  # noqa: F401
                        mcmcVARshadowrateBlockHybrid)

@@ -249,7 +249,7 @@ struct ccmm_chains {
   bool big = false;
   int nGroups = 0;
   DBuf<int4> bigGroups;
-  DBuf<double> Ubuf;
+  DBuf<double> Ubuf, Dinv;
   // profiling
   bool profiling = false;
   struct Ev {
@@ -879,21 +879,22 @@ struct ccmm_chains {
   int big_mask = std::getenv("CCMM_BIG_MASK") ? std::atoi(std::getenv("CCMM_BIG_MASK")) : 7;
   void run_cta_big(const RngArgs& ra, const ChainState& cs) {
     Ubuf.alloc((size_t)d.B * d.N * d.TP);
+    Dinv.alloc((size_t)d.nmat * d.KP * 64);
     launch(KID_WEIGHTS, [&] {
       hipLaunchKernelGGL(k_cta_weights, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0,
                          ctx->stream, d, Tslot.p, cs, 0);
     });
     launch(KID_GRAMBIG, [&] {
       HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
-                              nGroups, rdiag.p, ra, Ubuf.p, 1 & big_mask));
+                              nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 1 & big_mask));
     });
     launch(KID_CHOLBIG, [&] {
       HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
-                              nGroups, rdiag.p, ra, Ubuf.p, 2 & big_mask));
+                              nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 2 & big_mask));
     });
     launch(KID_SOLVEBIG, [&] {
       HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
-                              nGroups, rdiag.p, ra, Ubuf.p, 4 & big_mask));
+                              nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 4 & big_mask));
     });
   }
 

@@ -12,10 +12,11 @@ constexpr int kBigMaxKP = 1536;
 size_t big_solve_lds_bytes(const Dims& d);
 
 // groups: ngroups x int4 systems (c*N + j) sharing one design X slab (-1 padded);
-// phase_mask: 1 Gram, 2 Cholesky, 4 solve.  Ubuf: B x N x TP scratch (U = E A').
+// phase_mask: 1 Gram, 2 Cholesky, 4 solve.  Ubuf: B x N x TP scratch (U = E A');
+// Dinv: nmat x (KP/64) x 64 x 64 inverses of the Cholesky factor's diagonal blocks.
 hipError_t big_launch_cta(hipStream_t st, const Dims& d, const int* Tslot, const int* slotIV,
                           const double* iVdiag, const double* iVb, XSel xs, ChainState cs,
                           const int4* groups, int ngroups, double* rdiag, RngArgs ra, double* Ubuf,
-                          int phase_mask);
+                          double* Dinv, int phase_mask);
 
 }  // namespace ccmm

@@ -19,6 +19,8 @@
 //                    instead of re-forming E_t A(i,:)' for every (t, i >= j).
 #include "ccmm_big.h"
 
+#include <cstdlib>
+
 namespace ccmm {
 
 constexpr int kBT = 64;      // tile / block width
@@ -109,17 +111,21 @@ __global__ __launch_bounds__(256) void k_gram_big(Dims d, const int* __restrict_
 
 // ============================================================== Cholesky (per system)
 // In place on G_cj + diag(iV_j) (CTA.m:73-74): the lower triangle becomes L, rdiag = 1 / L_kk.
-// LDS: Bs = L(kb, k0:k0+32) staged, As = L(ib_w, k0:k0+32) per wave; after the update the
-// As region holds Li = L_kk^{-1} and Lk holds the factored diagonal block.
-constexpr int kCK = 32;  // k columns per staged chunk of the update
+// Update phase: each wave owns one 64-row block; its MFMA A fragments come straight from
+// HBM into registers one 16-column chunk ahead of use, the shared L(kb, k) chunk is
+// double-buffered in LDS (one barrier per chunk).  Factor phase: the LDS holds the
+// diagonal block and its inverse instead (a union: 66.5 KB, two systems per CU).
+constexpr int kCK = 16;  // k columns per pipelined chunk of the update
 constexpr int kLiLd = 65;
 __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict__ slotIV,
-                                                  const double* __restrict__ iVdiag, ChainState cs,
-                                                  double* __restrict__ rdiag) {
-  __shared__ double Bs[kCK][kBLd];       // Bs[k][j] = L(kb*64 + j, k0 + k)
-  __shared__ double As[4][kCK][kBLd];    // As[w][k][i] = L(ib_w*64 + i, k0 + k)   (80 KB)
-  __shared__ double Lk[kBT][kLiLd];      // Lk[i][k] = L_kk(i, k)
-  double* Li = &As[0][0][0];             // Li[j * kLiLd + k] = (L_kk^{-1})(j, k)  (aliases As)
+                                                     const double* __restrict__ iVdiag, ChainState cs,
+                                                     double* __restrict__ rdiag,
+                                                     double* __restrict__ Dinv, int skip) {
+  // skip: timing-only phase ablation (CCMM_CHOL_SKIP; results invalid): 1 update, 2 factor,
+  // 4 panel
+  __shared__ double smu[2 * kBT * kLiLd];  // update: Bs[2][kCK][kBLd]; factor: Lk | Li
+  double* Lk = smu;                        // Lk[i * kLiLd + k] = L_kk(i, k)
+  double* Li = smu + kBT * kLiLd;          // Li[j * kLiLd + k] = (L_kk^{-1})(j, k)
   const int mat = blockIdx.x;
   const int c = mat / d.N, j = mat % d.N;
   const int KP = d.KP;
@@ -128,15 +134,17 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
   const double* iv = iVdiag + ((size_t)slotIV[c] * d.N + j) * KP;
   double* rd = rdiag + (size_t)mat * KP;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
   for (int a = tid; a < KP; a += 256) A[(size_t)a * KP + a] += iv[a];
   __syncthreads();
   int bad = 0;
   for (int kb = 0; kb < nb; ++kb) {
     const int kcol = kb * kBT;
+    const int nch = kcol / kCK;
     // ---- 1. update of block column kb, four row blocks at a time (one per wave)
-    for (int ib0 = kb; ib0 < nb; ib0 += 4) {
-      const int ib = ib0 + wave;
-      const bool act = ib < nb;
+    for (int ib0 = kb; ib0 < nb && !(skip & 1); ib0 += 4) {
+      const int ib = min(ib0 + wave, nb - 1);  // idle waves shadow the last block, store nothing
+      const bool act = ib0 + wave < nb;
       const int irow = ib * kBT;
       dbl4 acc[4][4];
 #pragma unroll
@@ -144,38 +152,63 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
 #pragma unroll
         for (int y = 0; y < 4; ++y)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int i = irow + x * 16 + (lane >> 4) + 4 * r;
-            const int jj = kcol + y * 16 + (lane & 15);
-            acc[x][y][r] = act ? A[(size_t)jj * KP + i] : 0.0;
-          }
-      for (int k0 = 0; k0 < kcol; k0 += kCK) {
-        for (int e = tid; e < kCK * kBT; e += 256) {
-          const int k = e >> 6, r = e & 63;
-          Bs[k][r] = A[(size_t)(k0 + k) * KP + kcol + r];
+          for (int r = 0; r < 4; ++r)
+            acc[x][y][r] = A[(size_t)(kcol + y * 16 + lr) * KP + irow + x * 16 + lk + 4 * r];
+      if (nch > 0) {
+        double an[16], bv[4];
+        // chunk 0 -> registers -> LDS buffer 0
 #pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const int ibw = ib0 + w;
-            As[w][k][r] = (ibw < nb) ? A[(size_t)(k0 + k) * KP + ibw * kBT + r] : 0.0;
-          }
+        for (int q = 0; q < 16; ++q)
+          an[q] = A[(size_t)((q >> 2) * 4 + lk) * KP + irow + (q & 3) * 16 + lr];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = tid + 256 * q;
+          bv[q] = A[(size_t)(e >> 6) * KP + kcol + (e & 63)];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = tid + 256 * q;
+          smu[(e >> 6) * kBLd + (e & 63)] = bv[q];
         }
         __syncthreads();
+        for (int ch = 0; ch < nch; ++ch) {
+          double ac[16];
 #pragma unroll
-        for (int ks = 0; ks < kCK / 4; ++ks) {
-          const int k = ks * 4 + (lane >> 4);
-          double fa[4], fb[4];
+          for (int q = 0; q < 16; ++q) ac[q] = -an[q];
+          const bool more = ch + 1 < nch;
+          if (more) {
+            const int k0 = (ch + 1) * kCK;
 #pragma unroll
-          for (int x = 0; x < 4; ++x) {
-            fa[x] = -As[wave][k][x * 16 + (lane & 15)];  // MFMA A: row i, col k (negated)
-            fb[x] = Bs[k][x * 16 + (lane & 15)];         // MFMA B: B[k][col j] = L(j, k)
+            for (int q = 0; q < 16; ++q)
+              an[q] = A[(size_t)(k0 + (q >> 2) * 4 + lk) * KP + irow + (q & 3) * 16 + lr];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int e = tid + 256 * q;
+              bv[q] = A[(size_t)(k0 + (e >> 6)) * KP + kcol + (e & 63)];
+            }
           }
+          const double* Bs = smu + (ch & 1) * kCK * kBLd;
 #pragma unroll
-          for (int x = 0; x < 4; ++x)
+          for (int ks = 0; ks < kCK / 4; ++ks) {
+            double fb[4];
 #pragma unroll
-            for (int y = 0; y < 4; ++y)
-              acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[x], fb[y], acc[x][y], 0, 0, 0);
+            for (int y = 0; y < 4; ++y) fb[y] = Bs[(ks * 4 + lk) * kBLd + y * 16 + lr];
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+              for (int y = 0; y < 4; ++y)
+                acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[ks * 4 + x], fb[y], acc[x][y], 0, 0, 0);
+          }
+          if (more) {
+            double* Bn = smu + ((ch + 1) & 1) * kCK * kBLd;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int e = tid + 256 * q;
+              Bn[(e >> 6) * kBLd + (e & 63)] = bv[q];
+            }
+          }
+          __syncthreads();
         }
-        __syncthreads();
       }
       if (act) {
 #pragma unroll
@@ -183,16 +216,13 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
 #pragma unroll
           for (int y = 0; y < 4; ++y)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int i = irow + x * 16 + (lane >> 4) + 4 * r;
-              const int jj = kcol + y * 16 + (lane & 15);
-              A[(size_t)jj * KP + i] = acc[x][y][r];
-            }
+            for (int r = 0; r < 4; ++r)
+              A[(size_t)(kcol + y * 16 + lr) * KP + irow + x * 16 + lk + 4 * r] = acc[x][y][r];
       }
     }
     __syncthreads();
-    // ---- 2. factor the diagonal block (wave 0, lane = row; readlane broadcasts)
-    if (wave == 0) {
+    // ---- 2. factor the diagonal block (wave 0, lane = row; readlane broadcasts), invert it
+    if (wave == 0 && !(skip & 2)) {
       double row[kBT];
       double mydiag = 1.0;
 #pragma unroll
@@ -221,51 +251,67 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
 #pragma unroll
       for (int m = 0; m < kBT; ++m) {
         const double v = (m <= lane) ? row[m] : 0.0;
-        Lk[lane][m] = v;
+        Lk[lane * kLiLd + m] = v;
         if (m <= lane) A[(size_t)(kcol + m) * KP + kcol + lane] = v;
       }
       rd[kcol + lane] = 1.0 / mydiag;
-      // column `lane` of L_kk^{-1} by forward substitution, kept in LDS (no unrolled state)
+      // column `lane` of L_kk^{-1} by forward substitution, kept in LDS
       for (int i = 0; i < kBT; ++i) {
-        double s = (i == lane) ? 1.0 : 0.0;
-        for (int k = lane; k < i; ++k) s = fma(-Lk[i][k], Li[k * kLiLd + lane], s);
-        Li[i * kLiLd + lane] = (i >= lane) ? s / Lk[i][i] : 0.0;
+        double s0 = (i == lane) ? 1.0 : 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        int k = lane;
+        for (; k + 3 < i; k += 4) {  // four independent LDS read / FMA chains
+          s0 = fma(-Lk[i * kLiLd + k], Li[k * kLiLd + lane], s0);
+          s1 = fma(-Lk[i * kLiLd + k + 1], Li[(k + 1) * kLiLd + lane], s1);
+          s2 = fma(-Lk[i * kLiLd + k + 2], Li[(k + 2) * kLiLd + lane], s2);
+          s3 = fma(-Lk[i * kLiLd + k + 3], Li[(k + 3) * kLiLd + lane], s3);
+        }
+        for (; k < i; ++k) s0 = fma(-Lk[i * kLiLd + k], Li[k * kLiLd + lane], s0);
+        Li[i * kLiLd + lane] = (i >= lane) ? ((s0 + s1) + (s2 + s3)) / Lk[i * kLiLd + i] : 0.0;
       }
     }
     __syncthreads();
-    // ---- 3. panel below: L(r, kb) = C(r, kb) L_kk^{-T} on MFMA, 64-row tiles per wave
-    for (int rt = kb + 1 + wave; rt < nb; rt += 4) {
+    // the diagonal block's inverse, row-major 64 x 64, for the solve's block substitutions
+    {
+      double* Dk = Dinv + ((size_t)mat * nb + kb) * kBT * kBT;
+      for (int e = tid; e < kBT * kBT; e += 256) Dk[e] = Li[(e >> 6) * kLiLd + (e & 63)];
+    }
+    // ---- 3. panel below: L(r, kb) = C(r, kb) L_kk^{-T} on MFMA, 64-row tiles per wave;
+    //         the tile's C fragments are loaded in two bursts of 32 per lane
+    for (int rt = kb + 1 + wave; rt < nb && !(skip & 4); rt += 4) {
       const int r0 = rt * kBT;
       dbl4 acc[4][4];
 #pragma unroll
       for (int x = 0; x < 4; ++x)
 #pragma unroll
         for (int y = 0; y < 4; ++y) acc[x][y] = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-      for (int ks = 0; ks < kBT / 4; ++ks) {
-        const int k = ks * 4 + (lane >> 4);
-        double fa[4], fb[4];
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          fa[x] = A[(size_t)(kcol + k) * KP + r0 + x * 16 + (lane & 15)];  // C(r, k)
-          fb[x] = Li[(x * 16 + (lane & 15)) * kLiLd + k];                   // Linv(jj, k)
+      for (int half = 0; half < 4; ++half) {
+        double fa[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int k = half * 16 + (q >> 2) * 4 + lk;
+          fa[q] = A[(size_t)(kcol + k) * KP + r0 + (q & 3) * 16 + lr];
         }
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
+        for (int ks = 0; ks < 4; ++ks) {
+          const int k = half * 16 + ks * 4 + lk;
+          double fb[4];
 #pragma unroll
-          for (int y = 0; y < 4; ++y)
-            acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[x], fb[y], acc[x][y], 0, 0, 0);
+          for (int y = 0; y < 4; ++y) fb[y] = Li[(y * 16 + lr) * kLiLd + k];
+#pragma unroll
+          for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+              acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ks * 4 + x], fb[y], acc[x][y], 0, 0, 0);
+        }
       }
 #pragma unroll
       for (int x = 0; x < 4; ++x)
 #pragma unroll
         for (int y = 0; y < 4; ++y)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = r0 + x * 16 + (lane >> 4) + 4 * r;
-            const int jj = kcol + y * 16 + (lane & 15);
-            A[(size_t)jj * KP + row] = acc[x][y][r];
-          }
+          for (int r = 0; r < 4; ++r)
+            A[(size_t)(kcol + y * 16 + lr) * KP + r0 + x * 16 + lk + 4 * r] = acc[x][y][r];
     }
     __syncthreads();
   }
@@ -273,17 +319,30 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
 }
 
 // ============================================================== sequential solve (per chain)
+// One workgroup of 16 waves per chain.  Every phase of an equation keeps many independent
+// loads in flight per lane (the phases are latency- and bandwidth-bound through one CU):
+//   v / U      thread per t, the i loop unrolled by 4
+//   X' v       four columns per wave at a time, lanes over t, DPP wave sums
+//   L y = r    64-row diagonal blocks by wave 0, the rows below by a thread each
+//   L' x = y   left-looking: for block b the columns c of L below the block are contiguous,
+//              so lanes run over their rows and a DPP sum gives (L' x)_c
+//   X x        the K columns split in 8 slices x T in 64-row chunks, partial sums in LDS
 constexpr int kBSLd = 65;
+constexpr int kResSlices = 8;
 __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __restrict__ Tslot,
                                                         const double* __restrict__ iVb, XSel xs,
                                                         ChainState cs, const double* __restrict__ rdiag,
-                                                        RngArgs ra, double* __restrict__ Ubuf) {
+                                                        RngArgs ra, double* __restrict__ Ubuf,
+                                                        const double* __restrict__ Dinv, int skip) {
+  // skip: timing-only phase ablation (CCMM_SOLVE_SKIP; results invalid): 1 v/U, 2 X'v,
+  // 4 forward, 8 backward, 16 residual
   extern __shared__ double sm[];
   const int N = d.N, KP = d.KP, TP = d.TP, K = d.K;
-  double* v = sm;                 // TP
-  double* yv = v + TP;            // KP
-  double* rdl = yv + KP;          // KP
-  double* Ls = rdl + KP;          // 64 x kBSLd
+  double* v = sm;                    // TP
+  double* yv = v + TP;               // KP
+  double* rdl = yv + KP;             // KP
+  double* Ls = rdl + KP;             // 64 x kBSLd
+  double* part = Ls + 64 * kBSLd;    // kResSlices x TP
   const int c = blockIdx.x;
   const int s = cs.slot[c];
   const int T = Tslot[s];
@@ -304,18 +363,35 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
     U[q] = u;
   }
   __syncthreads();
+  const int nb = (K + 63) / 64;
   for (int j = 0; j < N; ++j) {
     const int mat = c * N + j;
     const double* X = xs.pool + (size_t)xs.idx[mat] * KP * TP;
     const double* L = cs.G + (size_t)mat * KP * KP;
     // ---- E(:,j) = Y(:,j) (PAI(:,j) = 0, CTA.m:63); U(:,i) += dE A(i,j), i >= j; v_t
-    for (int t = tid; t < TP; t += NT) {
+    for (int t = tid; t < TP && !(skip & 1); t += NT) {
       double acc = 0.0;
       if (t < T) {
         const double yj = Y[(size_t)j * TP + t];
         const double dl = yj - E[(size_t)j * TP + t];
         E[(size_t)j * TP + t] = yj;
-        for (int i = j; i < N; ++i) {
+        int i = j;
+        for (; i + 7 < N; i += 8) {
+          double u[8], h[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            u[q] = U[(size_t)(i + q) * TP + t];
+            h[q] = sh[(size_t)(i + q) * TP + t];
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const double aij = Ac[i + q + j * N];
+            u[q] = fma(dl, aij, u[q]);
+            U[(size_t)(i + q) * TP + t] = u[q];
+            acc += aij * (u[q] / h[q]) / h[q];
+          }
+        }
+        for (; i < N; ++i) {
           const double aij = Ac[i + j * N];
           const double u = fma(dl, aij, U[(size_t)i * TP + t]);
           U[(size_t)i * TP + t] = u;
@@ -327,81 +403,138 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
     }
     for (int a = tid; a < KP; a += NT) rdl[a] = rdiag[(size_t)mat * KP + a];
     __syncthreads();
-    // ---- rhs = iVb_j + X' v (wave per column)
+    // ---- rhs = iVb_j + X' v: four columns per wave at a time
     const double* ivb = iVb + ((size_t)s * N + j) * KP;
-    for (int a = wave; a < KP; a += NW) {
-      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-      if (a < K) {
-        const double* xa = X + (size_t)a * TP;
-        int t = lane;
-        for (; t + 192 < TP; t += 256) {
-          p0 = fma(xa[t], v[t], p0);
-          p1 = fma(xa[t + 64], v[t + 64], p1);
-          p2 = fma(xa[t + 128], v[t + 128], p2);
-          p3 = fma(xa[t + 192], v[t + 192], p3);
+    for (int a0 = wave * 4; a0 < KP && !(skip & 2); a0 += NW * 4) {
+      double p[4] = {0.0, 0.0, 0.0, 0.0};
+      const double* xc[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xc[q] = X + (size_t)min(a0 + q, K - 1) * TP;
+      int t = lane;
+      for (; t + 64 * 3 < TP; t += 64 * 4) {  // 16 loads in flight per lane
+        double xv[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) xv[u][q] = xc[q][t + 64 * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const double vt = v[t + 64 * u];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) p[q] = fma(xv[u][q], vt, p[q]);
         }
-        for (; t < TP; t += 64) p0 = fma(xa[t], v[t], p0);
       }
-      const double p = wave_sum((p0 + p1) + (p2 + p3));
-      if (lane == 0) yv[a] = ivb[a] + p;
+      for (; t < TP; t += 64) {
+        const double vt = v[t];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = fma(xc[q][t], vt, p[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double tot = wave_sum_dpp(a0 + q < K ? p[q] : 0.0);
+        if (lane == 0 && a0 + q < KP) yv[a0 + q] = ivb[a0 + q] + tot;
+      }
     }
     __syncthreads();
-    const int nb = (K + 63) / 64;
-    // ---- forward substitution L y = rhs (64 x 64 diagonal blocks by wave 0, GEMV by all)
-    for (int b = 0; b < nb; ++b) {
+    // ---- forward substitution L y = rhs: per 64-row block y_b = Linv_bb (r_b) (the stored
+    //      diagonal-block inverse, a 64 x 64 GEMV on wave 0), then the rows below
+    //      r_r -= L(r, b) y_b (a thread per row, two bursts of 32 loads); the next block's
+    //      inverse is prefetched into registers while the current one is applied
+    const double* Dm = Dinv + (size_t)mat * nb * 4096;
+    double dpre[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dpre[q] = Dm[tid + NT * q];
+    for (int b = 0; b < nb && !(skip & 4); ++b) {
       const int r0 = b * 64;
-      for (int e = tid; e < 64 * 64; e += NT) {
-        const int i = e & 63, k = e >> 6;
-        Ls[i * kBSLd + k] = (k <= i) ? L[(size_t)(r0 + k) * KP + r0 + i] : 0.0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = tid + NT * q;
+        Ls[(e >> 6) * kBSLd + (e & 63)] = dpre[q];
       }
       __syncthreads();
+      if (b + 1 < nb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dpre[q] = Dm[(size_t)(b + 1) * 4096 + tid + NT * q];
       if (wave == 0) {
-        double yi = yv[r0 + lane];
-        const int kend = min(64, K - r0);
-        for (int k = 0; k < kend; ++k) {
-          const double yk = readlane_d(yi, k) * rdl[r0 + k];
-          yi = (lane == k) ? yk : ((lane > k) ? fma(-Ls[lane * kBSLd + k], yk, yi) : yi);
-        }
+        double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 16
+        for (int k = 0; k < 64; ++k) a4[k & 3] = fma(Ls[lane * kBSLd + k], yv[r0 + k], a4[k & 3]);
+        const double yi = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        __builtin_amdgcn_wave_barrier();
         yv[r0 + lane] = yi;
       }
       __syncthreads();
       for (int r = r0 + 64 + tid; r < KP; r += NT) {
-        double a0 = 0.0, a1 = 0.0;
-#pragma unroll 8
-        for (int k = 0; k < 64; k += 2) {
-          a0 = fma(L[(size_t)(r0 + k) * KP + r], yv[r0 + k], a0);
-          a1 = fma(L[(size_t)(r0 + k + 1) * KP + r], yv[r0 + k + 1], a1);
+        double acc4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // two bursts of 32 loads in flight per thread
+          double lv[32];
+#pragma unroll
+          for (int k = 0; k < 32; ++k) lv[k] = L[(size_t)(r0 + 32 * h + k) * KP + r];
+#pragma unroll
+          for (int k = 0; k < 32; ++k) acc4[k & 3] = fma(lv[k], yv[r0 + 32 * h + k], acc4[k & 3]);
         }
-        yv[r] -= a0 + a1;
+        yv[r] -= (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
       }
       __syncthreads();
     }
     // ---- + z_j (randn(K,N) of CTA.m:58, column j)
     for (int a = tid; a < K; a += NT) yv[a] += rng.normal(CCMM_RNG_PAI, (uint32_t)(a + K * j));
     __syncthreads();
-    // ---- back substitution L' x = y
-    for (int b = nb - 1; b >= 0; --b) {
+    // ---- back substitution L' x = y, left-looking by 64-column blocks: (L' x)_c over the
+    //      rows below the block (columns of L are contiguous), then x_b = Linv_bb' (y_b - s_b)
+    if (!(skip & 8)) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dpre[q] = Dm[(size_t)(nb - 1) * 4096 + tid + NT * q];
+    }
+    for (int b = nb - 1; b >= 0 && !(skip & 8); --b) {
       const int r0 = b * 64;
-      for (int e = tid; e < 64 * 64; e += NT) {
-        const int i = e & 63, k = e >> 6;
-        Ls[i * kBSLd + k] = (k <= i) ? L[(size_t)(r0 + k) * KP + r0 + i] : 0.0;
-      }
-      __syncthreads();
-      if (wave == 0) {
-        double ci = yv[r0 + lane];
-        const int kend = min(64, K - r0);
-        for (int k = kend - 1; k >= 0; --k) {
-          const double xk = readlane_d(ci, k) * rdl[r0 + k];
-          ci = (lane == k) ? xk : ((lane < k) ? fma(-Ls[k * kBSLd + lane], xk, ci) : ci);
+      const int rb = r0 + 64;  // rows below the block: rb .. KP-1 (x there is final)
+      {
+        const int cq = wave * 4;
+        double pq[4] = {0.0, 0.0, 0.0, 0.0};
+        int r = rb + lane;
+        for (; r + 64 * 3 < KP; r += 64 * 4) {  // 16 loads in flight per lane
+          double lv[4][4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) lv[u][q] = L[(size_t)(r0 + cq + q) * KP + r + 64 * u];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const double xr = yv[r + 64 * u];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pq[q] = fma(lv[u][q], xr, pq[q]);
+          }
         }
-        if (lane < kend) yv[r0 + lane] = ci;
+        for (; r < KP; r += 64) {
+          const double xr = yv[r];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pq[q] = fma(L[(size_t)(r0 + cq + q) * KP + r], xr, pq[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double tot = wave_sum_dpp(pq[q]);
+          if (lane == 0) part[cq + q] = tot;   // part is free until the residual phase
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = tid + NT * q;
+        Ls[(e >> 6) * kBSLd + (e & 63)] = dpre[q];
       }
       __syncthreads();
-      // x(r) -= sum_k L(r0+k, r) x(r0+k) for r < r0: the rows of the transposed block are
-      // columns r of L, k contiguous -> one wave per row r (coalesced over k)
-      for (int r = wave; r < r0; r += NW) {
-        const double p = wave_sum(L[(size_t)r * KP + r0 + lane] * yv[r0 + lane]);
-        if (lane == 0) yv[r] -= p;
+      if (b > 0)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dpre[q] = Dm[(size_t)(b - 1) * 4096 + tid + NT * q];
+      if (wave == 0) {
+        const double ri = yv[r0 + lane] - part[lane];
+        part[64 + lane] = ri;
+        __builtin_amdgcn_wave_barrier();
+        double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 16
+        for (int k = 0; k < 64; ++k) a4[k & 3] = fma(Ls[k * kBSLd + lane], part[64 + k], a4[k & 3]);
+        yv[r0 + lane] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
       }
       __syncthreads();
     }
@@ -413,17 +546,38 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
       yv[a] = val;
     }
     __syncthreads();
-    for (int t = tid; t < T; t += NT) {
-      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-      int a = 0;
-      for (; a + 3 < K; a += 4) {
-        a0 = fma(X[(size_t)a * TP + t], yv[a], a0);
-        a1 = fma(X[(size_t)(a + 1) * TP + t], yv[a + 1], a1);
-        a2 = fma(X[(size_t)(a + 2) * TP + t], yv[a + 2], a2);
-        a3 = fma(X[(size_t)(a + 3) * TP + t], yv[a + 3], a3);
+    {
+      const int nchunk = (T + 63) / 64;
+      const int per = (K + kResSlices - 1) / kResSlices;
+      for (int item = wave; item < nchunk * kResSlices && !(skip & 16); item += NW) {
+        const int slc = item % kResSlices, tch = item / kResSlices;
+        const int t = tch * 64 + lane;
+        const int a_lo = slc * per, a_hi = min(K, a_lo + per);
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        if (t < T) {
+          int a = a_lo;
+          for (; a + 15 < a_hi; a += 16) {  // 16 loads in flight per lane
+            double xv[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) xv[q] = X[(size_t)(a + q) * TP + t];
+#pragma unroll
+            for (int q = 0; q < 16; q += 4) {
+              a0 = fma(xv[q], yv[a + q], a0);
+              a1 = fma(xv[q + 1], yv[a + q + 1], a1);
+              a2 = fma(xv[q + 2], yv[a + q + 2], a2);
+              a3 = fma(xv[q + 3], yv[a + q + 3], a3);
+            }
+          }
+          for (; a < a_hi; ++a) a0 = fma(X[(size_t)a * TP + t], yv[a], a0);
+        }
+        if (t < TP) part[slc * TP + t] = (t < T) ? (a0 + a1) + (a2 + a3) : 0.0;
       }
-      for (; a < K; ++a) a0 = fma(X[(size_t)a * TP + t], yv[a], a0);
-      const double xp = (a0 + a1) + (a2 + a3);
+    }
+    __syncthreads();
+    for (int t = tid; t < T; t += NT) {
+      double xp = 0.0;
+#pragma unroll
+      for (int q = 0; q < kResSlices; ++q) xp += part[q * TP + t];
       E[(size_t)j * TP + t] = Y[(size_t)j * TP + t] - xp;
       for (int i = j; i < N; ++i) U[(size_t)i * TP + t] = fma(-xp, Ac[i + j * N], U[(size_t)i * TP + t]);
     }
@@ -433,26 +587,29 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
 
 // ============================================================== host launchers
 size_t big_solve_lds_bytes(const Dims& d) {
-  return (size_t)(d.TP + 2 * d.KP + 64 * kBSLd) * sizeof(double);
+  return (size_t)(d.TP + 2 * d.KP + 64 * kBSLd + kResSlices * d.TP) * sizeof(double);
 }
 
 hipError_t big_launch_cta(hipStream_t st, const Dims& d, const int* Tslot, const int* slotIV,
                           const double* iVdiag, const double* iVb, XSel xs, ChainState cs,
                           const int4* groups, int ngroups, double* rdiag, RngArgs ra, double* Ubuf,
-                          int phase_mask) {
+                          double* Dinv, int phase_mask) {
+  static const int skip = std::getenv("CCMM_SOLVE_SKIP") ? std::atoi(std::getenv("CCMM_SOLVE_SKIP")) : 0;
+  static const int cskip = std::getenv("CCMM_CHOL_SKIP") ? std::atoi(std::getenv("CCMM_CHOL_SKIP")) : 0;
   const int nt = d.KP / kBT;
   if (phase_mask & 1)
     hipLaunchKernelGGL(k_gram_big, dim3(nt * (nt + 1) / 2, ngroups), dim3(256), 0, st, d, Tslot, xs, cs,
                        groups);
   if (phase_mask & 2)
-    hipLaunchKernelGGL(k_chol_big, dim3(d.nmat), dim3(256), 0, st, d, slotIV, iVdiag, cs, rdiag);
+    hipLaunchKernelGGL(k_chol_big, dim3(d.nmat), dim3(256), 0, st, d, slotIV, iVdiag, cs, rdiag, Dinv,
+                       cskip);
   if (phase_mask & 4) {
     const size_t lds = big_solve_lds_bytes(d);
     hipError_t e = hipFuncSetAttribute((const void*)k_cta_solve_big,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_cta_solve_big, dim3(d.B), dim3(1024), lds, st, d, Tslot, iVb, xs, cs, rdiag,
-                       ra, Ubuf);
+                       ra, Ubuf, Dinv, skip);
   }
   return hipGetLastError();
 }
