@@ -17,6 +17,7 @@
 #include "ccmm_lag.h"
 #include "ccmm_svpart.h"
 #include "ccmm_big.h"
+#include "ccmm_bign.h"
 #include <cstdlib>
 
 using namespace ccmm;
@@ -82,7 +83,7 @@ struct DBuf {
   }
 };
 
-// small dense host helpers (N <= 32): lower Cholesky and SPD inverse, column-major
+// small dense host helpers (N <= 128): lower Cholesky and SPD inverse, column-major
 void host_chol(std::vector<double>& A, int n) {
   for (int j = 0; j < n; ++j) {
     double s = A[j + j * n];
@@ -249,7 +250,7 @@ struct ccmm_chains {
   bool big = false;
   int nGroups = 0;
   DBuf<int4> bigGroups;
-  DBuf<double> Ubuf, Dinv;
+  DBuf<double> Ubuf, Dinv, bigW, bigScr;
   // profiling
   bool profiling = false;
   struct Ev {
@@ -868,11 +869,37 @@ struct ccmm_chains {
     });
   }
 
-  // large-N blocks (N > 32; ccmm_big.hip)
-  void run_astep_big(const RngArgs&) { throw ArgError("A-step for N > 32 not built yet"); }
-  void run_sv_big(const RngArgs&) { throw ArgError("SV block for N > 32 not built yet"); }
-  void run_phi_big(const RngArgs&) { throw ArgError("PHI block for N > 32 not built yet"); }
-  void run_elb_big(const RngArgs&) { throw ArgError("ELB step for N > 32 not built yet"); }
+  // large-N blocks (N > 32; ccmm_bign.hip)
+  void run_astep_big(const RngArgs& ra) {
+    bigW.alloc((size_t)d.B * d.N * d.TP);
+    ChainState cs = view();
+    launch(KID_ASTEP, [&] {
+      HIPCHECK(bign_launch_astep(ctx->stream, d, Tslot.p, cs, ra, cfg.logy2offset, bigW.p));
+    });
+  }
+  void run_sv_big(const RngArgs& ra) {
+    bigScr.alloc((size_t)d.B * bign_sv_scratch(d));
+    ChainState cs = view();
+    launch(KID_SVMIX, [&] {
+      hipLaunchKernelGGL(k_sv_mix, dim3((d.N * d.TP + 255) / 256, d.B), dim3(256), 0, ctx->stream,
+                         d, Tslot.p, cs, ra);
+    });
+    launch(KID_SVSAMPLE, [&] {
+      HIPCHECK(bign_launch_sv(ctx->stream, d, Tslot.p, V0inv.p, V0invm.p, cs, ra, bigScr.p));
+    });
+  }
+  void run_phi_big(const RngArgs& ra) {
+    Zphi.alloc((size_t)d.B * d.N * (d.TP + cfg.dPHI));
+    bigScr.alloc((size_t)d.B * bign_sv_scratch(d));  // >= 3 N^2 per chain
+    ChainState cs = view();
+    launch(KID_PHIGEN, [&] {
+      hipLaunchKernelGGL(k_phi_gen, dim3((d.N * (d.TP + cfg.dPHI) + 255) / 256, d.B), dim3(256), 0,
+                         ctx->stream, d, Tslot.p, cfg.dPHI, cs, ra);
+    });
+    launch(KID_PHI, [&] {
+      HIPCHECK(bign_launch_phi(ctx->stream, d, Tslot.p, cfg.dPHI, sPHI.p, cs, bigScr.p));
+    });
+  }
 
   // CTA for large systems (ccmm_big.hip): weights -> multi-equation MFMA Gram -> per-system
   // blocked Cholesky -> per-chain sequential solve
@@ -1018,22 +1045,21 @@ struct ccmm_chains {
   }
 
   void run_elb(const RngArgs& ra) {
-    if (d.N > kMaxNSmall) {
-      run_elb_big(ra);
-      return;
-    }
     if (cfg.elbTmax <= 0) return;
     ChainState cs = view();
     ElbDev e = elb_view();
     const int N = d.N, p = cfg.p, Ns = cfg.Ns, Np = N * p;
-    const size_t lds_prep = (size_t)(N * (Np + 1) + 1 + Np) * sizeof(double);
+    // Φ staged in LDS when it fits (N = 20, p = 12: 40 KB); N = 120 reads it from e.Phi
+    size_t lds_prep = (size_t)(2 + Np + N * (Np + 1)) * sizeof(double);
+    const int phi_lds = lds_prep <= 160 * 1024 ? 1 : 0;
+    if (!phi_lds) lds_prep = (size_t)(2 + Np) * sizeof(double);
     launch(KID_ELBPREP, [&] {
       HIPCHECK(hipFuncSetAttribute((const void*)k_elb_prep, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds_prep));
-      hipLaunchKernelGGL(k_elb_prep, dim3(d.B), dim3(256), lds_prep, ctx->stream, d, e, xsel(), cs);
+      hipLaunchKernelGGL(k_elb_prep, dim3(d.B), dim3(256), lds_prep, ctx->stream, d, e, xsel(), cs, phi_lds);
     });
     const size_t lds_cond =
-        (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns) * sizeof(double);
+        (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns + N * Ns) * sizeof(double);
     launch(KID_ELBCOND, [&] {
       hipLaunchKernelGGL(k_elb_cond, dim3(e.elbTmax, d.B), dim3(64), lds_cond, ctx->stream, d, e, cs);
     });

@@ -1,0 +1,587 @@
+// Gibbs blocks for large N (33 <= N <= 128; the S120 configuration N = 120):
+//
+//   k_astep_big  (chain, row ii): the weighted Gram of RESID(:, 0:ii) with weights
+//                1 / sqrtht(:, ii)^2 (ZZ and Zz of mcmcVAR.m:240-244), Cholesky, the two
+//                triangular solves and the draw of A(ii, 0:ii-1) (:245-252)
+//   k_astep_fin  (chain): invA = A \ I (:254), logy2 = log((RESID A')^2 + offset) (:259)
+//   k_phi_big    (chain): the inverse-Wishart draw of mcmcVAR.m:268-274
+//   k_sv_big     (chain): KSC-mixture SV draw of h_0..h_T with the time-ordered block
+//                Cholesky factor of the block-tridiagonal posterior precision
+//                (oracle.sv_draw_sequential; the declared convention for N > 32, the
+//                reference's sampler lives in the absent em-matlabbox):
+//                  M_t = L_{t-1}^{-1} Q,  L_t = chol(D_t - M_t' M_t),
+//                  w_t = L_t^{-1} (b_t + M_t' w_{t-1}),
+//                  x_T = L_T^{-T}(w_T + z_T),  x_t = L_t^{-T}(w_t + z_t + M_{t+1} x_{t+1})
+//
+// The N x N matrices (115 KB at N = 120) no longer fit a CU's LDS several at a time, so
+// one of them lives in LDS (row-major, ld = 129 doubles) and the rest in per-chain global
+// scratch (L2 resident).  Workgroup primitives below: an LDS-staged Gram with 4 x 4
+// register tiles, a blocked Cholesky (32-wide panels: one wave factors the diagonal
+// block with readlane broadcasts, all threads update), blocked triangular solves.
+#include "ccmm_bign.h"
+
+namespace ccmm {
+
+constexpr int kNL = 129;   // LDS row stride of an N x N matrix (odd: spreads banks)
+constexpr int kPB = 16;    // Cholesky panel width (16: no spills at 1024 threads)
+constexpr int kGC = 32;    // Gram t-chunk
+
+// ---------------------------------------------------------------- Gram
+// G(a, b) = sum_{t < T} w(t) x_t(a) x_t(b) for the lower triangle a >= b of m x m (m <= 128),
+// x_t(a) = src[a * sa + t * st]; w = nullptr: unit weights, else w[t * sw].  G: LDS (ld kNL),
+// ALIASED with the staging area (written after the last chunk).  Returns after a barrier.
+template <int NT>
+__device__ void wg_gram(double* G, const double* __restrict__ src, int sa, int st, int m, int T,
+                        const double* __restrict__ w, int sw) {
+  constexpr int NTL = (32 * 33 / 2 + NT - 1) / NT;  // 4 x 4 tiles per thread (m <= 128)
+  double* stage = G;                                // [kGC][kNL] + weights [kGC]
+  double* wst = G + kGC * kNL;
+  const int tid = threadIdx.x;
+  const int mt = (m + 3) / 4;
+  const int ntile = mt * (mt + 1) / 2;
+  int ta[NTL], tb[NTL];
+#pragma unroll
+  for (int q = 0; q < NTL; ++q) {
+    int tile = tid + NT * q, ti = 0;
+    if (tile < ntile) {
+      while (tile > ti) {
+        tile -= ti + 1;
+        ++ti;
+      }
+      ta[q] = ti * 4;
+      tb[q] = tile * 4;
+    } else {
+      ta[q] = -1;
+      tb[q] = 0;
+    }
+  }
+  double acc[NTL][16];
+#pragma unroll
+  for (int q = 0; q < NTL; ++q)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[q][e] = 0.0;
+  for (int t0 = 0; t0 < T; t0 += kGC) {
+    const int nt = min(kGC, T - t0);
+    if (st == 1) {  // t contiguous for fixed a
+      for (int e = tid; e < m * kGC; e += NT) {
+        const int a = e / kGC, tt = e - a * kGC;
+        stage[tt * kNL + a] = (tt < nt) ? src[(size_t)a * sa + t0 + tt] : 0.0;
+      }
+    } else {        // a contiguous for fixed t
+      for (int e = tid; e < m * kGC; e += NT) {
+        const int tt = e / m, a = e - tt * m;
+        stage[tt * kNL + a] = (tt < nt) ? src[(size_t)a * sa + (size_t)(t0 + tt) * st] : 0.0;
+      }
+    }
+    for (int tt = tid; tt < kGC; tt += NT) wst[tt] = (tt < nt) ? (w ? w[(size_t)(t0 + tt) * sw] : 1.0) : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NTL; ++q) {
+      if (ta[q] < 0) continue;
+      for (int tt = 0; tt < kGC; ++tt) {
+        const double* row = stage + tt * kNL;
+        const double wv = wst[tt];
+        double xa[4], xb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          xa[i] = row[min(ta[q] + i, 127)] * wv;
+          xb[i] = row[min(tb[q] + i, 127)];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) acc[q][i * 4 + jj] = fma(xa[i], xb[jj], acc[q][i * 4 + jj]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < NTL; ++q) {
+    if (ta[q] < 0) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int a = ta[q] + i, b = tb[q] + jj;
+        if (a < m && b <= a) G[a * kNL + b] = acc[q][i * 4 + jj];
+      }
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- Cholesky (LDS)
+// In place on the lower triangle of S (n x n, ld kNL, n <= 128): blocked right-looking with
+// 32-wide panels.  Wave 0 factors the diagonal block (lane = row, readlane broadcasts);
+// the panel below and the trailing update use every thread.  Upper triangle zeroed.
+// *bad set on a non-positive pivot (the pivot is then taken as 1).
+template <int NT>
+__device__ void wg_chol(double* S, int n, int* bad) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int p0 = 0; p0 < n; p0 += kPB) {
+    const int pw = min(kPB, n - p0);
+    if (wave == 0) {
+      double row[kPB];
+#pragma unroll
+      for (int m = 0; m < kPB; ++m) row[m] = (lane < pw && m <= lane && m < pw) ? S[(p0 + lane) * kNL + p0 + m] : 0.0;
+#pragma unroll
+      for (int kk = 0; kk < kPB; ++kk) {
+        if (kk < pw) {
+          double dkk = readlane_d(row[kk], kk);
+          if (!(dkk > 0.0)) {
+            *bad = 1;
+            dkk = 1.0;
+          }
+          const double piv = sqrt(dkk);
+          if (lane == kk) row[kk] = piv;
+          if (lane > kk) row[kk] /= piv;
+          const double lik = row[kk];
+#pragma unroll
+          for (int m = kk + 1; m < kPB; ++m) {
+            const double lmk = readlane_d(lik, m);
+            if (lane >= m) row[m] = fma(-lik, lmk, row[m]);
+          }
+        }
+      }
+      if (lane < pw)
+#pragma unroll
+        for (int m = 0; m < kPB; ++m)
+          if (m < pw) S[(p0 + lane) * kNL + p0 + m] = (m <= lane) ? row[m] : 0.0;
+    }
+    __syncthreads();
+    // panel: L(i, p0:p0+pw) = S(i, p0:p0+pw) L_pp^{-T}, thread per row i >= p0 + pw
+    for (int i = p0 + pw + tid; i < n; i += NT) {
+      double x[kPB];
+#pragma unroll
+      for (int m = 0; m < kPB; ++m) x[m] = (m < pw) ? S[i * kNL + p0 + m] : 0.0;
+#pragma unroll
+      for (int m = 0; m < kPB; ++m) {
+        if (m < pw) {
+          double s = x[m];
+#pragma unroll
+          for (int q = 0; q < m; ++q) s = fma(-x[q], S[(p0 + m) * kNL + p0 + q], s);
+          x[m] = s / S[(p0 + m) * kNL + p0 + m];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < kPB; ++m)
+        if (m < pw) S[i * kNL + p0 + m] = x[m];
+    }
+    __syncthreads();
+    // trailing update: S(i, j) -= L(i, panel) . L(j, panel), i >= j >= p0 + pw; 4 x 4 tiles
+    const int r0 = p0 + pw, nr = n - r0;
+    const int mt = (nr + 3) / 4, ntile = mt * (mt + 1) / 2;
+    for (int tile = tid; tile < ntile; tile += NT) {
+      int ti = 0, tj = tile;
+      while (tj > ti) {
+        tj -= ti + 1;
+        ++ti;
+      }
+      const int a0 = r0 + 4 * ti, b0 = r0 + 4 * tj;
+      double acc[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.0;
+      for (int m = 0; m < pw; ++m) {
+        double la[4], lb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          la[i] = S[min(a0 + i, 127) * kNL + p0 + m];
+          lb[i] = S[min(b0 + i, 127) * kNL + p0 + m];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) acc[i * 4 + jj] = fma(la[i], lb[jj], acc[i * 4 + jj]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (a0 + i < n && b0 + jj <= a0 + i) S[(a0 + i) * kNL + b0 + jj] -= acc[i * 4 + jj];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < n * n; e += NT) {
+    const int i = e / n, j = e - i * n;
+    if (j > i) S[i * kNL + j] = 0.0;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- one-vector solves (wave 0)
+// L (n x n lower, row stride ld, LDS or global), v (LDS, n): v <- L^{-1} v  or  L^{-T} v.
+// Lanes own rows lane and lane + 64.  Called by wave 0 only.
+__device__ void wave_trsv_lower(const double* L, int ld, double* v, int n) {
+  const int lane = threadIdx.x & 63;
+  double r0 = lane < n ? v[lane] : 0.0, r1 = lane + 64 < n ? v[lane + 64] : 0.0;
+  for (int k = 0; k < n; ++k) {
+    const double vk = (k < 64 ? readlane_d(r0, k) : readlane_d(r1, k - 64)) / L[(size_t)k * ld + k];
+    if (k < 64 && lane == k) r0 = vk;
+    if (k >= 64 && lane == k - 64) r1 = vk;
+    if (lane > k && lane < n) r0 = fma(-L[(size_t)lane * ld + k], vk, r0);
+    if (lane + 64 > k && lane + 64 < n) r1 = fma(-L[(size_t)(lane + 64) * ld + k], vk, r1);
+  }
+  if (lane < n) v[lane] = r0;
+  if (lane + 64 < n) v[lane + 64] = r1;
+}
+
+__device__ void wave_trsv_lower_t(const double* L, int ld, double* v, int n) {
+  const int lane = threadIdx.x & 63;
+  double r0 = lane < n ? v[lane] : 0.0, r1 = lane + 64 < n ? v[lane + 64] : 0.0;
+  for (int k = n - 1; k >= 0; --k) {
+    const double vk = (k < 64 ? readlane_d(r0, k) : readlane_d(r1, k - 64)) / L[(size_t)k * ld + k];
+    if (k < 64 && lane == k) r0 = vk;
+    if (k >= 64 && lane == k - 64) r1 = vk;
+    if (lane < k) r0 = fma(-L[(size_t)k * ld + lane], vk, r0);
+    if (lane + 64 < k) r1 = fma(-L[(size_t)k * ld + lane + 64], vk, r1);
+  }
+  if (lane < n) v[lane] = r0;
+  if (lane + 64 < n) v[lane + 64] = r1;
+}
+
+// ================================================================ A-step
+// One workgroup per (row ii = 1..N-1, chain).  Regressors RESID(:, 0:ii-1) / sqrtht(:, ii),
+// regressand RESID(:, ii) / sqrtht(:, ii): the (ii+1) x (ii+1) weighted Gram of RESID(:, 0:ii)
+// with weights 1 / sqrtht(:, ii)^2 holds ZZ (leading block) and Zz (last row).
+__global__ __launch_bounds__(256) void k_astep_big(Dims d, const int* __restrict__ Tslot,
+                                                   ChainState cs, RngArgs ra, double* __restrict__ wbuf) {
+  extern __shared__ double sm[];
+  const int ii = blockIdx.x + 1, c = blockIdx.y;
+  const int N = d.N, TP = d.TP;
+  const int T = Tslot[cs.slot[c]];
+  const int tid = threadIdx.x;
+  const Rng rng = ra.make(c);
+  double* G = sm;                    // (ii+1) x (ii+1), ld kNL
+  double* vec = sm + 128 * kNL;      // ii
+  double* wv = wbuf + ((size_t)c * N + ii) * TP;  // 1 / sqrtht(:, ii)^2
+  const double* E = cs.E + (size_t)c * N * TP;
+  const double* sh = cs.sqrtht + ((size_t)c * N + ii) * TP;
+  for (int t = tid; t < T; t += 256) {
+    const double h = sh[t];
+    wv[t] = 1.0 / (h * h);
+  }
+  __syncthreads();
+  wg_gram<256>(G, E, TP, 1, ii + 1, T, wv, 1);
+  const int n = ii;
+  for (int a = tid; a < n; a += 256) vec[a] = G[n * kNL + a];  // Zz
+  __syncthreads();
+  int bad = 0;
+  wg_chol<256>(G, n, &bad);
+  if (tid < 64) {
+    wave_trsv_lower(G, kNL, vec, n);  // tilde = L \ Zz   (sqrtiVAlpha_post' \ Zz)
+    const int zoff = ii * (ii - 1) / 2;
+    for (int r = tid; r < n; r += 64) vec[r] += rng.normal(CCMM_RNG_A, (uint32_t)(zoff + r));
+    wave_trsv_lower_t(G, kNL, vec, n);  // alpha = L' \ (tilde + z)
+  }
+  __syncthreads();
+  double* Ac = cs.A + (size_t)c * N * N;
+  for (int q = tid; q < n; q += 256) Ac[ii + q * N] = -vec[q];
+  if (bad && tid == 0) atomicOr(&cs.status[c], 4);
+}
+
+// invA = A \ I and logy2 = log((RESID A')^2 + offset); unit diagonal / zero upper of A.
+__global__ __launch_bounds__(256) void k_astep_fin(Dims d, const int* __restrict__ Tslot, ChainState cs,
+                                                   double logy2offset) {
+  extern __shared__ double sm[];
+  const int c = blockIdx.x;
+  const int N = d.N, TP = d.TP;
+  const int T = Tslot[cs.slot[c]];
+  const int tid = threadIdx.x;
+  double* Ac = cs.A + (size_t)c * N * N;
+  double* As = sm;  // N x N column-major
+  for (int q = tid; q < N * N; q += 256) {
+    const int r = q % N, col = q / N;
+    const double v = (r == col) ? 1.0 : (r > col ? Ac[q] : 0.0);
+    As[q] = v;
+    Ac[q] = v;
+  }
+  __syncthreads();
+  double* Ai = cs.invA + (size_t)c * N * N;
+  for (int col = tid; col < N; col += 256) {  // forward substitution, column col
+    for (int r = 0; r < N; ++r) {
+      double s = (r == col) ? 1.0 : 0.0;
+      if (r > col)
+        for (int q = col; q < r; ++q) s = fma(-As[r + q * N], Ai[q + col * N], s);
+      Ai[r + col * N] = (r >= col) ? s : 0.0;
+    }
+  }
+  const double* E = cs.E + (size_t)c * N * TP;
+  double* ly = cs.logy2 + (size_t)c * N * TP;
+  for (int q = tid; q < N * TP; q += 256) {
+    const int i = q / TP, t = q - i * TP;
+    double s = 0.0;
+    if (t < T)
+      for (int k = 0; k <= i; ++k) s = fma(E[(size_t)k * TP + t], As[i + k * N], s);
+    ly[q] = (t < T) ? log(s * s + logy2offset) : 0.0;
+  }
+}
+
+// ================================================================ PHI (inverse Wishart)
+// mcmcVAR.m:268-274 with scr = 3 N x N per chain (row-major, ld N): Lpost, L2 = chol(Z Z')'
+// (R = L2'), Sq.  1024 threads per chain.
+__global__ __launch_bounds__(1024) void k_phi_big(Dims d, const int* __restrict__ Tslot, int dPHI,
+                                                  const double* __restrict__ sPHIall, ChainState cs,
+                                                  double* __restrict__ scr) {
+  extern __shared__ double sm[];
+  const int c = blockIdx.x;
+  const int s = cs.slot[c];
+  const int N = d.N, TP = d.TP;
+  const int T = Tslot[s];
+  const int TZ = T + dPHI, TZmax = TP + dPHI;
+  const int tid = threadIdx.x;
+  double* M = sm;  // N x N, ld kNL
+  double* Lp = scr + (size_t)c * 3 * N * N;
+  double* L2 = Lp + N * N;
+  double* Sq = L2 + N * N;
+  const double* sP = sPHIall + (size_t)s * N * N;
+  int bad = 0;
+  // Lpost = chol(s_PHI + eta'eta, 'lower')
+  wg_gram<1024>(M, cs.eta + (size_t)c * N * TP, TP, 1, N, T, nullptr, 0);
+  for (int e = tid; e < N * N; e += 1024) {
+    const int r = e / N, col = e - r * N;
+    if (col <= r) M[r * kNL + col] += sP[r + col * N];
+  }
+  __syncthreads();
+  wg_chol<1024>(M, N, &bad);
+  for (int e = tid; e < N * N; e += 1024) Lp[e] = M[(e / N) * kNL + e % N];
+  __syncthreads();
+  // R = chol(Zdraw Zdraw') (upper) = L2'
+  wg_gram<1024>(M, cs.Zphi + (size_t)c * N * TZmax, 1, N, N, TZ, nullptr, 0);
+  wg_chol<1024>(M, N, &bad);
+  for (int e = tid; e < N * N; e += 1024) L2[e] = M[(e / N) * kNL + e % N];
+  __syncthreads();
+  // sqrtPHI_ = Lpost / R: Sq L2' = Lpost, row r by forward substitution (thread per row)
+  for (int r = tid; r < N; r += 1024) {
+    for (int col = 0; col < N; ++col) {
+      double v = (col <= r) ? Lp[r * N + col] : 0.0;
+      for (int q = 0; q < col; ++q) v = fma(-Sq[r * N + q], L2[col * N + q], v);
+      Sq[r * N + col] = v / L2[col * N + col];
+    }
+  }
+  __syncthreads();
+  // PHI_ = Sq Sq'
+  double* PHI = cs.PHI + (size_t)c * N * N;
+  for (int e = tid; e < N * N; e += 1024) {
+    const int r = e / N, col = e - r * N;
+    if (col > r) continue;
+    double v = 0.0;
+    for (int q = 0; q < N; ++q) v = fma(Sq[r * N + q], Sq[col * N + q], v);
+    M[r * kNL + col] = v;
+    PHI[r + col * N] = v;
+    PHI[col + r * N] = v;
+  }
+  __syncthreads();
+  wg_chol<1024>(M, N, &bad);
+  double* sqo = cs.sqrtPHI + (size_t)c * N * N;
+  for (int e = tid; e < N * N; e += 1024) {
+    const int r = e % N, col = e / N;
+    sqo[e] = (col <= r) ? M[r * kNL + col] : 0.0;
+  }
+  if (bad && tid == 0) atomicOr(&cs.status[c], 16);
+}
+
+// ================================================================ SV (time-ordered sampler)
+// Per chain (1024 threads).  scratch per chain: Q (N x N), Lt (T+1 blocks N x N: L_t),
+// Mt (T+1 blocks: M_t = L_{t-1}^{-1} Q), w (T+1 x N); all row-major with ld N.
+__global__ __launch_bounds__(1024) void k_sv_big(Dims d, const int* __restrict__ Tslot,
+                                                 const double* __restrict__ V0inv,
+                                                 const double* __restrict__ V0invm, ChainState cs,
+                                                 RngArgs ra, double* __restrict__ scr, size_t scr_stride) {
+  extern __shared__ double sm[];
+  const int c = blockIdx.x;
+  const int s = cs.slot[c];
+  const int N = d.N, TP = d.TP;
+  const int T = Tslot[s];
+  const int tid = threadIdx.x;
+  const Rng rng = ra.make(c);
+  const size_t NN = (size_t)N * N;
+  double* Q = scr + (size_t)c * scr_stride;
+  double* Lt = Q + NN;                        // (T+1) x NN
+  double* Mt = Lt + (size_t)(TP + 1) * NN;    // (T+1) x NN
+  double* wv = Mt + (size_t)(TP + 1) * NN;    // (T+1) x N
+  double* S = sm;                             // N x N, ld kNL
+  double* vec = sm + 128 * kNL;               // N
+  double* vec2 = vec + 128;                   // N
+  const double* obs = cs.svobs + (size_t)c * N * TP;
+  const double* irv = cs.svir + (size_t)c * N * TP;
+  int bad = 0;
+  // Q = PHI^{-1} = sqrtPHI^{-T} sqrtPHI^{-1}: invert sqrtPHI (lower) column-wise into Lt[0]
+  {
+    const double* sq = cs.sqrtPHI + (size_t)c * NN;  // column-major lower
+    double* Li = Lt;                                 // scratch: Li(r, col) at r * N + col
+    for (int col = tid; col < N; col += 1024)
+      for (int r = 0; r < N; ++r) {
+        double v = (r == col) ? 1.0 : 0.0;
+        if (r > col)
+          for (int q = col; q < r; ++q) v = fma(-sq[r + q * N], Li[q * N + col], v);
+        Li[r * N + col] = (r >= col) ? v / sq[r + r * N] : 0.0;
+      }
+    __syncthreads();
+    for (int e = tid; e < N * N; e += 1024) {
+      const int a = e / N, b = e - a * N;
+      double v = 0.0;
+      for (int r = max(a, b); r < N; ++r) v = fma(Li[r * N + a], Li[r * N + b], v);
+      Q[e] = v;
+    }
+    __syncthreads();
+  }
+  // ---- forward: t = 0 .. T.  Entering step t (t >= 1) the LDS matrix holds L_{t-1}.
+  const int gj = tid >> 3, gq = tid & 7;  // lane group of 8 per column / row gj
+  const bool gact = gj < N;
+  for (int t = 0; t <= T; ++t) {
+    double* Lcur = Lt + (size_t)t * NN;
+    double* Mcur = Mt + (size_t)t * NN;
+    if (t > 0) {
+      // M_t = L_{t-1}^{-1} Q, left-looking by rows i; 8 lanes per column j, lane gq owns
+      // rows gq + 8m (registers y[m]), partial sums joined over the group.  Q(i, j) reaches
+      // the owner lane through qcur (row block of i), prefetched one block ahead in qnxt.
+      double y[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) y[m] = 0.0;
+      double qcur = (gact && gq < N) ? Q[gq * N + gj] : 0.0;
+      double qnxt = (gact && gq + 8 < N) ? Q[(gq + 8) * N + gj] : 0.0;
+      for (int i = 0; i < N; ++i) {
+        if (i > 0 && (i & 7) == 0) {
+          qcur = qnxt;
+          const int k = i + 8 + gq;
+          qnxt = (gact && k < N) ? Q[k * N + gj] : 0.0;
+        }
+        double sacc = 0.0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+          if (8 * m < i) {
+            const int k = gq + 8 * m;
+            const double l = (k < i) ? S[i * kNL + k] : 0.0;
+            sacc = fma(l, y[m], sacc);
+          }
+        sacc += dpp_d<0xB1>(sacc);
+        sacc += dpp_d<0x4E>(sacc);
+        sacc += dpp_d<0x141>(sacc);
+        const double yi = (qcur - sacc) / S[i * kNL + i];
+        if (gq == (i & 7)) {
+          const int mi = i >> 3;
+#pragma unroll
+          for (int m = 0; m < 16; ++m) y[m] = (m == mi) ? yi : y[m];
+        }
+      }
+      if (gact)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+          const int k = gq + 8 * m;
+          if (k < N) Mcur[k * N + gj] = y[m];
+        }
+      __syncthreads();
+      // M_t' M_t into the LDS matrix (L_{t-1} is kept in global Lt[t-1])
+      wg_gram<1024>(S, Mcur, 1, N, N, N, nullptr, 0);
+    }
+    // S = D_t - M_t' M_t, D_0 = V0inv + Q, D_t = 2Q + diag(ir_t) (t < T), D_T = Q + diag(ir_T)
+    const double* V0 = V0inv + (size_t)s * NN;
+    for (int e = tid; e < N * N; e += 1024) {
+      const int a = e / N, b = e - a * N;
+      if (b > a) continue;
+      double v;
+      if (t == 0) {
+        v = V0[a + b * N] + Q[e];
+      } else {
+        v = (t == T ? 1.0 : 2.0) * Q[e];
+        if (a == b) v += irv[(size_t)a * TP + t - 1];
+        v -= S[a * kNL + b];
+      }
+      S[a * kNL + b] = v;
+    }
+    // rhs: b_0 = V0inv h0mean; b_t = obs_t ir_t + M_t' w_{t-1} (8 lanes per entry)
+    if (t == 0) {
+      for (int a = tid; a < N; a += 1024) vec[a] = V0invm[(size_t)s * N + a];
+    } else {
+      const double* wp = wv + (size_t)(t - 1) * N;
+      double v = 0.0;
+      if (gact)
+        for (int i = gq; i < N; i += 8) v = fma(Mcur[i * N + gj], wp[i], v);
+      v += dpp_d<0xB1>(v);
+      v += dpp_d<0x4E>(v);
+      v += dpp_d<0x141>(v);
+      if (gact && gq == 0) vec[gj] = v + obs[(size_t)gj * TP + t - 1] * irv[(size_t)gj * TP + t - 1];
+    }
+    __syncthreads();
+    wg_chol<1024>(S, N, &bad);
+    if (tid < 64) wave_trsv_lower(S, kNL, vec, N);
+    __syncthreads();
+    for (int e = tid; e < N * N; e += 1024) Lcur[e] = S[(e / N) * kNL + e % N];
+    for (int a = tid; a < N; a += 1024) wv[(size_t)t * N + a] = vec[a];
+    __syncthreads();
+  }
+  // ---- backward: x_T = L_T^{-T}(w_T + z_T); x_t = L_t^{-T}(w_t + z_t + M_{t+1} x_{t+1})
+  double* hout = cs.h + (size_t)c * N * TP;
+  double* eta = cs.eta + (size_t)c * N * TP;
+  double* sqh = cs.sqrtht + (size_t)c * N * TP;
+  for (int t = T; t >= 0; --t) {
+    // L_t to LDS (L_T is still there)
+    if (t < T)
+      for (int e = tid; e < N * N; e += 1024) S[(e / N) * kNL + e % N] = Lt[(size_t)t * NN + e];
+    double v = 0.0;
+    if (t < T && gact) {
+      const double* Mn = Mt + (size_t)(t + 1) * NN;
+      for (int j = gq; j < N; j += 8) v = fma(Mn[gj * N + j], vec2[j], v);
+    }
+    v += dpp_d<0xB1>(v);
+    v += dpp_d<0x4E>(v);
+    v += dpp_d<0x141>(v);
+    if (gact && gq == 0) vec[gj] = v + wv[(size_t)t * N + gj] + rng.normal(CCMM_RNG_SVZ, (uint32_t)(gj + N * t));
+    __syncthreads();
+    if (tid < 64) wave_trsv_lower_t(S, kNL, vec, N);
+    __syncthreads();
+    // vec = x_t; vec2 = x_{t+1}
+    for (int a = tid; a < N; a += 1024) {
+      const double x = vec[a];
+      if (t >= 1) {
+        hout[(size_t)a * TP + t - 1] = x;
+        sqh[(size_t)a * TP + t - 1] = exp(0.5 * x);
+      }
+      if (t < T) eta[(size_t)a * TP + t] = vec2[a] - x;  // shock of period t+1: h_{t+1} - h_t
+      vec2[a] = x;
+    }
+    __syncthreads();
+  }
+  if (bad && tid == 0) atomicOr(&cs.status[c], 8);
+}
+
+// ================================================================ host launchers
+size_t bign_sv_scratch(const Dims& d) {
+  return (size_t)d.N * d.N * (1 + 2 * (size_t)(d.TP + 1)) + (size_t)(d.TP + 1) * d.N;
+}
+
+hipError_t bign_launch_astep(hipStream_t st, const Dims& d, const int* Tslot, ChainState cs, RngArgs ra,
+                             double logy2offset, double* wbuf) {
+  const size_t lds = (size_t)(128 * kNL + 128) * sizeof(double);
+  hipError_t e = hipFuncSetAttribute((const void*)k_astep_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_astep_big, dim3(d.N - 1, d.B), dim3(256), lds, st, d, Tslot, cs, ra, wbuf);
+  const size_t lds2 = (size_t)d.N * d.N * sizeof(double);
+  e = hipFuncSetAttribute((const void*)k_astep_fin, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_astep_fin, dim3(d.B), dim3(256), lds2, st, d, Tslot, cs, logy2offset);
+  return hipGetLastError();
+}
+
+hipError_t bign_launch_phi(hipStream_t st, const Dims& d, const int* Tslot, int dPHI, const double* sPHI,
+                           ChainState cs, double* scr) {
+  const size_t lds = (size_t)(128 * kNL) * sizeof(double);
+  hipError_t e = hipFuncSetAttribute((const void*)k_phi_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_phi_big, dim3(d.B), dim3(1024), lds, st, d, Tslot, dPHI, sPHI, cs, scr);
+  return hipGetLastError();
+}
+
+hipError_t bign_launch_sv(hipStream_t st, const Dims& d, const int* Tslot, const double* V0inv,
+                          const double* V0invm, ChainState cs, RngArgs ra, double* scr) {
+  const size_t lds = (size_t)(128 * kNL + 256) * sizeof(double);
+  hipError_t e = hipFuncSetAttribute((const void*)k_sv_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_sv_big, dim3(d.B), dim3(1024), lds, st, d, Tslot, V0inv, V0invm, cs, ra, scr,
+                     bign_sv_scratch(d));
+  return hipGetLastError();
+}
+
+}  // namespace ccmm

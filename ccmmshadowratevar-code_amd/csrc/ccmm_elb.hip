@@ -68,7 +68,8 @@ __host__ __device__ inline int elb_cond_stride(int Ns, int p) {
 // matrix is explosive, where the as-written form loses all digits to cancellation.
 //   Yt[τ] = Yb_τ   (the chain's Y with censored shadow-rate cells at 0)
 //   Et[τ] = ε_τ = Yb_τ - Σ_{l<=τ} Φ_l Yb_{τ-l} - e0_τ
-__global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, ChainState cs) {
+// phi_lds: stage Φ in LDS (N (Np + 1) doubles; N <= 32); else it is read back from e.Phi
+__global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, ChainState cs, int phi_lds) {
   extern __shared__ double sm[];
   const int c = blockIdx.x;
   const int s = cs.slot[c];
@@ -82,8 +83,8 @@ __global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, Cha
   double* Z = e.Y0 + (size_t)c * e.elbTmax * N;     // Yb - yhat
   double* Yt = e.Yt + (size_t)c * e.elbTmax * N;
   double* Et = e.Et + (size_t)c * e.elbTmax * N;
-  double* sPhi = sm;                 // N x ldp
-  double* X0 = sPhi + N * ldp;       // K: elb.X0 = X(elbT0+1, :)'
+  double* X0 = sm;                   // K: elb.X0 = X(elbT0+1, :)'
+  double* sPhi = sm + (2 + Np);      // N x ldp (phi_lds)
   // Φ = PAIshadow(2:1+Np, :)' with (ndxSHADOWRATELAGS, actualrateBlock) zeroed (:404-407)
   for (int q = tid; q < N * Np; q += 256) {
     const int i = q / Np, kp = q % Np;
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, Cha
       for (int si = 0; si < Ns; ++si) zero |= (kp % N) == e.ndxS[si];
     const double v = zero ? 0.0 : PAI[(size_t)i * KP + 1 + kp];
     Phi[q] = v;
-    sPhi[i * ldp + kp] = v;
+    if (phi_lds) sPhi[i * ldp + kp] = v;
   }
   const double* Xa = e.Xactual + (size_t)s * KP * TP;        // Xactual(t, k) at [k*TP + t]
   const double* Yc = xs.ypool + (size_t)xs.yidx[c] * N * TP;  // chain's Y(t, i) at [i*TP + t]
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, Cha
   // ε_τ = Z_τ - Σ_{l<=τ} Φ_l Z_{τ-l} - [τ = 0: w_{-1};  τ >= 1: c + Σ_{l>τ} Φ_l w_{τ-1-l}]
   for (int q = tid; q < T * N; q += 256) {
     const int t = q / N, i = q % N;
-    const double* ph = sPhi + i * ldp;
+    const double* ph = phi_lds ? sPhi + i * ldp : Phi + (size_t)i * Np;
     double v = Z[q];
     for (int l = 1; l <= p && t - l >= 0; ++l) {
       const double* zl = Z + (size_t)(t - l) * N;
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, Cha
 }
 
 // ---------------------------------------------------------------- conditionals
-// One wave per (censored month, chain).  Lanes i < N own element i of N-vectors;
+// One wave per (censored month, chain).  Lanes own elements lane, lane + 64 of N-vectors;
 // neighbour columns are spread over lanes; Ns x Ns algebra runs redundantly.
 __device__ inline void elb_small_inverse(const double* M, double* Minv, int n) {
   double W[kElbNsMax * kElbNsMax];
@@ -191,13 +192,13 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
   double* gS = Q + (p + 1) * Ns * N;           // (1 + ncol) x Ns
   double* Pm = gS + (1 + ncol) * Ns;           // Ns x Ns
   double* Om = Pm + Ns * Ns;                   // Ns x Ns
+  double* Wl = Om + Ns * Ns;                   // N x Ns: W = diag(1/SVol^2) (A or A Φ_k)[:, S]
   int S[kElbNsMax];
   for (int a = 0; a < kElbNsMax; ++a) S[a] = a < Ns ? e.ndxS[a] : 0;
   // ---- Q_0 = Λ_t[S, :], Q_k = B_k' Λ_{t+k};  Λ = A' diag(1/SVol^2) A
   for (int k = 0; k <= kmax; ++k) {
-    double w[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
-    if (lane < N) {
-      const int i = lane;
+    for (int i = lane; i < N; i += 64) {
+      double w[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
       const double sv = cs.sqrtht[((size_t)c * N + i) * d.TP + T0 + t + k];
       const double iv = 1.0 / (sv * sv);
       for (int a = 0; a < Ns; ++a) {
@@ -209,16 +210,17 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
         }
         w[a] = v * iv;
       }
+      for (int a = 0; a < Ns; ++a) Wl[i * Ns + a] = w[a];
     }
+    __syncthreads();
     // Q_k[a][j] = Σ_{i >= j} W[i][a] A(i,j)
-    for (int a = 0; a < Ns; ++a) {
-      double v = 0.0;
-      for (int i = 0; i < N; ++i) {
-        const double wi = __shfl(w[a], i);
-        if (lane < N && i >= lane) v = fma(wi, A[i + lane * N], v);
+    for (int a = 0; a < Ns; ++a)
+      for (int j = lane; j < N; j += 64) {
+        double v = 0.0;
+        for (int i = j; i < N; ++i) v = fma(Wl[i * Ns + a], A[i + j * N], v);
+        Q[((size_t)k * Ns + a) * N + j] = v;
       }
-      if (lane < N) Q[((size_t)k * Ns + a) * N + lane] = v;
-    }
+    __syncthreads();
   }
   __syncthreads();
   // ---- P = Λ_t,SS + Σ_k Q_k B_k
@@ -235,17 +237,17 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
   //      ε'_t = ε_t - E_S Yb_S,t,  ε'_{t+k} = ε_{t+k} + Φ_k[:,S] Yb_S,t
   {
     double g0[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
-    if (lane < N) {
+    for (int j = lane; j < N; j += 64) {
       bool isS = false;
-      for (int a = 0; a < Ns; ++a) isS |= (S[a] == lane);
-      const double et = Et[(size_t)t * N + lane];
-      const double u0 = isS ? Yt[(size_t)t * N + lane] - et : -et;  // -ε'_t
-      for (int a = 0; a < Ns; ++a) g0[a] = Q[(size_t)a * N + lane] * u0;
+      for (int a = 0; a < Ns; ++a) isS |= (S[a] == j);
+      const double et = Et[(size_t)t * N + j];
+      const double u0 = isS ? Yt[(size_t)t * N + j] - et : -et;  // -ε'_t
+      for (int a = 0; a < Ns; ++a) g0[a] = fma(Q[(size_t)a * N + j], u0, g0[a]);
       for (int k = 1; k <= kmax; ++k) {
-        double r = Et[(size_t)(t + k) * N + lane];
+        double r = Et[(size_t)(t + k) * N + j];
         for (int b = 0; b < Ns; ++b)
-          r = fma(Phi[(size_t)lane * Np + (k - 1) * N + S[b]], Yt[(size_t)t * N + S[b]], r);
-        for (int a = 0; a < Ns; ++a) g0[a] = fma(Q[((size_t)k * Ns + a) * N + lane], r, g0[a]);
+          r = fma(Phi[(size_t)j * Np + (k - 1) * N + S[b]], Yt[(size_t)t * N + S[b]], r);
+        for (int a = 0; a < Ns; ++a) g0[a] = fma(Q[((size_t)k * Ns + a) * N + j], r, g0[a]);
       }
     }
     for (int a = 0; a < Ns; ++a) {

@@ -8,7 +8,8 @@ here = Path(__file__).resolve().parent
 out = "".join(subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
                               "-c", tu, "-o", "/tmp/_ccmm_ru.o", "-Rpass-analysis=kernel-resource-usage"],
                              cwd=here, capture_output=True, text=True).stderr
-              for tu in ("ccmm_abi.hip", "ccmm_lag.hip", "ccmm_svpart.hip"))
+              for tu in ("ccmm_abi.hip", "ccmm_lag.hip", "ccmm_svpart.hip", "ccmm_big.hip",
+                         "ccmm_bign.hip"))
 rows, cur = [], None
 pats = {"vgpr": r"VGPRs: (\d+)", "agpr": r"AGPRs: (\d+)", "scratch": r"ScratchSize \[bytes/lane\]: (\d+)",
         "lds": r"LDS Size \[bytes/block\]: (\d+)", "occ": r"Occupancy \[waves/SIMD\]: (\d+)"}

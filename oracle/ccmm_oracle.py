@@ -388,7 +388,7 @@ def sv_precision(obs, ir, sqrtPHI, h0mean, h0vcvsqrt):
 
 def sv_draw_sequential(D, b, Q, z):
     """x = P^{-1} b + L^{-T} z with L the time-ordered block Cholesky factor
-    (the round-1 declared convention; kept as a cross-check of the moments)."""
+    (the declared convention for N > 32; for N <= 32 a cross-check of the moments)."""
     T1, N = b.shape
     Ld = np.empty_like(D)
     w = np.empty_like(b)
@@ -503,16 +503,17 @@ def sv_ksc_corrsqrt(y, hprev, sqrtPHI, h0mean, h0vcvsqrt, u, z):
     eps_t ~ N(0, diag(var_{s_t})); h_t = h_{t-1} + sqrtPHI e_t; h_0 ~ N(h0mean, V0),
     V0 = h0vcvsqrt h0vcvsqrt'.  Posterior precision of x = [h_0; ...; h_T] is
     block tridiagonal; x = P^{-1} b + Pi' L^{-T} z with L the block Cholesky factor
-    in the partitioned order of ``sv_draw_partitioned`` (declared convention: the
-    reference's sampler lives in the absent em-matlabbox).  z is N x (T+1), column t
-    for block t.  Returns h (N x T), h0 (N), shocks (N x T, h_t - h_{t-1}),
-    indicators (N x T int8).
+    in the partitioned order of ``sv_draw_partitioned`` for N <= 32 and in time order
+    (``sv_draw_sequential``, Pi = I) for N > 32 (declared conventions: the reference's
+    sampler lives in the absent em-matlabbox; the GPU follows the same split,
+    ccmm_svpart.hip / ccmm_bign.hip k_sv_big).  z is N x (T+1), column t for block t.
+    Returns h (N x T), h0 (N), shocks (N x T, h_t - h_{t-1}), indicators (N x T int8).
     """
     kai = ksc_indicators(y, hprev, u)
     obs = y - KSC_MEAN[kai - 1]
     ir = 1.0 / KSC_VAR[kai - 1]
     D, b, Q = sv_precision(obs, ir, sqrtPHI, h0mean, h0vcvsqrt)
-    x = sv_draw_partitioned(D, b, Q, z)
+    x = sv_draw_partitioned(D, b, Q, z) if y.shape[0] <= 32 else sv_draw_sequential(D, b, Q, z)
     h = x[1:].T.copy()
     shocks = (x[1:] - x[:-1]).T.copy()
     return h, x[0].copy(), shocks, kai
