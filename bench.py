@@ -54,6 +54,13 @@ def parse():
     ap.add_argument("--oos-steps", type=int, default=3,
                     help="timed kept sweeps (with forecasts) of the OOS line (configs[3]); 0 = skip")
     ap.add_argument("--oos-chains", default="1,8", help="chains per vintage of the OOS lines")
+    ap.add_argument("--s120-steps", type=int, default=2,
+                    help="timed sweeps of the S120 stress line (configs[4], N=120); 0 = skip")
+    ap.add_argument("--s120-warmup", type=int, default=1)
+    ap.add_argument("--s120-chains", default="64", help="chains per GPU of the S120 lines")
+    ap.add_argument("--s120-groups", type=int, default=2,
+                    help="chain groups (HIP streams driven from host threads) of the S120 lines")
+    ap.add_argument("--s120-only", action="store_true", help="run only the S120 lines (probe)")
     ap.add_argument("--cpu-workers", type=int, default=0,
                     help="parallel single-thread CPU baseline processes (0: min(16, cpus))")
     return ap.parse_args()
@@ -71,6 +78,17 @@ def main():
         torch.cuda.set_device(local)
         dist_.init_process_group("nccl")
         dist = dist_
+
+    if args.s120_only:
+        import __graft_entry__ as ge
+        pkg = ge.load_package()
+        ctx = pkg.Context(local)
+
+        def barrier0():
+            ctx.synchronize()
+        for b in args.s120_chains.split(","):
+            print(json.dumps(bench_s120(pkg, ctx, int(b), args, rank, barrier0, None)), flush=True)
+        return
 
     cpu = None
     if world == 1 and not args.no_cpu:
@@ -123,6 +141,10 @@ def main():
     if args.bh_steps > 0:
         bh = [bench_block_hybrid(pkg, ctx, d, int(b), args, rank, barrier, dist)
               for b in args.bh_chains.split(",") if b.strip()]
+    s120 = None
+    if args.s120_steps > 0:
+        s120 = [bench_s120(pkg, ctx, int(b), args, rank, barrier, dist)
+                for b in args.s120_chains.split(",") if b.strip()]
     oos = None
     if args.oos_steps > 0:
         oos = [bench_oos(pkg, ctx, d, int(c), args, rank, barrier, dist)
@@ -198,6 +220,8 @@ def main():
         out["block_hybrid"] = bh
     if oos is not None:
         out["oos"] = oos
+    if s120 is not None:
+        out["s120"] = s120
     if fc is not None:
         out["predictive"] = fc
     if cpu is not None:
@@ -363,6 +387,129 @@ def bench_block_hybrid(pkg, ctx, d, B, args, rank, barrier, dist):
                                 "bytes_per_launch": int(nbytes), "avg_launch_ms": round(ms, 4),
                                 "note": "one wave per chain, 101 sequential passes: latency-bound"}
     ch.close()
+    return res
+
+
+def _in_threads(fns):
+    """Run callables concurrently on host threads (the libccmm calls release the GIL), so
+    chain groups on separate HIP streams overlap on the device; re-raises the first error."""
+    import threading
+    errs = []
+
+    def wrap(f):
+        try:
+            f()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+    th = [threading.Thread(target=wrap, args=(f,)) for f in fns]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
+def bench_s120(pkg, ctx, B, args, rank, barrier, dist, groups=None):
+    """Stress line, BASELINE.json configs[4]: the block-hybrid shadow-rate
+    sweep at N = 120, p = 12, T = 750 (K = 1441) on the synthetic S120 panel
+    (ccmmshadowratevar-code_amd/synthetic.py: four shadow rates, two other yields, the last
+    ~15 % of months at the ELB).  Every block runs on the large path: multi-equation
+    FP64-MFMA Gram + blocked MFMA Cholesky + per-chain solve (ccmm_big.hip), the large-N
+    A / SV / PHI blocks (ccmm_bign.hip), the ELB Gibbs step (101 passes).
+
+    The B chains form G groups (chain sets) on G HIP streams (one context each), driven
+    from G host threads: the per-chain sequential blocks (SV recursion, CTA solve, ELB Gibbs;
+    one workgroup per chain) of one group overlap the MFMA Gram/Cholesky of another.  Same
+    timing protocol as the main line (barrier, K timed sweeps of every group, max over ranks);
+    the CTA kernels are priced against the FP64 MFMA peak from their per-launch times."""
+    import time as _t
+    G = groups or args.s120_groups
+    if B % G:
+        G = 1
+    Bg = B // G
+    p = 12
+    d = pkg.synthetic.s120()
+    mpm = np.ones(d["data"].shape[1])
+    ndxS, ndxO, _ = pkg.model.setShadowYields(d["ncode"], 0.25)
+    e0 = pkg.model.elbT0_of(d["data"], ndxS, 0.25, p)
+    bm = pkg.model.build_bh(len(d["ydates"]), p, 12, d["data"], d["ydates"], ndxS, ndxO, mpm,
+                            0.25, e0, True)
+    m = bm.var
+    Ns = len(bm.ndxS)
+    ctxs = [ctx] + [pkg.Context(ctx.device) for _ in range(G - 1)]
+    chs = []
+    for g, cx in enumerate(ctxs):
+        ch = pkg.Chains(cx, N=m.N, p=p, T=m.T, B=Bg, crn=False,
+                        store_capacity=args.s120_warmup + args.s120_steps,
+                        seed=1012023 + 7919 * rank + 2, model=pkg.MODEL_BLOCKHYBRID, Ns=Ns,
+                        elbTmax=bm.elbT, elb_gibbsburn=100, elb=0.25)
+        ch.set_rng_ids(np.arange(g * Bg, (g + 1) * Bg, dtype=np.uint32))
+        if G > 1:
+            ch.set_mfma_lock(1)
+        ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+        ch.set_elb_model(bm.ndxS, bm.actual_block)
+        ch.set_elb_slot(0, bm.elbT0, bm.sNaN)
+        st = pkg.model.initial_state(m, Bg)
+        ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+        chs.append(ch)
+    _in_threads([lambda c=c: c.sweep(args.s120_warmup, store=True) for c in chs])
+    for cx in ctxs:
+        cx.synchronize()
+    barrier()
+    if not args.no_profile:
+        for c in chs:
+            c.profile(True)
+    t0 = _t.perf_counter()
+    _in_threads([lambda c=c: c.sweep(args.s120_steps, store=True) for c in chs])
+    for cx in ctxs:
+        cx.synchronize()
+    barrier()
+    el = _t.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{ctx.device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    flagged = 0
+    for c in chs:
+        assert np.all(np.isfinite(c.get_shadowrate())), "non-finite shadow rates"
+        flagged += int(np.count_nonzero(c.get_status()))
+    world = dist.get_world_size() if dist is not None else 1
+    N, K, T = m.N, m.K, m.T
+    ncens = int(np.any(bm.sNaN, axis=0).sum())
+    res = {"workload": "configs[4]: S120 block-hybrid shadow-rate BVAR-SV, synthetic panel "
+                       f"N={N} p={p} T={T} K={K}, Ns={Ns}, elbT={bm.elbT}, {ncens} censored months, "
+                       f"ELB Gibbs (101 passes) every sweep, {B} chains per GPU in {G} stream group(s)",
+           "value": round(world * B * args.s120_steps / el, 4), "unit": "sweeps/s",
+           "ms_per_step": round(1e3 * el / args.s120_steps, 3), "steps": args.s120_steps,
+           "warmup": args.s120_warmup, "chains": B, "groups": G, "chains_flagged": flagged}
+    if not args.no_profile:
+        kt = {}
+        for c in chs:  # per-launch device times (events on each group's stream), all groups
+            for k, v in c.kernel_times().items():
+                a = kt.get(k, (0.0, 0))
+                kt[k] = (a[0] + v[0], a[1] + v[1])
+        res["kernel_ms_per_launch"] = {k: round(v[0] / v[1], 3) for k, v in kt.items() if v[1]}
+        # CTA on FP64 MFMA: Gram T K (K+1) and Cholesky K^3 / 3 per equation (SURVEY §8d),
+        # per launch of one group (Bg chains)
+        fg, fc = Bg * N * T * K * (K + 1), Bg * N * K ** 3 / 3
+        mf = {}
+        for kn, fl in (("k_gram_big", fg), ("k_chol_big", fc)):
+            if kt.get(kn, (0, 0))[1]:
+                ms = kt[kn][0] / kt[kn][1]
+                mf[kn] = {"achieved": round(fl / (ms * 1e-3) / 1e12, 3), "peak": FP64_MFMA_PEAK_TFLOPS,
+                          "unit": "TFLOP/s", "frac": round(fl / (ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                          "flop_per_launch": int(fl), "avg_launch_ms": round(ms, 3)}
+        ach = B * N * (T * K * (K + 1) + K ** 3 / 3) / (1e-3 * res["ms_per_step"]) / 1e12
+        mf["whole_sweep"] = {"achieved": round(ach, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                             "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4),
+                             "note": "CTA Gram + Cholesky flop of all chains over the whole sweep time"}
+        if G > 1:
+            mf["note"] = "groups overlap on the device: per-launch times include contention"
+        res["fp64_mfma"] = mf
+    for c in chs:
+        c.close()
     return res
 
 

@@ -72,6 +72,7 @@ _SIGS = {
     "ccmm_chains_stored": (C.c_int, [C.c_void_p]),
     "ccmm_chains_get_draws": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
     "ccmm_chains_set_rng_ids": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "ccmm_chains_set_mfma_lock": (C.c_int, [C.c_void_p, C.c_int]),
     "ccmm_chains_get_status": (C.c_int, [C.c_void_p, _ip]),
     "ccmm_chains_set_fcst": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, C.c_int]),
     "ccmm_chains_set_fcst_slot": (C.c_int, [C.c_void_p, C.c_int, _dp]),
@@ -294,7 +295,8 @@ class Chains:
     KERNELS = ("k_resid", "k_cta_weights", "k_syrk", "k_chol", "k_cta_solve", "k_astep",
                "k_sv_mix", "k_sv_part", "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
                "k_elb_prep", "k_elb_cond", "k_elb_gibbs", "k_elb_rebuild", "k_gram_chol_lag",
-               "k_cta_solve_lag", "k_fcst", "k_gram_big", "k_chol_big", "k_cta_solve_big")
+               "k_cta_solve_lag", "k_fcst", "k_gram_big", "k_chol_big", "k_cta_solve_big",
+               "k_astep_big", "k_sv_big", "k_phi_big")
 
     def __init__(self, ctx: Context, *, N, p, T, B, ndata=1, model=MODEL_LINEAR, crn=False,
                  store_capacity=0, logy2offset=1e-3, seed=1012023, dPHI=None, Ns=0, elbTmax=0,
@@ -365,6 +367,11 @@ class Chains:
         s = np.ascontiguousarray(slots, dtype=np.int32)
         _check(self.lib.ccmm_chains_set_slots(self.handle, s.ctypes.data_as(_ip)),
                "ccmm_chains_set_slots")
+
+    def set_mfma_lock(self, lock_id):
+        """Serialise the MFMA Gram + Cholesky phase with other chain sets of the same id
+        (ccmm_chains_set_mfma_lock); 0 turns it off."""
+        _check(self.lib.ccmm_chains_set_mfma_lock(self.handle, int(lock_id)), "ccmm_chains_set_mfma_lock")
 
     def set_rng_ids(self, ids):
         """Philox stream id per chain (None: the chain index)."""

@@ -5,6 +5,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -179,6 +182,9 @@ enum KernelId {
   KID_GRAMBIG,
   KID_CHOLBIG,
   KID_SOLVEBIG,
+  KID_ASTEPBIG,
+  KID_SVBIG,
+  KID_PHIBIG,
   KID_COUNT
 };
 static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syrk", "k_chol",
@@ -187,7 +193,26 @@ static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syr
                                               "k_elb_prep", "k_elb_cond", "k_elb_gibbs",
                                               "k_elb_rebuild", "k_gram_chol_lag",
                                               "k_cta_solve_lag", "k_fcst",
-                                              "k_gram_big", "k_chol_big", "k_cta_solve_big"};
+                                              "k_gram_big", "k_chol_big", "k_cta_solve_big",
+                                              "k_astep_big", "k_sv_big", "k_phi_big"};
+
+// MFMA phase lock: chain sets given the same id (ccmm_chains_set_mfma_lock) on one device
+// serialise their CTA Gram + Cholesky phase through a cross-stream event, so the groups fall
+// out of step and one group's per-chain sequential blocks (CTA solve, SV, ELB Gibbs) run
+// beside another group's MFMA phase instead of all groups contending for the CUs at once.
+struct PhaseLock {
+  std::mutex m;
+  hipEvent_t last = nullptr;  // event recorded after the latest enqueued locked phase
+};
+
+static PhaseLock& phase_lock(int device, int id) {
+  static std::mutex gm;
+  static std::map<std::pair<int, int>, std::unique_ptr<PhaseLock>> locks;
+  std::lock_guard<std::mutex> g(gm);
+  auto& p = locks[{device, id}];
+  if (!p) p.reset(new PhaseLock);
+  return *p;
+}
 
 struct ccmm_chains {
   ccmm_ctx* ctx = nullptr;
@@ -262,7 +287,16 @@ struct ccmm_chains {
   double kms[KID_COUNT] = {};
   int64_t kcount[KID_COUNT] = {};
 
+  int mfma_lock = 0;
+  hipEvent_t mfma_ev = nullptr;
+
   ~ccmm_chains() {
+    if (mfma_ev) {
+      PhaseLock& L = phase_lock(ctx->device, mfma_lock);
+      std::lock_guard<std::mutex> g(L.m);
+      if (L.last == mfma_ev) L.last = nullptr;
+      (void)hipEventDestroy(mfma_ev);
+    }
     for (auto& e : pending) {
       evpool.push_back(e.a);
       evpool.push_back(e.b);
@@ -873,7 +907,7 @@ struct ccmm_chains {
   void run_astep_big(const RngArgs& ra) {
     bigW.alloc((size_t)d.B * d.N * d.TP);
     ChainState cs = view();
-    launch(KID_ASTEP, [&] {
+    launch(KID_ASTEPBIG, [&] {
       HIPCHECK(bign_launch_astep(ctx->stream, d, Tslot.p, cs, ra, cfg.logy2offset, bigW.p));
     });
   }
@@ -884,7 +918,7 @@ struct ccmm_chains {
       hipLaunchKernelGGL(k_sv_mix, dim3((d.N * d.TP + 255) / 256, d.B), dim3(256), 0, ctx->stream,
                          d, Tslot.p, cs, ra);
     });
-    launch(KID_SVSAMPLE, [&] {
+    launch(KID_SVBIG, [&] {
       HIPCHECK(bign_launch_sv(ctx->stream, d, Tslot.p, V0inv.p, V0invm.p, cs, ra, bigScr.p));
     });
   }
@@ -896,7 +930,7 @@ struct ccmm_chains {
       hipLaunchKernelGGL(k_phi_gen, dim3((d.N * (d.TP + cfg.dPHI) + 255) / 256, d.B), dim3(256), 0,
                          ctx->stream, d, Tslot.p, cfg.dPHI, cs, ra);
     });
-    launch(KID_PHI, [&] {
+    launch(KID_PHIBIG, [&] {
       HIPCHECK(bign_launch_phi(ctx->stream, d, Tslot.p, cfg.dPHI, sPHI.p, cs, bigScr.p));
     });
   }
@@ -907,6 +941,14 @@ struct ccmm_chains {
   void run_cta_big(const RngArgs& ra, const ChainState& cs) {
     Ubuf.alloc((size_t)d.B * d.N * d.TP);
     Dinv.alloc((size_t)d.nmat * d.KP * 64);
+    std::unique_lock<std::mutex> lk;
+    PhaseLock* L = nullptr;
+    if (mfma_lock > 0) {
+      L = &phase_lock(ctx->device, mfma_lock);
+      lk = std::unique_lock<std::mutex>(L->m);
+      if (L->last) HIPCHECK(hipStreamWaitEvent(ctx->stream, L->last, 0));
+      if (!mfma_ev) HIPCHECK(hipEventCreateWithFlags(&mfma_ev, hipEventDisableTiming));
+    }
     launch(KID_WEIGHTS, [&] {
       hipLaunchKernelGGL(k_cta_weights, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0,
                          ctx->stream, d, Tslot.p, cs, 0);
@@ -919,6 +961,11 @@ struct ccmm_chains {
       HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
                               nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 2 & big_mask));
     });
+    if (L) {
+      HIPCHECK(hipEventRecord(mfma_ev, ctx->stream));
+      L->last = mfma_ev;
+      lk.unlock();
+    }
     launch(KID_SOLVEBIG, [&] {
       HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
                               nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 4 & big_mask));
@@ -1654,6 +1701,15 @@ int ccmm_chains_set_slots(ccmm_chains* ch, const int* slot_of_chain) {
     require(ch && slot_of_chain, "null argument");
     HIPCHECK(hipSetDevice(ch->ctx->device));
     ch->set_slots(slot_of_chain);
+    return 0;
+  });
+}
+
+int ccmm_chains_set_mfma_lock(ccmm_chains* ch, int id) {
+  return guarded([&] {
+    require(ch != nullptr && id >= 0, "bad argument");
+    require(ch->mfma_ev == nullptr || id == ch->mfma_lock, "MFMA lock id already set");
+    ch->mfma_lock = id;
     return 0;
   });
 }

@@ -20,6 +20,8 @@
 // block with readlane broadcasts, all threads update), blocked triangular solves.
 #include "ccmm_bign.h"
 
+#include <cstdlib>
+
 namespace ccmm {
 
 constexpr int kNL = 129;   // LDS row stride of an N x N matrix (odd: spreads banks)
@@ -379,14 +381,172 @@ __global__ __launch_bounds__(1024) void k_phi_big(Dims d, const int* __restrict_
   if (bad && tid == 0) atomicOr(&cs.status[c], 16);
 }
 
+// ================================================================ Cholesky + inverse (LDS)
+// S (n x n lower, ld kNL, n <= 128) <- L^{-1} for S = L L': blocked right-looking Cholesky
+// with 16-wide panels, the inverse built row block by row block as the panels complete.
+//   panel i (rows p0 .. p0+15):
+//     wave 0: factor the diagonal block, invert it (Dv_i) and store Dv_i over it
+//     all:    L(r, panel) = S(r, panel) Dv_i' for the rows below;
+//             T = L(block i, 0:p0) Linv(0:p0, 0:p0)                   (2 x 2 tiles, Tb)
+//     all:    trailing update;  Linv(block i, 0:p0) = -Dv_i T
+// Only the lower triangle is read or written.  Tb: LDS scratch, kCB x 128 doubles.
+constexpr int kCB = 16;
+
+template <int NT>
+__device__ void wg_chol_inv(double* S, int n, double* Tb, int* bad) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int p0 = 0; p0 < n; p0 += kCB) {
+    const int pw = min(kCB, n - p0);
+    if (wave == 0) {
+      double row[kCB], dv[kCB];
+#pragma unroll
+      for (int m = 0; m < kCB; ++m) row[m] = (lane < pw && m <= lane) ? S[(p0 + lane) * kNL + p0 + m] : 0.0;
+#pragma unroll
+      for (int kk = 0; kk < kCB; ++kk) {
+        if (kk < pw) {
+          double dkk = readlane_d(row[kk], kk);
+          if (!(dkk > 0.0)) {
+            *bad = 1;
+            dkk = 1.0;
+          }
+          const double piv = sqrt(dkk), ip = 1.0 / piv;
+          if (lane == kk) row[kk] = piv;
+          if (lane > kk) row[kk] *= ip;
+          const double lik = row[kk];
+#pragma unroll
+          for (int m = kk + 1; m < kCB; ++m) {
+            const double lmk = readlane_d(lik, m);
+            if (lane >= m) row[m] = fma(-lik, lmk, row[m]);
+          }
+        }
+      }
+      // Dv = L_b^{-1}, lane r holding row r: right-looking over the rows k of L_b
+#pragma unroll
+      for (int c = 0; c < kCB; ++c) dv[c] = (lane == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < kCB; ++k) {
+        if (k < pw) {
+          const double lkk = readlane_d(row[k], k);
+          if (lane == k) {
+            const double il = 1.0 / lkk;
+#pragma unroll
+            for (int c = 0; c <= k; ++c) dv[c] *= il;
+          }
+          const double lrk = row[k];
+#pragma unroll
+          for (int c = 0; c <= k; ++c) {
+            const double dkc = readlane_d(dv[c], k);
+            if (lane > k) dv[c] = fma(-lrk, dkc, dv[c]);
+          }
+        }
+      }
+      if (lane < pw)
+#pragma unroll
+        for (int m = 0; m < kCB; ++m)
+          if (m <= lane) S[(p0 + lane) * kNL + p0 + m] = dv[m];
+    }
+    __syncthreads();
+    const double* Dv = S + p0 * kNL + p0;  // Dv(r, q) = Dv[r * kNL + q], q <= r
+    // (a) panel rows below: L(r, p0 + m) = sum_{q <= m} S(r, p0 + q) Dv(m, q)
+    for (int r = p0 + pw + tid; r < n; r += NT) {
+      double x[kCB];
+#pragma unroll
+      for (int q = 0; q < kCB; ++q) x[q] = (q < pw) ? S[r * kNL + p0 + q] : 0.0;
+#pragma unroll
+      for (int m = 0; m < kCB; ++m) {
+        if (m < pw) {
+          double sacc = 0.0;
+#pragma unroll
+          for (int q = 0; q <= m; ++q) sacc = fma(x[q], Dv[m * kNL + q], sacc);
+          S[r * kNL + p0 + m] = sacc;
+        }
+      }
+    }
+    // (b) T(r, j) = sum_{k = j}^{p0-1} L(p0 + r, k) Linv(k, j), 2 x 2 tiles over (r, j)
+    const int tr = (pw + 1) / 2, tc = p0 / 2;
+    for (int e = tid; e < tr * tc; e += NT) {
+      const int r0 = 2 * (e / tc), j0 = 2 * (e % tc);
+      const int ra = p0 + r0, rb = p0 + min(r0 + 1, pw - 1);
+      double t00 = 0.0, t01 = 0.0, t10 = 0.0, t11 = 0.0;
+      {  // k = j0: Linv(j0, j0 + 1) = 0
+        const double la = S[ra * kNL + j0], lb = S[rb * kNL + j0], v0 = S[j0 * kNL + j0];
+        t00 = la * v0;
+        t10 = lb * v0;
+      }
+      for (int k = j0 + 1; k < p0; ++k) {
+        const double la = S[ra * kNL + k], lb = S[rb * kNL + k];
+        const double v0 = S[k * kNL + j0], v1 = S[k * kNL + j0 + 1];
+        t00 = fma(la, v0, t00);
+        t01 = fma(la, v1, t01);
+        t10 = fma(lb, v0, t10);
+        t11 = fma(lb, v1, t11);
+      }
+      Tb[r0 * 128 + j0] = t00;
+      Tb[r0 * 128 + j0 + 1] = t01;
+      if (r0 + 1 < pw) {
+        Tb[(r0 + 1) * 128 + j0] = t10;
+        Tb[(r0 + 1) * 128 + j0 + 1] = t11;
+      }
+    }
+    __syncthreads();
+    // (c) trailing update, 4 x 4 tiles: S(i, j) -= L(i, panel) . L(j, panel)
+    const int r0 = p0 + pw, nr = n - r0;
+    const int mt = (nr + 3) / 4, ntile = mt * (mt + 1) / 2;
+    for (int tile = tid; tile < ntile; tile += NT) {
+      int ti = 0, tj = tile;
+      while (tj > ti) {
+        tj -= ti + 1;
+        ++ti;
+      }
+      const int a0 = r0 + 4 * ti, b0 = r0 + 4 * tj;
+      double acc[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.0;
+      for (int m = 0; m < pw; ++m) {
+        double la[4], lb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          la[i] = S[min(a0 + i, n - 1) * kNL + p0 + m];
+          lb[i] = S[min(b0 + i, n - 1) * kNL + p0 + m];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) acc[i * 4 + jj] = fma(la[i], lb[jj], acc[i * 4 + jj]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (a0 + i < n && b0 + jj <= a0 + i) S[(a0 + i) * kNL + b0 + jj] -= acc[i * 4 + jj];
+    }
+    // (d) Linv(p0 + r, j) = -sum_{q <= r} Dv(r, q) T(q, j), j < p0
+    for (int e = tid; e < pw * p0; e += NT) {
+      const int r = e / p0, j = e - r * p0;
+      double v = 0.0;
+      for (int q = 0; q <= r; ++q) v = fma(Dv[r * kNL + q], Tb[q * 128 + j], v);
+      S[(p0 + r) * kNL + j] = -v;
+    }
+    __syncthreads();
+  }
+}
+
 // ================================================================ SV (time-ordered sampler)
-// Per chain (1024 threads).  scratch per chain: Q (N x N), Lt (T+1 blocks N x N: L_t),
-// Mt (T+1 blocks: M_t = L_{t-1}^{-1} Q), w (T+1 x N); all row-major with ld N.
-__global__ __launch_bounds__(1024) void k_sv_big(Dims d, const int* __restrict__ Tslot,
-                                                 const double* __restrict__ V0inv,
-                                                 const double* __restrict__ V0invm, ChainState cs,
-                                                 RngArgs ra, double* __restrict__ scr, size_t scr_stride) {
+// Per chain (kSvNT threads).  scratch per chain (row-major, ld N): Q = PHI^{-1}; Lt[t] =
+// L_t^{-1}; Mt[t] = M_t = L_{t-1}^{-1} Q; w[t].  Per block t:
+//   M_t = Linv_{t-1} Q (GEMM, Linv_{t-1} in LDS)   -> G = M_t' M_t (Gram, into LDS)
+//   S = D_t - G, r = b_t + M_t' w_{t-1}             -> Linv_t = chol(S)^{-1} (wg_chol_inv)
+//   w_t = Linv_t r
+// backward: x_t = Linv_t' (w_t + z_t + M_{t+1} x_{t+1}).
+constexpr int kSvNT = 512;
+
+__global__ __launch_bounds__(kSvNT) void k_sv_big(Dims d, const int* __restrict__ Tslot,
+                                                  const double* __restrict__ V0inv,
+                                                  const double* __restrict__ V0invm, ChainState cs,
+                                                  RngArgs ra, double* __restrict__ scr, size_t scr_stride,
+                                                  int skip) {
   extern __shared__ double sm[];
+  constexpr int NT = kSvNT;
   const int c = blockIdx.x;
   const int s = cs.slot[c];
   const int N = d.N, TP = d.TP;
@@ -395,20 +555,22 @@ __global__ __launch_bounds__(1024) void k_sv_big(Dims d, const int* __restrict__
   const Rng rng = ra.make(c);
   const size_t NN = (size_t)N * N;
   double* Q = scr + (size_t)c * scr_stride;
-  double* Lt = Q + NN;                        // (T+1) x NN
+  double* Lt = Q + NN;                        // (T+1) x NN: Linv_t
   double* Mt = Lt + (size_t)(TP + 1) * NN;    // (T+1) x NN
   double* wv = Mt + (size_t)(TP + 1) * NN;    // (T+1) x N
   double* S = sm;                             // N x N, ld kNL
-  double* vec = sm + 128 * kNL;               // N
-  double* vec2 = vec + 128;                   // N
+  double* Tb = sm + N * kNL;                  // kCB x 128
+  double* vec = Tb + kCB * 128;               // 128
+  double* vec2 = vec + 128;                   // 128
   const double* obs = cs.svobs + (size_t)c * N * TP;
   const double* irv = cs.svir + (size_t)c * N * TP;
   int bad = 0;
+  const int gj = tid >> 3, gq = tid & 7;  // 8-lane group per row / column gj (64 groups)
   // Q = PHI^{-1} = sqrtPHI^{-T} sqrtPHI^{-1}: invert sqrtPHI (lower) column-wise into Lt[0]
   {
     const double* sq = cs.sqrtPHI + (size_t)c * NN;  // column-major lower
     double* Li = Lt;                                 // scratch: Li(r, col) at r * N + col
-    for (int col = tid; col < N; col += 1024)
+    for (int col = tid; col < N; col += NT)
       for (int r = 0; r < N; ++r) {
         double v = (r == col) ? 1.0 : 0.0;
         if (r > col)
@@ -416,7 +578,7 @@ __global__ __launch_bounds__(1024) void k_sv_big(Dims d, const int* __restrict__
         Li[r * N + col] = (r >= col) ? v / sq[r + r * N] : 0.0;
       }
     __syncthreads();
-    for (int e = tid; e < N * N; e += 1024) {
+    for (int e = tid; e < N * N; e += NT) {
       const int a = e / N, b = e - a * N;
       double v = 0.0;
       for (int r = max(a, b); r < N; ++r) v = fma(Li[r * N + a], Li[r * N + b], v);
@@ -424,58 +586,46 @@ __global__ __launch_bounds__(1024) void k_sv_big(Dims d, const int* __restrict__
     }
     __syncthreads();
   }
-  // ---- forward: t = 0 .. T.  Entering step t (t >= 1) the LDS matrix holds L_{t-1}.
-  const int gj = tid >> 3, gq = tid & 7;  // lane group of 8 per column / row gj
-  const bool gact = gj < N;
+  const double* V0 = V0inv + (size_t)s * NN;
+  const int nt4 = (N + 3) / 4;
+  // ---- forward: t = 0 .. T.  Entering step t >= 1 the LDS matrix holds Linv_{t-1}.
   for (int t = 0; t <= T; ++t) {
-    double* Lcur = Lt + (size_t)t * NN;
     double* Mcur = Mt + (size_t)t * NN;
     if (t > 0) {
-      // M_t = L_{t-1}^{-1} Q, left-looking by rows i; 8 lanes per column j, lane gq owns
-      // rows gq + 8m (registers y[m]), partial sums joined over the group.  Q(i, j) reaches
-      // the owner lane through qcur (row block of i), prefetched one block ahead in qnxt.
-      double y[16];
+      if (!(skip & 1)) {
+        // M_t = Linv_{t-1} Q, 4 x 4 tiles (Linv lower: k <= row)
+        for (int tile = tid; tile < nt4 * nt4; tile += NT) {
+          const int i0 = 4 * (tile / nt4), j0 = 4 * (tile % nt4);
+          double acc[16];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) y[m] = 0.0;
-      double qcur = (gact && gq < N) ? Q[gq * N + gj] : 0.0;
-      double qnxt = (gact && gq + 8 < N) ? Q[(gq + 8) * N + gj] : 0.0;
-      for (int i = 0; i < N; ++i) {
-        if (i > 0 && (i & 7) == 0) {
-          qcur = qnxt;
-          const int k = i + 8 + gq;
-          qnxt = (gact && k < N) ? Q[k * N + gj] : 0.0;
-        }
-        double sacc = 0.0;
+          for (int e = 0; e < 16; ++e) acc[e] = 0.0;
+          const int kend = min(i0 + 4, N);
+          for (int k = 0; k < kend; ++k) {
+            double a[4], b[4];
 #pragma unroll
-        for (int m = 0; m < 16; ++m)
-          if (8 * m < i) {
-            const int k = gq + 8 * m;
-            const double l = (k < i) ? S[i * kNL + k] : 0.0;
-            sacc = fma(l, y[m], sacc);
+            for (int r = 0; r < 4; ++r) {
+              const int i = min(i0 + r, N - 1);
+              a[r] = (k <= i0 + r) ? S[i * kNL + k] : 0.0;
+              b[r] = Q[k * N + min(j0 + r, N - 1)];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int cc = 0; cc < 4; ++cc) acc[r * 4 + cc] = fma(a[r], b[cc], acc[r * 4 + cc]);
           }
-        sacc += dpp_d<0xB1>(sacc);
-        sacc += dpp_d<0x4E>(sacc);
-        sacc += dpp_d<0x141>(sacc);
-        const double yi = (qcur - sacc) / S[i * kNL + i];
-        if (gq == (i & 7)) {
-          const int mi = i >> 3;
 #pragma unroll
-          for (int m = 0; m < 16; ++m) y[m] = (m == mi) ? yi : y[m];
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc)
+              if (i0 + r < N && j0 + cc < N) Mcur[(i0 + r) * N + j0 + cc] = acc[r * 4 + cc];
         }
       }
-      if (gact)
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-          const int k = gq + 8 * m;
-          if (k < N) Mcur[k * N + gj] = y[m];
-        }
       __syncthreads();
-      // M_t' M_t into the LDS matrix (L_{t-1} is kept in global Lt[t-1])
-      wg_gram<1024>(S, Mcur, 1, N, N, N, nullptr, 0);
+      // G = M_t' M_t into the LDS matrix (Linv_{t-1} is kept in global Lt[t-1])
+      if (!(skip & 2)) wg_gram<NT>(S, Mcur, 1, N, N, N, nullptr, 0);
     }
-    // S = D_t - M_t' M_t, D_0 = V0inv + Q, D_t = 2Q + diag(ir_t) (t < T), D_T = Q + diag(ir_T)
-    const double* V0 = V0inv + (size_t)s * NN;
-    for (int e = tid; e < N * N; e += 1024) {
+    // S = D_t - G, D_0 = V0inv + Q, D_t = 2Q + diag(ir_t) (t < T), D_T = Q + diag(ir_T)
+    for (int e = tid; e < N * N; e += NT) {
       const int a = e / N, b = e - a * N;
       if (b > a) continue;
       double v;
@@ -490,54 +640,78 @@ __global__ __launch_bounds__(1024) void k_sv_big(Dims d, const int* __restrict__
     }
     // rhs: b_0 = V0inv h0mean; b_t = obs_t ir_t + M_t' w_{t-1} (8 lanes per entry)
     if (t == 0) {
-      for (int a = tid; a < N; a += 1024) vec[a] = V0invm[(size_t)s * N + a];
+      for (int a = tid; a < N; a += NT) vec[a] = V0invm[(size_t)s * N + a];
     } else {
       const double* wp = wv + (size_t)(t - 1) * N;
+      for (int a0 = 0; a0 < N; a0 += NT / 8) {
+        const int a = a0 + gj;
+        double v = 0.0;
+        if (a < N)
+          for (int i = gq; i < N; i += 8) v = fma(Mcur[i * N + a], wp[i], v);
+        v += dpp_d<0xB1>(v);
+        v += dpp_d<0x4E>(v);
+        v += dpp_d<0x141>(v);
+        if (a < N && gq == 0) vec[a] = v + obs[(size_t)a * TP + t - 1] * irv[(size_t)a * TP + t - 1];
+      }
+    }
+    __syncthreads();
+    if (!(skip & 4)) wg_chol_inv<NT>(S, N, Tb, &bad);
+    // w_t = Linv_t r (8 lanes per row), Linv_t -> global
+    double* Lcur = Lt + (size_t)t * NN;
+    for (int a0 = 0; a0 < N; a0 += NT / 8) {
+      const int a = a0 + gj;
       double v = 0.0;
-      if (gact)
-        for (int i = gq; i < N; i += 8) v = fma(Mcur[i * N + gj], wp[i], v);
+      if (a < N && !(skip & 8))
+        for (int k = gq; k <= a; k += 8) v = fma(S[a * kNL + k], vec[k], v);
       v += dpp_d<0xB1>(v);
       v += dpp_d<0x4E>(v);
       v += dpp_d<0x141>(v);
-      if (gact && gq == 0) vec[gj] = v + obs[(size_t)gj * TP + t - 1] * irv[(size_t)gj * TP + t - 1];
+      if (a < N && gq == 0) wv[(size_t)t * N + a] = v;
     }
-    __syncthreads();
-    wg_chol<1024>(S, N, &bad);
-    if (tid < 64) wave_trsv_lower(S, kNL, vec, N);
-    __syncthreads();
-    for (int e = tid; e < N * N; e += 1024) Lcur[e] = S[(e / N) * kNL + e % N];
-    for (int a = tid; a < N; a += 1024) wv[(size_t)t * N + a] = vec[a];
+    if (!(skip & 32))
+      for (int e = tid; e < N * N; e += NT) {
+        const int a = e / N, b = e - a * N;
+        Lcur[e] = (b <= a) ? S[a * kNL + b] : 0.0;
+      }
     __syncthreads();
   }
-  // ---- backward: x_T = L_T^{-T}(w_T + z_T); x_t = L_t^{-T}(w_t + z_t + M_{t+1} x_{t+1})
+  // ---- backward: x_T = Linv_T'(w_T + z_T); x_t = Linv_t'(w_t + z_t + M_{t+1} x_{t+1})
   double* hout = cs.h + (size_t)c * N * TP;
   double* eta = cs.eta + (size_t)c * N * TP;
   double* sqh = cs.sqrtht + (size_t)c * N * TP;
-  for (int t = T; t >= 0; --t) {
-    // L_t to LDS (L_T is still there)
-    if (t < T)
-      for (int e = tid; e < N * N; e += 1024) S[(e / N) * kNL + e % N] = Lt[(size_t)t * NN + e];
-    double v = 0.0;
-    if (t < T && gact) {
-      const double* Mn = Mt + (size_t)(t + 1) * NN;
-      for (int j = gq; j < N; j += 8) v = fma(Mn[gj * N + j], vec2[j], v);
+  for (int t = (skip & 16) ? -1 : T; t >= 0; --t) {
+    // v = w_t + z_t + M_{t+1} x_{t+1}  (x_{t+1} in vec2)
+    const double* Mn = Mt + (size_t)(t + 1) * NN;
+    for (int a0 = 0; a0 < N; a0 += NT / 8) {
+      const int a = a0 + gj;
+      double v = 0.0;
+      if (a < N && t < T)
+        for (int j = gq; j < N; j += 8) v = fma(Mn[a * N + j], vec2[j], v);
+      v += dpp_d<0xB1>(v);
+      v += dpp_d<0x4E>(v);
+      v += dpp_d<0x141>(v);
+      if (a < N && gq == 0)
+        vec[a] = v + wv[(size_t)t * N + a] + rng.normal(CCMM_RNG_SVZ, (uint32_t)(a + N * t));
     }
-    v += dpp_d<0xB1>(v);
-    v += dpp_d<0x4E>(v);
-    v += dpp_d<0x141>(v);
-    if (gact && gq == 0) vec[gj] = v + wv[(size_t)t * N + gj] + rng.normal(CCMM_RNG_SVZ, (uint32_t)(gj + N * t));
     __syncthreads();
-    if (tid < 64) wave_trsv_lower_t(S, kNL, vec, N);
-    __syncthreads();
-    // vec = x_t; vec2 = x_{t+1}
-    for (int a = tid; a < N; a += 1024) {
-      const double x = vec[a];
-      if (t >= 1) {
-        hout[(size_t)a * TP + t - 1] = x;
-        sqh[(size_t)a * TP + t - 1] = exp(0.5 * x);
+    // x_t(a) = sum_{i >= a} Linv_t(i, a) v(i)
+    const double* Li = Lt + (size_t)t * NN;
+    for (int a0 = 0; a0 < N; a0 += NT / 8) {
+      const int a = a0 + gj;
+      double x = 0.0;
+      if (a < N)
+        for (int i = a + gq; i < N; i += 8) x = fma(Li[i * N + a], vec[i], x);
+      x += dpp_d<0xB1>(x);
+      x += dpp_d<0x4E>(x);
+      x += dpp_d<0x141>(x);
+      if (a < N && gq == 0) {
+        if (t >= 1) {
+          hout[(size_t)a * TP + t - 1] = x;
+          sqh[(size_t)a * TP + t - 1] = exp(0.5 * x);
+        }
+        if (t < T) eta[(size_t)a * TP + t] = vec2[a] - x;  // shock of period t+1: h_{t+1} - h_t
+        vec2[a] = x;  // every other read of vec2 precedes the barrier above
       }
-      if (t < T) eta[(size_t)a * TP + t] = vec2[a] - x;  // shock of period t+1: h_{t+1} - h_t
-      vec2[a] = x;
     }
     __syncthreads();
   }
@@ -575,12 +749,15 @@ hipError_t bign_launch_phi(hipStream_t st, const Dims& d, const int* Tslot, int 
 
 hipError_t bign_launch_sv(hipStream_t st, const Dims& d, const int* Tslot, const double* V0inv,
                           const double* V0invm, ChainState cs, RngArgs ra, double* scr) {
-  const size_t lds = (size_t)(128 * kNL + 256) * sizeof(double);
+  const size_t lds = (size_t)(d.N * kNL + kCB * 128 + 256) * sizeof(double);
   hipError_t e = hipFuncSetAttribute((const void*)k_sv_big, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_sv_big, dim3(d.B), dim3(1024), lds, st, d, Tslot, V0inv, V0invm, cs, ra, scr,
-                     bign_sv_scratch(d));
+  // CCMM_SV_SKIP: timing ablation of k_sv_big phases (1 M_t, 2 M_t'M_t, 4 Cholesky + inverse,
+  // 8 forward product, 16 backward pass, 32 Linv_t store); results are wrong when set
+  static const int skip = std::getenv("CCMM_SV_SKIP") ? std::atoi(std::getenv("CCMM_SV_SKIP")) : 0;
+  hipLaunchKernelGGL(k_sv_big, dim3(d.B), dim3(kSvNT), lds, st, d, Tslot, V0inv, V0invm, cs, ra, scr,
+                     bign_sv_scratch(d), skip);
   return hipGetLastError();
 }
 

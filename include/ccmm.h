@@ -171,6 +171,12 @@ int ccmm_chains_set_state(ccmm_chains* ch, const double* PAI, const double* A,
  * the chain index).  A batch driver keys chains by their global (vintage, chain) unit so
  * draws do not depend on how units are sharded over GPUs or packed into chain sets. */
 int ccmm_chains_set_rng_ids(ccmm_chains* ch, const uint32_t* ids);
+/* Opt-in MFMA phase lock (id > 0; 0 = none).  Chain sets on one device given the same id
+ * serialise the MFMA Gram + Cholesky phase of their coefficient block (large-system path,
+ * K > 512 or N > 32) through a cross-stream event.  Groups of chains driven on separate
+ * contexts then fall out of step, and the per-chain sequential blocks of one group (CTA
+ * solve, SV recursion, ELB Gibbs) overlap another group's MFMA phase.  Draws are unchanged. */
+int ccmm_chains_set_mfma_lock(ccmm_chains* ch, int id);
 /* Per-chain status word since set_state (B ints, OR of: 2 CTA Cholesky, 4 A-step
  * Cholesky, 8 SV sampler, 16 PHI Cholesky found a non-positive pivot; the block
  * then continued with a unit pivot, so the chain's draws are invalid).  Returns 1 if any
