@@ -73,6 +73,10 @@ _SIGS = {
     "ccmm_chains_get_draws": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
     "ccmm_chains_set_rng_ids": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "ccmm_chains_set_mfma_lock": (C.c_int, [C.c_void_p, C.c_int]),
+    "ccmm_gibbs_shadowrates": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), _dp, _dp, _dp,
+                                         _dp, _dp, _dp, C.c_double, C.c_int, C.c_int, _dp, _dp,
+                                         C.POINTER(C.c_uint8)]),
     "ccmm_chains_get_status": (C.c_int, [C.c_void_p, _ip]),
     "ccmm_chains_set_fcst": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, C.c_int]),
     "ccmm_chains_set_fcst_slot": (C.c_int, [C.c_void_p, C.c_int, _dp]),
@@ -215,6 +219,31 @@ class Context:
                                   _ptr(hT), _ptr(h0), _ptr(sh), kai.ctypes.data_as(_i8p))
         _check(rc, "ccmm_sv_ksc")
         return hT, h0, sh, kai
+
+    def gibbs_shadowrates(self, Y, STATE0, YHAT0, ndxS, sNaN, p, C, Psi, SVol, elbBound,
+                          burnin=100, u=None, Ndraws=1, flags=False):
+        """gibbsdrawShadowrates (ccmm_gibbs_shadowrates), batched over a trailing chain axis.
+
+        Y Ny x elbT [x B], STATE0 K [x B], YHAT0 Ny x elbT [x B] or None, ndxS bool Ny,
+        sNaN bool Ns x elbT, C K x K [x B], Psi K x Ny [x B], SVol Ny x elbT [x B],
+        u Ns x elbT x (burnin + Ndraws) [x B] or None.  Returns draws Ns x elbT x Ndraws x B
+        (and the drawTruncNormal branch flags Ns x elbT x passes x B when flags=True)."""
+        Y = _f(Y)
+        Ny, T = Y.shape[:2]
+        B = Y.shape[2] if Y.ndim == 3 else 1
+        nd = np.ascontiguousarray(np.asarray(ndxS, dtype=bool), dtype=np.uint8)
+        sN = np.asfortranarray(np.asarray(sNaN, dtype=bool).astype(np.uint8))
+        Ns = int(sN.shape[0])
+        passes = burnin + Ndraws
+        out = np.zeros((Ns, T, Ndraws, B), order="F")
+        fl = np.zeros((Ns, T, passes, B), dtype=np.uint8, order="F") if flags else None
+        rc = self.lib.ccmm_gibbs_shadowrates(
+            self.handle, B, Ny, T, Ns, int(p), _ptr(nd, _u8p), _ptr(sN, _u8p), _ptr(Y),
+            _ptr(_f(STATE0)), _ptr(_f(YHAT0)) if YHAT0 is not None else None, _ptr(_f(C)),
+            _ptr(_f(Psi)), _ptr(_f(SVol)), float(elbBound), int(Ndraws), int(burnin),
+            _ptr(_f(u)) if u is not None else None, _ptr(out), _ptr(fl, _u8p) if flags else None)
+        _check(rc, "ccmm_gibbs_shadowrates")
+        return (out, fl) if flags else out
 
     def phi_iw(self, eta, sPHI, dPHI, Zdraw=None):
         eta = _f(eta)

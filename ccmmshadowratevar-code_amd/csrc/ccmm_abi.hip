@@ -8,6 +8,8 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <atomic>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -568,6 +570,8 @@ struct ccmm_chains {
     HIPCHECK(hipMemset(eScur.p, 0, eScur.n * sizeof(double)));
   }
 
+  const double* elb_yhat = nullptr;  // ccmm_gibbs_shadowrates: explicit YHAT0
+  uint8_t* elb_flags = nullptr;      // ccmm_gibbs_shadowrates: drawTruncNormal branch flags
   ElbDev elb_view() const {
     ElbDev e{};
     e.Ns = cfg.Ns;
@@ -593,6 +597,8 @@ struct ccmm_chains {
     e.kshadow = cfg.N * cfg.p + 1;
     e.K = cfg.K;
     e.mode = elb_mode;
+    e.yhat = elb_yhat;
+    e.flags = elb_flags;
     return e;
   }
 
@@ -1022,7 +1028,7 @@ struct ccmm_chains {
     svLd.alloc((size_t)d.B * (d.TP + 1) * NN * NN);
     svw.alloc((size_t)d.B * (d.TP + 1) * NN);
     svSep.alloc((size_t)d.B * sv_sep_len(d.N));
-    svG.alloc((size_t)d.B * (d.TP + 1) * NN);
+    svG.alloc((size_t)2 * d.B * (d.TP + 1) * NN);  // fill vectors g | SV normals z
   }
 
   void run_sv(const RngArgs& ra) {
@@ -1228,9 +1234,120 @@ struct ccmm_chains {
     ++fstored;
   }
 
+  // ---------------------------------------------------------------- QR fallback
+  // CTA.m:80-92: a chain whose coefficient block met a non-positive Cholesky pivot
+  // (status bit 2) is redrawn on the host (host_cta_chain: Cholesky, or the Householder QR
+  // of Kailath's array where it fails) from the same previous draw and normals; status
+  // bit 2 is then replaced by bit 1 ("QR fallback used", informational).  CCMM_FORCE_QR=1
+  // routes every chain through the host QR branch (tests); CCMM_NO_QR_FALLBACK=1 disables.
+  bool qr_fallback = std::getenv("CCMM_NO_QR_FALLBACK") == nullptr;
+  bool force_qr = std::getenv("CCMM_FORCE_QR") != nullptr;
+  DBuf<double> paiPrev, zHost;
+  int64_t qr_count = 0;
+
+  void snapshot_pai() {
+    if (!qr_fallback) return;
+    paiPrev.alloc(PAI.n);
+    HIPCHECK(hipMemcpyAsync(paiPrev.p, PAI.p, PAI.n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+  }
+
+  // returns the chains redrawn
+  int cta_fallback(const RngArgs& ra) {
+    if (!qr_fallback) return 0;
+    const int B = d.B, N = d.N, K = d.K, KP = d.KP, TP = d.TP;
+    std::vector<int> st(B);
+    HIPCHECK(hipMemcpyAsync(st.data(), status.p, B * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    std::vector<int> bad;
+    for (int c = 0; c < B; ++c)
+      if (force_qr || (st[c] & 2)) bad.push_back(c);
+    if (bad.empty()) return 0;
+    auto dl = [&](const auto* src, size_t n, auto& dst) {
+      dst.resize(n);
+      HIPCHECK(hipMemcpy(dst.data(), src, n * sizeof(dst[0]), hipMemcpyDeviceToHost));
+    };
+    std::vector<int> hslot, hT, hxi, hyi;
+    dl(slot.p, (size_t)B, hslot);
+    dl(Tslot.p, (size_t)cfg.ndata, hT);
+    dl(xidx.p, (size_t)B * N, hxi);
+    dl(yidx.p, (size_t)B, hyi);
+    zHost.alloc((size_t)K * N);
+    // inputs of every flagged chain to the host, the redraws in parallel, PAI back
+    struct Job {
+      int c, T, fl = 0;
+      std::vector<double> Y, A, sh, ivd, ivb, pai, z;
+      std::vector<std::vector<double>> X;
+      std::vector<const double*> Xs;
+    };
+    std::vector<Job> jobs(bad.size());
+    for (size_t q = 0; q < bad.size(); ++q) {
+      Job& jb = jobs[q];
+      const int c = bad[q], s = hslot[c];
+      jb.c = c;
+      jb.T = hT[s];
+      dl(Ypool.p + (size_t)hyi[c] * N * TP, (size_t)N * TP, jb.Y);
+      dl(A.p + (size_t)c * N * N, (size_t)N * N, jb.A);
+      dl(sqrtht.p + (size_t)c * N * TP, (size_t)N * TP, jb.sh);
+      dl(iVdiag.p + (size_t)s * N * KP, (size_t)N * KP, jb.ivd);
+      dl(iVb.p + (size_t)s * N * KP, (size_t)N * KP, jb.ivb);
+      dl(paiPrev.p + (size_t)c * N * KP, (size_t)N * KP, jb.pai);
+      hipLaunchKernelGGL(k_rng_normals, dim3((K * N + 255) / 256), dim3(256), 0, ctx->stream, ra, c,
+                         (int)CCMM_RNG_PAI, K * N, zHost.p);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipStreamSynchronize(ctx->stream));
+      dl(zHost.p, (size_t)K * N, jb.z);
+      jb.X.assign(N, {});
+      jb.Xs.assign(N, nullptr);
+      for (int j = 0; j < N; ++j) {
+        int first = j;  // equations sharing a slab share the download
+        for (int r = 0; r < j; ++r)
+          if (hxi[(size_t)c * N + r] == hxi[(size_t)c * N + j]) {
+            first = r;
+            break;
+          }
+        if (first == j) dl(Xpool.p + (size_t)hxi[(size_t)c * N + j] * KP * TP, (size_t)KP * TP, jb.X[j]);
+      }
+      for (int j = 0; j < N; ++j) {
+        int first = j;
+        for (int r = 0; r < j; ++r)
+          if (hxi[(size_t)c * N + r] == hxi[(size_t)c * N + j]) {
+            first = r;
+            break;
+          }
+        jb.Xs[j] = jb.X[first].data();
+      }
+    }
+    {
+      std::atomic<size_t> next{0};
+      auto work = [&] {
+        for (size_t q; (q = next++) < jobs.size();) {
+          Job& jb = jobs[q];
+          jb.fl = host_cta_chain(N, K, jb.T, jb.Y.data(), TP, jb.Xs.data(), TP, jb.A.data(), jb.sh.data(), TP,
+                                 jb.ivd.data(), jb.ivb.data(), KP, jb.pai.data(), jb.z.data(), force_qr);
+        }
+      };
+      const unsigned nth = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
+      std::vector<std::thread> th;
+      for (unsigned i = 1; i < std::min<size_t>(nth, jobs.size()); ++i) th.emplace_back(work);
+      work();
+      for (auto& t : th) t.join();
+    }
+    for (Job& jb : jobs) {
+      HIPCHECK(hipMemcpy(PAI.p + (size_t)jb.c * N * KP, jb.pai.data(), (size_t)N * KP * sizeof(double),
+                         hipMemcpyHostToDevice));
+      st[jb.c] = (st[jb.c] & ~2) | ((jb.fl & 1) ? 1 : 0) | ((jb.fl & 2) ? 2 : 0);
+      qr_count += (jb.fl & 1) ? 1 : 0;
+    }
+    HIPCHECK(hipMemcpy(status.p, st.data(), B * sizeof(int), hipMemcpyHostToDevice));
+    run_resid();  // RESID of the redrawn coefficients for the A-step
+    return (int)bad.size();
+  }
+
   void sweep_once(const double* dcrn, int64_t stride, bool store) {
     const RngArgs ra = rng_args(dcrn, stride);
+    snapshot_pai();
     run_cta(ra);
+    cta_fallback(ra);
     run_astep(ra);
     run_sv(ra);
     run_phi(ra);
@@ -1244,7 +1361,7 @@ struct ccmm_chains {
     std::vector<int> st(d.B);
     HIPCHECK(hipMemcpy(st.data(), status.p, d.B * sizeof(int), hipMemcpyDeviceToHost));
     int any = 0;
-    for (int v : st) any |= v;
+    for (int v : st) any |= v & ~1;  // bit 1: QR fallback used (not an error)
     if (any) {
       HIPCHECK(hipMemset(status.p, 0, d.B * sizeof(int)));
       g_err = "non positive-definite matrix in a Gibbs block (status bits " + std::to_string(any) + ")";
@@ -1355,19 +1472,25 @@ int ccmm_cta(ccmm_ctx* ctx, int B, int T, int N, int K, const double* Y, int y_p
     }
     RngArgs ra = ch.rng_args(dz.p, (int64_t)K * N);
     ra.off[CCMM_RNG_PAI] = 0;
+    ch.snapshot_pai();
     ch.run_cta(ra);
+    ch.cta_fallback(ra);  // CTA.m:80-92 for the chains whose Cholesky failed
     HIPCHECK(hipStreamSynchronize(ctx->stream));
     ch.download_KN(ch.PAI.p, B, PAI);
     std::vector<int> st(B);
     HIPCHECK(hipMemcpy(st.data(), ch.status.p, B * sizeof(int), hipMemcpyDeviceToHost));
     int any = 0;
     for (int c = 0; c < B; ++c) {
-      if (status) status[c] = st[c];
+      if (status) status[c] = st[c] & 1;
       any |= st[c];
     }
-    if (any) {
-      g_err = "posterior precision not positive definite (QR fallback not available on device)";
+    if (any & ~1) {
+      g_err = "posterior precision singular: QR fallback failed";
       return CCMM_ERR_NOTSPD;
+    }
+    if (any & 1) {
+      g_err = "switching to QR routine";  // CTA.m:82
+      return CCMM_WARN_QR_FALLBACK;
     }
     return 0;
   });
@@ -1650,6 +1773,126 @@ int ccmm_draw_trunc_normal_batch(ccmm_ctx* ctx, int n, const double* mu, const d
 }
 
 // ------------------------------------------------------------ sweep-level API
+int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p, const uint8_t* ndxS,
+                           const uint8_t* sNaN, const double* Y, const double* STATE0,
+                           const double* YHAT0, const double* C, const double* Psi, const double* SVol,
+                           double elbBound, int Ndraws, int burnin, const double* u, double* out,
+                           uint8_t* flags) {
+  return guarded([&] {
+    require(ctx && ndxS && sNaN && Y && STATE0 && C && Psi && SVol && out, "null argument");
+    require(B >= 1 && Ny >= 1 && Ny <= 128 && p >= 1 && elbT >= 1 && burnin >= 0, "bad size");
+    require(Ndraws == 1, "Ndraws must be 1 (the value used at mcmcVARshadowrateBlockHybrid.m:436)");
+    std::vector<int> nd;
+    for (int i = 0; i < Ny; ++i)
+      if (ndxS[i]) nd.push_back(i);
+    if ((int)nd.size() != Ns) {  // gibbsdrawShadowrates.m:50-52
+      g_err = "dimension mismatch";
+      return CCMM_ERR_DIM;
+    }
+    require(Ns >= 1 && Ns <= 4, "Ns must be in [1, 4]");
+    HIPCHECK(hipSetDevice(ctx->device));
+    const int K = Ny * p + 1, T = elbT, passes = burnin + Ndraws;
+    ccmm_chain_config cf{};
+    cf.model = CCMM_MODEL_BLOCKHYBRID;
+    cf.B = B;
+    cf.N = Ny;
+    cf.p = p;
+    cf.T = T;
+    cf.K = K;
+    cf.ndata = B;  // one data slot per chain: its own Y window and STATE0
+    cf.dPHI = Ny + 1;
+    cf.logy2offset = 1e-3;
+    cf.Ns = Ns;
+    cf.elbTmax = T;
+    cf.elb_gibbsburn = burnin;
+    cf.elb = elbBound;
+    cf.rng_crn = u ? 1 : 0;
+    cf.seed = 0;
+    ccmm_chains ch;
+    ch.init(ctx, cf, 2 * B, 2 * B);
+    const size_t KK = (size_t)K * K;
+    std::vector<double> Xc((size_t)T * K, 0.0), Yc((size_t)T * Ny), ivd((size_t)K * Ny, 1.0),
+        ivb((size_t)K * Ny, 0.0), sP((size_t)Ny * Ny, 0.0), h0m(Ny, 0.0), h0v((size_t)Ny * Ny, 0.0);
+    for (int i = 0; i < Ny; ++i) sP[i + (size_t)i * Ny] = h0v[i + (size_t)i * Ny] = 1.0;
+    std::vector<int> sl(B);
+    for (int c = 0; c < B; ++c) {
+      // X row 1 = STATE0 (elb.X0 = X(elbT0+1,:)', mcmcVARshadowrateBlockHybrid.m:417), Y = the window
+      for (int k = 0; k < K; ++k) Xc[(size_t)k * T] = STATE0[(size_t)c * K + k];
+      for (int t = 0; t < T; ++t)
+        for (int i = 0; i < Ny; ++i) Yc[t + (size_t)i * T] = Y[((size_t)c * T + t) * Ny + i];
+      ch.set_T(c, T);
+      ch.upload_X(c, T, Xc.data());
+      ch.upload_TN(ch.Ypool.p + (size_t)c * ch.d.N * ch.d.TP, 1, T, Yc.data(), 0.0);
+      ch.set_slot_prior(c, ivd.data(), ivb.data(), sP.data(), h0m.data(), h0v.data());
+      ch.have_slot[c] = true;
+      sl[c] = c;
+    }
+    ch.set_slots(sl.data());
+    std::vector<uint8_t> none(Ny, 0);
+    ch.set_elb_model(nd.data(), none.data());
+    for (int c = 0; c < B; ++c) ch.set_elb_slot(c, 0, sNaN);
+    // state: PAI = C(2:Ny+1, :)' (elb.A rows, :404-407), A = Psi(2:Ny+1, :) \ I, sqrtht = SVol'
+    std::vector<double> PAI((size_t)K * Ny * B), A((size_t)Ny * Ny * B, 0.0), sh((size_t)T * Ny * B),
+        hh((size_t)T * Ny * B), sq((size_t)Ny * Ny * B, 0.0);
+    for (int c = 0; c < B; ++c) {
+      const double* Cc = C + (size_t)c * KK;
+      const double* Pc = Psi + (size_t)c * K * Ny;
+      for (int i = 0; i < Ny; ++i)
+        for (int k = 0; k < K; ++k) PAI[((size_t)c * Ny + i) * K + k] = Cc[(1 + i) + (size_t)k * K];
+      double* Ac = A.data() + (size_t)c * Ny * Ny;
+      for (int col = 0; col < Ny; ++col)  // forward substitution with the lower triangle of invA
+        for (int r = col; r < Ny; ++r) {
+          double v = (r == col) ? 1.0 : 0.0;
+          for (int q = col; q < r; ++q) v -= Pc[(1 + r) + (size_t)q * K] * Ac[q + (size_t)col * Ny];
+          Ac[r + (size_t)col * Ny] = v / Pc[(1 + r) + (size_t)r * K];
+        }
+      for (int i = 0; i < Ny; ++i) {
+        sq[(size_t)c * Ny * Ny + i + (size_t)i * Ny] = 1.0;
+        for (int t = 0; t < T; ++t) {
+          const double v = SVol[((size_t)c * T + t) * Ny + i];
+          sh[((size_t)c * Ny + i) * T + t] = v;
+          hh[((size_t)c * Ny + i) * T + t] = 2.0 * std::log(v);
+        }
+      }
+    }
+    ch.upload_KN(ch.PAI.p, B, PAI.data(), 0.0);
+    HIPCHECK(hipMemcpy(ch.A.p, A.data(), A.size() * sizeof(double), hipMemcpyHostToDevice));
+    ch.upload_TN(ch.sqrtht.p, B, T, sh.data(), 1.0);
+    ch.upload_TN(ch.h.p, B, T, hh.data(), 0.0);
+    HIPCHECK(hipMemcpy(ch.sqrtPHI.p, sq.data(), sq.size() * sizeof(double), hipMemcpyHostToDevice));
+    ch.have_elb_model = true;
+    ch.reset_chain_slabs();
+    // YHAT0 (Ny x elbT per chain, or zeros) -> [B][elbT][Ny]
+    DBuf<double> dyh;
+    dyh.alloc((size_t)B * T * Ny);
+    {
+      std::vector<double> yh((size_t)B * T * Ny, 0.0);
+      if (YHAT0) std::memcpy(yh.data(), YHAT0, yh.size() * sizeof(double));
+      HIPCHECK(hipMemcpy(dyh.p, yh.data(), yh.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    ch.elb_yhat = dyh.p;
+    DBuf<uint8_t> dfl;
+    if (flags) {
+      dfl.alloc((size_t)B * passes * T * Ns);
+      HIPCHECK(hipMemset(dfl.p, 0, dfl.n));
+      ch.elb_flags = dfl.p;
+    }
+    DBuf<double> du;
+    RngArgs ra = ch.rng_args(nullptr, 0);
+    if (u) {  // rand(Ns, elbT, burnin + Ndraws) per chain (gibbsdrawShadowrates.m:173)
+      du.alloc((size_t)B * Ns * T * passes);
+      HIPCHECK(hipMemcpy(du.p, u, du.n * sizeof(double), hipMemcpyHostToDevice));
+      ra = ch.rng_args(du.p, (int64_t)Ns * T * passes);
+      ra.off[CCMM_RNG_ELB] = 0;
+    }
+    ch.run_elb(ra);
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    HIPCHECK(hipMemcpy(out, ch.eScur.p, (size_t)B * Ns * T * sizeof(double), hipMemcpyDeviceToHost));
+    if (flags) HIPCHECK(hipMemcpy(flags, dfl.p, dfl.n, hipMemcpyDeviceToHost));
+    return 0;
+  });
+}
+
 ccmm_chains* ccmm_chains_create(ccmm_ctx* ctx, const ccmm_chain_config* cfg) {
   ccmm_chains* ch = nullptr;
   int rc = guarded([&] {
@@ -1737,7 +1980,7 @@ int ccmm_chains_get_status(ccmm_chains* ch, int* status) {
     HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
     HIPCHECK(hipMemcpy(status, ch->status.p, ch->cfg.B * sizeof(int), hipMemcpyDeviceToHost));
     int any = 0;
-    for (int c = 0; c < ch->cfg.B; ++c) any |= status[c];
+    for (int c = 0; c < ch->cfg.B; ++c) any |= status[c] & ~1;  // bit 1: QR fallback used
     return any ? 1 : 0;
   });
 }

@@ -49,6 +49,8 @@ struct ElbDev {
   int condStride;
   int kshadow, K;  // hybrid model: PAI rows kshadow..K-1 load the actual-rate lags (K > kshadow)
   int mode;        // CCMM_ELB_MODE timing ablation (0 in production)
+  const double* yhat;  // [B][elbTmax][N] explicit YHAT0 (ccmm_gibbs_shadowrates) or nullptr
+  uint8_t* flags;      // [B][passes][elbTmax][Ns] truncated-normal branch flags or nullptr
 };
 
 // condition record per censored month (doubles):
@@ -103,15 +105,19 @@ __global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, Cha
   for (int q = tid; q < T * N; q += 256) {
     const int t = q / N, i = q % N;
     double yh = 0.0;
-    // hybrid: Yhatactual = Xffrlags(elbT0+t, :) * PAIactual (mcmcVARhybridGibbs.m:429-431)
-    for (int k = e.kshadow; k < e.K; ++k) yh = fma(Xa[(size_t)k * TP + T0 + t], PAI[(size_t)i * KP + k], yh);
-    // block hybrid: Yhatactual from the actual-rate block's shadow-rate lags (:400-403)
-    if (e.actual[i])
-      for (int l = 0; l < p; ++l)
-        for (int si = 0; si < Ns; ++si) {
-          const int k = 1 + l * N + e.ndxS[si];
-          yh = fma(Xa[(size_t)k * TP + T0 + t], PAI[(size_t)i * KP + k], yh);
-        }
+    if (e.yhat) {  // gibbsdrawShadowrates' YHAT0 argument (ccmm_gibbs_shadowrates)
+      yh = e.yhat[((size_t)c * e.elbTmax + t) * N + i];
+    } else {
+      // hybrid: Yhatactual = Xffrlags(elbT0+t, :) * PAIactual (mcmcVARhybridGibbs.m:429-431)
+      for (int k = e.kshadow; k < e.K; ++k) yh = fma(Xa[(size_t)k * TP + T0 + t], PAI[(size_t)i * KP + k], yh);
+      // block hybrid: Yhatactual from the actual-rate block's shadow-rate lags (:400-403)
+      if (e.actual[i])
+        for (int l = 0; l < p; ++l)
+          for (int si = 0; si < Ns; ++si) {
+            const int k = 1 + l * N + e.ndxS[si];
+            yh = fma(Xa[(size_t)k * TP + T0 + t], PAI[(size_t)i * KP + k], yh);
+          }
+    }
     double yb = Yc[(size_t)i * TP + T0 + t];
     for (int si = 0; si < Ns; ++si)
       if (e.ndxS[si] == i && sN[t * Ns + si]) yb = 0.0;
@@ -363,6 +369,16 @@ __device__ __forceinline__ double elb_trunc_normal(double mu, double sig, double
   return mu;
 }
 
+// branch flags of drawTruncNormal.m: bit 0 sigma > tol (:31), bit 1 PHIbar > eps (:44)
+__device__ __forceinline__ uint8_t elb_trunc_flags(double mu, double sig, double elb) {
+  const double tol = 1e-10;
+  const double eps = 2.220446049250313080847e-16;
+  sig = fabs(sig);
+  if (!(sig > tol)) return 0;
+  const double PHIbar = 0.5 * erfc(-0.70710678118654752440 * ((elb - mu) / sig));
+  return (uint8_t)(1 | ((PHIbar > eps) ? 2 : 0));
+}
+
 // ---------------------------------------------------------------- Gibbs passes (per chain)
 // One wave per chain.  Each lane owns neighbour columns lane and lane + 64 of every
 // month's record and prefetches the next month's while the current one is drawn;
@@ -452,6 +468,8 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
           ++y;
         }
         cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a]);
+        if (e.flags && lane == 0)  // drawTruncNormal.m branch taken (oracle.draw_trunc_normal flags)
+          e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = elb_trunc_flags(mu, so[a], e.elb);
       }
       for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
       for (int q = 0; q < kHd; ++q) hd[q] = hdn[q];

@@ -188,4 +188,9 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
   return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
 }
 
+// host CTA draw of one chain with the QR branch of CTA.m:80-92 (ccmm_host_cta.cpp)
+int host_cta_chain(int N, int K, int T, const double* Y, int ldy, const double* const* Xs, int ldx,
+                   const double* A, const double* sqrtht, int ldh, const double* iVdiag,
+                   const double* iVb, int ldk, double* PAI, const double* z, bool force_qr);
+
 }  // namespace ccmm

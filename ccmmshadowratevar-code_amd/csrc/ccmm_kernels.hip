@@ -775,6 +775,15 @@ __global__ void k_truncnorm(int n, const double* mu, const double* sig, double e
 
 // ============================================================== diagnostics
 // MFMA f64 layout self-test: D = A(16x4) * B(4x16) with the lane maps used above.
+// normals of one chain's RNG block (CRN page or Philox), out[q] = normal(block, q): the
+// host QR fallback of the coefficient block replays the chain's randn(K, N) (CTA.m:58)
+__global__ void k_rng_normals(RngArgs ra, int c, int block, int n, double* __restrict__ out) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  const Rng rng = ra.make(c);
+  out[q] = rng.normal(block, (uint32_t)q);
+}
+
 __global__ void k_mfma_selftest(const double* A, const double* B, double* D) {
   const int l = threadIdx.x;
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};

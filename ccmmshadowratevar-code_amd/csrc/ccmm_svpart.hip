@@ -131,7 +131,7 @@ __device__ __forceinline__ double sv_bwd(double r, const double (&lc)[NN], const
   return r;
 }
 
-template <int NN, int NW>
+template <int NN, int NW, bool PACK>
 __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restrict__ Tslot,
                                                       const double* __restrict__ V0inv,
                                                       const double* __restrict__ V0invm, ChainState cs,
@@ -164,6 +164,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   double* Wg = cs.svw + (size_t)c * (TP + 1) * NN;
   double* rec = sepbuf + (size_t)c * (kSvMaxSeg - 1) * R::LEN;
   double* Gb = gbuf + (size_t)c * (TP + 1) * NN;
+  double* Zg = gbuf + (size_t)(d.B + c) * (TP + 1) * NN;  // the chain's SV normals, block-major
   double* hout = cs.h + (size_t)c * n * TP;
   double* eta = cs.eta + (size_t)c * n * TP;
   double* sqh = cs.sqrtht + (size_t)c * n * TP;
@@ -226,18 +227,23 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
     if (t == 0) return real ? V0m[ln] : 0.0;
     return real ? obt * irt : 0.0;
   };
+  // the normals z_t (block t, row ln) are drawn by all waves at the start of phase C
+  // (independent work off the serial block loops) and read back from Zg
   auto zdraw = [&](int t) __attribute__((always_inline)) -> double {
-    return real ? rng.normal(CCMM_RNG_SVZ, (uint32_t)(ln + n * t)) : 0.0;
+    if (mode & 32) return 0.0;  // timing ablation only
+    return real ? Zg[(size_t)t * NN + ln] : 0.0;
   };
-  // C_t row (lane < NN) -> LDS and HBM, diagonal as its reciprocal
+  // C_t row (lane < NN) -> LDS, and its lower triangle packed by rows to HBM
+  // (Ct[i (i + 1) / 2 + m], m <= i), the diagonal as its reciprocal
   auto store_factor = [&](int t, const double (&sr)[NN], const double (&rps)[NN], double w)
                           __attribute__((always_inline)) {
     double* Ct = Cg + (size_t)t * NN2;
     if (lane < NN) {
+      const int rb = PACK ? (ln * (ln + 1)) / 2 : ln * NN;
 #pragma unroll
       for (int m = 0; m < NN; ++m) {
         myC[lane * CLD + m] = sr[m];
-        Ct[lane * NN + m] = sr[m];
+        if (!PACK || m <= ln) Ct[rb + m] = sr[m];
       }
       myw[lane] = w;
       Wg[(size_t)t * NN + lane] = w;
@@ -434,14 +440,57 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   __syncthreads();
 
   // ---------------------------------------------------------------- phase C: back substitution
+  for (int e = tid; e < (T + 1) * n; e += 64 * NW) {
+    const int t = e / n, i = e - t * n;
+    Zg[(size_t)t * NN + i] = rng.normal(CCMM_RNG_SVZ, (uint32_t)(i + n * t));
+  }
+  __syncthreads();
   double qrow[NN];
 #pragma unroll
   for (int m = 0; m < NN; ++m) qrow[m] = Ql[ln * NN + m];
   // C_t -> LDS (whole wave), then row / column / reciprocal diagonal per lane
+  auto unpack_at = [&](int e) __attribute__((always_inline)) -> int {  // packed e -> row*CLD + col
+    if (!PACK) return (e / NN) * CLD + (e % NN);
+    int r = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+    r += ((r + 1) * (r + 2)) / 2 <= e ? 1 : 0;
+    r -= (r * (r + 1)) / 2 > e ? 1 : 0;
+    return r * CLD + (e - (r * (r + 1)) / 2);
+  };
+  constexpr int NP = PACK ? NN * (NN + 1) / 2 : NN * NN;
   auto load_factor = [&](int t, double (&lr)[NN], double (&lc)[NN], double (&rps)[NN])
                          __attribute__((always_inline)) {
     const double* Ct = Cg + (size_t)t * NN2;
-    for (int e = lane; e < NN2; e += 64) myC[(e / NN) * CLD + (e % NN)] = Ct[e];
+    for (int e = lane; e < NP; e += 64) myC[unpack_at(e)] = Ct[e];
+    sv_wave_sync();
+#pragma unroll
+    for (int m = 0; m < NN; ++m) {
+      lr[m] = myC[ln * CLD + m];
+      lc[m] = myC[m * CLD + ln];
+      rps[m] = myC[m * CLD + m];
+    }
+    sv_wave_sync();
+  };
+  // software-pipelined form (NN <= 20): the next block's factor is fetched into registers
+  // (kPF per lane) while the current block's substitutions run, so the serial block loops
+  // of phase C no longer wait a full HBM latency per block
+  constexpr bool kPipe = NN <= 20;
+  constexpr int kPF = kPipe ? (NP + 63) / 64 : 1;
+  int upk[kPF];  // unpacked LDS offsets of this lane's packed entries
+#pragma unroll
+  for (int i = 0; i < kPF; ++i) upk[i] = unpack_at(min(lane + 64 * i, NP - 1));
+  auto fetch_factor = [&](int t, double (&pf)[kPF]) __attribute__((always_inline)) {
+    const double* Ct = Cg + (size_t)t * NN2;
+#pragma unroll
+    for (int i = 0; i < kPF; ++i) {
+      const int e = lane + 64 * i;
+      pf[i] = (e < NP) ? __builtin_nontemporal_load(Ct + e) : 0.0;
+    }
+  };
+  auto commit_factor = [&](const double (&pf)[kPF], double (&lr)[NN], double (&lc)[NN], double (&rps)[NN])
+                           __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < kPF; ++i)
+      if (lane + 64 * i < NP) myC[upk[i]] = pf[i];
     sv_wave_sync();
 #pragma unroll
     for (int m = 0; m < NN; ++m) {
@@ -482,11 +531,18 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
       double g = 0.0;
 #pragma unroll
       for (int m = 0; m < NN; ++m) g = fma(-qrow[m], xsep[(q - 1) * NN + m], g);
+      double pf[kPF];
+      if (kPipe && first < last) fetch_factor(first, pf);
       for (int t = first; t <= last; ++t) {
         if (lane < NN) Gb[(size_t)t * NN + lane] = g;
         if (t < last) {
           double lr[NN], lc[NN], rps[NN];
-          load_factor(t, lr, lc, rps);
+          if constexpr (kPipe) {
+            commit_factor(pf, lr, lc, rps);
+            if (t + 1 < last) fetch_factor(t + 1, pf);
+          } else {
+            load_factor(t, lr, lc, rps);
+          }
           double v = sv_fwd<NN>(g, lr, rps, lane);
           v = sv_bwd<NN>(v, lc, rps, lane);
           if (lane < NN) myw[lane] = v;
@@ -501,9 +557,16 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
     // successor of `last`: the right separator (x known) or nothing (t == T)
     if (hasR && lane < NN) myw[lane] = xsep[q * NN + lane];
     sv_wave_sync();
+    double pfb[kPF];
+    if (kPipe) fetch_factor(last, pfb);
     for (int t = last; t >= first; --t) {
       double lr[NN], lc[NN], rps[NN];
-      load_factor(t, lr, lc, rps);
+      if constexpr (kPipe) {
+        commit_factor(pfb, lr, lc, rps);
+        if (t > first) fetch_factor(t - 1, pfb);
+      } else {
+        load_factor(t, lr, lc, rps);
+      }
       double acc = 0.0, xn = 0.0;
       if (t < T) {
 #pragma unroll
@@ -512,8 +575,13 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
       }
       if (hasL && lane < NN) acc += Gb[(size_t)t * NN + ln];
       double rv = (lane < NN) ? Wg[(size_t)t * NN + ln] + zdraw(t) : 0.0;
-      rv -= sv_fwd<NN>(acc, lr, rps, lane);
-      const double x = sv_bwd<NN>(rv, lc, rps, lane);
+      double x;
+      if (mode & 64) {  // timing ablation only
+        x = rv - acc;
+      } else {
+        rv -= sv_fwd<NN>(acc, lr, rps, lane);
+        x = sv_bwd<NN>(rv, lc, rps, lane);
+      }
       if (real) {
         if (t >= 1) {
           hout[(size_t)ln * TP + t - 1] = x;
@@ -537,18 +605,28 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   if (bad && lane == 0) atomicOr(&cs.status[c], 8);
 }
 
-template <int NN, int NW>
-static hipError_t sv_launch_one(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
+template <int NN, int NW, bool PACK>
+static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
                                 const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
                                 int mode) {
   constexpr int CLD = NN + 1, XLD = 2 * NN + 1;
   const size_t lds = (size_t)(2 * NN * NN + kSvMaxSeg * NN + NW * sv_wave_lds(NN)) * sizeof(double);
-  hipError_t e = hipFuncSetAttribute((const void*)k_sv_part<NN, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)lds);
+  hipError_t e = hipFuncSetAttribute((const void*)k_sv_part<NN, NW, PACK>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_sv_part<NN, NW>), dim3(d.B), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm, cs, ra,
-                     sep, gbuf, mode);
+  hipLaunchKernelGGL((k_sv_part<NN, NW, PACK>), dim3(d.B), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm, cs,
+                     ra, sep, gbuf, mode);
   return hipGetLastError();
+}
+
+// block factors stored as packed lower triangles (PACK) or full rows; mode bit 128 picks the
+// full-row layout (timing comparison)
+template <int NN, int NW>
+static hipError_t sv_launch_one(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
+                                const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
+                                int mode) {
+  if (mode & 128) return sv_launch_one_<NN, NW, false>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+  return sv_launch_one_<NN, NW, true>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
 }
 
 hipError_t sv_launch_part(int N, hipStream_t st, Dims d, const int* Tslot, const double* V0inv,

@@ -548,7 +548,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
         res, failed = {}, []
         for k, i in enumerate(vidx):
             cs = slice(k * C, (k + 1) * C)
-            if np.any(status[cs] != 0):
+            if np.any(status[cs] & ~1):  # bit 1: CTA QR fallback used (valid draws)
                 failed.append(i)
                 continue
             thisT, bm, yr = units[i]

@@ -90,7 +90,11 @@ int ccmm_synchronize(ccmm_ctx* ctx);
  *   PAI    K x N x B   in: previous draw (columns j+1..N used by CTAsys); out: new draw
  *   z      K x N x B   randn(K,N) of CTA.m:58, or NULL (Philox, block CCMM_RNG_PAI, sweep 0)
  *   status B           per-chain status (0 ok, 1 QR fallback used), may be NULL
- * Supports 1 <= N <= 64, K <= 1536. */
+ * A chain whose posterior precision fails the device Cholesky is redrawn on the host by
+ * the QR branch of CTA.m:80-92 (Householder QR of Kailath's array; same previous draw and
+ * normals); the call then returns CCMM_WARN_QR_FALLBACK.  CCMM_ERR_NOTSPD only when the
+ * QR factor itself is singular.
+ * Supports 1 <= N <= 128, K <= 1536. */
 int ccmm_cta(ccmm_ctx* ctx, int B, int T, int N, int K,
              const double* Y, int y_per_chain,
              const double* X, int nx, int x_per_chain,
@@ -121,6 +125,27 @@ int ccmm_sv_ksc(ccmm_ctx* ctx, int B, int T, int N, const double* logy2T, const 
  *   sqrtPHI out N x N x B (lower Cholesky of PHI_), PHI out N x N x B */
 int ccmm_phi_iw(ccmm_ctx* ctx, int B, int T, int N, const double* eta, const double* sPHI,
                 int dPHI, const double* Zdraw, double* sqrtPHI, double* PHI);
+
+/* Gibbs draw of the ELB-censored shadow rates given the VAR state space, batched over B
+ * independent calls.  Replaces gibbsdrawShadowrates.m:1-245 (called at
+ * mcmcVARshadowrateBlockHybrid.m:436,462,494 and mcmcVARhybridGibbs.m:481,513).
+ *   ndxS   Ny (logical)            sNaN  Ns x elbT (logical; censored cells)
+ *   Y      Ny x elbT x B           the window, previous shadow values in censored cells
+ *   STATE0 K x B (K = Ny p + 1)    YHAT0 Ny x elbT x B or NULL (zeros)
+ *   C      K x K x B  (elb.A)      Psi   K x Ny x B (elb.B: invA in rows 2..Ny+1)
+ *   SVol   Ny x elbT x B           u     Ns x elbT x (burnin + Ndraws) x B uniforms
+ *                                        (rand(rndStream, Ns, elbT, .), :173) or NULL (Philox)
+ *   out    Ns x elbT x Ndraws x B  flags Ns x elbT x (burnin + Ndraws) x B (drawTruncNormal
+ *                                        branches, as ccmm_draw_trunc_normal) or NULL
+ * Ndraws must be 1 (the reference's only use).  Evaluated in the stable residual form of the
+ * device ELB step (ccmm_elb.hip): the same conditional moments as the QR formulation of
+ * gibbsdrawShadowrates.m:74-145 in exact arithmetic.  CCMM_ERR_DIM: sum(ndxS) != Ns
+ * (gibbsdrawShadowrates.m:50-52). */
+int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p, const uint8_t* ndxS,
+                           const uint8_t* sNaN, const double* Y, const double* STATE0,
+                           const double* YHAT0, const double* C, const double* Psi, const double* SVol,
+                           double elbBound, int Ndraws, int burnin, const double* u, double* out,
+                           uint8_t* flags);
 
 /* One draw from N(mu, sig^2) truncated to (-inf, elb] by inverse CDF
  * (drawTruncNormal.m:31-86) with a pre-drawn uniform u (the numeric-stream
@@ -179,9 +204,11 @@ int ccmm_chains_set_rng_ids(ccmm_chains* ch, const uint32_t* ids);
 int ccmm_chains_set_mfma_lock(ccmm_chains* ch, int id);
 /* Per-chain status word since set_state (B ints, OR of: 2 CTA Cholesky, 4 A-step
  * Cholesky, 8 SV sampler, 16 PHI Cholesky found a non-positive pivot; the block
- * then continued with a unit pivot, so the chain's draws are invalid).  Returns 1 if any
- * chain is flagged, 0 otherwise; the batch driver re-runs flagged units
- * (goVARshadowrateBlockHybrid.m:287-310). */
+ * then continued with a unit pivot, so the chain's draws are invalid).  A CTA Cholesky
+ * failure is repaired within the sweep by the host QR branch of CTA.m:80-92, which
+ * replaces bit 2 by bit 1 ("QR fallback used", informational: the draws are valid).
+ * Returns 1 if any chain carries a bit other than 1, 0 otherwise; the batch driver re-runs
+ * flagged units (goVARshadowrateBlockHybrid.m:287-310). */
 int ccmm_chains_get_status(ccmm_chains* ch, int* status);
 /* Any output pointer may be NULL.  invA, PHI, RESID are those of the last sweep. */
 int ccmm_chains_get_state(ccmm_chains* ch, double* PAI, double* A, double* invA, double* sqrtht,

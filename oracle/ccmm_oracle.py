@@ -216,12 +216,15 @@ def draw_crn(rng, N, K, T, dPHI):
 # --------------------------------------------------------------------------
 # CTA / CTAsys (CTA.m:57-98; CTAsys.m:57-108)
 # --------------------------------------------------------------------------
-def _cta_post(Xj, Yj, iVd, iVbj, zj, K):
-    """Posterior moments and draw for one equation (CTA.m:72-96)."""
+def _cta_post(Xj, Yj, iVd, iVbj, zj, K, force_qr=False):
+    """Posterior moments and draw for one equation (CTA.m:72-96).  force_qr: take the QR
+    branch (CTA.m:80-92) as if chol had failed (test hook for the device fallback)."""
     Ik = np.eye(K)
     iVpost = np.diag(iVd) + Xj.T @ Xj
     status = 0
     try:
+        if force_qr:
+            raise np.linalg.LinAlgError("forced")
         L = np.linalg.cholesky(iVpost)
         Vchol = solve_triangular(L, Ik, lower=True).T  # (iVchol_post \ Ik)'
     except np.linalg.LinAlgError:  # Kailath fast-array QR fallback (CTA.m:80-92)
@@ -235,7 +238,7 @@ def _cta_post(Xj, Yj, iVd, iVbj, zj, K):
     return b + Vchol @ zj, status, np.sqrt(np.diag(Vpost))
 
 
-def cta(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z, return_sd=False):
+def cta(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z, return_sd=False, force_qr=False):
     """CTA.m:57-98 as written (kron-materialised X_j, explicit inverse).
     return_sd: also return the posterior sd of each coefficient (K x N), the
     scale of the parity metric |delta| / max(|x|, sd_post)."""
@@ -247,14 +250,14 @@ def cta(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z, return_sd=False):
         lam = sqrtht[:, j:].ravel(order="F")
         Yj = ((Y - X @ PAI) @ A[j:, :].T).ravel(order="F") / lam
         Xj = np.kron(A[j:, j][:, None], X) / lam[:, None]
-        PAI[:, j], s, sd[:, j] = _cta_post(Xj, Yj, iVdiag[:, j], iVb[:, j], z[:, j], K)
+        PAI[:, j], s, sd[:, j] = _cta_post(Xj, Yj, iVdiag[:, j], iVb[:, j], z[:, j], K, force_qr)
         status |= s
     if return_sd:
         return PAI, status, sd
     return PAI, status
 
 
-def cta_sys(Y, XX, N, K, T, A, sqrtht, iVdiag, iVb, PAI, z, return_sd=False):
+def cta_sys(Y, XX, N, K, T, A, sqrtht, iVdiag, iVb, PAI, z, return_sd=False, force_qr=False):
     """CTAsys.m:57-108 as written; XX is T x K x N (one design per equation)."""
     PAI = np.array(PAI, dtype=float, copy=True)
     sd = np.zeros((K, N))
@@ -266,7 +269,7 @@ def cta_sys(Y, XX, N, K, T, A, sqrtht, iVdiag, iVb, PAI, z, return_sd=False):
         lam = sqrtht[:, j:].ravel(order="F")
         Yj = ((Y - XPAI) @ A[j:, :].T).ravel(order="F") / lam
         Xj = np.kron(A[j:, j][:, None], XX[:, :, j]) / lam[:, None]
-        PAI[:, j], s, sd[:, j] = _cta_post(Xj, Yj, iVdiag[:, j], iVb[:, j], z[:, j], K)
+        PAI[:, j], s, sd[:, j] = _cta_post(Xj, Yj, iVdiag[:, j], iVb[:, j], z[:, j], K, force_qr)
         status |= s
     if return_sd:
         return PAI, status, sd
@@ -539,12 +542,16 @@ def vech_lower(M):
 # --------------------------------------------------------------------------
 # One linear BVAR-SV sweep (mcmcVAR.m:211-274)
 # --------------------------------------------------------------------------
-def linear_sweep(st, su: Setup, crn, cta_form="kron"):
-    """cta_form: "kron" = CTA.m as written; "syrk" = the algorithmic form (cta_syrk)."""
+def linear_sweep(st, su: Setup, crn, cta_form="kron", force_qr=False):
+    """cta_form: "kron" = CTA.m as written; "syrk" = the algorithmic form (cta_syrk).
+    force_qr: every equation takes CTA.m's QR branch (kron form only)."""
     N, K, T = su.N, su.K, su.T
-    f = cta if cta_form == "kron" else cta_syrk
-    PAI, status = f(su.Y, su.X, N, K, st["A"], st["sqrtht"], su.iVdiag, su.iVb, st["PAI"],
-                    crn["zPAI"])
+    if cta_form == "kron":
+        PAI, status = cta(su.Y, su.X, N, K, st["A"], st["sqrtht"], su.iVdiag, su.iVb, st["PAI"],
+                          crn["zPAI"], force_qr=force_qr)
+    else:
+        PAI, status = cta_syrk(su.Y, su.X, N, K, st["A"], st["sqrtht"], su.iVdiag, su.iVb,
+                               st["PAI"], crn["zPAI"])
     RESID = su.Y - su.X @ PAI
     A, invA = a_step(RESID, st["sqrtht"], crn["zA"])
     logy2 = np.log((RESID @ A.T) ** 2 + su.logy2offset)
