@@ -202,6 +202,18 @@ def main():
                            "traffic": None if traffic is None else int(traffic),
                            "traffic_source": pmc_src if traffic is not None else None,
                            "flop_per_launch": int(flop), "avg_launch_ms": round(kms, 4)}
+        pk = pmc.get(kname, {})
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in pk:
+            # counter evidence (separate rocprofv3 --pmc pass over this workload, tools/pmc_summary.py):
+            # MFMA pipe busy fraction over the kernel and the F64 MFMA flop the hardware executed
+            # (algorithmic flop above excludes the padded diagonal tiles and the inverse)
+            out["roofline"]["counters"] = {
+                "mfma_busy_frac": round(pk.get("mfma_busy_frac", 0.0), 4),
+                "mfma_f64_flop_per_launch": int(pk.get("mfma_f64_flop", 0.0)),
+                "SQ_VALU_MFMA_BUSY_CYCLES": int(pk["SQ_VALU_MFMA_BUSY_CYCLES"]),
+                "SQ_INSTS_VALU_MFMA_MOPS_F64": int(pk.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0)),
+                "GRBM_GUI_ACTIVE": int(pk.get("GRBM_GUI_ACTIVE", 0)),
+                "source": pmc_src}
         # streamed (HBM-roofline) kernels: algorithmic bytes per launch / launch time
         # (B_SV = 33*T*N bytes per chain-sweep for the SV block)
         hb = {}

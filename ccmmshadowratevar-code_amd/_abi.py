@@ -73,6 +73,9 @@ _SIGS = {
     "ccmm_chains_get_draws": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
     "ccmm_chains_set_rng_ids": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "ccmm_chains_set_mfma_lock": (C.c_int, [C.c_void_p, C.c_int]),
+    "ccmm_chains_get_kai": (C.c_int, [C.c_void_p, _i8p]),
+    "ccmm_chains_record_elb_flags": (C.c_int, [C.c_void_p, C.c_int]),
+    "ccmm_chains_get_elb_flags": (C.c_int, [C.c_void_p, _u8p]),
     "ccmm_gibbs_shadowrates": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), _dp, _dp, _dp,
                                          _dp, _dp, _dp, C.c_double, C.c_int, C.c_int, _dp, _dp,
@@ -336,7 +339,7 @@ class Chains:
         self.cfg = ChainConfig(model, N, p, K, T, B, ndata, N + 3 if dPHI is None else dPHI,
                                int(crn), store_capacity, logy2offset, seed, Ns, elbTmax,
                                elb_gibbsburn, elb)
-        self.model, self.Ns, self.elbTmax = model, Ns, elbTmax
+        self.model, self.Ns, self.elbTmax, self.elb_gibbsburn = model, Ns, elbTmax, elb_gibbsburn
         h = self.lib.ccmm_chains_create(ctx.handle, C.byref(self.cfg))
         if not h:
             raise RuntimeError(f"ccmm_chains_create failed: {last_error()}")
@@ -396,6 +399,24 @@ class Chains:
         s = np.ascontiguousarray(slots, dtype=np.int32)
         _check(self.lib.ccmm_chains_set_slots(self.handle, s.ctypes.data_as(_ip)),
                "ccmm_chains_set_slots")
+
+    def get_kai(self):
+        """KSC indicators of the last SV block, T x N x B int8."""
+        k = np.zeros((self.T, self.N, self.B), dtype=np.int8, order="F")
+        _check(self.lib.ccmm_chains_get_kai(self.handle, k.ctypes.data_as(_i8p)), "ccmm_chains_get_kai")
+        return k
+
+    def record_elb_flags(self, enable=True):
+        _check(self.lib.ccmm_chains_record_elb_flags(self.handle, int(bool(enable))),
+               "ccmm_chains_record_elb_flags")
+
+    def get_elb_flags(self):
+        """drawTruncNormal branch flags of the last sweep's ELB step,
+        Ns x elbTmax x (gibbsburn + 1) x B uint8."""
+        f = np.zeros((self.Ns, self.elbTmax, self.elb_gibbsburn + 1, self.B), dtype=np.uint8, order="F")
+        _check(self.lib.ccmm_chains_get_elb_flags(self.handle, f.ctypes.data_as(_u8p)),
+               "ccmm_chains_get_elb_flags")
+        return f
 
     def set_mfma_lock(self, lock_id):
         """Serialise the MFMA Gram + Cholesky phase with other chain sets of the same id

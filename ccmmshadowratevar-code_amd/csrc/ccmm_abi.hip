@@ -571,7 +571,8 @@ struct ccmm_chains {
   }
 
   const double* elb_yhat = nullptr;  // ccmm_gibbs_shadowrates: explicit YHAT0
-  uint8_t* elb_flags = nullptr;      // ccmm_gibbs_shadowrates: drawTruncNormal branch flags
+  uint8_t* elb_flags = nullptr;      // drawTruncNormal branch flags of the last ELB step (or nullptr)
+  DBuf<uint8_t> dElbFlags;
   ElbDev elb_view() const {
     ElbDev e{};
     e.Ns = cfg.Ns;
@@ -1944,6 +1945,50 @@ int ccmm_chains_set_slots(ccmm_chains* ch, const int* slot_of_chain) {
     require(ch && slot_of_chain, "null argument");
     HIPCHECK(hipSetDevice(ch->ctx->device));
     ch->set_slots(slot_of_chain);
+    return 0;
+  });
+}
+
+int ccmm_chains_get_kai(ccmm_chains* ch, int8_t* kai) {
+  return guarded([&] {
+    require(ch && kai, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    const int B = ch->d.B, N = ch->d.N, TP = ch->d.TP, T = ch->cfg.T;
+    std::vector<int8_t> kk((size_t)B * N * TP);
+    HIPCHECK(hipMemcpy(kk.data(), ch->kai.p, kk.size(), hipMemcpyDeviceToHost));
+    for (int c = 0; c < B; ++c)
+      for (int i = 0; i < N; ++i)
+        for (int t = 0; t < T; ++t) kai[t + (size_t)T * (i + (size_t)N * c)] = kk[((size_t)c * N + i) * TP + t];
+    return 0;
+  });
+}
+
+int ccmm_chains_record_elb_flags(ccmm_chains* ch, int enable) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    require(ch->bh, "chain set was not created with CCMM_MODEL_BLOCKHYBRID / CCMM_MODEL_HYBRID");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    if (enable) {
+      ch->dElbFlags.alloc((size_t)ch->d.B * (ch->cfg.elb_gibbsburn + 1) * std::max(ch->cfg.elbTmax, 1) *
+                          ch->cfg.Ns);
+      HIPCHECK(hipMemset(ch->dElbFlags.p, 0, ch->dElbFlags.n));
+      ch->elb_flags = ch->dElbFlags.p;
+    } else {
+      ch->elb_flags = nullptr;
+    }
+    return 0;
+  });
+}
+
+int ccmm_chains_get_elb_flags(ccmm_chains* ch, uint8_t* flags) {
+  return guarded([&] {
+    require(ch && flags, "null argument");
+    require(ch->elb_flags != nullptr, "ccmm_chains_record_elb_flags(ch, 1) was not called");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    HIPCHECK(hipMemcpy(flags, ch->dElbFlags.p, ch->dElbFlags.n, hipMemcpyDeviceToHost));
     return 0;
   });
 }

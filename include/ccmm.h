@@ -202,6 +202,14 @@ int ccmm_chains_set_rng_ids(ccmm_chains* ch, const uint32_t* ids);
  * contexts then fall out of step, and the per-chain sequential blocks of one group (CTA
  * solve, SV recursion, ELB Gibbs) overlap another group's MFMA phase.  Draws are unchanged. */
 int ccmm_chains_set_mfma_lock(ccmm_chains* ch, int id);
+/* KSC mixture indicators of the last SV block (T x N x B int8, 1..7; the draw of the
+ * em-matlabbox sampler, mcmcVAR.m:261). */
+int ccmm_chains_get_kai(ccmm_chains* ch, int8_t* kai);
+/* Record the drawTruncNormal branch flags (as ccmm_draw_trunc_normal: bit0 |sig| > 1e-10,
+ * bit1 PHIbar > eps) of every ELB step; get_elb_flags returns the last sweep's as
+ * Ns x elbTmax x (gibbsburn + 1) x B uint8 (0 for uncensored cells). */
+int ccmm_chains_record_elb_flags(ccmm_chains* ch, int enable);
+int ccmm_chains_get_elb_flags(ccmm_chains* ch, uint8_t* flags);
 /* Per-chain status word since set_state (B ints, OR of: 2 CTA Cholesky, 4 A-step
  * Cholesky, 8 SV sampler, 16 PHI Cholesky found a non-positive pivot; the block
  * then continued with a unit pivot, so the chain's draws are invalid).  A CTA Cholesky

@@ -148,9 +148,10 @@ def bh_sweep(st, bs: BHSetup, crn, return_flags=False, elb_impl="qr"):
             out["shadowrate_qr"] = draws[:, :, 0]
         if elb_impl in ("stable", "both"):
             from .elb_fast import gibbsdraw_shadowrates_stable
-            draws = gibbsdraw_shadowrates_stable(elbY, bs.X0, Yhatactual, bs.ndxSmask, bs.sNaN,
-                                                 lin.p, C, Psi, SVol, bs.ELB, 1, bs.gibbsburn,
-                                                 crn["uELB"])
+            draws, sflags = gibbsdraw_shadowrates_stable(elbY, bs.X0, Yhatactual, bs.ndxSmask,
+                                                         bs.sNaN, lin.p, C, Psi, SVol, bs.ELB, 1,
+                                                         bs.gibbsburn, crn["uELB"], return_flags=True)
+            out["elb_flags_stable"] = sflags
         shadowrate = draws[:, :, 0]
         Xn, Yn = rebuild_XY(bs, shadowrate)
         out.update(X=Xn, Y=Yn, shadowrate=shadowrate, elb_flags=flags)

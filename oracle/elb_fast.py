@@ -250,9 +250,10 @@ def elb_conditionals_stable(Yb, e0, ndxS, sNaN, p, C, Psi, SVol):
 
 
 def gibbsdraw_shadowrates_stable(Y, STATE0, YHAT0, ndxS, sNaN, p, C, Psi, SVol, elbBound, Ndraws,
-                                 burnin, udraws):
+                                 burnin, udraws, return_flags=False):
     """gibbsdrawShadowrates in the stable residual form (same conditionals in exact
-    arithmetic; accurate when the shadow companion matrix is explosive)."""
+    arithmetic; accurate when the shadow companion matrix is explosive).  return_flags: also
+    the drawTruncNormal branch flags, Ns x T x (burnin + Ndraws) uint8."""
     ndxS = np.asarray(ndxS, bool)
     Ny, T = Y.shape
     S = np.flatnonzero(ndxS)
@@ -265,6 +266,7 @@ def gibbsdraw_shadowrates_stable(Y, STATE0, YHAT0, ndxS, sNaN, p, C, Psi, SVol, 
     Yb[S, :] = tmp
     cond = elb_conditionals_stable(Yb, e0, ndxS, sNaN, p, C, Psi, SVol)
     draws = np.full((Ns, T, Ndraws), np.nan)
+    flags = np.zeros((Ns, T, burnin + Ndraws), dtype=np.uint8)
     prec = {}
     for t, (base, coef, Om) in cond.items():
         b1 = np.zeros((Ns, max(Ns - 1, 0)))
@@ -287,7 +289,7 @@ def gibbsdraw_shadowrates_stable(Y, STATE0, YHAT0, ndxS, sNaN, p, C, Psi, SVol, 
             for s in np.flatnonzero(sNaN[:, t]):
                 o = np.arange(Ns) != s
                 mu = Sp[s] + (b1[s] @ (Scur[o, t] - Sp[o]) if Ns > 1 else 0.0)
-                Scur[s, t] = draw_trunc_normal(mu, so[s], elbBound, udraws[s, t, n])[0]
+                Scur[s, t], flags[s, t, n] = draw_trunc_normal(mu, so[s], elbBound, udraws[s, t, n])
         if n >= burnin:
             draws[:, :, n - burnin] = Scur
-    return draws
+    return (draws, flags) if return_flags else draws

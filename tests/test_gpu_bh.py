@@ -52,8 +52,11 @@ def _run(pkg, ctx, oracle, bh, bs, B, nsweeps, seed):
                                                                "sqrtPHI")])
     flat = np.stack([np.stack([bh_crn_flat(bh, crns[c][m], bs) for m in range(nsweeps)], -1)
                      for c in range(B)], -1)
+    ch.record_elb_flags(True)
     ch.sweep(nsweeps, crn=flat, store=True)
     got = ch.get_state()
+    got["kai"] = ch.get_kai()
+    got["elb_flags"] = ch.get_elb_flags()
     S = ch.get_shadowrate()
     X, Y = ch.get_xy()
     draws = ch.get_draws()
@@ -63,7 +66,7 @@ def _run(pkg, ctx, oracle, bh, bs, B, nsweeps, seed):
         hist = []
         for m in range(nsweeps):
             prev_sqrtht = st["sqrtht"]
-            st = bh.bh_sweep(st, bs, crns[c][m], elb_impl="both")
+            st = bh.bh_sweep(st, bs, crns[c][m], elb_impl="both", return_flags=True)
             hist.append(st["shadowrate"])
         st["prev_sqrtht"] = prev_sqrtht
         want.append((st, hist))
@@ -95,6 +98,13 @@ def _check(oracle, bs, got, S, X, Y, draws, want, tol_pai, tol_s):
         assert max(e["PAI"], e["A"], e["sqrtht"], e["sqrtPHI"]) < tol_pai, e
         sN = bs.sNaN
         assert np.all(S[:, :, c][sN] <= bs.ELB + 1e-12)
+        # KSC indicators and drawTruncNormal branches of the last sweep: bit-exact (the
+        # branches against the stable form the device evaluates; against the as-written QR
+        # form too where that form is itself accurate)
+        np.testing.assert_array_equal(got["kai"][..., c], st["kai"])
+        np.testing.assert_array_equal(got["elb_flags"][:, :bs.elbT, :, c], st["elb_flags_stable"])
+        if qr_gap < 1e-9:
+            np.testing.assert_array_equal(got["elb_flags"][:, :bs.elbT, :, c], st["elb_flags"])
         for m, sr in enumerate(hist):  # stored draws (shadowrate_all, :542)
             assert rel_err(draws["shadowrate_all"][m, :, :, c], sr, 0.1) < max(tol_s, 1e-6)
 

@@ -178,6 +178,7 @@ def test_linear_sweep_crn(pkg, ctx, oracle, fred, B, nsweeps, tol):
                      for c in range(B)], -1)
     ch.sweep(nsweeps, crn=flat)
     got = ch.get_state()
+    kai = ch.get_kai()
     prev = {}
     prev_sqrtht = prev.get
     for c in range(B):
@@ -193,6 +194,7 @@ def test_linear_sweep_crn(pkg, ctx, oracle, fred, B, nsweeps, tol):
              "sqrtPHI": rel_err(got["sqrtPHI"][..., c], st["sqrtPHI"], 1e-3)}
         print("chain", c, nsweeps, e)
         assert max(e.values()) < tol, e
+        np.testing.assert_array_equal(kai[..., c], st["kai"])  # KSC indicators: bit-exact
 
 
 def test_linear_sweep_philox_batch(pkg, ctx, oracle, fred):
