@@ -1113,8 +1113,10 @@ struct ccmm_chains {
       hipLaunchKernelGGL(k_elb_prep, dim3(d.B), dim3(256), lds_prep, ctx->stream, d, e, xsel(), cs, phi_lds);
     });
     const size_t lds_cond =
-        (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns + N * Ns) * sizeof(double);
+        (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns + N * Ns + N * p * Ns) * sizeof(double);
     launch(KID_ELBCOND, [&] {
+      HIPCHECK(hipFuncSetAttribute((const void*)k_elb_cond, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds_cond));
       hipLaunchKernelGGL(k_elb_cond, dim3(e.elbTmax, d.B), dim3(64), lds_cond, ctx->stream, d, e, cs);
     });
     const size_t lds_gibbs = (size_t)2 * e.elbTmax * Ns * sizeof(double);  // S | uniforms

@@ -199,8 +199,16 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
   double* Pm = gS + (1 + ncol) * Ns;           // Ns x Ns
   double* Om = Pm + Ns * Ns;                   // Ns x Ns
   double* Wl = Om + Ns * Ns;                   // N x Ns: W = diag(1/SVol^2) (A or A Φ_k)[:, S]
+  double* PS = Wl + N * Ns;                    // N x p x Ns: Φ's shadow-rate columns
+                                               //   PS[(j p + l) Ns + b] = Φ_{l+1}(j, S_b)
   int S[kElbNsMax];
   for (int a = 0; a < kElbNsMax; ++a) S[a] = a < Ns ? e.ndxS[a] : 0;
+  // every Φ read below is a shadow-rate column: stage those N p Ns values once per wave
+  for (int q = lane; q < N * p * Ns; q += 64) {
+    const int b = q % Ns, jl = q / Ns, l = jl % p, jj = jl / p;
+    PS[q] = Phi[(size_t)jj * Np + l * N + e.ndxS[b]];
+  }
+  __syncthreads();
   // ---- Q_0 = Λ_t[S, :], Q_k = B_k' Λ_{t+k};  Λ = A' diag(1/SVol^2) A
   for (int k = 0; k <= kmax; ++k) {
     for (int i = lane; i < N; i += 64) {
@@ -212,7 +220,7 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
         if (k == 0) {
           v = A[i + S[a] * N];
         } else {
-          for (int j = 0; j <= i; ++j) v = fma(A[i + j * N], Phi[(size_t)j * Np + (k - 1) * N + S[a]], v);
+          for (int j = 0; j <= i; ++j) v = fma(A[i + j * N], PS[(j * p + k - 1) * Ns + a], v);
         }
         w[a] = v * iv;
       }
@@ -235,7 +243,7 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
     double v = Q[(size_t)a * N + S[b]];
     for (int k = 1; k <= kmax; ++k) {
       const double* Qk = Q + ((size_t)k * Ns + a) * N;
-      for (int j = 0; j < N; ++j) v = fma(Qk[j], Phi[(size_t)j * Np + (k - 1) * N + S[b]], v);
+      for (int j = 0; j < N; ++j) v = fma(Qk[j], PS[(j * p + k - 1) * Ns + b], v);
     }
     Pm[lane] = v;
   }
@@ -252,7 +260,7 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
       for (int k = 1; k <= kmax; ++k) {
         double r = Et[(size_t)(t + k) * N + j];
         for (int b = 0; b < Ns; ++b)
-          r = fma(Phi[(size_t)j * Np + (k - 1) * N + S[b]], Yt[(size_t)t * N + S[b]], r);
+          r = fma(PS[(j * p + k - 1) * Ns + b], Yt[(size_t)t * N + S[b]], r);
         for (int a = 0; a < Ns; ++a) g0[a] = fma(Q[((size_t)k * Ns + a) * N + j], r, g0[a]);
       }
     }
@@ -273,10 +281,10 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
       if (t - kp >= 0)
         for (int a = 0; a < Ns; ++a) {
           double v = 0.0;
-          for (int j = 0; j < N; ++j) v = fma(Q[(size_t)a * N + j], Phi[(size_t)j * Np + (kp - 1) * N + q], v);
+          for (int j = 0; j < N; ++j) v = fma(Q[(size_t)a * N + j], PS[(j * p + kp - 1) * Ns + sp], v);
           for (int k = 1; k <= kmax && k + kp <= p; ++k) {
             const double* Qk = Q + ((size_t)k * Ns + a) * N;
-            for (int j = 0; j < N; ++j) v = fma(-Qk[j], Phi[(size_t)j * Np + (k + kp - 1) * N + q], v);
+            for (int j = 0; j < N; ++j) v = fma(-Qk[j], PS[(j * p + k + kp - 1) * Ns + sp], v);
           }
           g[a] = v;
         }
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
           double v = Q[((size_t)kp * Ns + a) * N + q];
           for (int k = kp + 1; k <= kmax; ++k) {
             const double* Qk = Q + ((size_t)k * Ns + a) * N;
-            for (int j = 0; j < N; ++j) v = fma(-Qk[j], Phi[(size_t)j * Np + (k - kp - 1) * N + q], v);
+            for (int j = 0; j < N; ++j) v = fma(-Qk[j], PS[(j * p + k - kp - 1) * Ns + sp], v);
           }
           g[a] = v;
         }
@@ -356,27 +364,60 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
 
 // ---------------------------------------------------------------- truncated normal (device)
 // drawTruncNormal.m: z = -sqrt(2) erfcinv(2 u Φbar(ub)), ub = (elb - mu)/sig
-__device__ __forceinline__ double elb_trunc_normal(double mu, double sig, double elb, double u) {
+// Phi^{-1}(p) by Wichura's AS241 (PPND16, relative error ~1e-16): the truncated draw of
+// drawTruncNormal.m:47-48, z = -sqrt(2) erfcinv(2 u PHIbar), is Phi^{-1}(u PHIbar).  Inline
+// with wave-uniform branches (every lane draws the same cell); the library erfcinv inlined
+// into k_elb_gibbs's month loop needs ~480 registers (one wave per SIMD).
+__device__ __forceinline__ double elb_ppnd16(double p) {
+  const double q = p - 0.5;
+  if (fabs(q) <= 0.425) {
+    const double r = 0.180625 - q * q;
+    const double num = (((((((2509.0809287301226727 * r + 33430.575583588128105) * r + 67265.770927008700853) * r +
+                            45921.953931549871457) * r + 13731.693765509461125) * r + 1971.5909503065514427) * r +
+                          133.14166789178437745) * r + 3.387132872796366608);
+    const double den = (((((((5226.495278852545925 * r + 28729.085735721942674) * r + 39307.89580009271061) * r +
+                            21213.794301586595867) * r + 5394.1960214247511077) * r + 687.1870074920579083) * r +
+                          42.313330701600911252) * r + 1.0);
+    return q * num / den;
+  }
+  double r = (q < 0.0) ? p : 1.0 - p;
+  r = sqrt(-log(r));
+  double z;
+  if (r <= 5.0) {
+    r -= 1.6;
+    const double num = (((((((7.7454501427834140764e-4 * r + 0.0227238449892691845833) * r + 0.24178072517745061177) * r +
+                            1.27045825245236838258) * r + 3.64784832476320460504) * r + 5.7694972214606914055) * r +
+                          4.6303378461565452959) * r + 1.42343711074968357734);
+    const double den = (((((((1.05075007164441684324e-9 * r + 5.475938084995344946e-4) * r + 0.0151986665636164571966) * r +
+                            0.14810397642748007459) * r + 0.68976733498510000455) * r + 1.6763848301838038494) * r +
+                          2.05319162663775882187) * r + 1.0);
+    z = num / den;
+  } else {
+    r -= 5.0;
+    const double num = (((((((2.01033439929228813265e-7 * r + 2.71155556874348757815e-5) * r + 0.0012426609473880784386) * r +
+                            0.026532189526576123093) * r + 0.29656057182850489123) * r + 1.7848265399172913358) * r +
+                          5.4637849111641143699) * r + 6.6579046435011037772);
+    const double den = (((((((2.04426310338993978564e-15 * r + 1.4215117583164458887e-7) * r + 1.8463183175100546818e-5) * r +
+                            7.868691311456132591e-4) * r + 0.0148753612908506148525) * r + 0.13692988092273580531) * r +
+                          0.59983220655588793769) * r + 1.0);
+    z = num / den;
+  }
+  return (q < 0.0) ? -z : z;
+}
+
+__device__ __forceinline__ double elb_trunc_normal(double mu, double sig, double elb, double u, uint8_t& fl) {
   const double tol = 1e-10;
   const double eps = 2.220446049250313080847e-16;
   sig = fabs(sig);
-  if (sig > tol) {
+  fl = 0;
+  if (sig > tol) {  // drawTruncNormal.m branches: bit 0 sigma > tol (:31), bit 1 PHIbar > eps (:44)
     const double ub = (elb - mu) / sig;
     const double PHIbar = 0.5 * erfc(-0.70710678118654752440 * ub);
-    const double z = (PHIbar > eps) ? -1.41421356237309504880 * erfcinv(2.0 * u * PHIbar) : ub;
+    fl = (PHIbar > eps) ? 3 : 1;
+    const double z = (PHIbar > eps) ? elb_ppnd16(u * PHIbar) : ub;
     return mu + sig * z;
   }
   return mu;
-}
-
-// branch flags of drawTruncNormal.m: bit 0 sigma > tol (:31), bit 1 PHIbar > eps (:44)
-__device__ __forceinline__ uint8_t elb_trunc_flags(double mu, double sig, double elb) {
-  const double tol = 1e-10;
-  const double eps = 2.220446049250313080847e-16;
-  sig = fabs(sig);
-  if (!(sig > tol)) return 0;
-  const double PHIbar = 0.5 * erfc(-0.70710678118654752440 * ((elb - mu) / sig));
-  return (uint8_t)(1 | ((PHIbar > eps) ? 2 : 0));
 }
 
 // ---------------------------------------------------------------- Gibbs passes (per chain)
@@ -467,9 +508,10 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
           mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
           ++y;
         }
-        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a]);
+        uint8_t fl;
+        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a], fl);
         if (e.flags && lane == 0)  // drawTruncNormal.m branch taken (oracle.draw_trunc_normal flags)
-          e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = elb_trunc_flags(mu, so[a], e.elb);
+          e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
       }
       for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
       for (int q = 0; q < kHd; ++q) hd[q] = hdn[q];
