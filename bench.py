@@ -35,6 +35,11 @@ FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix (AMD spec)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec
 
 
+def _progress(msg):
+    """Progress on stderr (the one JSON result line stays alone on stdout)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,7 +98,9 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu:
         # before the GPU is initialised: the baseline runs in spawned single-thread processes
+        _progress("cpu baseline")
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_workers)
+        _progress("cpu baseline done")
 
     import __graft_entry__ as ge
     pkg = ge.load_package()
@@ -118,6 +125,7 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
+    _progress("main line")
     ch.sweep(args.warmup, store=True)
     barrier()
     if not args.no_profile:
@@ -138,6 +146,7 @@ def main():
     ch.close()
     # secondary lines (configs[2], configs[3]) run on every rank: own barrier/max-reduction
     bh = None
+    _progress("secondary lines")
     if args.bh_steps > 0:
         bh = [bench_block_hybrid(pkg, ctx, d, int(b), args, rank, barrier, dist)
               for b in args.bh_chains.split(",") if b.strip()]
@@ -275,6 +284,7 @@ def bench_oos(pkg, ctx, d, C, args, rank, barrier, dist, H=48, Nd=10):
     then plain (burn-in) sweeps.  value = units x sweeps / time summed over ranks (fixed
     total work: strong scaling).  The projected OOS wall time is 1000 burn-in + 1000 kept
     sweeps per unit at these rates."""
+    _progress(f"bench_oos {locals().get('B', locals().get('C'))}")
     import time as _t
     p = 12
     S = pkg.samplers
@@ -341,6 +351,7 @@ def bench_block_hybrid(pkg, ctx, d, B, args, rank, barrier, dist):
     with gibbsburn + 1 = 101 passes and inverse-CDF truncated normals -> X/Y rebuild,
     mcmcVARshadowrateBlockHybrid.m:332-520) at the 2022-08 jump-off: elbT = 165 months,
     109 censored months / 276 censored cells.  Same timing protocol as the main line."""
+    _progress(f"bench_block_hybrid {locals().get('B', locals().get('C'))}")
     import time as _t
     p = 12
     mpm = pkg.model.setMinnesotaMean(d["ncode"])
@@ -435,6 +446,7 @@ def bench_s120(pkg, ctx, B, args, rank, barrier, dist, groups=None):
     one workgroup per chain) of one group overlap the MFMA Gram/Cholesky of another.  Same
     timing protocol as the main line (barrier, K timed sweeps of every group, max over ranks);
     the CTA kernels are priced against the FP64 MFMA peak from their per-launch times."""
+    _progress(f"bench_s120 {locals().get('B', locals().get('C'))}")
     import time as _t
     G = groups or args.s120_groups
     if B % G:
