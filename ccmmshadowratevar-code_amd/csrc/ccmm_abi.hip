@@ -272,7 +272,7 @@ struct ccmm_chains {
   int lagNT = 0, ldd = 0, drows = 0;
   std::vector<bool> slot_lag;
   DBuf<double> Dpool;
-  DBuf<int> dColmap;
+  DBuf<int> dColmap, astepTab;
   // large-system CTA (ccmm_big.hip): K > 512 or N > 32, or CCMM_FORCE_BIG=1
   bool big = false;
   int nGroups = 0;
@@ -1016,9 +1016,20 @@ struct ccmm_chains {
         HIPCHECK(hipFuncSetAttribute((const void*)k_astep,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     }
+    if (!astepTab.p) {  // (ii, a, b) of every Gram entry, block ii = 1..N-1: packed lower ZZ, then Zz
+      std::vector<int> tab;
+      for (int ii = 1; ii < N; ++ii) {
+        for (int b = 0; b < ii; ++b)
+          for (int a = b; a < ii; ++a) tab.push_back(ii << 16 | a << 8 | b);
+        for (int a = 0; a < ii; ++a) tab.push_back(ii << 16 | a << 8 | ii);
+      }
+      tab.push_back(0);
+      astepTab.alloc(tab.size());
+      HIPCHECK(hipMemcpy(astepTab.p, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice));
+    }
     launch(KID_ASTEP, [&] {
       hipLaunchKernelGGL(k_astep, dim3(d.B), dim3(256), lds, ctx->stream, d, Tslot.p, cs, ra,
-                         cfg.logy2offset, es_off);
+                         cfg.logy2offset, es_off, astepTab.p);
     });
   }
 

@@ -380,8 +380,11 @@ __global__ __launch_bounds__(256) void k_cta_solve(Dims d, const int* __restrict
 // mcmcVAR.m:236-254 (flat prior: OMEGA_A_inv = 0, MU_A = 0, mcmcVAR.m:153-161),
 // invA = A \ I (mcmcVAR.m:254), logy2 = log((RESID*A').^2 + offset) (mcmcVAR.m:259).
 // LDS: per ii a packed lower ZZ (ii x ii) followed by Zz (ii).
+// gtab[g] = ii << 16 | a << 8 | b: the (regression, row, column) of Gram entry g (host-built,
+// replaces a per-entry decode loop)
 __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ Tslot, ChainState cs,
-                                               RngArgs ra, double logy2offset, int es_off) {
+                                               RngArgs ra, double logy2offset, int es_off,
+                                               const int* __restrict__ gtab) {
   extern __shared__ double sm[];
   const int c = blockIdx.x;
   const int N = d.N, TP = d.TP;
@@ -414,22 +417,10 @@ __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ T
   // entry g of block ii: (a, b) of the ii x ii Gram ZZ = E(:,0:ii-1)' diag(1/h_ii^2) E(:,0:ii-1)
   // (packed lower) or of Zz = E(:,0:ii-1)' diag(1/h_ii^2) E(:,ii)
   auto entry = [&](int g, int& ii, int& a, int& b) {
-    ii = 1;
-    while (ii < N - 1 && g >= boff[ii + 1]) ++ii;
-    const int e = g - boff[ii];
-    const int ntri = ii * (ii + 1) / 2;
-    if (e < ntri) {  // packed lower: column b, row a >= b
-      b = 0;
-      int rem = e;
-      while (rem >= ii - b) {
-        rem -= ii - b;
-        ++b;
-      }
-      a = b + rem;
-    } else {
-      a = e - ntri;  // Zz entry: X(:,a)' y
-      b = ii;
-    }
+    const int v = gtab[g];
+    ii = v >> 16;
+    a = (v >> 8) & 255;
+    b = v & 255;
   };
   constexpr int kAsTPL = 16;  // t values per lane on the wave-per-entry path (T <= 1024)
   if (T <= 64 * kAsTPL) {
@@ -520,16 +511,17 @@ __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ T
   }
   __syncthreads();
   for (int q = tid; q < N * N; q += blockDim.x) Ac[q] = Anew[q];
-  // invA: column col of A^{-1} by forward substitution (unit lower)
+  // invA: column col of A^{-1} by forward substitution (unit lower); the column is built
+  // in LDS (sm[0..N*N) is free after the solves) rather than a dynamically indexed array
+  double* Xs = sm;
   if (tid < N) {
     const int col = tid;
-    double x[kMaxNSmall];
     for (int r = 0; r < N; ++r) {
       double s = (r == col) ? 1.0 : 0.0;
-      for (int q = col; q < r; ++q) s -= Anew[r + q * N] * x[q];
-      x[r] = (r >= col) ? s : 0.0;
+      for (int q = col; q < r; ++q) s -= Anew[r + q * N] * Xs[q + col * N];
+      Xs[r + col * N] = (r >= col) ? s : 0.0;
     }
-    for (int r = 0; r < N; ++r) Ainv[r + col * N] = x[r];
+    for (int r = 0; r < N; ++r) Ainv[r + col * N] = Xs[r + col * N];
   }
   // logy2 = log((RESID * A').^2 + offset)
   double* ly = cs.logy2 + (size_t)c * N * TP;
