@@ -1123,12 +1123,26 @@ struct ccmm_chains {
                                    (int)lds_prep));
       hipLaunchKernelGGL(k_elb_prep, dim3(d.B), dim3(256), lds_prep, ctx->stream, d, e, xsel(), cs, phi_lds);
     });
-    const size_t lds_cond =
+    size_t lds_cond =
         (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns + N * Ns + N * p * Ns) * sizeof(double);
+    const int a_lds = (lds_cond + (size_t)N * N * sizeof(double) <= 64 * 1024) ? 1 : 0;
+    if (a_lds) lds_cond += (size_t)N * N * sizeof(double);
     launch(KID_ELBCOND, [&] {
-      HIPCHECK(hipFuncSetAttribute((const void*)k_elb_cond, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds_cond));
-      hipLaunchKernelGGL(k_elb_cond, dim3(e.elbTmax, d.B), dim3(64), lds_cond, ctx->stream, d, e, cs);
+      switch (Ns) {
+#define CASE_NSC(NS)                                                                                 \
+  case NS:                                                                                           \
+    HIPCHECK(hipFuncSetAttribute((const void*)k_elb_cond<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                 (int)lds_cond));                                                    \
+    hipLaunchKernelGGL(k_elb_cond<NS>, dim3(e.elbTmax, d.B), dim3(64), lds_cond, ctx->stream, d, e, cs, a_lds); \
+    break;
+        CASE_NSC(1)
+        CASE_NSC(2)
+        CASE_NSC(3)
+        CASE_NSC(4)
+#undef CASE_NSC
+        default:
+          throw ArgError("Ns must be in [1, 4]");
+      }
     });
     const size_t lds_gibbs = (size_t)2 * e.elbTmax * Ns * sizeof(double);  // S | uniforms
     launch(KID_ELBGIBBS, [&] {

@@ -178,13 +178,15 @@ __device__ inline void elb_small_inverse(const double* M, double* Minv, int n) {
   }
 }
 
-__global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs) {
+template <int NS>  // = e.Ns: compile-time, so the per-shadow-rate arrays below stay in registers
+__global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs, int a_lds) {
   extern __shared__ double sm[];
   const int c = blockIdx.y;
   const int s = cs.slot[c];
   const int ci = blockIdx.x;
   if (ci >= e.ncens[s]) return;
-  const int N = d.N, p = e.p, Ns = e.Ns, Np = N * p;
+  const int N = d.N, p = e.p, Np = N * p;
+  constexpr int Ns = NS;
   const int T = e.elbT[s], T0 = e.elbT0[s];
   const int t = e.cens[(size_t)s * e.elbTmax + ci];
   const int lane = threadIdx.x;
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
   const double* Phi = e.Phi + (size_t)c * N * Np;
   const double* Yt = e.Yt + (size_t)c * e.elbTmax * N;
   const double* Et = e.Et + (size_t)c * e.elbTmax * N;
-  const double* A = cs.A + (size_t)c * N * N;  // column-major A(i,j), unit lower
+  const double* Ag = cs.A + (size_t)c * N * N;  // column-major A(i,j), unit lower
   const int kmax = min(p, T - 1 - t);
   double* Q = sm;                              // (p+1) x Ns x N
   double* gS = Q + (p + 1) * Ns * N;           // (1 + ncol) x Ns
@@ -203,12 +205,17 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
                                                //   PS[(j p + l) Ns + b] = Φ_{l+1}(j, S_b)
   int S[kElbNsMax];
   for (int a = 0; a < kElbNsMax; ++a) S[a] = a < Ns ? e.ndxS[a] : 0;
-  // every Φ read below is a shadow-rate column: stage those N p Ns values once per wave
+  // every Φ read below is a shadow-rate column: stage those N p Ns values once per wave;
+  // A too when it fits (a_lds: N <= 64), so the dependent sums below read LDS, not L1/L2
   for (int q = lane; q < N * p * Ns; q += 64) {
     const int b = q % Ns, jl = q / Ns, l = jl % p, jj = jl / p;
     PS[q] = Phi[(size_t)jj * Np + l * N + e.ndxS[b]];
   }
+  double* Al = PS + N * p * Ns;
+  if (a_lds)
+    for (int q = lane; q < N * N; q += 64) Al[q] = Ag[q];
   __syncthreads();
+  const double* A = a_lds ? Al : Ag;
   // ---- Q_0 = Λ_t[S, :], Q_k = B_k' Λ_{t+k};  Λ = A' diag(1/SVol^2) A
   for (int k = 0; k <= kmax; ++k) {
     for (int i = lane; i < N; i += 64) {
