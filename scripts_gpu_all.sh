@@ -1,0 +1,8 @@
+#!/bin/bash
+# full GPU test suite + smoke, one pytest process, own time limits
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"; mkdir -p gpurun_out
+timeout -k 10 840 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/tests_all.log 2>&1
+rc=$?; echo "tests exit=$rc" >> gpurun_out/tests_all.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1
