@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--bh-warmup", type=int, default=1)
     ap.add_argument("--bh-chains", default="256,1024,4096",
                     help="chains per GPU of the block-hybrid lines (comma list)")
+    ap.add_argument("--hy-steps", type=int, default=3,
+                    help="timed sweeps of the hybrid-model lines (mcmcVARhybridGibbs, K = 277); 0 = skip")
+    ap.add_argument("--hy-chains", default="256,1024", help="chains per GPU of the hybrid lines")
     ap.add_argument("--oos-steps", type=int, default=3,
                     help="timed kept sweeps (with forecasts) of the OOS line (configs[3]); 0 = skip")
     ap.add_argument("--oos-chains", default="1,8", help="chains per vintage of the OOS lines")
@@ -150,6 +153,10 @@ def main():
     if args.bh_steps > 0:
         bh = [bench_block_hybrid(pkg, ctx, d, int(b), args, rank, barrier, dist)
               for b in args.bh_chains.split(",") if b.strip()]
+    hy = None
+    if args.hy_steps > 0:
+        hy = [bench_hybrid(pkg, ctx, d, int(b), args, rank, barrier, dist)
+              for b in args.hy_chains.split(",") if b.strip()]
     s120 = None
     if args.s120_steps > 0:
         s120 = [bench_s120(pkg, ctx, int(b), args, rank, barrier, dist)
@@ -198,6 +205,9 @@ def main():
             # fused weighted SYRK + Cholesky: N*[T*K(K+1) + K^3/3] flop per chain
             kname = "k_gram_chol"
             flop = B * N * (T * K * (K + 1) + K ** 3 / 3)
+        elif ktimes.get("k_gram_big", (0, 0))[1]:
+            kname = "k_gram_big"  # multi-equation Gram (large-system path): T K (K+1) per system
+            flop = B * N * T * K * (K + 1)
         else:
             kname = "k_syrk"
             flop = B * N * T * K * (K + 1)
@@ -243,6 +253,8 @@ def main():
         out["oos"] = oos
     if s120 is not None:
         out["s120"] = s120
+    if hy is not None:
+        out["hybrid"] = hy
     if fc is not None:
         out["predictive"] = fc
     if cpu is not None:
@@ -409,6 +421,61 @@ def bench_block_hybrid(pkg, ctx, d, B, args, rank, barrier, dist):
                                 "frac": round(gbs / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": int(nbytes), "avg_launch_ms": round(ms, 4),
                                 "note": "one wave per chain, 101 sequential passes: latency-bound"}
+    ch.close()
+    return res
+
+
+def bench_hybrid(pkg, ctx, d, B, args, rank, barrier, dist):
+    """Secondary line: the hybrid shadow-rate model (mcmcVARhybridGibbs.m, X = [1, lags,
+    Xffrlags]: K = 241 + Ns p = 277, KP = 320, the generic fused Gram + Cholesky path with
+    the ELB step), fredblockMD20 at the 2022-08 jump-off, ELB 0.25.  Same timing protocol."""
+    import time as _t
+    _progress(f"bench_hybrid {B}")
+    p = 12
+    mpm = pkg.model.setMinnesotaMean(d["ncode"])
+    ndxS, _, _ = pkg.model.setShadowYields(d["ncode"], 0.25)
+    e0 = pkg.model.elbT0_of(d["data"], ndxS, 0.25, p)
+    hm = pkg.model.build_hybrid(len(d["ydates"]), p, 12, d["data"], d["ydates"], ndxS, mpm, 0.25, e0, True)
+    m = hm.var
+    Ns = len(hm.ndxS)
+    ch = pkg.Chains(ctx, N=m.N, p=p, T=m.T, B=B, crn=False, store_capacity=args.hy_steps + 1,
+                    seed=1012023 + 7919 * rank + 3, model=pkg.MODEL_HYBRID, Ns=Ns, elbTmax=hm.elbT,
+                    elb_gibbsburn=100, elb=0.25)
+    ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    ch.set_elb_model(hm.ndxS, None)
+    ch.set_elb_slot(0, hm.elbT0, hm.sNaN)
+    st = pkg.model.initial_state(m, B)
+    ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+    ch.sweep(1, store=True)
+    barrier()
+    if not args.no_profile:
+        ch.profile(True)
+    t0 = _t.perf_counter()
+    ch.sweep(args.hy_steps, store=True)
+    barrier()
+    el = _t.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{ctx.device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    assert np.all(np.isfinite(ch.get_shadowrate())), "non-finite shadow rates"
+    world = dist.get_world_size() if dist is not None else 1
+    res = {"workload": f"hybrid shadow-rate BVAR-SV (mcmcVARhybridGibbs) N=20 p=12 T={m.T} K={m.K}, "
+                       f"Ns={Ns}, elbT={hm.elbT}, ELB Gibbs (101 passes) every sweep, {B} chains per GPU",
+           "value": round(world * B * args.hy_steps / el, 3), "unit": "sweeps/s",
+           "ms_per_step": round(1e3 * el / args.hy_steps, 4), "steps": args.hy_steps, "warmup": 1}
+    if not args.no_profile:
+        kt = ch.kernel_times()
+        res["kernel_ms_per_sweep"] = {k: round(v[0] / v[1], 4) for k, v in kt.items() if v[1]}
+        if kt.get("k_gram_chol", (0, 0))[1]:
+            K = m.K
+            fl = B * m.N * (m.T * K * (K + 1) + K ** 3 / 3)
+            ms = kt["k_gram_chol"][0] / kt["k_gram_chol"][1]
+            ach = fl / (ms * 1e-3) / 1e12
+            res["fp64_mfma"] = {"kernel": "k_gram_chol", "achieved": round(ach, 3), "peak": FP64_MFMA_PEAK_TFLOPS,
+                                "unit": "TFLOP/s", "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4),
+                                "flop_per_launch": int(fl), "avg_launch_ms": round(ms, 4)}
     ch.close()
     return res
 

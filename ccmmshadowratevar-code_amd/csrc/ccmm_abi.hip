@@ -404,7 +404,9 @@ struct ccmm_chains {
     d.B = cf.B;
     d.nmat = cf.B * cf.N;
     require(d.KP <= kBigMaxKP, "this build supports K <= 1536");
-    big = d.KP > 512 || cf.N > kMaxNSmall || std::getenv("CCMM_FORCE_BIG") != nullptr;
+    // KP > 256: the register-tiled fused Gram + Cholesky (k_gram_chol) stops at 16 tiles; the
+    // large path beats the generic SYRK + Cholesky there (hybrid model K = 277: 32 vs 41 ms)
+    big = d.KP > 256 || cf.N > kMaxNSmall || std::getenv("CCMM_FORCE_BIG") != nullptr;
     nslabX = nX;
     nslabY = nY;
     const size_t B = cf.B, N = cf.N, KP = d.KP, TP = d.TP;
