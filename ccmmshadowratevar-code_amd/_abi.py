@@ -24,7 +24,7 @@ MODEL_LINEAR = 0
 MODEL_BLOCKHYBRID = 1
 MODEL_HYBRID = 2  # mcmcVARhybridGibbs.m: K = N*p + 1 + Ns*p
 
-RNG_PAI, RNG_A, RNG_SVU, RNG_SVZ, RNG_PHI, RNG_ELB, RNG_FCST = 1, 2, 3, 4, 5, 6, 7
+RNG_PAI, RNG_A, RNG_SVU, RNG_SVZ, RNG_PHI, RNG_ELB, RNG_FCST, RNG_PS = 1, 2, 3, 4, 5, 6, 7, 8
 CCMM_WARN_MVNCDF = 3
 
 _dp = C.POINTER(C.c_double)
@@ -88,6 +88,8 @@ _SIGS = {
     "ccmm_chains_set_elb_model": (C.c_int, [C.c_void_p, _ip, _u8p]),
     "ccmm_chains_set_elb_slot": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p]),
     "ccmm_chains_get_shadowrate": (C.c_int, [C.c_void_p, _dp]),
+    "ccmm_chains_set_elb_ps": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "ccmm_chains_get_ps": (C.c_int, [C.c_void_p, _ip, _ip, _ip]),
     "ccmm_chains_get_xy": (C.c_int, [C.c_void_p, _dp, _dp]),
     "ccmm_chains_profile": (C.c_int, [C.c_void_p, C.c_int]),
     "ccmm_chains_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _dp, _i64p, C.c_char_p, C.c_int]),
@@ -328,7 +330,7 @@ class Chains:
                "k_sv_mix", "k_sv_part", "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
                "k_elb_prep", "k_elb_cond", "k_elb_gibbs", "k_elb_rebuild", "k_gram_chol_lag",
                "k_cta_solve_lag", "k_fcst", "k_gram_big", "k_chol_big", "k_cta_solve_big",
-               "k_astep_big", "k_sv_big", "k_phi_big")
+               "k_astep_big", "k_sv_big", "k_phi_big", "k_ps_chol", "k_ps_prop")
 
     def __init__(self, ctx: Context, *, N, p, T, B, ndata=1, model=MODEL_LINEAR, crn=False,
                  store_capacity=0, logy2offset=1e-3, seed=1012023, dPHI=None, Ns=0, elbTmax=0,
@@ -372,6 +374,8 @@ class Chains:
             blocks.append(("ELB", self.Ns * self.elbTmax * (cf.elb_gibbsburn + 1), "u"))
         if getattr(self, "fH", 0):
             blocks.append(("FCST", 2 * N * self.fH * self.fNd, "n"))
+        if getattr(self, "ps_np", 0):
+            blocks.append(("PS", self.Ns * self.elbTmax * self.ps_np, "n"))
         out, o = {}, 0
         for name, n, kind in blocks:
             out[name] = (o, n, kind)
@@ -541,6 +545,24 @@ class Chains:
         _check(self.lib.ccmm_chains_set_elb_slot(self.handle, int(slot), int(elbT0),
                                                  m.ctypes.data_as(_u8p) if m.size else None),
                "ccmm_chains_set_elb_slot")
+
+    def set_elb_ps(self, nproposals=1000, ps_from_m=1):
+        """Acceptance-sampling branch (mcmcVARshadowrateBlockHybrid.m:435-466) from sweep
+        m >= ps_from_m (1-based; the reference: ceil(MCMCburnin / 2)); 0 proposals disables."""
+        _check(self.lib.ccmm_chains_set_elb_ps(self.handle, int(nproposals), int(ps_from_m)),
+               "ccmm_chains_set_elb_ps")
+        self.ps_np = int(nproposals)
+
+    def get_ps(self):
+        """countAccept, countAcceptBurnin (B) and stackAccept (M x B, 0 = none) of the
+        stored draws (call before get_draws)."""
+        M, B = self.stored(), self.B
+        ca = np.zeros(B, np.int32)
+        cb = np.zeros(B, np.int32)
+        st = np.zeros((max(M, 1), B), np.int32, order="F")
+        _check(self.lib.ccmm_chains_get_ps(self.handle, ca.ctypes.data_as(_ip), cb.ctypes.data_as(_ip),
+                                           st.ctypes.data_as(_ip)), "ccmm_chains_get_ps")
+        return dict(countAccept=ca, countAcceptBurnin=cb, stackAccept=st[:M])
 
     def get_shadowrate(self):
         out = np.zeros((self.Ns, self.elbTmax, self.B), order="F")

@@ -18,6 +18,7 @@
 #include "ccmm_cta_solve.hip"
 #include "ccmm_gram_chol.hip"
 #include "ccmm_elb.hip"
+#include "ccmm_ps.hip"
 #include "ccmm_fcst.hip"
 #include "ccmm_lag.h"
 #include "ccmm_svpart.h"
@@ -187,6 +188,8 @@ enum KernelId {
   KID_ASTEPBIG,
   KID_SVBIG,
   KID_PHIBIG,
+  KID_PSCHOL,
+  KID_PSPROP,
   KID_COUNT
 };
 static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syrk", "k_chol",
@@ -196,7 +199,8 @@ static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syr
                                               "k_elb_rebuild", "k_gram_chol_lag",
                                               "k_cta_solve_lag", "k_fcst",
                                               "k_gram_big", "k_chol_big", "k_cta_solve_big",
-                                              "k_astep_big", "k_sv_big", "k_phi_big"};
+                                              "k_astep_big", "k_sv_big", "k_phi_big",
+                                              "k_ps_chol", "k_ps_prop"};
 
 // MFMA phase lock: chain sets given the same id (ccmm_chains_set_mfma_lock) on one device
 // serialise their CTA Gram + Cholesky phase through a cross-stream event, so the groups fall
@@ -245,6 +249,13 @@ struct ccmm_chains {
   DBuf<int> dNdxS, dElbT0, dElbT, dNcens, dCens;
   DBuf<uint8_t> dActual, dSNaN;
   DBuf<double> ePhi, eY0, eYt, eEt, eCond, eScur;
+  std::vector<std::vector<uint8_t>> hSNaN;  // per slot, elbTmax x Ns (t-major)
+  // acceptance-sampling branch (ccmm_ps.hip): ps_np proposals per sweep from sweep
+  // m = ps_from_m on (1-based, m = sweep + 1; the reference: m >= MCMCburnin/2, :435)
+  int ps_np = 0, ps_from_m = -1, psW = 0, ps_nmax = 0;
+  bool ps_dirty = true;
+  DBuf<double> eEtPS, psL, psY;
+  DBuf<int> psCell, psN, psAcc, psFlag, psCount, sAccept;
   int stored = 0;
   uint32_t sweep = 0;
   // predictive density of every stored sweep (mcmcVAR.m:298-381,
@@ -374,7 +385,7 @@ struct ccmm_chains {
   }
   XSel xsel() const { return XSel{Xpool.p, xidx.p, Ypool.p, yidx.p}; }
 
-  int64_t crn_off[8] = {};
+  int64_t crn_off[kRngBlocks] = {};
   int64_t crn_len = 0;
 
   void init(ccmm_ctx* c, const ccmm_chain_config& cf, int nX, int nY) {
@@ -479,6 +490,10 @@ struct ccmm_chains {
       crn_off[CCMM_RNG_FCST] = o;
       o += 2 * N * fH * fNd;
     }
+    if (bh && ps_np > 0) {  // randn(nmiss, Nproposals), column-major with leading dimension nmiss
+      crn_off[CCMM_RNG_PS] = o;
+      o += (int64_t)cf.Ns * cf.elbTmax * ps_np;
+    }
     crn_len = o;
   }
 
@@ -549,6 +564,7 @@ struct ccmm_chains {
   void init_elb() {
     const size_t B = cfg.B, N = cfg.N, Ns = cfg.Ns, ET = std::max(cfg.elbTmax, 1), nd = cfg.ndata;
     have_elb_slot.assign(nd, false);
+    hSNaN.assign(nd, std::vector<uint8_t>((size_t)ET * Ns, 0));
     hNdxS.assign(Ns, 0);
     hActual.assign(N, 1);
     hElbT0.assign(nd, cfg.T);
@@ -567,7 +583,7 @@ struct ccmm_chains {
     eY0.alloc(B * ET * N);
     eYt.alloc(B * ET * N);
     eEt.alloc(B * ET * N);
-    eCond.alloc(B * ET * (size_t)elb_cond_stride(cfg.Ns, cfg.p));
+    eCond.alloc(B * ET * (size_t)elb_cond_stride(cfg.Ns, cfg.p, ps_np > 0));
     eScur.alloc(B * ET * Ns);
     HIPCHECK(hipMemset(eScur.p, 0, eScur.n * sizeof(double)));
   }
@@ -596,12 +612,15 @@ struct ccmm_chains {
     e.Et = eEt.p;
     e.cond = eCond.p;
     e.Scur = eScur.p;
-    e.condStride = elb_cond_stride(cfg.Ns, cfg.p);
+    e.condStride = elb_cond_stride(cfg.Ns, cfg.p, ps_np > 0);
     e.kshadow = cfg.N * cfg.p + 1;
     e.K = cfg.K;
     e.mode = elb_mode;
     e.yhat = elb_yhat;
     e.flags = elb_flags;
+    e.ps = 0;
+    e.EtPS = eEtPS.p;
+    e.psFlag = nullptr;
     return e;
   }
 
@@ -642,6 +661,8 @@ struct ccmm_chains {
     }
     hElbT0[s] = elbT0;
     hElbT[s] = elbT;
+    hSNaN[s] = m;
+    ps_dirty = true;
     HIPCHECK(hipMemcpy(dSNaN.p + (size_t)s * ET * Ns, m.data(), m.size(), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(dCens.p + (size_t)s * ET, cl.data(), ET * sizeof(int), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(dNcens.p + s, &nc, sizeof(int), hipMemcpyHostToDevice));
@@ -804,7 +825,7 @@ struct ccmm_chains {
     ra.seed = cfg.seed;
     ra.sweep = sweep;
     ra.ids = have_ids ? rngIds.p : nullptr;
-    for (int i = 0; i < 8; ++i) ra.off[i] = crn_off[i];
+    for (int i = 0; i < kRngBlocks; ++i) ra.off[i] = crn_off[i];
     return ra;
   }
 
@@ -1107,14 +1128,129 @@ struct ccmm_chains {
         hipLaunchKernelGGL(k_elb_store, dim3(d.B), dim3(256), 0, ctx->stream, e, cs, sShadow.p,
                            cfg.store_capacity, stored);
       });
+      if (ps_np > 0) {  // stackAccept (:457): ndxAccept of the stored sweep, 0 = none / Gibbs
+        sAccept.alloc(B * cap);
+        launch(KID_STORE, [&] {
+          hipLaunchKernelGGL(k_ps_store, dim3((d.B + 255) / 256), dim3(256), 0, ctx->stream,
+                             last_ps ? psFlag.p : nullptr, sAccept.p, d.B, cfg.store_capacity, stored);
+        });
+      }
     }
     ++stored;
   }
 
-  void run_elb(const RngArgs& ra) {
+  // ---------------------------------------------------------------- PS branch
+  void set_elb_ps(int np, int from_m) {
+    require(np >= 0 && np <= (1 << 20), "Nproposals must be in [0, 2^20]");
+    const int old = ps_np;
+    ps_np = np;
+    ps_from_m = np > 0 ? from_m : -1;
+    if ((old > 0) != (np > 0) && cfg.elbTmax > 0) {
+      const size_t B = cfg.B, ET = std::max(cfg.elbTmax, 1);
+      eCond.alloc(B * ET * (size_t)elb_cond_stride(cfg.Ns, cfg.p, np > 0));
+    }
+    ps_dirty = true;
+    layout_crn();
+  }
+  // band width of the censored-cell precision and the largest cell count over the slots
+  void ps_layout() {
+    if (!ps_dirty) return;
+    const int Ns = cfg.Ns, p = cfg.p, ET = std::max(cfg.elbTmax, 1);
+    int wmax = 1, nmax = 1;
+    for (int sl = 0; sl < cfg.ndata; ++sl) {
+      if (!have_elb_slot[sl]) continue;
+      std::vector<int> tcell;  // month of every censored cell, in cell order
+      for (int t = 0; t < hElbT[sl]; ++t)
+        for (int a = 0; a < Ns; ++a)
+          if (hSNaN[sl][(size_t)t * Ns + a]) tcell.push_back(t);
+      const int n = (int)tcell.size();
+      nmax = std::max(nmax, n);
+      int first = 0;  // first cell within p months before the current one
+      for (int i = 0; i < n; ++i) {
+        while (tcell[first] < tcell[i] - p) ++first;
+        wmax = std::max(wmax, i - first + 1);
+      }
+    }
+    require(wmax <= kPsWMax, "PS branch: censored-cell band width exceeds 64 (Ns (p + 1) too large)");
+    psW = wmax <= 16 ? 16 : wmax <= 32 ? 32 : wmax <= 48 ? 48 : 64;
+    ps_nmax = nmax;
+    const size_t B = cfg.B;
+    eEtPS.alloc(B * ET * cfg.N);
+    psL.alloc(B * (size_t)nmax * psW);
+    psY.alloc(B * (size_t)nmax);
+    psCell.alloc(B * (size_t)nmax);
+    psN.alloc(B);
+    psFlag.alloc(B);
+    HIPCHECK(hipMemset(psFlag.p, 0, B * sizeof(int)));
+    if (!psAcc.p) {
+      psAcc.alloc(B);
+      std::vector<int> big(B, INT_MAX);
+      HIPCHECK(hipMemcpy(psAcc.p, big.data(), B * sizeof(int), hipMemcpyHostToDevice));
+    }
+    if (!psCount.p) {
+      psCount.alloc(2 * B);
+      HIPCHECK(hipMemset(psCount.p, 0, 2 * B * sizeof(int)));
+    }
+    ps_dirty = false;
+  }
+  bool ps_active() const { return ps_np > 0 && ps_from_m > 0 && (int64_t)sweep + 1 >= ps_from_m; }
+  PsDev ps_view() const {
+    PsDev ps{};
+    ps.nmax = ps_nmax;
+    ps.W = psW;
+    ps.NP = ps_np;
+    ps.elb = cfg.elb;
+    ps.L = psL.p;
+    ps.ybar = psY.p;
+    ps.cell = psCell.p;
+    ps.n = psN.p;
+    ps.acc = psAcc.p;
+    ps.flag = psFlag.p;
+    ps.count = psCount.p;
+    return ps;
+  }
+  int last_ps = 0;  // whether the last ELB step ran the PS branch (draw store bookkeeping)
+
+  void run_ps(const RngArgs& ra, ElbDev& e, bool kept) {
+    ChainState cs = view();
+    const PsDev ps = ps_view();
+    const size_t lds = (size_t)(psW * psW + 2 * psW) * sizeof(double) + (size_t)ps_nmax * sizeof(int);
+    require(lds <= 160 * 1024, "PS branch: cell list does not fit LDS");
+    launch(KID_PSCHOL, [&] {
+      HIPCHECK(hipFuncSetAttribute((const void*)k_ps_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k_ps_chol, dim3(d.B), dim3(64), lds, ctx->stream, d, e, ps, cs);
+    });
+    launch(KID_PSPROP, [&] {
+      const dim3 g((ps_np + 255) / 256, d.B);
+      switch (psW) {
+#define CASE_PSW(W)                                                                                   \
+  case W:                                                                                             \
+    hipLaunchKernelGGL(k_ps_prop<W>, g, dim3(256), 0, ctx->stream, e, ps, ra);                        \
+    hipLaunchKernelGGL(k_ps_apply<W>, dim3(d.B), dim3(1), 0, ctx->stream, e, ps, ra, kept ? 1 : 0); \
+    break;
+        CASE_PSW(16)
+        CASE_PSW(32)
+        CASE_PSW(48)
+        CASE_PSW(64)
+#undef CASE_PSW
+        default:
+          throw ArgError("PS band width");
+      }
+    });
+    e.psFlag = psFlag.p;
+  }
+
+  void run_elb(const RngArgs& ra, bool kept) {
     if (cfg.elbTmax <= 0) return;
     ChainState cs = view();
     ElbDev e = elb_view();
+    const bool ps = ps_active();
+    last_ps = ps ? 1 : 0;
+    if (ps) {
+      ps_layout();
+      e = elb_view();
+      e.ps = 1;
+    }
     const int N = d.N, p = cfg.p, Ns = cfg.Ns, Np = N * p;
     // Φ staged in LDS when it fits (N = 20, p = 12: 40 KB); N = 120 reads it from e.Phi
     size_t lds_prep = (size_t)(2 + Np + N * (Np + 1)) * sizeof(double);
@@ -1146,6 +1282,7 @@ struct ccmm_chains {
           throw ArgError("Ns must be in [1, 4]");
       }
     });
+    if (ps) run_ps(ra, e, kept);
     const size_t lds_gibbs = (size_t)2 * e.elbTmax * Ns * sizeof(double);  // S | uniforms
     launch(KID_ELBGIBBS, [&] {
       switch (Ns) {
@@ -1381,7 +1518,7 @@ struct ccmm_chains {
     run_astep(ra);
     run_sv(ra);
     run_phi(ra);
-    if (bh) run_elb(ra);
+    if (bh) run_elb(ra, store);
     if (store) run_store();
     if (store && have_fcst) run_fcst(ra);
     ++sweep;
@@ -1915,7 +2052,7 @@ int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p
       ra = ch.rng_args(du.p, (int64_t)Ns * T * passes);
       ra.off[CCMM_RNG_ELB] = 0;
     }
-    ch.run_elb(ra);
+    ch.run_elb(ra, false);
     HIPCHECK(hipStreamSynchronize(ctx->stream));
     HIPCHECK(hipMemcpy(out, ch.eScur.p, (size_t)B * Ns * T * sizeof(double), hipMemcpyDeviceToHost));
     if (flags) HIPCHECK(hipMemcpy(flags, dfl.p, dfl.n, hipMemcpyDeviceToHost));
@@ -2086,6 +2223,7 @@ int ccmm_chains_set_state(ccmm_chains* ch, const double* PAI, const double* A,
     ch->sweep = 0;
     ch->stored = 0;
     HIPCHECK(hipMemset(ch->status.p, 0, ch->cfg.B * sizeof(int)));
+    if (ch->psCount.p) HIPCHECK(hipMemset(ch->psCount.p, 0, 2 * (size_t)ch->cfg.B * sizeof(int)));
     if (ch->have_fcst) ch->reset_fcst();
     ch->resid_valid = false;
     ch->have_state = true;
@@ -2283,6 +2421,41 @@ int ccmm_chains_set_elb_slot(ccmm_chains* ch, int slot, int elbT0, const uint8_t
     HIPCHECK(hipSetDevice(ch->ctx->device));
     HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
     ch->set_elb_slot(slot, elbT0, sNaN);
+    return 0;
+  });
+}
+
+int ccmm_chains_set_elb_ps(ccmm_chains* ch, int nproposals, int ps_from_m) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    require(ch->bh, "chain set was not created with CCMM_MODEL_BLOCKHYBRID / CCMM_MODEL_HYBRID");
+    require(nproposals == 0 || ps_from_m >= 1, "ps_from_m must be >= 1");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    ch->set_elb_ps(nproposals, ps_from_m);
+    return 0;
+  });
+}
+
+int ccmm_chains_get_ps(ccmm_chains* ch, int* countAccept, int* countAcceptBurnin, int* stackAccept) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    require(ch->ps_np > 0, "ccmm_chains_set_elb_ps was not called");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    const size_t B = ch->cfg.B, cap = ch->cfg.store_capacity, M = ch->stored;
+    std::vector<int> cnt(2 * B, 0);
+    if (ch->psCount.p) HIPCHECK(hipMemcpy(cnt.data(), ch->psCount.p, cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+    for (size_t c = 0; c < B; ++c) {
+      if (countAcceptBurnin) countAcceptBurnin[c] = cnt[2 * c];
+      if (countAccept) countAccept[c] = cnt[2 * c + 1];
+    }
+    if (stackAccept && M) {
+      std::vector<int> buf(B * cap, 0);
+      if (ch->sAccept.p) HIPCHECK(hipMemcpy(buf.data(), ch->sAccept.p, buf.size() * sizeof(int), hipMemcpyDeviceToHost));
+      for (size_t c = 0; c < B; ++c)
+        for (size_t m = 0; m < M; ++m) stackAccept[m + M * c] = buf[c * cap + m];
+    }
     return 0;
   });
 }

@@ -51,14 +51,25 @@ struct ElbDev {
   int mode;        // CCMM_ELB_MODE timing ablation (0 in production)
   const double* yhat;  // [B][elbTmax][N] explicit YHAT0 (ccmm_gibbs_shadowrates) or nullptr
   uint8_t* flags;      // [B][passes][elbTmax][Ns] truncated-normal branch flags or nullptr
+  // acceptance-sampling branch (mcmcVARshadowrateBlockHybrid.m:438-466, ccmm_ps.hip)
+  int ps;              // 1: k_elb_prep / k_elb_cond also build the PS precision records
+  double* EtPS;        // [B][elbTmax][N] residuals of the PS model (Yhatactual as intercept)
+  const int* psFlag;   // [B] PS outcome of this sweep: > 0 accepted (k_elb_gibbs skips the chain)
 };
 
 // condition record per censored month (doubles):
 //   a_t [Ns] | beta1 [Ns][Ns-1] | sqrtOmega1 [Ns] | Ω [Ns][Ns] | G [2p Ns][Ns]
 // G column col = kk*Ns + s': kk < p past lag kk+1, kk >= p future lead kk-p+1.
+// With the PS branch (e.ps) the record continues (elb_cond_ps_off):
+//   P [Ns][Ns] (the month's precision, Ω^-1) | b_PS [Ns] | gP [p Ns][Ns]
+// b_PS = the PS model's linear term with every censored cell at 0; gP = the raw unit
+// responses of the past neighbours (-gP = the off-diagonal precision blocks).
 __host__ __device__ inline int elb_cond_head(int Ns) { return Ns + Ns * (Ns - 1) + Ns + Ns * Ns; }
-__host__ __device__ inline int elb_cond_stride(int Ns, int p) {
+__host__ __device__ inline int elb_cond_ps_off(int Ns, int p) {
   return elb_cond_head(Ns) + 2 * p * Ns * Ns;
+}
+__host__ __device__ inline int elb_cond_stride(int Ns, int p, int ps = 0) {
+  return elb_cond_ps_off(Ns, p) + (ps ? Ns * Ns + Ns + p * Ns * Ns : 0);
 }
 
 // ---------------------------------------------------------------- prep (per chain)
@@ -148,6 +159,21 @@ __global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, Cha
       v -= w;
     }
     Et[q] = v;
+    if (e.ps) {
+      // PS model (mcmcVARshadowrateBlockHybrid.m:423-426): ε_τ = Yb_τ - c - yhat_τ
+      //   - Σ_{l<=τ} Φ_l Yb_{τ-l} - Σ_{l>τ} Φ_l w_{τ-l}   (w_{-1-i} = lag block i of elb.X0)
+      double u = Z[q] - PAI[(size_t)i * KP] * X0[0];  // Z = Yb - yhat
+      for (int l = 1; l <= p; ++l) {
+        if (t - l >= 0) {
+          const double* yl = Yt + (size_t)(t - l) * N;
+          for (int r = 0; r < N; ++r) u = fma(-ph[(l - 1) * N + r], yl[r], u);
+        } else {
+          const double* wl = X0 + 1 + (l - t - 1) * N;
+          for (int r = 0; r < N; ++r) u = fma(-ph[(l - 1) * N + r], wl[r], u);
+        }
+      }
+      e.EtPS[(size_t)c * e.elbTmax * N + q] = u;
+    }
   }
 }
 
@@ -367,6 +393,28 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
       G[(size_t)col * Ns + a] = v;
     }
   }
+  if (e.ps) {
+    // PS precision record (ccmm_ps.hip): P, the PS model's linear term
+    //   b_PS = -(Λ_t ε_t)_S + Σ_k B_k' Λ_{t+k} ε_{t+k}  (ε of the PS model, censored cells at 0),
+    // and the past neighbours' unit responses
+    double* ext = rec + elb_cond_ps_off(Ns, p);
+    if (lane < Ns * Ns) ext[lane] = Pm[lane];
+    const double* EP = e.EtPS + (size_t)c * e.elbTmax * N;
+    double bp[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
+    for (int j = lane; j < N; j += 64) {
+      const double u0 = -EP[(size_t)t * N + j];
+      for (int a = 0; a < Ns; ++a) bp[a] = fma(Q[(size_t)a * N + j], u0, bp[a]);
+      for (int k = 1; k <= kmax; ++k) {
+        const double r = EP[(size_t)(t + k) * N + j];
+        for (int a = 0; a < Ns; ++a) bp[a] = fma(Q[((size_t)k * Ns + a) * N + j], r, bp[a]);
+      }
+    }
+    for (int a = 0; a < Ns; ++a) {
+      const double tot = wave_sum_dpp(bp[a]);
+      if (lane == 0) ext[Ns * Ns + a] = tot;
+    }
+    for (int q = lane; q < p * Ns * Ns; q += 64) ext[Ns * Ns + Ns + q] = gS[Ns + q];
+  }
 }
 
 // ---------------------------------------------------------------- truncated normal (device)
@@ -439,6 +487,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
   const int p = e.p;
   const int T = e.elbT[s], nc = e.ncens[s];
   if (nc == 0) return;
+  if (e.psFlag && e.psFlag[c] > 0) return;  // a PS proposal was accepted (:453-454)
   const int lane = threadIdx.x;
   const Rng rng = ra.make(c);
   const int ncol = 2 * p * NS;

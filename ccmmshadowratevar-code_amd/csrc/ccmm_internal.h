@@ -18,6 +18,8 @@ inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 // ---------------------------------------------------------------- RNG
 // Philox4x32-10 (Salmon et al. 2011), counter = (pair index, chain, sweep, block),
 // key = 64-bit seed.  Two doubles per call; normals by Box-Muller.
+constexpr int kRngBlocks = 9;  // CCMM_RNG_* ids 1..8
+
 struct u32x4 {
   uint32_t x, y, z, w;
 };
@@ -50,7 +52,7 @@ struct Rng {
   const double* crn;  // this chain's CRN base for this sweep (nullptr: Philox)
   uint64_t seed;
   uint32_t chain, sweep;
-  int64_t off[8];     // CRN block offsets (indexed by CCMM_RNG_* id)
+  int64_t off[kRngBlocks];  // CRN block offsets (indexed by CCMM_RNG_* id)
 
   __host__ __device__ inline u32x4 raw(int block, uint32_t pair) const {
     return philox4x32_10(u32x4{pair, chain, sweep, (uint32_t)block}, (uint32_t)seed,
@@ -132,7 +134,7 @@ struct RngArgs {
   int64_t crn_chain_stride;
   uint64_t seed;
   uint32_t sweep;
-  int64_t off[8];
+  int64_t off[kRngBlocks];
   const uint32_t* ids;     // Philox stream id of chain c (counter word 1), nullptr: c
 
   __device__ inline Rng make(int c) const {
@@ -142,7 +144,7 @@ struct RngArgs {
     r.chain = ids ? ids[c] : (uint32_t)c;
     r.sweep = sweep;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) r.off[i] = off[i];
+    for (int i = 0; i < kRngBlocks; ++i) r.off[i] = off[i];
     return r;
   }
 };

@@ -1,0 +1,206 @@
+// Acceptance-sampling branch of the ELB step (mcmcVARshadowrateBlockHybrid.m:438-466):
+// Nproposals unconstrained draws of the censored shadow-rate cells from their joint
+// Gaussian given the VAR (the em-matlabbox precision sampler VARTVPSVprecisionsamplerNaN,
+// restated in oracle/ccmm_oracle_bh.precision_sampler_nan), the first proposal whose
+// censored cells all lie below the ELB is accepted, else the Gibbs draw serves the sweep.
+//
+// The joint precision P of the n censored cells (month-major, variables in index order,
+// the vec order of elb.yNaN) is block-banded: cells more than p months apart do not
+// interact.  k_elb_cond already evaluates its blocks per censored month (the month's
+// precision and the unit responses of the past neighbours) and, for the PS model, the
+// linear term b (Yhatactual as an intercept, :423).  Then
+//
+//   k_ps_chol  per chain, one wave: banded Cholesky P = L L' with a W x W window in LDS
+//              that streams the assembled rows in and the finished columns out (band
+//              storage L(i + j, i), j < W), and the forward solve ybar = L^-1 b
+//   k_ps_prop  per (chain, 256 proposals): x_k = L'^-1 (ybar + z_k) by back substitution,
+//              one proposal per thread with its last W values in registers (a shift
+//              window, static indices), acceptance = all x < ELB,
+//              the smallest accepted index by an LDS then a global atomic min
+//   k_ps_apply per chain: recompute the accepted proposal into the chain's shadow rates
+//              (k_elb_gibbs skips those chains), bookkeeping of :453-460
+#pragma once
+#include "ccmm_elb.hip"
+
+namespace ccmm {
+
+constexpr int kPsWMax = 64;  // band width limit: Ns (p + 1) <= 64 (Ns = 4 with p = 12: 52)
+
+struct PsDev {
+  int nmax, W, NP;  // max censored cells over slots, band width, proposals per sweep
+  double elb;
+  double* L;        // [B][nmax][W]  L(i + j, i) at [i][j], zero beyond n
+  double* ybar;     // [B][nmax]     L^-1 b
+  int* cell;        // [B][nmax]     shadow-rate offset t Ns + a of censored cell i
+  int* n;           // [B]           censored cells (0: PS skipped this sweep)
+  int* acc;         // [B]           smallest accepted proposal (0-based), INT_MAX none
+  int* flag;        // [B]           ndxAccept of this sweep (1-based), 0 none
+  int* count;       // [B][2]        accepted sweeps: [0] burn-in, [1] kept (countELBaccept*)
+};
+
+// ---------------------------------------------------------------- banded Cholesky
+__global__ __launch_bounds__(64) void k_ps_chol(Dims d, ElbDev e, PsDev ps, ChainState cs) {
+  extern __shared__ double sm[];
+  const int c = blockIdx.x;
+  const int s = cs.slot[c];
+  const int lane = threadIdx.x;
+  const int Ns = e.Ns, p = e.p, N = d.N, W = ps.W;
+  const int nc = e.ncens[s];
+  double* win = sm;                 // W x W: A(row, col) at [(row % W) W + col % W]
+  double* lv = win + W * W;         // W: the current column of L
+  double* bb = lv + W;              // W: forward-solve right-hand sides, slot i % W
+  int* info = (int*)(bb + W);       // nmax: (censored-month index << 3) | variable
+  __shared__ int sn;
+  if (lane == 0) {
+    int n = 0;
+    for (int ci = 0; ci < nc; ++ci) {
+      const int t = e.cens[(size_t)s * e.elbTmax + ci];
+      for (int a = 0; a < Ns; ++a)
+        if (e.sNaN[((size_t)s * e.elbTmax + t) * Ns + a]) info[n++] = (ci << 3) | a;
+    }
+    sn = n;
+  }
+  __syncthreads();
+  const int n = sn;
+  for (int i = lane; i < n; i += 64) {
+    const int ci = info[i] >> 3, a = info[i] & 7;
+    ps.cell[(size_t)c * ps.nmax + i] = e.cens[(size_t)s * e.elbTmax + ci] * Ns + a;
+  }
+  if (lane == 0) ps.n[c] = n;
+  if (n == 0) return;
+  const double* recs = e.cond + (size_t)c * e.elbTmax * e.condStride;
+  const int xo = elb_cond_ps_off(Ns, p);
+  // P(i, j), i >= j, from the month records (ccmm_elb.hip: P | b_PS | gP)
+  auto pentry = [&](int i, int j) -> double {
+    const int ci = info[i] >> 3, ai = info[i] & 7, cj = info[j] >> 3, aj = info[j] & 7;
+    const int kp = e.cens[(size_t)s * e.elbTmax + ci] - e.cens[(size_t)s * e.elbTmax + cj];
+    const double* x = recs + (size_t)ci * e.condStride + xo;
+    if (kp == 0) return x[ai * Ns + aj];
+    if (kp > p) return 0.0;
+    return -x[Ns * Ns + Ns + ((kp - 1) * Ns + aj) * Ns + ai];
+  };
+  // b(i): the PS linear term given the month's observed (uncensored) shadow rates
+  auto rhs = [&](int i) -> double {
+    const int ci = info[i] >> 3, ai = info[i] & 7;
+    const int t = e.cens[(size_t)s * e.elbTmax + ci];
+    const double* x = recs + (size_t)ci * e.condStride + xo;
+    double v = x[Ns * Ns + ai];
+    for (int b = 0; b < Ns; ++b)
+      if (!e.sNaN[((size_t)s * e.elbTmax + t) * Ns + b])
+        v -= x[ai * Ns + b] * e.Yt[((size_t)c * e.elbTmax + t) * N + e.ndxS[b]];
+    return v;
+  };
+  for (int q = lane; q < W * W; q += 64) {
+    const int r = q / W, cc = q % W;
+    win[q] = (cc <= r && r < n) ? pentry(r, cc) : 0.0;
+  }
+  if (lane < W) bb[lane] = lane < n ? rhs(lane) : 0.0;
+  __syncthreads();
+  double* Lg = ps.L + (size_t)c * ps.nmax * W;
+  bool fail = false;
+  for (int k = 0; k < n; ++k) {
+    const int r = lane;
+    const double v = (r < W && k + r < n) ? win[((k + r) % W) * W + k % W] : 0.0;
+    const double dkk = readlane_d(v, 0);
+    fail |= !(dkk > 0.0);
+    const double lkk = sqrt(fabs(dkk) > 0.0 ? fabs(dkk) : 1.0);
+    const double l = (r == 0) ? lkk : v / lkk;
+    if (r < W) {
+      Lg[(size_t)k * W + r] = l;
+      lv[r] = l;
+    }
+    const double yk = bb[k % W] / lkk;
+    if (r == 0) ps.ybar[(size_t)c * ps.nmax + k] = yk;
+    __syncthreads();
+    if (r >= 1 && r < W && k + r < n) {
+      bb[(k + r) % W] -= l * yk;
+      double* row = win + ((k + r) % W) * W;
+      for (int cc = 1; cc <= r; ++cc) row[(k + cc) % W] -= l * lv[cc];
+    }
+    __syncthreads();
+    // row k + W enters the window (its entries left of column k + 1 are outside the band)
+    const int nr = k + W;
+    if (nr < n) {
+      if (r < W) win[(nr % W) * W + (nr - r) % W] = pentry(nr, nr - r);
+      if (r == 0) bb[nr % W] = rhs(nr);
+    }
+    __syncthreads();
+  }
+  if (fail) {  // not positive definite: no proposals, the Gibbs draw serves the sweep
+    if (lane == 0) {
+      ps.n[c] = 0;
+      cs.status[c] |= 32;
+    }
+  }
+}
+
+// x = L'^-1 (ybar + z_k): one proposal by back substitution, the W - 1 values x_{i+1..i+W-1}
+// in registers (win[j - 1] = x_{i + j}, shifted down one slot per step so every index is
+// static).  out != nullptr writes x into the chain's shadow rates.  Returns whether every
+// cell lies below the ELB.
+template <int W>
+__device__ inline bool ps_backsub(const double* __restrict__ Lc, const double* __restrict__ yb, int n,
+                                  const Rng& rng, int k, double elb, double* out, const int* cell) {
+  double win[W - 1];
+#pragma unroll
+  for (int j = 0; j < W - 1; ++j) win[j] = 0.0;
+  bool ok = true;
+  for (int i = n - 1; i >= 0; --i) {
+    const double* li = Lc + (size_t)i * W;
+    double v = yb[i] + rng.normal(CCMM_RNG_PS, (uint32_t)(i + n * k));
+#pragma unroll
+    for (int j = 1; j < W; ++j) v = fma(-li[j], win[j - 1], v);
+    v /= li[0];
+#pragma unroll
+    for (int j = W - 2; j >= 1; --j) win[j] = win[j - 1];
+    win[0] = v;
+    ok = ok && (v < elb);
+    if (out) out[cell[i]] = v;
+  }
+  return ok;
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_ps_prop(ElbDev e, PsDev ps, RngArgs ra) {
+  const int c = blockIdx.y;
+  const int n = ps.n[c];
+  if (n == 0) return;
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  __shared__ int kmin;
+  if (threadIdx.x == 0) kmin = INT_MAX;
+  __syncthreads();
+  if (k < ps.NP) {
+    const Rng rng = ra.make(c);
+    const bool ok = ps_backsub<W>(ps.L + (size_t)c * ps.nmax * W, ps.ybar + (size_t)c * ps.nmax, n, rng, k,
+                                  ps.elb, nullptr, nullptr);
+    if (ok) atomicMin(&kmin, k);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && kmin != INT_MAX) atomicMin(ps.acc + c, kmin);
+}
+
+template <int W>
+__global__ __launch_bounds__(64) void k_ps_apply(ElbDev e, PsDev ps, RngArgs ra, int kept) {
+  const int c = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  const int n = ps.n[c];
+  const int kmin = ps.acc[c];
+  ps.acc[c] = INT_MAX;
+  if (n == 0 || kmin == INT_MAX) {
+    ps.flag[c] = 0;
+    return;
+  }
+  const Rng rng = ra.make(c);
+  (void)ps_backsub<W>(ps.L + (size_t)c * ps.nmax * W, ps.ybar + (size_t)c * ps.nmax, n, rng, kmin, ps.elb,
+                      e.Scur + (size_t)c * e.elbTmax * e.Ns, ps.cell + (size_t)c * ps.nmax);
+  ps.flag[c] = kmin + 1;
+  ps.count[2 * c + (kept ? 1 : 0)] += 1;
+}
+
+// stackAccept(thisMCMCdraw) = ndxAccept (:457), 0 when the sweep fell back to Gibbs
+__global__ void k_ps_store(const int* flag, int* out, int B, int cap, int m) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < B) out[(size_t)c * cap + m] = flag ? flag[c] : 0;
+}
+
+}  // namespace ccmm

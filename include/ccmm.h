@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define CCMM_ABI_VERSION 2
+#define CCMM_ABI_VERSION 3
 
 /* return codes */
 #define CCMM_OK 0
@@ -62,6 +62,7 @@ extern "C" {
 #define CCMM_RNG_PHI 5   /* randn(N,T+d_PHI)      mcmcVAR.m:268 */
 #define CCMM_RNG_ELB 6   /* rand(Ns,elbT,101)     gibbsdrawShadowrates.m:173 */
 #define CCMM_RNG_FCST 7  /* randn(N,H*Nd) then randn(N,H,Nd)  mcmcVAR.m:302,306 */
+#define CCMM_RNG_PS 8    /* randn(nmiss,Nproposals)  PS proposals, mcmcVARshadowrateBlockHybrid.m:439-441 */
 
 typedef struct ccmm_ctx ccmm_ctx;
 typedef struct ccmm_chains ccmm_chains;
@@ -293,6 +294,23 @@ int ccmm_chains_set_elb_model(ccmm_chains* ch, const int* ndxS, const uint8_t* a
  * sNaN Ns x elbT (column-major, elbT = T_slot - elbT0): nonzero where the shadow
  * rate is censored (data <= ELB, :163-171).  Call after ccmm_chains_set_data. */
 int ccmm_chains_set_elb_slot(ccmm_chains* ch, int slot, int elbT0, const uint8_t* sNaN);
+/* Acceptance-sampling branch of the ELB step (mcmcVARshadowrateBlockHybrid.m:435-466):
+ * from sweep m >= ps_from_m (1-based; the reference: m >= MCMCburnin/2, i.e.
+ * ps_from_m = ceil(MCMCburnin/2)) every sweep first draws nproposals (elb.Nproposals =
+ * 1e3, :188) unconstrained proposals of the censored cells from their joint Gaussian
+ * given the VAR — the em-matlabbox sampler VARTVPSVprecisionsamplerNaN (:439-441), restated
+ * as the precision sampler y_m = L' \ (L \ b + z_k), P = L L' — and accepts the first
+ * whose censored cells all lie below the ELB (:446-452); otherwise the Gibbs draw of
+ * gibbsdrawShadowrates serves the sweep (:462-463).  CRN mode appends randn(nmiss,
+ * nproposals) (block CCMM_RNG_PS, nmiss x nproposals column-major, sized Ns elbTmax
+ * nproposals) to every sweep's record.  nproposals = 0: Gibbs every sweep (default).
+ * Requires Ns (p + 1) <= 64. */
+int ccmm_chains_set_elb_ps(ccmm_chains* ch, int nproposals, int ps_from_m);
+/* PS bookkeeping (:303-305, 453-460): countAccept / countAcceptBurnin B ints since set_state
+ * (sweeps whose proposal was accepted after / during burn-in), stackAccept M x B ints
+ * (ndxAccept of each stored draw, 0 = no proposal accepted or Gibbs sweep; M = stored draws;
+ * call before ccmm_chains_get_draws, which resets the store).  Any pointer may be NULL. */
+int ccmm_chains_get_ps(ccmm_chains* ch, int* countAccept, int* countAcceptBurnin, int* stackAccept);
 /* Current shadow rates, Ns x elbTmax x B (the last sweep's draw). */
 int ccmm_chains_get_shadowrate(ccmm_chains* ch, double* shadowrate);
 /* Current per-chain data: X T x K x B, Y T x N x B (block-hybrid: the chain's

@@ -5,10 +5,10 @@ PARITY UNPINNED (MATLAB reference, no fixtures).  Follows the reference as
 written: CTAsys with per-equation designs (actual-rate X for the macro block,
 shadow-rate X for the yield block), the linear A/SV/PHI blocks, then the ELB
 step with gibbsdrawShadowrates (QR smoothing weights, 100 burn-in + 1 Gibbs
-passes: the ``m < MCMCburnin*.5`` branch, mcmcVARshadowrateBlockHybrid.m:435-437,
-forced every sweep — the PS-proposal branch needs the absent em-matlabbox
-sampler VARTVPSVprecisionsamplerNaN), and the rebuild of X, Y from the shadow
-draws (:501-520).
+passes: the ``m < MCMCburnin*.5`` branch, mcmcVARshadowrateBlockHybrid.m:435-437)
+or the acceptance-sampling branch (:438-466) on a restatement of the absent
+em-matlabbox sampler VARTVPSVprecisionsamplerNaN (precision_sampler_nan), and
+the rebuild of X, Y from the shadow draws (:501-520).
 """
 from __future__ import annotations
 
@@ -62,15 +62,20 @@ def bh_setup(thisT, p, np_, data0, ydates0, ndxS, ndxO, minnesotaPriorMean, ELBb
                    sNaN=sNaN, X0=lin.X[elbT0, :].copy(), ELB=ELBbound)
 
 
-def bh_crn_sizes(bs: BHSetup):
+def bh_crn_sizes(bs: BHSetup, nproposals=0):
+    """Per-sweep CRN blocks; nproposals > 0 appends the PS proposal normals
+    randn(nmiss, Nproposals) (VARTVPSVprecisionsamplerNaN, :439-441)."""
     lin = bs.lin
-    return O.crn_sizes(lin.N, lin.K, lin.T, lin.dPHI) + [
+    out = O.crn_sizes(lin.N, lin.K, lin.T, lin.dPHI) + [
         ("uELB", (len(bs.ndxS), bs.elbT, bs.gibbsburn + 1))]
+    if nproposals:
+        out.append(("zPS", (int(bs.sNaN.sum()), int(nproposals))))
+    return out
 
 
-def bh_draw_crn(rng, bs: BHSetup):
+def bh_draw_crn(rng, bs: BHSetup, nproposals=0):
     out = {}
-    for name, shape in bh_crn_sizes(bs):
+    for name, shape in bh_crn_sizes(bs, nproposals):
         out[name] = rng.random(shape) if name.startswith("u") else rng.standard_normal(shape)
     return out
 
@@ -103,13 +108,96 @@ def rebuild_XY(bs: BHSetup, shadowrate):
     return X, Y
 
 
+def precision_sampler_nan(pai3, invbbb, Y, yNaN, Y0, pai0, z):
+    """Missing-value draws of the VAR with time-varying volatility given the observed
+    cells: the interface of em-matlabbox VARTVPSVprecisionsamplerNaN (called at
+    mcmcVARshadowrateBlockHybrid.m:428,439-441,471-473,483-485; source absent, PARITY
+    UNPINNED — restated as the precision-based sampler its name and arguments describe).
+
+      model:  invbbb_t (y_t - pai0_t - sum_l pai3_l y_{t-l}) = e_t ~ N(0, I),  t = 1..T,
+              y_{1-l} = Y0(:, l) (the fixed pre-window lags, :426)
+      stack:  AA vec(Y) = cc + e;  split vec(Y) into missing m / observed o (yNaN):
+              P = AA_m' AA_m,  b = AA_m' (cc - AA_o y_o),  P = L L' (lower Cholesky)
+      draw k: y_m = L' \\ (L \\ b + z_k)   (= P^-1 b + L'^-1 z_k),  z = randn(nmiss, Ndraws)
+
+    pai3 N x N x p (pai3(:,:,l) = Phi_l), invbbb N x N x T, Y N x T (missing cells
+    ignored), yNaN N x T bool, Y0 N x p, pai0 N x T, z nmiss x Ndraws (missing cells in
+    vec order: month-major, variables in index order).  Returns YYdraws N*T x Ndraws
+    (observed cells copied)."""
+    N, T = Y.shape
+    p = pai3.shape[2]
+    NT = N * T
+    AA = np.zeros((NT, NT))
+    cc = np.zeros(NT)
+    for t in range(T):
+        Bt = invbbb[:, :, t]
+        r = slice(t * N, (t + 1) * N)
+        AA[r, r] = Bt
+        c = pai0[:, t].copy()
+        for l in range(1, p + 1):
+            if t - l >= 0:
+                AA[r, (t - l) * N:(t - l + 1) * N] = -Bt @ pai3[:, :, l - 1]
+            else:
+                c += pai3[:, :, l - 1] @ Y0[:, l - t - 1]
+        cc[r] = Bt @ c
+    m = np.asarray(yNaN, bool).ravel(order="F")
+    y = np.asarray(Y, float).ravel(order="F").copy()
+    y[m] = 0.0
+    Am = AA[:, m]
+    P = Am.T @ Am
+    b = Am.T @ (cc - AA[:, ~m] @ y[~m])
+    L = np.linalg.cholesky(P)
+    from scipy.linalg import solve_triangular
+    ybar = solve_triangular(L, b, lower=True)
+    xm = solve_triangular(L.T, ybar[:, None] + np.asarray(z, float).reshape(m.sum(), -1),
+                          lower=False)
+    out = np.repeat(y[:, None], xm.shape[1], axis=1)
+    out[m, :] = xm
+    return out
+
+
+def ps_inputs(bs: BHSetup, PAI, A, sqrtht):
+    """Arguments of the VARTVPSVprecisionsamplerNaN calls (mcmcVARshadowrateBlockHybrid.m:
+    400-426): pai3, invbbb, elb.Y (missing cells 0), elb.yNaN, elbY0, pai0."""
+    lin = bs.lin
+    N, p = lin.N, lin.p
+    _, _, SVol, Yhatactual = elb_state_space(bs, PAI, np.linalg.inv(A), sqrtht)
+    PAIshadow = PAI.copy()
+    PAIshadow[np.ix_(bs.lagmask, bs.actualrateBlock)] = 0.0
+    pai0 = PAIshadow[0, :][:, None] + Yhatactual                                    # :423
+    pai3 = PAIshadow[1:, :].T.reshape(N, N, p, order="F")                           # :424
+    invbbb = A[:, :, None] / SVol[:, None, :]                                        # :425
+    elbY0 = bs.X0[1:].reshape(N, p, order="F")                                       # :426
+    yNaN = np.zeros((N, bs.elbT), bool)
+    yNaN[bs.ndxS, :] = bs.sNaN
+    Y = np.where(yNaN, 0.0, bs.Ydata[lin.p + bs.elbT0:, :].T)
+    return pai3, invbbb, Y, yNaN, elbY0, pai0
+
+
+def ps_shadowrate(bs: BHSetup, PAI, A, sqrtht, zPS):
+    """Acceptance-sampling branch of the ELB step (m >= MCMCburnin/2,
+    mcmcVARshadowrateBlockHybrid.m:438-460): Nproposals unconstrained draws of the
+    censored cells, the first whose censored cells all lie below the ELB is accepted.
+    Returns (shadowrate Ns x elbT or None, ndxAccept 1-based or 0)."""
+    N = bs.lin.N
+    YY = precision_sampler_nan(*ps_inputs(bs, PAI, A, sqrtht), zPS)
+    YY = YY.reshape(N, bs.elbT, -1, order="F")
+    props = YY[bs.ndxS, :, :]                                                        # :444
+    for k in range(props.shape[2]):                                                  # :446-452
+        if np.all(props[:, :, k][bs.sNaN] < bs.ELB):
+            return props[:, :, k], k + 1
+    return None, 0
+
+
 def bh_init_state(bs: BHSetup):
     st = O.init_state(bs.lin)  # Y = Y0, X = X0 (actual data), mcmcVARshadowrateBlockHybrid.m:310-316
     return st
 
 
-def bh_sweep(st, bs: BHSetup, crn, return_flags=False, elb_impl="qr"):
-    """One sweep m < MCMCburnin/2 of mcmcVARshadowrateBlockHybrid.m:322-523.
+def bh_sweep(st, bs: BHSetup, crn, return_flags=False, elb_impl="qr", use_ps=False):
+    """One sweep of mcmcVARshadowrateBlockHybrid.m:322-523: the Gibbs ELB branch
+    (m < MCMCburnin/2, :435-437), or with use_ps the acceptance-sampling branch
+    (:438-466: PS proposals crn["zPS"], the first accepted, else the Gibbs draw).
 
     elb_impl: "qr" = gibbsdrawShadowrates as written; "stable" = the same
     conditionals in the residual form of elb_fast.gibbsdraw_shadowrates_stable
@@ -140,6 +228,14 @@ def bh_sweep(st, bs: BHSetup, crn, return_flags=False, elb_impl="qr"):
         C, Psi, SVol, Yhatactual = elb_state_space(bs, PAI, invA, sqrtht)
         elbY = Y[bs.elbT0:, :].T
         flags = None
+        if use_ps:
+            sr, k = ps_shadowrate(bs, PAI, A, sqrtht, crn["zPS"])
+            out["ps_accept"] = k
+            if k:
+                Xn, Yn = rebuild_XY(bs, sr)
+                out.update(X=Xn, Y=Yn, shadowrate=sr, shadowrate_qr=sr, elb_flags=None,
+                           elb_flags_stable=None)
+                return out
         if elb_impl in ("qr", "both"):
             res = O.gibbsdraw_shadowrates(elbY, bs.X0, Yhatactual, bs.ndxSmask, bs.sNaN, lin.p, C,
                                           Psi, SVol, bs.ELB, 1, bs.gibbsburn, crn["uELB"],

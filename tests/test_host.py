@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_host_entry_points(pkg):
     lib = pkg.load_library()
-    assert lib.ccmm_abi_version() == 2
+    assert lib.ccmm_abi_version() == 3
     # the ChainConfig ctypes mirror has the header's fields in order
     src = (ROOT / "include" / "ccmm.h").read_text()
     start = src.index("typedef struct {", src.index("sweep-level")) + len("typedef struct {")

@@ -139,3 +139,61 @@ def test_bh_sweep_oracle_toy(bh):
     for l in range(1, p + 1):  # X lag columns hold the shadow rates
         np.testing.assert_array_equal(out["X"][bs.elbT0 + l:, 1 + (l - 1) * N + bs.ndxS],
                                       out["Y"][bs.elbT0:bs.lin.T - l, bs.ndxS])
+
+
+def test_ps_joint_matches_gibbs_conditionals(bh):
+    """The PS proposal density (precision_sampler_nan: joint Gaussian of all censored cells
+    from the stacked VAR likelihood) and the Gibbs sampler's per-month conditionals
+    (elb_fast, what k_elb_cond evaluates) share the precision: the conditional covariance
+    of month t's censored cells given the other censored cells agrees.  The means differ by
+    the reference's own model difference: gibbsdrawShadowrates.m:157-165 treats YHAT0 as a
+    measurement offset of a VAR on Y - Y0 (and lags Y0 one period), while the PS call
+    enters Yhatactual as an intercept (pai0, mcmcVARshadowrateBlockHybrid.m:423); the
+    device evaluates each branch's own mean (k_elb_cond: Gibbs a_t, PS b_t)."""
+    from oracle import elb_fast as F
+    bs = toy_bh_setup(bh)
+    O, st, C, Psi, SVol, Yhat, _ = _elb_inputs(bh, bs, 11)
+    rng = np.random.default_rng(11)
+    lin = bs.lin
+    A = np.linalg.inv(Psi[1:1 + lin.N, :])
+    sqrtht = np.ones((lin.T, lin.N))
+    sqrtht[bs.elbT0:, :] = SVol.T
+    args = bh.ps_inputs(bs, st["PAI"], A, sqrtht)
+    n = int(bs.sNaN.sum())
+    Z = np.concatenate([np.zeros((n, 1)), np.eye(n)], axis=1)
+    YY = bh.precision_sampler_nan(*args, Z)
+    m = args[3].ravel(order="F")
+    X = YY[m, :]
+    mu = X[:, 0]
+    Lt = X[:, 1:] - mu[:, None]                 # L'^-1
+    Sig = Lt @ Lt.T
+    Prec = np.linalg.inv(Sig)
+    # cell index of (series si, month t) in the missing vector (month-major)
+    idx = -np.ones(bs.sNaN.shape, int)
+    idx.T[bs.sNaN.T] = np.arange(n)
+    elbY = st["Y"][bs.elbT0:, :].T
+    Yb = elbY.copy()
+    S = np.flatnonzero(bs.ndxSmask)
+    tmp = Yb[S, :]
+    tmp[bs.sNaN] = 0.0
+    Yb[S, :] = tmp
+    e0 = F.e0_path(C, bs.X0, Yhat, lin.N, bs.elbT, lin.p)
+    cond = F.elb_conditionals_stable(Yb, e0, bs.ndxSmask, bs.sNaN, lin.p, C, Psi, SVol)
+    worst = 0.0
+    for t, (base, coef, Om) in cond.items():
+        c = np.flatnonzero(bs.sNaN[:, t])
+        o = np.flatnonzero(~bs.sNaN[:, t])
+        ci = idx[c, t]
+        # joint: covariance of x_c given the other censored cells
+        jc = np.linalg.inv(Prec[np.ix_(ci, ci)])
+        # Gibbs record: all Ns cells of month t given the neighbours, then given the observed
+        gc = Om[np.ix_(c, c)]
+        if o.size:
+            gc = gc - Om[np.ix_(c, o)] @ np.linalg.solve(Om[np.ix_(o, o)], Om[np.ix_(o, c)])
+        worst = max(worst, np.max(np.abs(jc - gc)) / np.max(np.abs(gc)))
+    assert worst < 1e-9, worst
+    # and the draws: proposal k = mu + L'^-1 z_k
+    z = rng.standard_normal((n, 3))
+    YY3 = bh.precision_sampler_nan(*args, z)
+    assert np.allclose(YY3[m, :], mu[:, None] + Lt @ z, atol=1e-10)
+    assert np.array_equal(YY3[~m, :], np.repeat(args[2].ravel(order="F")[~m][:, None], 3, 1))
