@@ -121,13 +121,16 @@ def mcmcVARshadowrateBlockHybrid(thisT, MCMCdraws, p, np_, data0, ydates0, actua
                                  check_stationarity=0, IRF1scale=None, IRFcumcode=None,
                                  yrealized=None, fcstNdraws=None, fcstNhorizons=None,
                                  rndStream=1012023, doprogress=False, *, nchains=1, device=0,
-                                 burnin=None, gibbsburn=100):
+                                 burnin=None, gibbsburn=100, Nproposals=1000, elb_ps=True,
+                                 stats=None):
     """mcmcVARshadowrateBlockHybrid.m:1-14, outputs PAI_all, PHI_all, invA_all,
     sqrtht_all, shadowrate_all (M x Nshadowrates x elbT), missingrate_all (NaN).
 
-    The ELB step is the Gibbs sampler of the ``m < MCMCburnin*.5`` branch
-    (:435-437) at every sweep: the acceptance-sampling branch needs
-    VARTVPSVprecisionsamplerNaN from the absent em-matlabbox toolbox.
+    The ELB step follows :433-466: the Gibbs sampler for m < MCMCburnin/2, then the
+    acceptance-sampling branch (Nproposals draws of the precision sampler restated from
+    the absent VARTVPSVprecisionsamplerNaN, first accepted, else the Gibbs draw).
+    elb_ps=False keeps the Gibbs branch at every sweep.  ``stats`` (a dict, optional)
+    receives countELBaccept / countELBacceptBurnin / stackAccept (:303-305, 453-460).
     Indices are 0-based; actualrateBlock is a bool vector of length N."""
     if check_stationarity:
         raise NotImplementedError("check_stationarity=1 is not supported; the reference drivers "
@@ -160,6 +163,8 @@ def mcmcVARshadowrateBlockHybrid(thisT, MCMCdraws, p, np_, data0, ydates0, actua
     ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
     ch.set_elb_model(bm.ndxS, bm.actual_block)
     ch.set_elb_slot(0, bm.elbT0, bm.sNaN)
+    if elb_ps and Nproposals:
+        ch.set_elb_ps(Nproposals, max(1, -(-burn // 2)))  # m >= MCMCburnin * .5 (:435)
     st = initial_state(m, B)
     ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
     if doPredictiveDensity:
@@ -173,6 +178,10 @@ def mcmcVARshadowrateBlockHybrid(thisT, MCMCdraws, p, np_, data0, ydates0, actua
     _run_chain_set(ch, burn, MCMCdraws, doprogress)
     if doPredictiveDensity:
         fc = ch.get_fcst(paths=True)
+    if stats is not None and elb_ps and Nproposals:
+        ps = ch.get_ps()
+        stats.update(countELBaccept=ps["countAccept"], countELBacceptBurnin=ps["countAcceptBurnin"],
+                     stackAccept=ps["stackAccept"])
     out = ch.get_draws()
     ch.close()
     sr = out.get("shadowrate_all", np.full((MCMCdraws, len(bm.ndxS), 0, B), np.nan))
@@ -195,14 +204,14 @@ def mcmcVARhybridGibbs(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateWeigh
                        doELBsampleAlternate, ELBbound, elbT0, check_stationarity=0, IRF1scale=None,
                        IRFcumcode=None, yrealized=None, fcstNdraws=None, fcstNhorizons=None,
                        rndStream=1012023, doprogress=False, *, nchains=1, device=0, burnin=None,
-                       gibbsburn=100):
+                       gibbsburn=100, Nproposals=1000, elb_ps=True, stats=None):
     """mcmcVARhybridGibbs.m:1-14, outputs PAI_all (M x K x N, K = 1 + N p + Ns p),
     PHI_all, invA_all, sqrtht_all, shadowrate_all (M x Nshadowrates x elbT),
     missingrate_all (NaN: it is the first PS proposal, :486).
 
-    The reference draws the shadow rates by accept-first PS proposals with the Gibbs
-    sampler as fallback (:458-483); the proposal sampler VARTVPSVprecisionsamplerNaN
-    is in the absent em-matlabbox toolbox, so the Gibbs draw serves every sweep.
+    The shadow rates are drawn by accept-first PS proposals at every sweep with the Gibbs
+    sampler as fallback (:458-483), the proposal sampler restated from the absent
+    em-matlabbox VARTVPSVprecisionsamplerNaN (elb_ps=False: Gibbs every sweep).
     actualrateWeight is unused, as in the reference (:16).  Indices are 0-based."""
     if check_stationarity:
         import warnings
@@ -227,9 +236,15 @@ def mcmcVARhybridGibbs(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateWeigh
     ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
     ch.set_elb_model(hm.ndxS, None)
     ch.set_elb_slot(0, hm.elbT0, hm.sNaN)
+    if elb_ps and Nproposals:
+        ch.set_elb_ps(Nproposals, 1)                   # every sweep (:458)
     st = initial_state(m, B)
     ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
     _run_chain_set(ch, burn, MCMCdraws, doprogress)
+    if stats is not None and elb_ps and Nproposals:
+        ps = ch.get_ps()
+        stats.update(countELBaccept=ps["countAccept"] + ps["countAcceptBurnin"],
+                     stackAccept=ps["stackAccept"])
     out = ch.get_draws()
     ch.close()
     sr = out.get("shadowrate_all", np.full((MCMCdraws, len(hm.ndxS), 0, B), np.nan))
@@ -435,7 +450,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                                      MCMCdraws=1000, fcstNdraws=None, fcstNhorizons=48,
                                      ELBbound=0.25, doRATSprior=True, nchains=1, burnin=None,
                                      gibbsburn=100, rndStream=1012023, dist=None, device=None,
-                                     chunk=50, max_retries=2, keep_draws=False, progress=False):
+                                     chunk=50, max_retries=2, keep_draws=False, progress=False,
+                                     Nproposals=1000, elb_ps=True):
     """The quasi-real-time OOS run of goVARshadowrateBlockHybrid.m:126-517 for the block-
     hybrid shadow-rate VAR, as ONE device-resident chain set per rank: every vintage
     thisT in Tjumpoffs (default: ydates > 2008-12, :127) is a data slot of the set with
@@ -446,9 +462,9 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
 
     Per chain: MCMCdraws burn-in + MCMCdraws kept sweeps (mcmcVARshadowrateBlockHybrid.m:
     56-58); every kept sweep stores the draw and simulates fcstNdraws / MCMCdraws forecast
-    paths on the device (:550-625).  The ELB step is the Gibbs sampler at every sweep (the
-    PS-proposal branch, :438-466, needs the absent em-matlabbox sampler; the reference
-    falls back to the same Gibbs draw).  Philox streams are keyed by the global unit
+    paths on the device (:550-625).  The ELB step is the Gibbs sampler for m < MCMCburnin/2
+    and the accept-first PS proposals (Nproposals) after, as mcmcVARshadowrateBlockHybrid.m:
+    433-466 (elb_ps=False: Gibbs every sweep).  Philox streams are keyed by the global unit
     (vintage index * nchains + chain), so results do not depend on the number of ranks.
 
     Failure recovery (:287-310): chains whose blocks flagged a non-SPD pivot
@@ -508,6 +524,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                                           store_capacity=chunk, gibbsburn=gibbsburn,
                                           ELBbound=ELBbound, ndxYIELDS=ndxYIELDS,
                                           fcstNhorizons=H, Nd=Nd)
+        if elb_ps and Nproposals and ch.elbTmax:
+            ch.set_elb_ps(Nproposals, max(1, -(-burn // 2)))  # m >= MCMCburnin * .5 (:435)
         B = ch.B
         done = 0
         while done < burn:
@@ -544,6 +562,10 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
             if progress:
                 print(f"[rank {rank}] kept {done}/{MCMCdraws}", flush=True)
         status = ch.get_status()
+        nacc = None
+        if elb_ps and Nproposals and ch.elbTmax:
+            psd = ch.get_ps()
+            nacc = psd["countAccept"] + psd["countAcceptBurnin"]
         ch.close()
         res, failed = {}, []
         for k, i in enumerate(vidx):
@@ -554,6 +576,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
             thisT, bm, yr = units[i]
             nk = MCMCdraws * C
             r = dict(thisT=thisT, yrealized=yr,
+                     countELBaccept=None if nacc is None else int(nacc[cs].sum()),
                      logscore=_logmeanexp(scores[:, :, 1, cs].ravel()),
                      logscoreX=_logmeanexp(scores[:, :, 2, cs].ravel()),
                      logscoreI=_logmeanexp(scores[:, :, 3, cs].ravel()),
@@ -604,6 +627,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                fcstYmvlogscoreI=np.full(V, np.nan), fcstYhat=np.full((N, H, V), np.nan),
                fcstShadowYhat=np.full((Ny, H, V), np.nan), fcstYrealized=np.full((N, H, V), np.nan),
                PAImean=np.full((K, N, V), np.nan), PAIstdev=np.full((K, N, V), np.nan),
+               countELBaccept=np.full(V, -1),
                shadowrateVintagesMid=np.full((Tdata, Ns, V), np.nan),
                shadowrateVintagesTails=np.full((Tdata, Ns, 4, V), np.nan))
     if keep_draws:
@@ -621,6 +645,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
         out["fcstYrealized"][..., v] = r["yrealized"]
         out["PAImean"][..., v] = r["PAImean"]
         out["PAIstdev"][..., v] = r["PAIstdev"]
+        if r.get("countELBaccept") is not None:
+            out["countELBaccept"][v] = r["countELBaccept"]
         if "shadowrateMid" in r:
             thisT = r["thisT"]
             out["shadowrateVintagesMid"][jumpoff:thisT, :, v] = r["shadowrateMid"]

@@ -94,15 +94,43 @@ def hybrid_setup(thisT, p, np_, data0, ydates0, ndxS, minnesotaPriorMean, ELBbou
                        Ydata=Ydata, elbT0=elbT0, elbT=elbT, sNaN=sNaN, X0=X0, ELB=ELBbound)
 
 
-def hybrid_crn_sizes(hs: HybridSetup):
+def hybrid_crn_sizes(hs: HybridSetup, nproposals=0):
     lin = hs.lin
-    return O.crn_sizes(lin.N, lin.K, lin.T, lin.dPHI) + [
+    out = O.crn_sizes(lin.N, lin.K, lin.T, lin.dPHI) + [
         ("uELB", (len(hs.ndxS), hs.elbT, hs.gibbsburn + 1))]
+    if nproposals:
+        out.append(("zPS", (int(hs.sNaN.sum()), int(nproposals))))
+    return out
 
 
-def hybrid_draw_crn(rng, hs: HybridSetup):
+def hybrid_draw_crn(rng, hs: HybridSetup, nproposals=0):
     return {name: (rng.random(shape) if name.startswith("u") else rng.standard_normal(shape))
-            for name, shape in hybrid_crn_sizes(hs)}
+            for name, shape in hybrid_crn_sizes(hs, nproposals)}
+
+
+def ps_shadowrate(hs: HybridSetup, PAI, A, sqrtht, zPS):
+    """mcmcVARhybridGibbs.m:446-483: PS proposals from the precision sampler
+    (ccmm_oracle_bh.precision_sampler_nan) with PAIshadow = PAI(1:Kshadow,:) and the
+    actual-rate lags' fit as intercept; returns (shadowrate or None, ndxAccept)."""
+    from .ccmm_oracle_bh import precision_sampler_nan
+    lin = hs.lin
+    N, p, Ks = lin.N, lin.p, hs.Kshadow
+    _, _, SVol, Yhatactual = elb_state_space(hs, PAI, np.linalg.inv(A), sqrtht)
+    PAIshadow = PAI[:Ks, :]
+    pai0 = PAIshadow[0, :][:, None] + Yhatactual                                    # :448
+    pai3 = PAIshadow[1:, :].T.reshape(N, N, p, order="F")                           # :449
+    invbbb = A[:, :, None] / SVol[:, None, :]                                        # :450
+    elbY0 = hs.X0[1:1 + N * p].reshape(N, p, order="F")
+    yNaN = np.zeros((N, hs.elbT), bool)
+    yNaN[hs.ndxS, :] = hs.sNaN
+    Y = np.where(yNaN, 0.0, hs.Ydata[lin.p + hs.elbT0:, :].T)
+    YY = precision_sampler_nan(pai3, invbbb, Y, yNaN, elbY0, pai0, zPS).reshape(N, hs.elbT, -1,
+                                                                                order="F")
+    props = YY[hs.ndxS, :, :]
+    for k in range(props.shape[2]):                                                  # :466-471
+        if np.all(props[:, :, k][hs.sNaN] < hs.ELB):
+            return props[:, :, k], k + 1
+    return None, 0
 
 
 def elb_state_space(hs: HybridSetup, PAI, invA, sqrtht):
@@ -134,8 +162,9 @@ def hybrid_init_state(hs: HybridSetup):
     return O.init_state(hs.lin)  # :351-359 (PAI = X0\Y0 with the hybrid X0)
 
 
-def hybrid_sweep(st, hs: HybridSetup, crn, elb_impl="stable"):
-    """One sweep of mcmcVARhybridGibbs.m:362-539 with the Gibbs ELB draw.
+def hybrid_sweep(st, hs: HybridSetup, crn, elb_impl="stable", use_ps=False):
+    """One sweep of mcmcVARhybridGibbs.m:362-539 with the Gibbs ELB draw, or with use_ps the
+    reference's PS proposals first (:458-483, crn["zPS"]) and the Gibbs draw as fallback.
     elb_impl as in ccmm_oracle_bh.bh_sweep ("qr", "stable" or "both")."""
     lin = hs.lin
     N, K = lin.N, lin.K
@@ -155,6 +184,13 @@ def hybrid_sweep(st, hs: HybridSetup, crn, elb_impl="stable"):
     if hs.elbT > 0:
         C, Psi, SVol, Yhatactual = elb_state_space(hs, PAI, invA, sqrtht)
         elbY = Y[hs.elbT0:, :].T
+        if use_ps:
+            sr, k = ps_shadowrate(hs, PAI, A, sqrtht, crn["zPS"])
+            out["ps_accept"] = k
+            if k:
+                Xn, Yn = rebuild_XY(hs, sr)
+                out.update(X=Xn, Y=Yn, shadowrate=sr)
+                return out
         if elb_impl in ("qr", "both"):
             draws = O.gibbsdraw_shadowrates(elbY, hs.X0, Yhatactual, hs.ndxSmask, hs.sNaN, lin.p,
                                             C, Psi, SVol, hs.ELB, 1, hs.gibbsburn, crn["uELB"])

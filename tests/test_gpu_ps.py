@@ -162,3 +162,58 @@ def test_ps_philox_batch(pkg, ctx, oracle, bh, fred):
     acc = (ps["stackAccept"][1:] > 0).sum(axis=0)
     assert np.array_equal(acc, ps["countAccept"])
     assert np.all(ps["stackAccept"] <= 1000)
+
+
+def test_ps_hybrid_toy(pkg, ctx, oracle, bh):
+    """Hybrid model (mcmcVARhybridGibbs.m:446-483): PS proposals at every sweep with
+    PAIshadow = PAI(1:Kshadow,:) and Yhatactual = Xffrlags PAIactual as intercept."""
+    from oracle import ccmm_oracle_hybrid as hy
+    N, p, Tobs, ndxS = 5, 2, 150, (2, 3)
+    bs = _toy_bs(bh, (114, 120), valley=True)
+    data = bs.lin.data
+    hs = hy.hybrid_setup(Tobs, p, 12, data, np.arange(Tobs, dtype=float), np.asarray(ndxS),
+                         np.ones(N), 0.25, bs.elbT0)
+    lin = hs.lin
+    B, nsw, NP = 4, 2, 300
+    sts = []
+    for c in range(B):
+        st = random_state(oracle, lin, seed=40 + c)
+        st["X"], st["Y"] = lin.X.copy(), lin.Y.copy()
+        sts.append(st)
+    rng = np.random.default_rng(40)
+    crns = [[hy.hybrid_draw_crn(rng, hs, NP) for _ in range(nsw)] for _ in range(B)]
+    ch = pkg.Chains(ctx, N=lin.N, p=lin.p, T=lin.T, B=B, crn=True, model=pkg.MODEL_HYBRID,
+                    Ns=len(hs.ndxS), elbTmax=hs.elbT, elb_gibbsburn=hs.gibbsburn, elb=hs.ELB,
+                    store_capacity=nsw)
+    ch.set_data(0, lin.Y, lin.X, lin.iVdiag, lin.iVb, lin.sPHI, lin.Vol_0mean, lin.Vol_0vcvsqrt)
+    ch.set_elb_model(hs.ndxS, None)
+    ch.set_elb_slot(0, hs.elbT0, hs.sNaN)
+    ch.set_elb_ps(NP, 1)
+    ch.set_state(*[np.stack([s[k] for s in sts], -1) for k in ("PAI", "A", "sqrtht", "h", "sqrtPHI")])
+
+    def flat(crn):
+        parts = [crn[k].ravel(order="F") for k, _ in hy.hybrid_crn_sizes(hs)]
+        z = crn["zPS"].ravel(order="F")
+        parts.append(np.concatenate([z, np.zeros(len(hs.ndxS) * hs.elbT * NP - z.size)]))
+        return np.concatenate(parts)
+
+    F = np.stack([np.stack([flat(crns[c][m]) for m in range(nsw)], -1) for c in range(B)], -1)
+    assert F.shape[0] == ch.crn_len
+    ch.sweep(nsw, crn=F, store=True)
+    got = ch.get_state()
+    S = ch.get_shadowrate()
+    ps = ch.get_ps()
+    n_acc = 0
+    for c in range(B):
+        st = sts[c]
+        acc = []
+        for m in range(nsw):
+            st = hy.hybrid_sweep(st, hs, crns[c][m], use_ps=True)
+            acc.append(st["ps_accept"])
+        n_acc += sum(1 for a in acc if a)
+        assert list(ps["stackAccept"][:, c]) == acc, (c, ps["stackAccept"][:, c], acc)
+        e = {"PAI": rel_err(got["PAI"][..., c], st["PAI"], 1e-2),
+             "shadowrate": rel_err(S[:, :, c], st["shadowrate"], 0.1)}
+        print("hybrid chain", c, "ndxAccept", acc, e)
+        assert max(e.values()) < 1e-7, e
+    assert n_acc > 0
