@@ -89,6 +89,10 @@ _SIGS = {
     "ccmm_chains_set_elb_slot": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p]),
     "ccmm_chains_get_shadowrate": (C.c_int, [C.c_void_p, _dp]),
     "ccmm_chains_set_elb_ps": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "ccmm_draw_summaries": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, C.c_int, _dp, _dp, _dp,
+                                      _dp, _dp, _dp]),
+    "ccmm_chains_summaries": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, _u8p, _dp, C.c_int, _dp,
+                                        _dp, _dp, _dp, _dp, _dp]),
     "ccmm_chains_get_ps": (C.c_int, [C.c_void_p, _ip, _ip, _ip]),
     "ccmm_chains_get_xy": (C.c_int, [C.c_void_p, _dp, _dp]),
     "ccmm_chains_profile": (C.c_int, [C.c_void_p, C.c_int]),
@@ -308,6 +312,25 @@ class Context:
         _check(rc, "ccmm_draw_trunc_normal_batch")
         return out, fl
 
+    def draw_summaries(self, draws, realized=None, pct=()):
+        """Per-series summaries of draws (n x S, each column one series): dict of mean,
+        median, quantiles (S x nq), stdev (std(., 1)), crps (when realized, S, is given)."""
+        X = _f(draws)
+        n, S = X.shape
+        pct = _f(np.asarray(pct, float).ravel())
+        out = dict(mean=np.zeros(S), median=np.zeros(S), quantiles=np.zeros((S, pct.size), order="F"),
+                   stdev=np.zeros(S))
+        rz = None
+        if realized is not None:
+            rz = _f(np.asarray(realized, float).ravel())
+            out["crps"] = np.zeros(S)
+        _check(self.lib.ccmm_draw_summaries(self.handle, S, n, _ptr(X), _ptr(rz), pct.size,
+                                            _ptr(pct) if pct.size else None, _ptr(out["mean"]),
+                                            _ptr(out["median"]), _ptr(out["quantiles"]) if pct.size else None,
+                                            _ptr(out["stdev"]), _ptr(out.get("crps"))),
+               "ccmm_draw_summaries")
+        return out
+
     def selftest_mfma_f64(self, A16x4, B4x16):
         D = np.zeros((16, 16), order="F")
         _check(self.lib.ccmm_selftest_mfma_f64(self.handle, _ptr(_f(A16x4)), _ptr(_f(B4x16)),
@@ -475,15 +498,15 @@ class Chains:
     def stored(self):
         return int(self.lib.ccmm_chains_stored(self.handle))
 
-    def get_draws(self):
+    def get_draws(self, which=None):
+        """Stored draws (then reset); ``which``: names to fetch (default all)."""
         M = self.stored()
         N, K, T, B = self.N, self.K, self.T, self.B
-        out = dict(PAI_all=np.zeros((M, K, N, B), order="F"),
-                   PHI_all=np.zeros((M, N * (N + 1) // 2, B), order="F"),
-                   invA_all=np.zeros((M, N, N, B), order="F"),
-                   sqrtht_all=np.zeros((M, T, N, B), order="F"))
+        shapes = dict(PAI_all=(M, K, N, B), PHI_all=(M, N * (N + 1) // 2, B), invA_all=(M, N, N, B),
+                      sqrtht_all=(M, T, N, B))
         if self.model in (MODEL_BLOCKHYBRID, MODEL_HYBRID):
-            out["shadowrate_all"] = np.zeros((M, self.Ns, self.elbTmax, B), order="F")
+            shapes["shadowrate_all"] = (M, self.Ns, self.elbTmax, B)
+        out = {k: np.zeros(v, order="F") for k, v in shapes.items() if which is None or k in which}
         rc = self.lib.ccmm_chains_get_draws(self.handle, *[_ptr(out.get(k)) for k in
                                                            ("PAI_all", "PHI_all", "invA_all",
                                                             "sqrtht_all", "shadowrate_all")])
@@ -563,6 +586,33 @@ class Chains:
         _check(self.lib.ccmm_chains_get_ps(self.handle, ca.ctypes.data_as(_ip), cb.ctypes.data_as(_ip),
                                            st.ctypes.data_as(_ip)), "ccmm_chains_get_ps")
         return dict(countAccept=ca, countAcceptBurnin=cb, stackAccept=st[:M])
+
+    def summaries(self, source, slot, rows=None, cumcode=None, realized=None, pct=()):
+        """Device summaries of the kept draws of data slot ``slot`` (ccmm_chains_summaries):
+        source 0 paths / 1 censored paths (series = rows x H) / 2 PAI (K x N)."""
+        N = self.N
+        if source in (0, 1):
+            nr = N if rows is None else int(np.count_nonzero(rows))
+            S = nr * self.fH
+        else:
+            S = self.K * N
+        pct = _f(np.asarray(pct, float).ravel())
+        out = dict(mean=np.zeros(S), median=np.zeros(S), quantiles=np.zeros((S, pct.size), order="F"),
+                   stdev=np.zeros(S))
+        rz = None
+        if realized is not None:
+            rz = _f(np.asarray(realized, float).ravel(order="F"))
+            assert rz.size == S
+            out["crps"] = np.zeros(S)
+        rw = None if rows is None else np.ascontiguousarray(np.asarray(rows, bool), dtype=np.uint8)
+        cc = None if cumcode is None else np.ascontiguousarray(np.asarray(cumcode, bool), dtype=np.uint8)
+        _check(self.lib.ccmm_chains_summaries(
+            self.handle, int(source), int(slot), None if rw is None else rw.ctypes.data_as(_u8p),
+            None if cc is None else cc.ctypes.data_as(_u8p), _ptr(rz), pct.size,
+            _ptr(pct) if pct.size else None, _ptr(out["mean"]), _ptr(out["median"]),
+            _ptr(out["quantiles"]) if pct.size else None, _ptr(out["stdev"]), _ptr(out.get("crps"))),
+            "ccmm_chains_summaries")
+        return out
 
     def get_shadowrate(self):
         out = np.zeros((self.Ns, self.elbTmax, self.B), order="F")

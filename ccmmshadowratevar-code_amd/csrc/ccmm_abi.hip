@@ -24,6 +24,7 @@
 #include "ccmm_svpart.h"
 #include "ccmm_big.h"
 #include "ccmm_bign.h"
+#include "ccmm_post.h"
 #include <cstdlib>
 
 using namespace ccmm;
@@ -1365,6 +1366,83 @@ struct ccmm_chains {
     fstored = 0;
   }
 
+  // ---------------------------------------------------------------- post-processing
+  // summaries over the kept draws of the chains of one data slot (ccmm_post.hip)
+  DBuf<double> postA, postB, postOut;
+  DBuf<char> postWs;
+  DBuf<int> postRows;
+  DBuf<uint8_t> postCum;
+  void summaries(int source, int sl, const uint8_t* rows, const uint8_t* cumcode, const double* realized, int nq,
+                 const double* pct, double* mean, double* median, double* quant, double* sdev, double* crps) {
+    require(sl >= 0 && sl < cfg.ndata, "slot out of range");
+    require(nq >= 0 && (nq == 0 || pct), "bad quantile list");
+    std::vector<int> hs(cfg.B);
+    HIPCHECK(hipMemcpy(hs.data(), slot.p, cfg.B * sizeof(int), hipMemcpyDeviceToHost));
+    int c0 = -1, C = 0;
+    for (int c = 0; c < cfg.B; ++c)
+      if (hs[c] == sl) {
+        if (c0 < 0) c0 = c;
+        require(c == c0 + C, "the chains of the slot must be contiguous");
+        ++C;
+      }
+    require(C > 0, "no chain bound to the slot");
+    const int N = cfg.N, K = cfg.K;
+    int S = 0, n = 0;
+    if (source == 0 || source == 1) {
+      require(have_fcst && fKeep, "forecast paths were not kept (ccmm_chains_set_fcst keep_paths)");
+      require(fstored > 0, "no forecast records");
+      std::vector<int> rl;
+      for (int i = 0; i < N; ++i)
+        if (!rows || rows[i]) rl.push_back(i);
+      require(!rl.empty(), "no rows selected");
+      S = (int)rl.size() * fH;
+      n = C * fstored * fNd;
+      postRows.alloc(rl.size());
+      HIPCHECK(hipMemcpy(postRows.p, rl.data(), rl.size() * sizeof(int), hipMemcpyHostToDevice));
+      if (cumcode) {
+        postCum.alloc(N);
+        HIPCHECK(hipMemcpy(postCum.p, cumcode, N, hipMemcpyHostToDevice));
+      }
+      postA.alloc((size_t)S * n);
+      HIPCHECK(post_gather_fcst(ctx->stream, source == 0 ? fPaths.p : fPathsC.p, c0, C, fstored, fNd, fH, N,
+                                cfg.store_capacity, postRows.p, (int)rl.size(), cumcode ? postCum.p : nullptr,
+                                postA.p));
+    } else if (source == 2) {
+      require(stored > 0 && sPAI.p, "no stored draws");
+      S = K * N;
+      n = C * stored;
+      postA.alloc((size_t)S * n);
+      HIPCHECK(post_gather_pai(ctx->stream, sPAI.p, c0, C, stored, cfg.store_capacity, K * N, postA.p));
+    } else {
+      throw ArgError("source must be 0 (paths), 1 (censored paths) or 2 (PAI draws)");
+    }
+    postB.alloc((size_t)S * n);
+    const size_t wb = post_workspace_bytes(S, n);
+    postWs.alloc(wb);
+    // device scratch: pct | realized | mean | median | sd | crps | quantiles
+    postOut.alloc((size_t)nq + (size_t)S * (5 + nq));
+    double* dp = postOut.p;
+    double* dr = dp + nq;
+    double* dm = dr + S;
+    double* dmed = dm + S;
+    double* dsd = dmed + S;
+    double* dcr = dsd + S;
+    double* dq = dcr + S;
+    if (nq) HIPCHECK(hipMemcpy(dp, pct, nq * sizeof(double), hipMemcpyHostToDevice));
+    if (realized) HIPCHECK(hipMemcpy(dr, realized, S * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(post_summaries(ctx->stream, S, n, postA.p, postB.p, postWs.p, wb, realized ? dr : nullptr, nq, dp,
+                            dm, dmed, nq ? dq : nullptr, dsd, crps ? dcr : nullptr));
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    auto get = [&](double* dst, const double* src, size_t cnt) {
+      if (dst) HIPCHECK(hipMemcpy(dst, src, cnt * sizeof(double), hipMemcpyDeviceToHost));
+    };
+    get(mean, dm, S);
+    get(median, dmed, S);
+    get(sdev, dsd, S);
+    get(crps, dcr, S);
+    get(quant, dq, (size_t)S * nq);
+  }
+
   void run_fcst(const RngArgs& ra) {
     if (fstored >= cfg.store_capacity) throw ArgError("forecast store full: call ccmm_chains_get_fcst");
     static const GLNodes gl = make_gl_nodes();
@@ -2456,6 +2534,58 @@ int ccmm_chains_get_ps(ccmm_chains* ch, int* countAccept, int* countAcceptBurnin
       for (size_t c = 0; c < B; ++c)
         for (size_t m = 0; m < M; ++m) stackAccept[m + M * c] = buf[c * cap + m];
     }
+    return 0;
+  });
+}
+
+int ccmm_draw_summaries(ccmm_ctx* ctx, int S, int n, const double* draws, const double* realized, int nq,
+                        const double* pct, double* mean, double* median, double* quantiles, double* stdev,
+                        double* crps) {
+  return guarded([&] {
+    require(ctx && draws, "null argument");
+    require(S >= 1 && n >= 1 && (size_t)S * n < (1ull << 31), "S x n must be in [1, 2^31)");
+    require(nq >= 0 && (nq == 0 || pct), "bad quantile list");
+    HIPCHECK(hipSetDevice(ctx->device));
+    DBuf<double> A, Bs, out;
+    DBuf<char> ws;
+    A.alloc((size_t)S * n);
+    Bs.alloc((size_t)S * n);
+    HIPCHECK(hipMemcpy(A.p, draws, (size_t)S * n * sizeof(double), hipMemcpyHostToDevice));
+    const size_t wb = post_workspace_bytes(S, n);
+    ws.alloc(wb);
+    out.alloc((size_t)nq + (size_t)S * (5 + nq));
+    double* dp = out.p;
+    double* dr = dp + nq;
+    double* dm = dr + S;
+    double* dmed = dm + S;
+    double* dsd = dmed + S;
+    double* dcr = dsd + S;
+    double* dq = dcr + S;
+    if (nq) HIPCHECK(hipMemcpy(dp, pct, nq * sizeof(double), hipMemcpyHostToDevice));
+    if (realized) HIPCHECK(hipMemcpy(dr, realized, S * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(post_summaries(ctx->stream, S, n, A.p, Bs.p, ws.p, wb, realized ? dr : nullptr, nq, dp, dm, dmed,
+                            nq ? dq : nullptr, dsd, crps ? dcr : nullptr));
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    auto get = [&](double* dst, const double* src, size_t cnt) {
+      if (dst) HIPCHECK(hipMemcpy(dst, src, cnt * sizeof(double), hipMemcpyDeviceToHost));
+    };
+    get(mean, dm, S);
+    get(median, dmed, S);
+    get(stdev, dsd, S);
+    get(crps, dcr, S);
+    get(quantiles, dq, (size_t)S * nq);
+    return 0;
+  });
+}
+
+int ccmm_chains_summaries(ccmm_chains* ch, int source, int slot, const uint8_t* rows, const uint8_t* cumcode,
+                          const double* realized, int nq, const double* pct, double* mean, double* median,
+                          double* quantiles, double* stdev, double* crps) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    ch->summaries(source, slot, rows, cumcode, realized, nq, pct, mean, median, quantiles, stdev, crps);
     return 0;
   });
 }

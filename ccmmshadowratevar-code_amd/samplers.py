@@ -383,6 +383,69 @@ def datenum(y, m, d):
     return float(datetime.date(y, m, d).toordinal() + 366)
 
 
+def _normcdf(x):
+    import math
+    return 0.5 * math.erfc(-x / math.sqrt(2.0))
+
+
+# goVARshadowrateBlockHybrid.m:141
+SET_QUANTILES = np.array([.5, 2.5, 5, _normcdf(-1) * 100, 25, 75, (1 - _normcdf(-1)) * 100, 95, 97.5,
+                          99.5])
+
+
+def max_var_roots(PAI_all, N, p, threads=16):
+    """max(abs(eig(comp))) of every draw's companion matrix (goVARshadowrateBlockHybrid.m:
+    384-392), PAI_all M x K x N; host LAPACK (dgeev) over a thread pool."""
+    from concurrent.futures import ThreadPoolExecutor
+    M = PAI_all.shape[0]
+    Np = N * p
+
+    def one(P):
+        comp = np.zeros((Np, Np))
+        comp[N:, :Np - N] = np.eye(Np - N)
+        comp[:N, :] = P[1:1 + Np, :].T
+        return float(np.max(np.abs(np.linalg.eigvals(comp))))
+
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        return np.array(list(ex.map(one, [PAI_all[m] for m in range(M)])))
+
+
+def save_qrt_mat(filename, res, *, data, ydates, p, ncode, tcode, cumcode, ndxSHADOWRATE,
+                 ndxOTHERYIELDS, ELBbound, actualrateBlock, datalabel, modellabel, MCMCdraws,
+                 fcstNhorizons, doQuarterly=False):
+    """The QRT summary file of goVARshadowrateBlockHybrid.m:641-669 (varlist: data, ydates, p,
+    Tjumpoffs, N, ncode, tcode, cumcode, fcst*, fcstNhorizons, PAI*, shadowrate*, missingrate*,
+    ndx*, ELBbound, ELBdummy, actualrateBlock, datalabel, modellabel, doQuarterly,
+    setQuantiles, MCMCdraws) from a goVARshadowrateBlockHybrid_batch result.  MATLAB
+    -v7.3 is HDF5; this writes the same names and shapes as a v5 MAT-file (scipy.io.savemat).
+    Index variables are 1-based as in MATLAB; missingrate* are NaN (doELBsampleAlternate is
+    false in the driver)."""
+    from scipy.io import savemat
+    data = np.asarray(data, float)
+    ndxS1 = np.asarray(ndxSHADOWRATE, int) + 1
+    ndxO1 = np.asarray(ndxOTHERYIELDS, int) + 1
+    Tdata = data.shape[0]
+    Ns = ndxS1.size
+    V = len(res["Tjumpoffs"])
+    m = dict(data=data, ydates=np.asarray(ydates, float)[:, None], p=float(p),
+             Tjumpoffs=np.asarray(res["Tjumpoffs"], float)[:, None], N=float(data.shape[1]),
+             ncode=np.array(list(ncode), dtype=object)[None, :], tcode=np.asarray(tcode, float)[None, :],
+             cumcode=np.asarray(cumcode, bool)[None, :], fcstNhorizons=float(fcstNhorizons),
+             ndxSHADOWRATE=ndxS1.astype(float)[None, :], ndxOTHERYIELDS=ndxO1.astype(float)[None, :],
+             ndxYIELDS=np.union1d(ndxS1, ndxO1).astype(float)[None, :], ELBbound=float(ELBbound),
+             ELBdummy=data[:, ndxS1 - 1] <= ELBbound,
+             actualrateBlock=np.asarray(actualrateBlock, bool)[None, :], datalabel=datalabel,
+             modellabel=modellabel, doQuarterly=bool(doQuarterly), MCMCdraws=float(MCMCdraws),
+             setQuantiles=np.asarray(res.get("setQuantiles", SET_QUANTILES), float)[None, :],
+             missingrateVintagesMid=np.full((Tdata, Ns, V), np.nan),
+             missingrateVintagesTails=np.full((Tdata, Ns, 4, V), np.nan))
+    for k, v in res.items():
+        if k.startswith(("fcst", "PAI", "shadowrate")) and isinstance(v, np.ndarray):
+            m[k] = v[None, :] if v.ndim == 1 else v
+    savemat(filename, m, do_compression=True)
+    return sorted(m)
+
+
 def matlab_prctile(x, pct, axis=0):
     """MATLAB prctile (Statistics Toolbox): sorted values sit at percentiles
     100 (i - 0.5) / n, linear interpolation between, clamped outside = numpy 'hazen'."""
@@ -451,7 +514,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                                      ELBbound=0.25, doRATSprior=True, nchains=1, burnin=None,
                                      gibbsburn=100, rndStream=1012023, dist=None, device=None,
                                      chunk=50, max_retries=2, keep_draws=False, progress=False,
-                                     Nproposals=1000, elb_ps=True):
+                                     Nproposals=1000, elb_ps=True, postprocess=False, cumcode=None,
+                                     setQuantiles=None, maxlambda=False):
     """The quasi-real-time OOS run of goVARshadowrateBlockHybrid.m:126-517 for the block-
     hybrid shadow-rate VAR, as ONE device-resident chain set per rank: every vintage
     thisT in Tjumpoffs (default: ydates > 2008-12, :127) is a data slot of the set with
@@ -476,7 +540,15 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
     censored paths), fcstShadowYhat (Nyields x H x V), fcstYrealized, fcstYhaterror,
     PAImean / PAIstdev (K x N x V, :376-378), shadowrateVintagesMid / Tails
     (Tdata x Ns (x 4) x V, median and prctile [5 25 75 95] of the kept shadow rates,
-    :331-334,497-506), plus run statistics."""
+    :331-334,497-506), plus run statistics.
+
+    postprocess=True adds the per-vintage post-processing of :349-480 on the device
+    (ccmm_chains_summaries; every kept draw and forecast path of the set stays in HBM):
+    fcstYmedian / fcstYmederror / fcstYcrps / fcstYquantiles (N x H (x Nq) x V), their
+    cumulated forms fcstYcum* (cumsum over horizons for ``cumcode``), fcstShadowYmedian /
+    fcstShadowYquantiles, PAImedian / PAIquantiles, the score draws fcstYmvlogscore*Draws;
+    setQuantiles default goVARshadowrateBlockHybrid.m:141.  maxlambda=True adds
+    drawsMaxVARroot (max |eig| of each draw's companion matrix, :382-392, host LAPACK)."""
     import time
     from . import distributed as dm
     data0 = np.asarray(data0, float)
@@ -514,16 +586,22 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
     Ns = ndxSHADOWRATE.size
     chunk = max(1, min(int(chunk), MCMCdraws))
 
+    cumcode = None if cumcode is None else np.asarray(cumcode, bool)
+    pct = np.asarray(SET_QUANTILES if setQuantiles is None else setQuantiles, float)
+
     def run(vidx, attempt):
         """Run the vintages vidx (indices into `mine`); returns per-vintage results and
         the list of vintages whose chains were flagged."""
         us = [units[i] for i in vidx]
         ids = np.array([(mine[i] * C + c) + attempt * 1_000_003 for i in vidx for c in range(C)],
                        dtype=np.uint32)
+        # postprocess: every kept draw and forecast path stays on the device until the
+        # per-vintage summaries (ccmm_chains_summaries) have been taken
         ch, slots, yields = _bh_chain_set(ctx, us, C, seed=rndStream, ids=ids,
-                                          store_capacity=chunk, gibbsburn=gibbsburn,
-                                          ELBbound=ELBbound, ndxYIELDS=ndxYIELDS,
-                                          fcstNhorizons=H, Nd=Nd)
+                                          store_capacity=MCMCdraws if postprocess else chunk,
+                                          gibbsburn=gibbsburn, ELBbound=ELBbound,
+                                          ndxYIELDS=ndxYIELDS, fcstNhorizons=H, Nd=Nd,
+                                          keep_paths=postprocess)
         if elb_ps and Nproposals and ch.elbTmax:
             ch.set_elb_ps(Nproposals, max(1, -(-burn // 2)))  # m >= MCMCburnin * .5 (:435)
         B = ch.B
@@ -541,26 +619,49 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
         P2sum = np.zeros((K, N, B))
         elbTmax = ch.elbTmax
         shadow = np.empty((MCMCdraws, Ns, elbTmax, B)) if elbTmax else None
-        PAIdraws = np.empty((MCMCdraws, K, N, B)) if keep_draws else None
+        PAIdraws = np.empty((MCMCdraws, K, N, B)) if (keep_draws or maxlambda) else None
+        post = {}
         done = 0
         while done < MCMCdraws:
             n = min(chunk, MCMCdraws - done)
             ch.sweep(n, store=True)
-            fc = ch.get_fcst()
-            dr = ch.get_draws()
-            scores[:, done:done + n] = fc["scores"]
-            fYsum += fc["fYsum"]
-            fYcsum += fc["fYcsum"]
-            P = dr["PAI_all"]
-            Psum += P.sum(axis=0)
-            P2sum += (P * P).sum(axis=0)
-            if shadow is not None:
-                shadow[done:done + n] = dr["shadowrate_all"]
-            if PAIdraws is not None:
-                PAIdraws[done:done + n] = P
+            if not postprocess:
+                fc = ch.get_fcst()
+                dr = ch.get_draws(which={"PAI_all", "shadowrate_all"})
+                scores[:, done:done + n] = fc["scores"]
+                fYsum += fc["fYsum"]
+                fYcsum += fc["fYcsum"]
+                P = dr["PAI_all"]
+                Psum += P.sum(axis=0)
+                P2sum += (P * P).sum(axis=0)
+                if shadow is not None:
+                    shadow[done:done + n] = dr["shadowrate_all"]
+                if PAIdraws is not None:
+                    PAIdraws[done:done + n] = P
             done += n
             if progress:
                 print(f"[rank {rank}] kept {done}/{MCMCdraws}", flush=True)
+        if postprocess:
+            # goVARshadowrateBlockHybrid.m:349-480 on the device, per vintage (data slot)
+            for k, i in enumerate(vidx):
+                thisT, bm, yr = units[i]
+                ycr = np.array(yr, float)
+                if cumcode is not None:
+                    ycr[cumcode] = np.cumsum(ycr[cumcode], axis=1)              # :353
+                yd = ch.summaries(1, k, realized=yr, pct=pct)                   # ydraws
+                yc = ch.summaries(1, k, cumcode=cumcode, realized=ycr, pct=pct)  # ycumdraws
+                sh = ch.summaries(0, k, rows=yields, pct=pct)                   # shadowratedraws
+                pa = ch.summaries(2, k, pct=pct)                                # PAI_all
+                post[i] = dict(yd=yd, yc=yc, sh=sh, pa=pa, ycr=ycr)
+            fc = ch.get_fcst()
+            scores[:] = fc["scores"]
+            fYsum[:] = fc["fYsum"]
+            fYcsum[:] = fc["fYcsum"]
+            dr = ch.get_draws(which={"shadowrate_all"} | ({"PAI_all"} if PAIdraws is not None else set()))
+            if shadow is not None:
+                shadow[:] = dr["shadowrate_all"]
+            if PAIdraws is not None:
+                PAIdraws[:] = dr["PAI_all"]
         status = ch.get_status()
         nacc = None
         if elb_ps and Nproposals and ch.elbTmax:
@@ -568,6 +669,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
             nacc = psd["countAccept"] + psd["countAcceptBurnin"]
         ch.close()
         res, failed = {}, []
+        Ny = int(np.count_nonzero(yields))
         for k, i in enumerate(vidx):
             cs = slice(k * C, (k + 1) * C)
             if np.any(status[cs] & ~1):  # bit 1: CTA QR fallback used (valid draws)
@@ -581,17 +683,45 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                      logscoreX=_logmeanexp(scores[:, :, 2, cs].ravel()),
                      logscoreI=_logmeanexp(scores[:, :, 3, cs].ravel()),
                      fcstYhat=fYcsum[:, :, cs].sum(axis=2) / (nk * Nd),
-                     fcstShadowYhat=fYsum[ndxYIELDS][:, :, cs].sum(axis=2) / (nk * Nd),
-                     PAImean=Psum[:, :, cs].sum(axis=2) / nk)
-            var = P2sum[:, :, cs].sum(axis=2) / nk - r["PAImean"] ** 2
-            r["PAIstdev"] = np.sqrt(np.maximum(var, 0.0))               # std(.,1,1): 1/n
+                     fcstShadowYhat=fYsum[ndxYIELDS][:, :, cs].sum(axis=2) / (nk * Nd))
+            if i in post:
+                q = post[i]
+                nq = pct.size
+                r["PAImean"] = q["pa"]["mean"].reshape(K, N, order="F")
+                r["PAIstdev"] = q["pa"]["stdev"].reshape(K, N, order="F")
+                r["PAImedian"] = q["pa"]["median"].reshape(K, N, order="F")
+                r["PAIquantiles"] = q["pa"]["quantiles"].reshape(K, N, nq, order="F")
+                r["fcstYmedian"] = q["yd"]["median"].reshape(N, H, order="F")
+                r["fcstYcrps"] = q["yd"]["crps"].reshape(N, H, order="F")
+                r["fcstYquantiles"] = q["yd"]["quantiles"].reshape(N, H, nq, order="F")
+                yh = r["fcstYhat"].copy()
+                if cumcode is not None:
+                    yh[cumcode] = np.cumsum(yh[cumcode], axis=1)                # :355
+                r["fcstYcumrealized"] = q["ycr"]
+                r["fcstYcumhat"] = yh
+                r["fcstYcummedian"] = q["yc"]["median"].reshape(N, H, order="F")
+                r["fcstYcumcrps"] = q["yc"]["crps"].reshape(N, H, order="F")
+                r["fcstYcumquantiles"] = q["yc"]["quantiles"].reshape(N, H, nq, order="F")
+                r["fcstShadowYmedian"] = q["sh"]["median"].reshape(Ny, H, order="F")
+                r["fcstShadowYquantiles"] = q["sh"]["quantiles"].reshape(Ny, H, nq, order="F")
+                r["fcstYmvlogscoreDraws"] = scores[:, :, 1, cs].ravel(order="F")
+                r["fcstYmvlogscoreXdraws"] = scores[:, :, 2, cs].ravel(order="F")
+                r["fcstYmvlogscoreIdraws"] = scores[:, :, 3, cs].ravel(order="F")
+            else:
+                r["PAImean"] = Psum[:, :, cs].sum(axis=2) / nk
+                var = P2sum[:, :, cs].sum(axis=2) / nk - r["PAImean"] ** 2
+                r["PAIstdev"] = np.sqrt(np.maximum(var, 0.0))               # std(.,1,1): 1/n
             if shadow is not None and bm.elbT > 0:
                 # shadowrate_all permuted to (Nobs, Ns, draws) (:329-334)
                 sr = shadow[:, :, :bm.elbT, cs].transpose(2, 1, 0, 3).reshape(bm.elbT, Ns, -1)
                 r["shadowrateMid"] = np.median(sr, axis=2)
                 r["shadowrateTails"] = np.moveaxis(matlab_prctile(sr, [5, 25, 75, 95], axis=2), 0, 2)
             if PAIdraws is not None:
-                r["PAI_all"] = PAIdraws[..., cs]
+                P = PAIdraws[..., cs]
+                if keep_draws:
+                    r["PAI_all"] = P
+                if maxlambda:
+                    r["drawsMaxVARroot"] = max_var_roots(np.moveaxis(P, 3, 1).reshape(-1, K, N), N, p)
             res[mine[i]] = r
         return res, failed
 
@@ -632,6 +762,19 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                shadowrateVintagesTails=np.full((Tdata, Ns, 4, V), np.nan))
     if keep_draws:
         out["PAI_all"] = {}
+    nq = pct.size
+    if postprocess:
+        for nm, shp in (("fcstYmedian", (N, H)), ("fcstYcrps", (N, H)), ("fcstYquantiles", (N, H, nq)),
+                        ("fcstYcumrealized", (N, H)), ("fcstYcumhat", (N, H)), ("fcstYcummedian", (N, H)),
+                        ("fcstYcumcrps", (N, H)), ("fcstYcumquantiles", (N, H, nq)),
+                        ("fcstShadowYmedian", (Ny, H)), ("fcstShadowYquantiles", (Ny, H, nq)),
+                        ("PAImedian", (K, N)), ("PAIquantiles", (K, N, nq)),
+                        ("fcstYmvlogscoreDraws", (fcstNdraws * C,)),
+                        ("fcstYmvlogscoreXdraws", (fcstNdraws * C,)),
+                        ("fcstYmvlogscoreIdraws", (fcstNdraws * C,))):
+            out[nm] = np.full(shp + (V,), np.nan)
+    if maxlambda:
+        out["drawsMaxVARroot"] = np.full((MCMCdraws * C, V), np.nan)
     jumpoff = p + elbT0                                                  # :497
     for v in range(V):
         r = allv.get(v)
@@ -653,7 +796,18 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
             out["shadowrateVintagesTails"][jumpoff:thisT, :, :, v] = r["shadowrateTails"]
         if keep_draws and "PAI_all" in r:
             out["PAI_all"][v] = r["PAI_all"]
-    out["fcstYhaterror"] = out["fcstYrealized"] - out["fcstYhat"]
+        for nm in ("fcstYmedian", "fcstYcrps", "fcstYquantiles", "fcstYcumrealized", "fcstYcumhat",
+                   "fcstYcummedian", "fcstYcumcrps", "fcstYcumquantiles", "fcstShadowYmedian",
+                   "fcstShadowYquantiles", "PAImedian", "PAIquantiles", "fcstYmvlogscoreDraws",
+                   "fcstYmvlogscoreXdraws", "fcstYmvlogscoreIdraws", "drawsMaxVARroot"):
+            if nm in r and nm in out:
+                out[nm][..., v] = r[nm]
+    out["fcstYhaterror"] = out["fcstYrealized"] - out["fcstYhat"]                      # :453
+    if postprocess:
+        out["fcstYmederror"] = out["fcstYrealized"] - out["fcstYmedian"]              # :454
+        out["fcstYcumhaterror"] = out["fcstYcumrealized"] - out["fcstYcumhat"]        # :463
+        out["fcstYcummederror"] = out["fcstYcumrealized"] - out["fcstYcummedian"]     # :464
+        out["setQuantiles"] = pct
     n_units = len(mine) * C
     out["stats"] = dict(rank=rank, world=size, device=device, vintages_local=len(mine),
                         units_local=n_units, sweeps_local=n_units * (burn + MCMCdraws),

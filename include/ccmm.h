@@ -322,6 +322,29 @@ int ccmm_chains_profile(ccmm_chains* ch, int enable);
 int ccmm_chains_kernel_times(ccmm_chains* ch, int max, double* ms, int64_t* launches,
                              char* names, int names_len);
 
+/* ------------------------------------------------------------ post-processing
+ * Per-vintage summaries of kept draws (goVARshadowrateBlockHybrid.m:349-480), on the
+ * device: for each series the mean, median, quantiles at pct[0..nq-1] (MATLAB prctile:
+ * the i-th sorted draw sits at percentile 100 (i - 0.5)/n, linear in between), std(., 1)
+ * and, when realized is given, crpsDraws (the CRPS of the draws' empirical distribution,
+ * mean|x - y| - sum_ij |x_i - x_j| / (2 n^2); em-matlabbox source absent).  Outputs
+ * mean/median/stdev/crps S, quantiles S x nq (series fastest); any may be NULL. */
+/* Host draws n x S (each series' n draws contiguous), realized S or NULL. */
+int ccmm_draw_summaries(ccmm_ctx* ctx, int S, int n, const double* draws, const double* realized, int nq,
+                        const double* pct, double* mean, double* median, double* quantiles, double* stdev,
+                        double* crps);
+/* The kept draws of the chains bound to data slot `slot` (contiguous chain indices), pooled:
+ *   source 0  forecast paths (keep_paths; linear fcstYdraws, block hybrid the uncensored
+ *             shadow-rate paths), series = selected rows x H (row fastest), draws = chains x
+ *             kept records x Nd
+ *   source 1  censored forecast paths (linear fcstYcensorDraws, block hybrid fcstYdraws)
+ *   source 2  PAI draws, series = K x N, draws = chains x stored draws
+ * rows: N bytes selecting the variables (NULL: all); cumcode: N bytes, cumsum over the
+ * horizons for those variables first (:353-355; NULL: none). */
+int ccmm_chains_summaries(ccmm_chains* ch, int source, int slot, const uint8_t* rows, const uint8_t* cumcode,
+                          const double* realized, int nq, const double* pct, double* mean, double* median,
+                          double* quantiles, double* stdev, double* crps);
+
 /* ------------------------------------------------------------ diagnostics */
 
 /* Predictive density of one kept draw per chain, batched over B chains.
