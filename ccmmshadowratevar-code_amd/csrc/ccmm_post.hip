@@ -39,9 +39,17 @@ __device__ __forceinline__ double block_sum_256(double v, double* red) {
   return r;
 }
 
+// numpy's _lerp with every operation rounded separately (the TU is built with
+// -ffp-contract=off), so the quantiles are bit-identical to numpy.percentile(method="hazen")
 __device__ __forceinline__ double lerp_np(double a, double b, double t) {
   const double d = b - a;
-  return (t >= 0.5) ? b - d * (1.0 - t) : a + d * t;  // numpy _lerp
+  return (t >= 0.5) ? b - d * (1.0 - t) : a + d * t;
+}
+
+// numpy's _compute_virtual_index: n q + (alpha + q (1 - alpha - beta)) - 1, alpha = beta = 0.5
+__device__ __forceinline__ double hazen_index(int n, double pc) {
+  const double q = pc / 100.0;
+  return ((double)n * q + 0.5) - 1.0;
 }
 
 __global__ __launch_bounds__(256) void k_post_stats(int S, int n, const double* __restrict__ sorted,
@@ -79,7 +87,7 @@ __global__ __launch_bounds__(256) void k_post_stats(int S, int n, const double* 
     if (sd) sd[s] = sqrt(var);
   }
   auto pq = [&](double pc) {
-    const double vi = ((double)n * (pc / 100.0) + 0.5) - 1.0;  // numpy's evaluation order
+    const double vi = hazen_index(n, pc);
     const double fl = floor(vi);
     int lo = (int)fl, hi = lo + 1;
     double gam = vi - fl;
