@@ -91,6 +91,9 @@ _SIGS = {
     "ccmm_chains_set_elb_ps": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "ccmm_draw_summaries": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, C.c_int, _dp, _dp, _dp,
                                       _dp, _dp, _dp]),
+    "ccmm_girf": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp,
+                            _dp, C.c_int, _u8p, _u8p, C.c_double, _u8p, C.c_double, C.c_double, _dp,
+                            _dp, C.c_uint64, _dp]),
     "ccmm_chains_summaries": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, _u8p, _dp, C.c_int, _dp,
                                         _dp, _dp, _dp, _dp, _dp]),
     "ccmm_chains_get_ps": (C.c_int, [C.c_void_p, _ip, _ip, _ip]),
@@ -329,6 +332,27 @@ class Context:
                                             _ptr(out["median"]), _ptr(out["quantiles"]) if pct.size else None,
                                             _ptr(out["stdev"]), _ptr(out.get("crps"))),
                "ccmm_draw_summaries")
+        return out
+
+    def girf(self, PAI, invA, sqrtPHI, SV0, Xjumpoff, H, nsim, shock11, *, bh=False, actual=None,
+             ndxYields=None, elb=0.25, cumcode=None, np_=12, z=None, svz=None, seed=1012023):
+        """Generalized impulse responses (ccmm_girf): PAI K x N x M, invA / sqrtPHI N x N x M,
+        SV0 N x M, Xjumpoff (K [+ Ny p]) x M; z, svz N x H x nsim x M or None (Philox).
+        Returns N x H x 3 x M (baseline, +shock, -shock mean paths)."""
+        PAI = _f(PAI)
+        K, N, M = PAI.shape
+        p = (K - 1) // N
+        u8 = lambda m: None if m is None else np.ascontiguousarray(np.asarray(m, bool), dtype=np.uint8)
+        act, yl, cc = u8(actual), u8(ndxYields), u8(cumcode)
+        out = np.zeros((N, int(H), 3, M), order="F")
+        zz = None if z is None else _f(z)
+        sz = None if svz is None else _f(svz)
+        _check(self.lib.ccmm_girf(self.handle, M, N, p, int(H), int(nsim), _ptr(PAI), _ptr(_f(invA)),
+                                  _ptr(_f(sqrtPHI)), _ptr(_f(SV0)), _ptr(_f(Xjumpoff)), int(bool(bh)),
+                                  None if act is None else act.ctypes.data_as(_u8p),
+                                  None if yl is None else yl.ctypes.data_as(_u8p), float(elb),
+                                  None if cc is None else cc.ctypes.data_as(_u8p), float(np_), float(shock11),
+                                  _ptr(zz), _ptr(sz), int(seed), _ptr(out)), "ccmm_girf")
         return out
 
     def selftest_mfma_f64(self, A16x4, B4x16):

@@ -25,6 +25,7 @@
 #include "ccmm_big.h"
 #include "ccmm_bign.h"
 #include "ccmm_post.h"
+#include "ccmm_girf.h"
 #include <cstdlib>
 
 using namespace ccmm;
@@ -2586,6 +2587,62 @@ int ccmm_chains_summaries(ccmm_chains* ch, int source, int slot, const uint8_t* 
     HIPCHECK(hipSetDevice(ch->ctx->device));
     HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
     ch->summaries(source, slot, rows, cumcode, realized, nq, pct, mean, median, quantiles, stdev, crps);
+    return 0;
+  });
+}
+
+int ccmm_girf(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const double* PAI, const double* invA,
+              const double* sqrtPHI, const double* SV0, const double* Xjumpoff, int bh, const uint8_t* actual,
+              const uint8_t* ndxYields, double elb, const uint8_t* cumcode, double np_, double shock11,
+              const double* z, const double* svz, uint64_t seed, double* yhat) {
+  return guarded([&] {
+    require(ctx && PAI && invA && sqrtPHI && SV0 && Xjumpoff && yhat, "null argument");
+    require(M >= 1 && N >= 1 && N <= 32 && p >= 1 && H >= 1 && nsim >= 1, "bad dimensions (N <= 32)");
+    require(!bh || (actual && ndxYields), "block hybrid needs actual and ndxYields");
+    require((z == nullptr) == (svz == nullptr), "z and svz: both or neither");
+    HIPCHECK(hipSetDevice(ctx->device));
+    const int K = N * p + 1;
+    std::vector<int> yi;
+    if (bh)
+      for (int i = 0; i < N; ++i)
+        if (ndxYields[i]) yi.push_back(i);
+    const int Ny = (int)yi.size();
+    const int ldX = K + Ny * p;
+    require((K + Ny * p + N + 3) / 4 <= 96, "state too large for the GIRF kernel (K + Ny p + N <= 384)");
+    const size_t nch = (size_t)(nsim + 3) / 4;
+    DBuf<double> dPAI, dA, dS, dSV, dX, dZ, dSZ, dPart, dOut;
+    DBuf<uint8_t> dAct, dCum;
+    DBuf<int> dY;
+    auto up = [&](auto& buf, const auto* src, size_t n) {
+      buf.alloc(n);
+      HIPCHECK(hipMemcpy(buf.p, src, n * sizeof(src[0]), hipMemcpyHostToDevice));
+    };
+    // PAI K x N x M column-major == [M][N][K]
+    up(dPAI, PAI, (size_t)K * N * M);
+    up(dA, invA, (size_t)N * N * M);
+    up(dS, sqrtPHI, (size_t)N * N * M);
+    up(dSV, SV0, (size_t)N * M);
+    up(dX, Xjumpoff, (size_t)ldX * M);
+    if (z) {
+      up(dZ, z, (size_t)N * H * nsim * M);
+      up(dSZ, svz, (size_t)N * H * nsim * M);
+    }
+    if (bh) {
+      up(dAct, actual, (size_t)N);
+      up(dY, yi.data(), yi.size());
+    }
+    if (cumcode) up(dCum, cumcode, (size_t)N);
+    dPart.alloc((size_t)M * 3 * nch * H * N);
+    dOut.alloc((size_t)M * 3 * H * N);
+    GirfArgs a{};
+    a.M = M; a.N = N; a.p = p; a.H = H; a.nsim = nsim; a.bh = bh ? 1 : 0; a.Ny = Ny;
+    a.PAI = dPAI.p; a.invA = dA.p; a.sqrtPHI = dS.p; a.SV0 = dSV.p; a.Xj = dX.p; a.ldX = ldX;
+    a.actual = bh ? dAct.p : nullptr; a.yidx = bh ? dY.p : nullptr; a.elb = elb; a.shock11 = shock11;
+    a.z = z ? dZ.p : nullptr; a.svz = z ? dSZ.p : nullptr; a.seed = seed;
+    a.cumcode = cumcode ? dCum.p : nullptr; a.np_ = np_; a.part = dPart.p; a.out = dOut.p;
+    HIPCHECK(girf_launch(ctx->stream, a));
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    HIPCHECK(hipMemcpy(yhat, dOut.p, dOut.n * sizeof(double), hipMemcpyDeviceToHost));
     return 0;
   });
 }

@@ -345,6 +345,25 @@ int ccmm_chains_summaries(ccmm_chains* ch, int source, int slot, const uint8_t* 
                           const double* realized, int nq, const double* pct, double* mean, double* median,
                           double* quantiles, double* stdev, double* crps);
 
+/* ------------------------------------------------------------ GIRF
+ * Generalized impulse responses by antithetic simulation, batched over M MCMC draws
+ * (generateGIRF2linear.m / generateGIRF2blockhybrid.m:199-259 with antitheticSim and
+ * simVAR / simVARshadowrateBlockHybrid): per draw, nsim shock paths (SV paths
+ * exp(cumsum(sqrtPHI randn)/2)) x 4 antithetic sets (+-z .* SV^{+-1} .* SV0) x 3 scenarios
+ * (shock11 = 0, +shock11, -shock11 added to variable 1 at horizon 1), mapped by invA and
+ * simulated over H horizons (bh != 0: actual-rate states max(shadow, ELB), yields floored at
+ * the ELB in the output), cumcode variables cumsum / np, averaged over the 4 nsim paths.
+ *   PAI K x N x M, invA N x N x M, sqrtPHI N x N x M (chol(PHI, 'lower')), SV0 N x M (jump-off
+ *   sqrtht), Xjumpoff (K + Ny p) x M (linear: K), actual / ndxYields N bytes (bh), cumcode N
+ *   bytes or NULL; z, svz N x H x nsim x M (randn(N, H, nsim), randn(N, H*nsim)) or both NULL
+ *   (Philox keyed by (seed, draw)).
+ *   yhat out N x H x 3 x M: fcstYHATdraws, fcstYHATdraws1plus, fcstYHATdraws1minus.
+ * N <= 32. */
+int ccmm_girf(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const double* PAI, const double* invA,
+              const double* sqrtPHI, const double* SV0, const double* Xjumpoff, int bh, const uint8_t* actual,
+              const uint8_t* ndxYields, double elb, const uint8_t* cumcode, double np_, double shock11,
+              const double* z, const double* svz, uint64_t seed, double* yhat);
+
 /* ------------------------------------------------------------ diagnostics */
 
 /* Predictive density of one kept draw per chain, batched over B chains.

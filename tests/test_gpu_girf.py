@@ -1,0 +1,81 @@
+"""GPU parity of the generalized impulse responses (ccmm_girf.hip; generateGIRF2linear.m /
+generateGIRF2blockhybrid.m:199-259 with antitheticSim and simVAR*) against the oracle
+(oracle/ccmm_oracle_girf.girf_draw) on common random numbers, and the linear model's exact
+property at the reference size: the antithetic mean of a linear simulation is the
+deterministic path, so +shock minus baseline is the impulse response invA e1 shock11
+propagated by the companion matrix."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gi():
+    from oracle import ccmm_oracle_girf
+    return ccmm_oracle_girf
+
+
+def _draws(rng, N, p, M, bh, Ny):
+    """M random stable draws: PAI K x N x M, invA (unit lower), sqrtPHI, SV0, Xjumpoff."""
+    K = 1 + N * p
+    PAI = np.zeros((K, N, M))
+    invA = np.zeros((N, N, M))
+    sqrtPHI = np.zeros((N, N, M))
+    for m in range(M):
+        PAI[0, :, m] = 0.1 * rng.standard_normal(N)
+        for l in range(p):
+            PAI[1 + l * N:1 + (l + 1) * N, :, m] = (0.5 / (l + 1) ** 2) * np.eye(N) + \
+                0.03 * rng.standard_normal((N, N))
+        invA[..., m] = np.eye(N) + np.tril(0.2 * rng.standard_normal((N, N)), -1)
+        sqrtPHI[..., m] = np.tril(0.02 * rng.standard_normal((N, N)), -1) + np.diag(0.05 + 0.1 * rng.random(N))
+    SV0 = 0.5 + rng.random((N, M))
+    ns = K + (Ny * p if bh else 0)
+    Xj = np.zeros((ns, M))
+    Xj[0] = 1.0
+    Xj[1:] = 0.3 * rng.standard_normal((ns - 1, M)) + 0.2
+    return PAI, invA, sqrtPHI, SV0, Xj
+
+
+@pytest.mark.parametrize("bh", [False, True])
+def test_girf_crn_toy(ctx, gi, bh):
+    rng = np.random.default_rng(7 + bh)
+    N, p, H, nsim, M = 5, 2, 9, 6, 3
+    yields = np.array([False, False, True, True, True])
+    actual = ~yields
+    cum = np.array([True, False, False, False, True])
+    PAI, invA, sqrtPHI, SV0, Xj = _draws(rng, N, p, M, bh, int(yields.sum()))
+    z = rng.standard_normal((N, H, nsim, M))
+    svz = rng.standard_normal((N, H, nsim, M))
+    got = ctx.girf(PAI, invA, sqrtPHI, SV0, Xj, H, nsim, 0.7, bh=bh, actual=actual, ndxYields=yields,
+                   elb=0.25, cumcode=cum, np_=12, z=z, svz=svz)
+    for m in range(M):
+        want = gi.girf_draw(PAI[..., m], invA[..., m], sqrtPHI[..., m], SV0[:, m], Xj[:, m], z[..., m],
+                            svz[..., m], 0.7, cum, 12, bh=bh, actual=actual, yields=yields, elb=0.25)
+        for sc in range(3):
+            err = np.max(np.abs(got[:, :, sc, m] - want[sc]) / np.maximum(np.abs(want[sc]), 1.0))
+            assert err < 1e-12, (m, sc, err)
+
+
+def test_girf_linear_reference_size(ctx, gi):
+    """N = 20, p = 12, H = 120, 1000 shock paths, 8 draws, Philox: +shock - baseline and
+    baseline - (-shock) equal the deterministic impulse response (antithetic cancellation)."""
+    rng = np.random.default_rng(3)
+    N, p, H, nsim, M = 20, 12, 120, 1000, 8
+    PAI, invA, sqrtPHI, SV0, Xj = _draws(rng, N, p, M, False, 0)
+    cum = np.zeros(N, bool)
+    cum[:4] = True
+    out = ctx.girf(PAI, invA, sqrtPHI, SV0, Xj, H, nsim, 1.0, cumcode=cum, np_=12, seed=11)
+    assert np.all(np.isfinite(out))
+    for m in range(M):
+        A = gi.companion(PAI[..., m], N, p)
+        x = np.zeros(A.shape[0])
+        x[1:1 + N] = invA[:, 0, m]
+        irf = np.zeros((N, H))
+        for h in range(H):
+            irf[:, h] = x[1:1 + N]
+            x = A @ x
+        irf[cum] = np.cumsum(irf[cum], axis=1) / 12
+        scale = max(np.max(np.abs(out[:, :, 0, m])), 1.0)
+        assert np.max(np.abs(out[:, :, 1, m] - out[:, :, 0, m] - irf)) < 1e-10 * scale
+        assert np.max(np.abs(out[:, :, 0, m] - out[:, :, 2, m] - irf)) < 1e-10 * scale
