@@ -813,3 +813,72 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                         units_local=n_units, sweeps_local=n_units * (burn + MCMCdraws),
                         setup_s=t_setup, run_s=t_run, retries=retries)
     return out
+
+
+# ---------------------------------------------------------------------------------------
+# Generalized impulse responses (generateGIRF2linear.m / generateGIRF2blockhybrid.m)
+
+def _ivech(v, N):
+    """ivech of PHI_all's vech (PHI_((tril(PHI_))~=0), column-major lower triangle)."""
+    M = np.zeros((N, N))
+    r, c = np.nonzero(np.tril(np.ones((N, N))).T)   # column-major order of the lower triangle
+    M[c, r] = v
+    return np.tril(M) + np.tril(M, -1).T
+
+
+def generateGIRF(data, ydates, irfDate, PAI_all, invA_all, PHI_all, sqrtht_all, *, p=12, np_=12,
+                 cumcode=None, shock11=1.0, irfNdraws=1000, irfHorizon=120, blockhybrid=False,
+                 ndxSHADOWRATE=None, ndxOTHERYIELDS=None, ELBbound=0.25, shadowrate_all=None,
+                 elbT0=None, seed=1012023, device=0):
+    """The GIRF simulation of generateGIRF2linear.m / generateGIRF2blockhybrid.m:176-283 for
+    one irfDate and shock scale (shock11 = IRF1scale * shocksize) over the M kept draws,
+    on the device (ccmm_girf): returns fcstYhat / fcstYhat1plus / fcstYhat1minus (medians over
+    the draws of the simulated mean paths), IRF1plus / IRF1minus (medians of +shock - base and
+    -shock - base) with their prc70 tails (normcdf([-1 1]) * 100), and the draws themselves.
+    PAI_all M x K x N, invA_all M x N x N, PHI_all M x N(N+1)/2, sqrtht_all M x T x N (VAR rows
+    p+1..), shadowrate_all M x Ns x elbT (block hybrid); indices 0-based."""
+    data = np.asarray(data, float)
+    ydates = np.asarray(ydates, float)
+    M, K, N = PAI_all.shape
+    t0 = int(np.flatnonzero(ydates == irfDate)[0])               # ndxIRFT0 - 1 (0-based)
+    cum = np.zeros(N, bool) if cumcode is None else np.asarray(cumcode, bool)
+    if blockhybrid:
+        yidx = np.union1d(ndxSHADOWRATE, ndxOTHERYIELDS)
+        yields = np.zeros(N, bool)
+        yields[yidx] = True
+        actual = ~yields
+        ns = K + yidx.size * p
+    else:
+        yields = actual = None
+        ns = K
+    Xj = np.zeros((ns, M))
+    for mm in range(M):
+        thisData = data[:t0 + 1].copy()                           # jumpoffData (:198-201)
+        if blockhybrid and shadowrate_all is not None and t0 + 1 - elbT0 - p > 0:
+            n = t0 + 1 - elbT0 - p                                # (:166-172, 207-209)
+            thisData[p + elbT0:t0 + 1, ndxSHADOWRATE] = shadowrate_all[mm, :, :n].T
+        Xj[0, mm] = 1.0
+        for l in range(p):
+            Xj[1 + l * N:1 + (l + 1) * N, mm] = thisData[t0 - l, :N]
+            if blockhybrid:                                       # (:215-218)
+                Xj[K + l * yidx.size:K + (l + 1) * yidx.size, mm] = thisData[t0 - l, yidx]
+    SV0 = np.asarray(sqrtht_all, float)[:, t0 - p, :].T          # SVjumpoffDraws (:164)
+    sqrtPHI = np.stack([np.linalg.cholesky(_ivech(PHI_all[m], N)) for m in range(M)], -1)
+    out = context(device).girf(np.moveaxis(PAI_all, 0, -1), np.moveaxis(invA_all, 0, -1), sqrtPHI, SV0,
+                               Xj, irfHorizon, irfNdraws, shock11, bh=blockhybrid, actual=actual,
+                               ndxYields=yields, elb=ELBbound, cumcode=cum, np_=np_, seed=seed)
+    base, plus, minus = out[:, :, 0, :], out[:, :, 1, :], out[:, :, 2, :]
+    prc70 = np.array([_normcdf(-1), _normcdf(1)]) * 100
+    ctx = context(device)
+
+    def med_tails(d):          # median / prctile over the draws (dimension 3)
+        s = ctx.draw_summaries(d.reshape(N * irfHorizon, M).T, pct=prc70)
+        return s["median"].reshape(N, irfHorizon), s["quantiles"].reshape(N, irfHorizon, 2)
+
+    res = dict(fcstYHATdraws=base, fcstYHATdraws1plus=plus, fcstYHATdraws1minus=minus)
+    res["fcstYhat"] = med_tails(base)[0]
+    res["fcstYhat1plus"] = med_tails(plus)[0]
+    res["fcstYhat1minus"] = med_tails(minus)[0]
+    res["IRF1plus"], res["IRF1plusTails"] = med_tails(plus - base)       # :268-276
+    res["IRF1minus"], res["IRF1minusTails"] = med_tails(minus - base)
+    return res

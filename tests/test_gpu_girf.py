@@ -79,3 +79,32 @@ def test_girf_linear_reference_size(ctx, gi):
         scale = max(np.max(np.abs(out[:, :, 0, m])), 1.0)
         assert np.max(np.abs(out[:, :, 1, m] - out[:, :, 0, m] - irf)) < 1e-10 * scale
         assert np.max(np.abs(out[:, :, 0, m] - out[:, :, 2, m] - irf)) < 1e-10 * scale
+
+
+def test_generate_girf_driver_linear(pkg, gi, fred):
+    """samplers.generateGIRF (generateGIRF2linear.m:176-283) on synthetic kept draws: the
+    median IRF over the draws equals the median of the deterministic responses."""
+    rng = np.random.default_rng(5)
+    N, p, M, H = 20, 12, 16, 24
+    PAI, invA, sqrtPHI, SV0, _ = _draws(rng, N, p, M, False, 0)
+    PHI = np.einsum("ijm,kjm->ikm", sqrtPHI, sqrtPHI)
+    vech = np.array([[PHI[i, j, m] for j in range(N) for i in range(N) if i >= j] for m in range(M)])
+    T = len(fred["ydates"]) - p
+    sqrtht = np.repeat(SV0.T[:, None, :], T, axis=1)
+    irfDate = fred["ydates"][-30]
+    res = pkg.samplers.generateGIRF(fred["data"], fred["ydates"], irfDate, np.moveaxis(PAI, -1, 0),
+                                    np.moveaxis(invA, -1, 0), vech, sqrtht, p=p, shock11=0.5,
+                                    irfNdraws=64, irfHorizon=H, cumcode=fred["cumcode"])
+    irfs = np.zeros((N, H, M))
+    for m in range(M):
+        A = gi.companion(PAI[..., m], N, p)
+        x = np.zeros(A.shape[0])
+        x[1:1 + N] = 0.5 * invA[:, 0, m]
+        for h in range(H):
+            irfs[:, h, m] = x[1:1 + N]
+            x = A @ x
+        irfs[fred["cumcode"], :, m] = np.cumsum(irfs[fred["cumcode"], :, m], axis=1) / 12
+    want = np.median(irfs, axis=2)
+    assert np.max(np.abs(res["IRF1plus"] - want)) < 1e-9 * max(1.0, np.abs(want).max())
+    assert np.max(np.abs(res["IRF1minus"] + want)) < 1e-9 * max(1.0, np.abs(want).max())
+    assert res["IRF1plusTails"].shape == (N, H, 2)
