@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--s120-groups", type=int, default=2,
                     help="chain groups (HIP streams driven from host threads) of the S120 lines")
     ap.add_argument("--s120-only", action="store_true", help="run only the S120 lines (probe)")
+    ap.add_argument("--girf-draws", type=int, default=256,
+                    help="MCMC draws of the block-hybrid GIRF line (generateGIRF2blockhybrid, 1000 shock "
+                         "paths x 120 horizons x 12 sims per draw); 0 = skip")
     ap.add_argument("--cpu-workers", type=int, default=0,
                     help="parallel single-thread CPU baseline processes (0: min(16, cpus))")
     return ap.parse_args()
@@ -161,6 +164,9 @@ def main():
     if args.s120_steps > 0:
         s120 = [bench_s120(pkg, ctx, int(b), args, rank, barrier, dist)
                 for b in args.s120_chains.split(",") if b.strip()]
+    girf = None
+    if args.girf_draws > 0:
+        girf = bench_girf(pkg, ctx, d, args.girf_draws, rank, barrier, dist)
     oos = None
     if args.oos_steps > 0:
         oos = [bench_oos(pkg, ctx, d, int(c), args, rank, barrier, dist)
@@ -255,6 +261,8 @@ def main():
         out["s120"] = s120
     if hy is not None:
         out["hybrid"] = hy
+    if girf is not None:
+        out["girf"] = girf
     if fc is not None:
         out["predictive"] = fc
     if cpu is not None:
@@ -369,6 +377,52 @@ def bench_oos(pkg, ctx, d, C, args, rank, barrier, dist, H=48, Nd=10):
     if kt:
         res["kernel_ms_per_sweep"] = {k: round(v[0] / v[1], 4) for k, v in kt.items() if v[1]}
     return res
+
+
+def bench_girf(pkg, ctx, d, M, rank, barrier, dist, nsim=1000, H=120):
+    """generateGIRF2blockhybrid.m:199-259 on the device (ccmm_girf): M kept draws (synthetic
+    stable draws of the N = 20, p = 12 block-hybrid VAR), nsim = 1000 shock paths x 4
+    antithetic sets x 3 scenarios x 120 horizons each.  value = MCMC draws per second (units
+    shared over ranks: each rank simulates M draws).  MFMA work: 12 nsim H 2 N (K + Ny p + N)
+    algorithmic flop per draw."""
+    _progress(f"bench_girf {M}")
+    import time as _t
+    N, p = 20, 12
+    ndxS, ndxO, ndxY = pkg.model.setShadowYields(d["ncode"], 0.25)
+    yields = np.zeros(N, bool)
+    yields[ndxY] = True
+    K, Ny = 1 + N * p, int(yields.sum())
+    rng = np.random.default_rng(17 + rank)
+    PAI = np.zeros((K, N, M))
+    PAI[0] = 0.1 * rng.standard_normal((N, M))
+    for l in range(p):
+        PAI[1 + l * N:1 + (l + 1) * N] = ((0.5 / (l + 1) ** 2) * np.eye(N))[..., None] + \
+            0.01 * rng.standard_normal((N, N, M))
+    invA = np.repeat(np.eye(N)[..., None], M, -1) + 0.1 * np.tril(np.ones((N, N)), -1)[..., None] * \
+        rng.standard_normal((N, N, M))
+    sqrtPHI = np.repeat((0.1 * np.eye(N))[..., None], M, -1)
+    SV0 = 0.5 + rng.random((N, M))
+    Xj = np.vstack([np.ones((1, M)), 0.5 + 0.3 * rng.standard_normal((N * p + Ny * p, M))])
+    kw = dict(bh=True, actual=~yields, ndxYields=yields, elb=0.25, cumcode=d["cumcode"], np_=12)
+    ctx.girf(PAI[..., :2], invA[..., :2], sqrtPHI[..., :2], SV0[:, :2], Xj[:, :2], H, 64, 0.11, **kw)
+    barrier()
+    t0 = _t.perf_counter()
+    out = ctx.girf(PAI, invA, sqrtPHI, SV0, Xj, H, nsim, 0.11, **kw)
+    barrier()
+    el = _t.perf_counter() - t0
+    assert np.all(np.isfinite(out)), "non-finite GIRF"
+    world = dist.get_world_size() if dist is not None else 1
+    flop = 12.0 * nsim * H * 2 * N * (K + Ny * p + N) * M
+    flop_mfma = 12.0 * nsim * H * 2 * 16 * ((N + 15) // 16) * 4 * ((K + Ny * p + N + 3) // 4) * M
+    return {"workload": f"generateGIRF2blockhybrid: {M} MCMC draws x {nsim} shock paths x 4 antithetic "
+                        f"sets x 3 scenarios x {H} horizons (N = {N}, p = {p}, {Ny} yields), one call "
+                        f"incl. host<->device copies", "value": round(world * M / el, 2),
+            "unit": "MCMC draws/s", "seconds": round(el, 3), "draws": M,
+            "fp64_mfma": {"achieved": round(flop / el / 1e12, 2), "executed": round(flop_mfma / el / 1e12, 2),
+                          "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": round(flop / el / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                          "note": "achieved = algorithmic flop (unpadded N x states) / wall time; executed "
+                                  "counts the padded 16 x 16 x 4 tiles"}}
 
 
 def bench_block_hybrid(pkg, ctx, d, B, args, rank, barrier, dist):
