@@ -14,6 +14,7 @@ Layers:
   distributed.py   vintage/chain sharding over GPUs, end-of-run reductions
 """
 from . import _abi, distributed, model, samplers, synthetic  # noqa: F401
-from ._abi import MODEL_BLOCKHYBRID, MODEL_HYBRID, MODEL_LINEAR, Chains, Context, load_library  # noqa: F401
+from ._abi import (MODEL_BLOCKHYBRID, MODEL_HYBRID, MODEL_LINEAR, MODEL_SHADOWRATE, Chains,  # noqa: F401
+                   Context, load_library)
 from .samplers import (CTA, CTAsys, drawTruncNormal, mcmcVAR,  # noqa: F401
                        mcmcVARshadowrateBlockHybrid)

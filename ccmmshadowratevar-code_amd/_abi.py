@@ -23,6 +23,7 @@ CCMM_ERR_NOTSPD = -4
 MODEL_LINEAR = 0
 MODEL_BLOCKHYBRID = 1
 MODEL_HYBRID = 2  # mcmcVARhybridGibbs.m: K = N*p + 1 + Ns*p
+MODEL_SHADOWRATE = 3  # mcmcVARshadowrate.m: shadow-rate design for all equations, linear forecasts
 
 RNG_PAI, RNG_A, RNG_SVU, RNG_SVZ, RNG_PHI, RNG_ELB, RNG_FCST, RNG_PS = 1, 2, 3, 4, 5, 6, 7, 8
 CCMM_WARN_MVNCDF = 3
@@ -84,6 +85,7 @@ _SIGS = {
     "ccmm_chains_set_fcst": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, C.c_int]),
     "ccmm_chains_set_fcst_slot": (C.c_int, [C.c_void_p, C.c_int, _dp]),
     "ccmm_chains_fcst_stored": (C.c_int, [C.c_void_p]),
+    "ccmm_chains_set_fcst_censor": (C.c_int, [C.c_void_p, _u8p]),
     "ccmm_chains_get_fcst": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp, _dp]),
     "ccmm_chains_set_elb_model": (C.c_int, [C.c_void_p, _ip, _u8p]),
     "ccmm_chains_set_elb_slot": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p]),
@@ -417,7 +419,7 @@ class Chains:
         N, T = self.N, self.T
         blocks = [("PAI", self.K * N, "n"), ("A", N * (N - 1) // 2, "n"), ("SVU", N * T, "u"),
                   ("SVZ", N * (T + 1), "n"), ("PHI", N * (T + cf.dPHI), "n")]
-        if self.model in (MODEL_BLOCKHYBRID, MODEL_HYBRID):
+        if self.model in (MODEL_BLOCKHYBRID, MODEL_HYBRID, MODEL_SHADOWRATE):
             blocks.append(("ELB", self.Ns * self.elbTmax * (cf.elb_gibbsburn + 1), "u"))
         if getattr(self, "fH", 0):
             blocks.append(("FCST", 2 * N * self.fH * self.fNd, "n"))
@@ -528,7 +530,7 @@ class Chains:
         N, K, T, B = self.N, self.K, self.T, self.B
         shapes = dict(PAI_all=(M, K, N, B), PHI_all=(M, N * (N + 1) // 2, B), invA_all=(M, N, N, B),
                       sqrtht_all=(M, T, N, B))
-        if self.model in (MODEL_BLOCKHYBRID, MODEL_HYBRID):
+        if self.model in (MODEL_BLOCKHYBRID, MODEL_HYBRID, MODEL_SHADOWRATE):
             shapes["shadowrate_all"] = (M, self.Ns, self.elbTmax, B)
         out = {k: np.zeros(v, order="F") for k, v in shapes.items() if which is None or k in which}
         rc = self.lib.ccmm_chains_get_draws(self.handle, *[_ptr(out.get(k)) for k in
@@ -551,6 +553,13 @@ class Chains:
         y = _f(np.asarray(yrealized, float).reshape(self.N, -1, order="F")[:, 0])
         _check(self.lib.ccmm_chains_set_fcst_slot(self.handle, int(slot), _ptr(y)),
                "ccmm_chains_set_fcst_slot")
+
+    def set_fcst_censor(self, floor_in_recursion=None):
+        """Variables floored inside the censored simulation (None: ndxYields)."""
+        m = None if floor_in_recursion is None else \
+            np.ascontiguousarray(np.asarray(floor_in_recursion, bool), dtype=np.uint8)
+        _check(self.lib.ccmm_chains_set_fcst_censor(self.handle, None if m is None else m.ctypes.data_as(_u8p)),
+               "ccmm_chains_set_fcst_censor")
 
     def fcst_stored(self):
         return int(self.lib.ccmm_chains_fcst_stored(self.handle))

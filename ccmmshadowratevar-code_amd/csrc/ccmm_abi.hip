@@ -244,6 +244,7 @@ struct ccmm_chains {
   // hybrid model (mcmcVARhybridGibbs.m): same chain layout as bh, one design per chain
   // (CTA, no actual-rate block), trailing columns = censored actual-rate lags
   bool hybrid = false;
+  bool fcst_bh = false;  // block-hybrid companion in the predictive density (k_fcst a.bh)
   bool have_elb_model = false;
   std::vector<bool> have_elb_slot;
   std::vector<int> hNdxS, hElbT0, hElbT;
@@ -264,7 +265,8 @@ struct ccmm_chains {
   // mcmcVARshadowrateBlockHybrid.m:550-669), kept on the device
   bool have_fcst = false;
   int fH = 0, fNd = 0, fKeep = 0, fstored = 0, fldXj = 0, fnw = 1;
-  DBuf<uint8_t> fYields;
+  DBuf<uint8_t> fYields, fRecFloor;
+  bool have_rec_floor = false;
   std::vector<bool> have_fcst_slot;
   DBuf<double> fYreal, fXj, fY, fYc, fYhat, fSc, fYsum, fYcsum, fYhatsum, fScStore, fPaths, fPathsC;
   DBuf<int> fStatus;
@@ -393,7 +395,10 @@ struct ccmm_chains {
   void init(ccmm_ctx* c, const ccmm_chain_config& cf, int nX, int nY) {
     ctx = c;
     cfg = cf;
-    bh = cf.model == CCMM_MODEL_BLOCKHYBRID || cf.model == CCMM_MODEL_HYBRID;
+    bh = cf.model == CCMM_MODEL_BLOCKHYBRID || cf.model == CCMM_MODEL_HYBRID || cf.model == CCMM_MODEL_SHADOWRATE;
+    // mcmcVARshadowrate.m: the ELB step of the block hybrid, one shadow-rate design for every
+    // equation (no actual-rate block), the linear model's predictive density (:536-641)
+    fcst_bh = bh && cf.model != CCMM_MODEL_SHADOWRATE;
     hybrid = cf.model == CCMM_MODEL_HYBRID;
     if (bh) {
       require(cf.Ns >= 1 && cf.Ns <= kElbNsMax, "Ns must be in [1, 4]");
@@ -1349,7 +1354,7 @@ struct ccmm_chains {
       fPaths.alloc(B * cap * Nd * HN);
       fPathsC.alloc(B * cap * Nd * HN);
     }
-    int nw = std::min((bh ? Nd : Nd + 1), kFcstMaxWaves);
+    int nw = std::min((fcst_bh ? Nd : Nd + 1), kFcstMaxWaves);
     while (nw > 1 && fcst_lds_bytes(N, p, cfg.K, nw) > 160 * 1024) --nw;
     require(fcst_lds_bytes(N, p, cfg.K, nw) <= 160 * 1024, "forecast state does not fit LDS");
     fnw = nw;
@@ -1450,10 +1455,11 @@ struct ccmm_chains {
     const int N = d.N, B = d.B, H = fH, Nd = fNd;
     ChainState cs = view();
     FcstArgs a{};
-    a.B = B; a.N = N; a.p = cfg.p; a.K = cfg.K; a.H = H; a.Nd = Nd; a.bh = bh ? 1 : 0;
+    a.B = B; a.N = N; a.p = cfg.p; a.K = cfg.K; a.H = H; a.Nd = Nd; a.bh = fcst_bh ? 1 : 0;
     a.PAI = PAI.p; a.ldPAI = d.KP; a.invA = invA.p; a.logSV = h.p; a.ldSV = d.TP;
     a.svT = Tslot.p; a.slot = slot.p; a.sqrtPHI = sqrtPHI.p; a.Xj = fXj.p; a.ldXj = fldXj;
-    a.yreal = fYreal.p; a.ldY = N; a.ndxYields = fYields.p; a.actual = bh ? dActual.p : nullptr;
+    a.yreal = fYreal.p; a.ldY = N; a.ndxYields = fYields.p; a.actual = fcst_bh ? dActual.p : nullptr;
+    a.recFloor = have_rec_floor ? fRecFloor.p : nullptr;
     a.elb = cfg.elb;
     if (ra.crn) {
       a.svz = ra.crn + ra.off[CCMM_RNG_FCST];
@@ -1472,7 +1478,7 @@ struct ccmm_chains {
                                    (int)lds));
       hipLaunchKernelGGL(k_fcst, dim3(B), dim3(64 * fnw), lds, ctx->stream, a);
       hipLaunchKernelGGL(k_fcst_accum, dim3(B), dim3(256), 0, ctx->stream, N, H, Nd,
-                         cfg.store_capacity, fstored, fY.p, fYc.p, bh ? nullptr : fYhat.p, fSc.p,
+                         cfg.store_capacity, fstored, fY.p, fYc.p, fcst_bh ? nullptr : fYhat.p, fSc.p,
                          fYsum.p, fYcsum.p, fYhatsum.p, fScStore.p, fKeep ? fPaths.p : nullptr,
                          fKeep ? fPathsC.p : nullptr);
     });
@@ -2424,6 +2430,23 @@ int ccmm_chains_set_fcst_slot(ccmm_chains* ch, int slot, const double* yrealized
   });
 }
 
+int ccmm_chains_set_fcst_censor(ccmm_chains* ch, const uint8_t* floor_in_recursion) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    require(ch->have_fcst, "ccmm_chains_set_fcst must be called first");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    if (!floor_in_recursion) {
+      ch->have_rec_floor = false;
+      return 0;
+    }
+    ch->fRecFloor.alloc(ch->cfg.N);
+    HIPCHECK(hipMemcpy(ch->fRecFloor.p, floor_in_recursion, ch->cfg.N, hipMemcpyHostToDevice));
+    ch->have_rec_floor = true;
+    return 0;
+  });
+}
+
 int ccmm_chains_fcst_stored(const ccmm_chains* ch) { return ch && ch->have_fcst ? ch->fstored : -1; }
 
 int ccmm_chains_get_fcst(ccmm_chains* ch, double* scores, double* fYsum, double* fYcsum,
@@ -2476,13 +2499,14 @@ int ccmm_chains_set_elb_model(ccmm_chains* ch, const int* ndxS, const uint8_t* a
   return guarded([&] {
     require(ch && ndxS, "null argument");
     require(ch->bh, "chain set was not created with CCMM_MODEL_BLOCKHYBRID / CCMM_MODEL_HYBRID");
-    require(actual_block || ch->hybrid, "null argument");
+    const bool no_block = ch->hybrid || ch->cfg.model == CCMM_MODEL_SHADOWRATE;
+    require(actual_block || no_block, "null argument");
     HIPCHECK(hipSetDevice(ch->ctx->device));
     HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
     std::vector<uint8_t> none(ch->cfg.N, 0);
-    if (ch->hybrid) {
+    if (no_block) {
       for (int i = 0; actual_block && i < ch->cfg.N; ++i)
-        require(!actual_block[i], "hybrid model has no actual-rate block (pass NULL or zeros)");
+        require(!actual_block[i], "hybrid / shadow-rate model has no actual-rate block (pass NULL or zeros)");
       actual_block = none.data();
     }
     ch->set_elb_model(ndxS, actual_block);

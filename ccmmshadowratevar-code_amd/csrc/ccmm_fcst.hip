@@ -39,6 +39,9 @@ struct FcstArgs {
   const double* yreal;    // yrealized(:,1) of chain c at yreal + slot(c) * ldY
   int ldY;
   const uint8_t* ndxYields;  // [N]
+  const uint8_t* recFloor;   // [N] linear model: variables floored inside the censored recursion
+                             //   (nullptr: ndxYields, mcmcVAR.m:360-366; mcmcVARshadowrate.m:539-546
+                             //   floors ndxOTHERYIELDS only)
   const uint8_t* actual;     // [N] actualrateBlock (bh) or nullptr
   double elb;
   const double* svz;      // randn(N, H*Nd) of chain c at svz + c * crnStride, or nullptr (Philox)
@@ -305,6 +308,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   const double* zc = a.z ? a.z + (size_t)c * a.crnStride : nullptr;
   const bool isact = a.bh && lane < N && a.actual[lane];
   const bool isyield = lane < N && a.ndxYields[lane];
+  const bool isrec = lane < N && (a.recFloor ? a.recFloor[lane] : a.ndxYields[lane]);
   Rng rng;
   rng.crn = nullptr;
   rng.seed = a.seed;
@@ -371,7 +375,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
           yl = sl2 + nu;
           yc = sc + nu;
           // censored simulation (mcmcVAR.m:360-366)
-          if (isyield && yc < a.elb) yc = a.elb;
+          if (isrec && yc < a.elb) yc = a.elb;
         }
         if (mean_path) {
           a.yhat[((size_t)c * H + hh) * N + lane] = yl;

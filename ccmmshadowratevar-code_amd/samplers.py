@@ -199,6 +199,92 @@ def mcmcVARshadowrateBlockHybrid(thisT, MCMCdraws, p, np_, data0, ydates0, actua
     return tuple(res)
 
 
+def mcmcVARshadowrate(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMean, doRATSprior,
+                      doPAIactual, ndxSHADOWRATE, ndxOTHERYIELDS, doELBsampling, ELBbound, elbT0,
+                      check_stationarity=0, IRF1scale=None, IRFcumcode=None, yrealized=None,
+                      fcstNdraws=None, fcstNhorizons=None, rndStream=1012023, doprogress=False, *,
+                      nchains=1, device=0, burnin=None, gibbsburn=100, Nproposals=100, stats=None):
+    """mcmcVARshadowrate.m:1-17 (the shadow-rate VAR without the actual-rate block): CTA on
+    the shadow-rate design for every equation (:322-326), the ELB step of the block hybrid
+    with YHAT0 = [] (Gibbs for m < MCMCburnin/2, then elb.Nproposals = 100 PS proposals,
+    :397-436), and the linear model's predictive density whose censored recursion floors
+    ndxOTHERYIELDS only (:539-546), chain set model CCMM_MODEL_SHADOWRATE.  Outputs 1-17:
+    PAI_all, PHI_all, invA_all, sqrtht_all, shadowrate_all, missingrate_all, fcstYdraws,
+    fcstYhat, fcstYcensorDraws, fcstYcensorHat, fcstShadowrateDraws, fcstShadowrateHat,
+    fcstYhatRB, fcstLogscoreDraws, fcstLogscoreXdraws, fcstLogscoreIdraws, stackAccept
+    (:630-700).  Indices 0-based."""
+    if check_stationarity:
+        raise NotImplementedError("check_stationarity=1 is not supported; the reference drivers "
+                                  "all pass 0")
+    if doPAIactual:
+        raise NotImplementedError("doPAIactual = true (CTA on the actual data, :322-324) is not built")
+    if not doELBsampling:
+        raise NotImplementedError("doELBsampling = false (missing-data treatment) is not built")
+    if IRF1scale is not None:
+        raise NotImplementedError("in-sampler IRF outputs: use samplers.generateGIRF")
+    doPredictiveDensity = bool(fcstNdraws)
+    if doPredictiveDensity and fcstNdraws % MCMCdraws:
+        raise ValueError("fcstNdraws must be multiple of MCMCdraws")
+    N = np.asarray(data0).shape[1]
+    bm = build_bh(thisT, p, np_, data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS, minnesotaPriorMean,
+                  ELBbound, elbT0, doRATSprior, actualrateBlock=np.zeros(N, bool))
+    m = bm.var
+    B = int(nchains)
+    burn = MCMCdraws if burnin is None else int(burnin)
+    ch = _abi.Chains(context(device), N=m.N, p=m.p, T=m.T, B=B, ndata=1, crn=False,
+                     store_capacity=MCMCdraws, seed=int(rndStream), model=_abi.MODEL_SHADOWRATE,
+                     Ns=len(bm.ndxS), elbTmax=bm.elbT, elb_gibbsburn=gibbsburn, elb=ELBbound)
+    ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    ch.set_elb_model(bm.ndxS, None)
+    ch.set_elb_slot(0, bm.elbT0, bm.sNaN)
+    if Nproposals:
+        ch.set_elb_ps(Nproposals, max(1, -(-burn // 2)))      # m >= MCMCburnin * .5 (:403)
+    ndxY = np.union1d(bm.ndxS, bm.ndxO)
+    yields = np.zeros(N, bool)
+    yields[ndxY] = True
+    if doPredictiveDensity:
+        H, Nd = int(fcstNhorizons), fcstNdraws // MCMCdraws
+        ch.set_fcst(H, Nd, yields, keep_paths=True)
+        other = np.zeros(N, bool)
+        other[bm.ndxO] = True
+        ch.set_fcst_censor(other)                             # :539-546
+        ch.set_fcst_slot(0, np.asarray(yrealized, float).reshape(N, -1, order="F")[:, 0])
+    st = initial_state(m, B)
+    ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+    _run_chain_set(ch, burn, MCMCdraws, doprogress)
+    stack = np.zeros((MCMCdraws, B), np.int32)
+    if Nproposals:
+        ps = ch.get_ps()
+        stack = ps["stackAccept"]
+        if stats is not None:
+            stats.update(countELBaccept=ps["countAccept"], countELBacceptBurnin=ps["countAcceptBurnin"])
+    fc = ch.get_fcst(paths=True) if doPredictiveDensity else None
+    out = ch.get_draws()
+    ch.close()
+    sr = out.get("shadowrate_all", np.full((MCMCdraws, len(bm.ndxS), 0, B), np.nan))
+    res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"], sr,
+           np.full_like(sr, np.nan)]
+    if doPredictiveDensity:
+        fYd = fc["paths"].reshape(N, H, fcstNdraws, B, order="F").copy()
+        fSd = fYd[ndxY].copy()                                # fcstShadowrateDraws (:640)
+        yd = fYd[ndxY]
+        yd[yd < ELBbound] = ELBbound                          # :642-645
+        fYd[ndxY] = yd
+        fYc = fc["paths_censored"].reshape(N, H, fcstNdraws, B, order="F").copy()
+        yc = fYc[bm.ndxS]
+        yc[yc < ELBbound] = ELBbound                          # :676-681
+        fYc[bm.ndxS] = yc
+        RB = fc["yhatsum"] / MCMCdraws                        # :639
+        fYhat = RB.copy()
+        fYhat[ndxY] = fYd[ndxY].mean(axis=2)                  # :683-684
+        sc = [fc["scores"][:, :, k, :].reshape(fcstNdraws, B, order="F") for k in (1, 2, 3)]
+        res += [fYd, fYhat, fYc, fYc.mean(axis=2), fSd, RB[ndxY], RB, sc[0], sc[1], sc[2]]
+    res.append(stack)
+    if B == 1:
+        res = [a[..., 0] for a in res]
+    return tuple(res)
+
+
 def mcmcVARhybridGibbs(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateWeight,
                        minnesotaPriorMean, doRATSprior, ndxSHADOWRATE, ndxOTHERYIELDS, doELBsampling,
                        doELBsampleAlternate, ELBbound, elbT0, check_stationarity=0, IRF1scale=None,

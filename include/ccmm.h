@@ -53,6 +53,8 @@ extern "C" {
 #define CCMM_MODEL_LINEAR 0        /* mcmcVAR.m */
 #define CCMM_MODEL_BLOCKHYBRID 1   /* mcmcVARshadowrateBlockHybrid.m */
 #define CCMM_MODEL_HYBRID 2        /* mcmcVARhybridGibbs.m: K = N*p + 1 + Ns*p, X = [1, lags, Xffrlags] */
+#define CCMM_MODEL_SHADOWRATE 3    /* mcmcVARshadowrate.m: shadow-rate design for every equation, ELB step
+                                      as the block hybrid, the linear model's predictive density */
 
 /* RNG block ids (Philox counter word 3); also the order of the per-sweep CRN blocks */
 #define CCMM_RNG_PAI 1   /* randn(K,N)            CTA.m:58 / CTAsys.m:58 */
@@ -257,6 +259,10 @@ int ccmm_chains_set_fcst(ccmm_chains* ch, int H, int Nd, const uint8_t* ndxYield
 /* yrealized(:,1) of data slot `slot` (N values; goVARshadowrateBlockHybrid.m:267-283,
  * shadow rates floored at the ELB by the caller). */
 int ccmm_chains_set_fcst_slot(ccmm_chains* ch, int slot, const double* yrealized);
+/* Linear predictive density: the variables floored at the ELB inside the censored
+ * simulation (N bytes; NULL restores the default ndxYields, mcmcVAR.m:360-366).
+ * mcmcVARshadowrate.m:539-546 floors ndxOTHERYIELDS only. */
+int ccmm_chains_set_fcst_censor(ccmm_chains* ch, const uint8_t* floor_in_recursion);
 /* Kept draws with a forecast record so far (-1: not configured). */
 int ccmm_chains_fcst_stored(const ccmm_chains* ch);
 /* Copy out and reset the forecast records of the M kept draws so far:
