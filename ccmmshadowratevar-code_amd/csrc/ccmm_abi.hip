@@ -2150,7 +2150,7 @@ ccmm_chains* ccmm_chains_create(ccmm_ctx* ctx, const ccmm_chain_config* cfg) {
   int rc = guarded([&] {
     require(ctx && cfg, "null argument");
     require(cfg->model == CCMM_MODEL_LINEAR || cfg->model == CCMM_MODEL_BLOCKHYBRID ||
-                cfg->model == CCMM_MODEL_HYBRID, "unknown model");
+                cfg->model == CCMM_MODEL_HYBRID || cfg->model == CCMM_MODEL_SHADOWRATE, "unknown model");
     HIPCHECK(hipSetDevice(ctx->device));
     ch = new ccmm_chains;
     const int extra = cfg->model != CCMM_MODEL_LINEAR ? cfg->B : 0;

@@ -156,7 +156,6 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   const int c = blockIdx.x, s = cs.slot[c], T = Tslot[s];
   const int ln = lane < NN ? lane : 0;
   const bool real = lane < n;
-  const Rng rng = ra.make(c);
   const double* sq = cs.sqrtPHI + (size_t)c * n * n;  // column-major lower n x n
   const double* obs = cs.svobs + (size_t)c * n * TP;
   const double* irv = cs.svir + (size_t)c * n * TP;
@@ -227,8 +226,8 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
     if (t == 0) return real ? V0m[ln] : 0.0;
     return real ? obt * irt : 0.0;
   };
-  // the normals z_t (block t, row ln) are drawn by all waves at the start of phase C
-  // (independent work off the serial block loops) and read back from Zg
+  // the normals z_t (block t, row ln) are drawn grid-wide by k_sv_normals before this
+  // kernel (independent work off the per-chain serial path) and read back from Zg
   auto zdraw = [&](int t) __attribute__((always_inline)) -> double {
     if (mode & 32) return 0.0;  // timing ablation only
     return real ? Zg[(size_t)t * NN + ln] : 0.0;
@@ -440,11 +439,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   __syncthreads();
 
   // ---------------------------------------------------------------- phase C: back substitution
-  for (int e = tid; e < (T + 1) * n; e += 64 * NW) {
-    const int t = e / n, i = e - t * n;
-    Zg[(size_t)t * NN + i] = rng.normal(CCMM_RNG_SVZ, (uint32_t)(i + n * t));
-  }
-  __syncthreads();
+  // (the normals z_t were drawn into Zg by k_sv_normals before this kernel)
   double qrow[NN];
 #pragma unroll
   for (int m = 0; m < NN; ++m) qrow[m] = Ql[ln * NN + m];
@@ -605,6 +600,19 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   if (bad && lane == 0) atomicOr(&cs.status[c], 8);
 }
 
+// randn(N, T+1) of every chain (CCMM_RNG_SVZ; CRN: the host block) -> Zg, block-major
+// [t][NN]: drawn by the whole GPU ahead of k_sv_part instead of inside its serial chain
+__global__ void k_sv_normals(Dims d, const int* __restrict__ Tslot, ChainState cs, RngArgs ra, double* gbuf,
+                             int NN) {
+  const int c = blockIdx.y;
+  const int n = d.N, T = Tslot[cs.slot[c]];
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (T + 1) * n) return;
+  const int t = e / n, i = e - t * n;
+  const Rng rng = ra.make(c);
+  gbuf[(size_t)(d.B + c) * (d.TP + 1) * NN + (size_t)t * NN + i] = rng.normal(CCMM_RNG_SVZ, (uint32_t)(i + n * t));
+}
+
 template <int NN, int NW, bool PACK>
 static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
                                 const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
@@ -614,6 +622,8 @@ static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const
   hipError_t e = hipFuncSetAttribute((const void*)k_sv_part<NN, NW, PACK>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_sv_normals, dim3(((d.TP + 1) * d.N + 255) / 256, d.B), dim3(256), 0, st, d, Tslot, cs, ra,
+                     gbuf, NN);
   hipLaunchKernelGGL((k_sv_part<NN, NW, PACK>), dim3(d.B), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm, cs,
                      ra, sep, gbuf, mode);
   return hipGetLastError();
