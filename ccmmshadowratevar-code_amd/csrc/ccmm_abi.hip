@@ -2664,6 +2664,7 @@ int ccmm_girf(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const double*
     a.actual = bh ? dAct.p : nullptr; a.yidx = bh ? dY.p : nullptr; a.elb = elb; a.shock11 = shock11;
     a.z = z ? dZ.p : nullptr; a.svz = z ? dSZ.p : nullptr; a.seed = seed;
     a.cumcode = cumcode ? dCum.p : nullptr; a.np_ = np_; a.part = dPart.p; a.out = dOut.p;
+    a.force_generic = std::getenv("CCMM_GIRF_GENERIC") != nullptr ? 1 : 0;  // A/B of the specialised kernel
     HIPCHECK(girf_launch(ctx->stream, a));
     HIPCHECK(hipStreamSynchronize(ctx->stream));
     HIPCHECK(hipMemcpy(yhat, dOut.p, dOut.n * sizeof(double), hipMemcpyDeviceToHost));

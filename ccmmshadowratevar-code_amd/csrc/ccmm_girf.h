@@ -24,6 +24,7 @@ struct GirfArgs {
   double np_;
   double* part;                  // device workspace [M][3][ceil(nsim/4)][H][N]
   double* out;                   // device [M][3][H][N]: baseline, +shock, -shock mean paths
+  int force_generic;             // 1: the table-driven kernel even where a specialised one exists
 };
 
 size_t girf_lds_bytes(int N, int p, int KT);

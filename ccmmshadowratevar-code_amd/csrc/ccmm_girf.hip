@@ -204,6 +204,168 @@ __global__ __launch_bounds__(128) void k_girf(GirfDev g) {
   }
 }
 
+// Specialised form for compile-time p, N4 = ceil4(N), NY4 = ceil4(Ny): the state rows are laid
+// out so that every 4-row k-step lies inside one lag block (blocks padded to N4 / NY4, the
+// constant last), hence the B-operand row of k-step ks is (ring slot of its lag) * N4 + 4 kk
+// + lq with ks -> (lag, kk) known at compile time: no table lookups, the LDS loads of the whole
+// k-loop are independent of the MFMA results and can be issued ahead.
+//   rows: [P x N4 lag ring][P x NY4 actual-rate ring][N4 shocks][4: constant 1, 0, 0, 0]
+template <int P, int N4, int NY4>
+__global__ __launch_bounds__(128) void k_girf_fast(GirfDev g) {
+  constexpr int LAGR = P * N4, ACTR = P * NY4, SHR = LAGR + ACTR, CR = SHR + N4, KR = CR + 4;
+  constexpr int KS = KR / 4;
+  constexpr int NYD = NY4 > 0 ? NY4 : 1;  // divisor (the actual-rate branches are dead when NY4 = 0)
+  extern __shared__ double sm[];
+  const int chunk = blockIdx.x, scen = blockIdx.y, mm = blockIdx.z;
+  const int N = g.N, H = g.H, K = 1 + N * P;
+  const int tid = threadIdx.x, lane = tid & 63, et = tid >> 6, lq = lane >> 4;
+  double* X = sm;                            // [KR][kGS]
+  double* logsv = X + KR * kGS;              // [4][N]
+  double* ybuf = logsv + 4 * N;              // [N][kGS]
+  double* nrm = ybuf + N * kGS;              // [2][4][N]
+  const double* PAI = g.PAI + (size_t)mm * N * K;
+  const double* invA = g.invA + (size_t)mm * N * N;
+  const double* sqP = g.sqrtPHI + (size_t)mm * N * N;
+  const double* SV0 = g.SV0 + (size_t)mm * N;
+  const double* Xj = g.Xj + (size_t)mm * g.ldX;
+  const double s11 = scen == 0 ? 0.0 : (scen == 1 ? g.shock11 : -g.shock11);
+  double af[KS];
+  {
+    const int eq = 16 * et + (lane & 15);
+    const bool act = g.bh && eq < N && g.actual[eq];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = 4 * ks + lq;
+      double v = 0.0;
+      if (eq < N) {
+        if (k < LAGR) {
+          const int l = k / N4, j = k - l * N4;
+          if (j < N) {
+            v = PAI[(size_t)eq * K + 1 + l * N + j];
+            if (act)
+              for (int y = 0; y < g.Ny; ++y) v = (g.yidx[y] == j) ? 0.0 : v;
+          }
+        } else if (k < SHR) {
+          const int q = k - LAGR, l = q / NYD, jy = q - l * NYD;
+          if (jy < g.Ny && act) v = PAI[(size_t)eq * K + 1 + l * N + g.yidx[jy]];
+        } else if (k < CR) {
+          if (k - SHR < N) v = invA[eq + (size_t)(k - SHR) * N];
+        } else if (k == CR) {
+          v = PAI[(size_t)eq * K];
+        }
+      }
+      af[ks] = v;
+    }
+  }
+  for (int q = tid; q < KR * kGS; q += blockDim.x) {
+    const int r = q / kGS;
+    double v = 0.0;
+    if (r < LAGR) {
+      const int s = r / N4, j = r - s * N4, l = (s == 0) ? 0 : P - s;
+      if (j < N) v = Xj[1 + l * N + j];
+    } else if (r < SHR) {
+      const int s = (r - LAGR) / NYD, j = r - LAGR - s * NYD, l = (s == 0) ? 0 : P - s;
+      if (j < g.Ny) v = Xj[K + l * g.Ny + j];
+    } else if (r == CR) {
+      v = Xj[0];
+    }
+    X[q] = v;
+  }
+  for (int q = tid; q < 4 * N; q += blockDim.x) logsv[q] = 0.0;
+  Rng rng;
+  rng.crn = nullptr;
+  rng.seed = g.seed;
+  rng.chain = (uint32_t)mm;
+  rng.sweep = 0;
+  int head = 0;
+  __syncthreads();
+  for (int h = 0; h < H; ++h) {
+    for (int q = tid; q < 4 * N; q += blockDim.x) {
+      const int pl = q / N, i = q - pl * N;
+      const int nn = chunk * 4 + pl;
+      double zs = 0.0, zz = 0.0;
+      if (nn < g.nsim) {
+        const size_t base = ((size_t)nn * H + h) * N;
+        zs = g.svz ? g.svz[(size_t)mm * g.nsim * H * N + base + i] : rng.normal(10, (uint32_t)(base + i));
+        zz = g.z ? g.z[(size_t)mm * g.nsim * H * N + base + i] : rng.normal(9, (uint32_t)(base + i));
+      }
+      nrm[q] = zs;
+      nrm[4 * N + q] = zz;
+    }
+    __syncthreads();
+    for (int q = tid; q < 4 * N; q += blockDim.x) {
+      const int pl = q / N, i = q - pl * N;
+      const int nn = chunk * 4 + pl;
+      double u[4] = {0.0, 0.0, 0.0, 0.0};
+      if (nn < g.nsim) {
+        double inc = 0.0;
+        for (int j = 0; j <= i; ++j) inc = fma(sqP[i + (size_t)j * N], nrm[pl * N + j], inc);
+        const double ls = logsv[q] + inc;
+        logsv[q] = ls;
+        const double sv = exp(ls * 0.5);
+        const double zi = nrm[4 * N + q];
+        const double a = zi * sv * SV0[i], b = zi / sv * SV0[i];
+        const double add = (i == 0 && h == 0) ? s11 : 0.0;
+        u[0] = a + add;
+        u[1] = -a + add;
+        u[2] = b + add;
+        u[3] = -b + add;
+      }
+      for (int v = 0; v < 4; ++v) X[(size_t)(SHR + i) * kGS + v * 4 + pl] = u[v];
+    }
+    __syncthreads();
+    dbl4 acc[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) acc[a] = dbl4{0.0, 0.0, 0.0, 0.0};
+    const int hd = __builtin_amdgcn_readfirstlane(head);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k0 = 4 * ks;
+      int rb;
+      if (k0 < LAGR) {
+        const int l = k0 / N4;
+        const int sl = (hd - l < 0) ? hd - l + P : hd - l;
+        rb = sl * N4 + (k0 - l * N4);
+      } else if (k0 < SHR) {
+        const int l = (k0 - LAGR) / NYD;
+        const int sl = (hd - l < 0) ? hd - l + P : hd - l;
+        rb = LAGR + sl * NYD + (k0 - LAGR - l * NYD);
+      } else {
+        rb = k0;
+      }
+      const double b = X[(rb + lq) * kGS + (lane & 15)];
+      acc[ks & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[ks], b, acc[ks & 3], 0, 0, 0);
+    }
+    __syncthreads();
+    const int nh = (head + 1 == P) ? 0 : head + 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int eq = 16 * et + lq + 4 * r, sim = lane & 15;
+      const double y = (acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r]);
+      if (eq < N) {
+        X[(size_t)(nh * N4 + eq) * kGS + sim] = y;
+        double yo = y;
+        if (g.bh)
+          for (int q = 0; q < g.Ny; ++q)
+            if (g.yidx[q] == eq) {
+              const double ya = y < g.elb ? g.elb : y;
+              X[(size_t)(LAGR + nh * NYD + q) * kGS + sim] = ya;
+              yo = ya;
+            }
+        ybuf[eq * kGS + sim] = yo;
+      }
+    }
+    head = nh;
+    __syncthreads();
+    if (tid < N) {
+      double s = 0.0;
+      for (int sim = 0; sim < kGS; ++sim)
+        if (chunk * 4 + (sim & 3) < g.nsim) s += ybuf[tid * kGS + sim];
+      g.part[((((size_t)mm * 3 + scen) * g.nchunk + chunk) * H + h) * N + tid] = s;
+    }
+  }
+}
+
 __global__ void k_girf_reduce(int M, int N, int H, int nchunk, int nsim, const double* __restrict__ part,
                               const uint8_t* __restrict__ cumcode, double np_, double* out) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;  // (i, scen, mm)
@@ -250,7 +412,17 @@ hipError_t girf_launch(hipStream_t st, const GirfArgs& a) {
     return hipGetLastError();
   };
   hipError_t e;
-  if (nks <= 32) e = go(k_girf<32>);
+  const int N4 = (a.N + 3) / 4 * 4, NY4 = (g.Ny + 3) / 4 * 4;
+  const size_t lds_fast = ((size_t)(a.p * (N4 + NY4) + N4 + 4) * kGS + 12 * a.N + (size_t)a.N * kGS) * sizeof(double);
+  auto go_fast = [&](auto kern) -> hipError_t {
+    hipError_t e2 = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fast);
+    if (e2 != hipSuccess) return e2;
+    hipLaunchKernelGGL(kern, grid, block, lds_fast, st, g);
+    return hipGetLastError();
+  };
+  if (!a.force_generic && a.p == 12 && N4 == 20 && NY4 == 8) e = go_fast(k_girf_fast<12, 20, 8>);
+  else if (!a.force_generic && a.p == 12 && N4 == 20 && NY4 == 0) e = go_fast(k_girf_fast<12, 20, 0>);
+  else if (nks <= 32) e = go(k_girf<32>);
   else if (nks <= 64) e = go(k_girf<64>);
   else if (nks <= 96) e = go(k_girf<96>);
   else return hipErrorInvalidValue;

@@ -108,3 +108,26 @@ def test_generate_girf_driver_linear(pkg, gi, fred):
     assert np.max(np.abs(res["IRF1plus"] - want)) < 1e-9 * max(1.0, np.abs(want).max())
     assert np.max(np.abs(res["IRF1minus"] + want)) < 1e-9 * max(1.0, np.abs(want).max())
     assert res["IRF1plusTails"].shape == (N, H, 2)
+
+
+@pytest.mark.parametrize("bh", [False, True])
+def test_girf_reference_shape_crn(ctx, gi, bh):
+    """N = 20, p = 12 (the specialised aligned-layout kernel k_girf_fast) against the oracle
+    on common random numbers: 2 draws x 5 shock paths x 30 horizons."""
+    rng = np.random.default_rng(21 + bh)
+    N, p, H, nsim, M = 20, 12, 30, 5, 2
+    yields = np.zeros(N, bool)
+    yields[[14, 15, 16, 17, 18, 19]] = True
+    PAI, invA, sqrtPHI, SV0, Xj = _draws(rng, N, p, M, bh, 6)
+    z = rng.standard_normal((N, H, nsim, M))
+    svz = rng.standard_normal((N, H, nsim, M))
+    cum = np.zeros(N, bool)
+    cum[:5] = True
+    got = ctx.girf(PAI, invA, sqrtPHI, SV0, Xj, H, nsim, 0.11, bh=bh, actual=~yields, ndxYields=yields,
+                   elb=0.25, cumcode=cum, np_=12, z=z, svz=svz)
+    for m in range(M):
+        want = gi.girf_draw(PAI[..., m], invA[..., m], sqrtPHI[..., m], SV0[:, m], Xj[:, m], z[..., m],
+                            svz[..., m], 0.11, cum, 12, bh=bh, actual=~yields, yields=yields, elb=0.25)
+        for sc in range(3):
+            err = np.max(np.abs(got[:, :, sc, m] - want[sc]) / np.maximum(np.abs(want[sc]), 1.0))
+            assert err < 1e-12, (m, sc, err)
