@@ -403,6 +403,7 @@ struct ccmm_chains {
     if (bh) {
       require(cf.Ns >= 1 && cf.Ns <= kElbNsMax, "Ns must be in [1, 4]");
       require(cf.elbTmax >= 0 && cf.elbTmax <= cf.T, "elbTmax must be in [0, T]");
+      require(cf.elbTmax < 65536, "elbTmax must be < 65536");  // k_elb_gibbs month list
       require(cf.elb_gibbsburn >= 0, "elb_gibbsburn must be >= 0");
       require(2 * cf.p * cf.Ns <= kElbColMax, "2 p Ns must be <= 128");
       require(cf.p >= 1, "p must be >= 1");
@@ -1290,7 +1291,8 @@ struct ccmm_chains {
       }
     });
     if (ps) run_ps(ra, e, kept);
-    const size_t lds_gibbs = (size_t)2 * e.elbTmax * Ns * sizeof(double);  // S | uniforms
+    const size_t lds_gibbs =  // S | uniforms | month list
+        (size_t)2 * e.elbTmax * Ns * sizeof(double) + (size_t)e.elbTmax * sizeof(int);
     launch(KID_ELBGIBBS, [&] {
       switch (Ns) {
 #define CASE_NS(NS)                                                                            \

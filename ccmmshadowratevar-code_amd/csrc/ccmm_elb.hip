@@ -477,8 +477,12 @@ __device__ __forceinline__ double elb_trunc_normal(double mu, double sig, double
 
 // ---------------------------------------------------------------- Gibbs passes (per chain)
 // One wave per chain.  Each lane owns neighbour columns lane and lane + 64 of every
-// month's record and prefetches the next month's while the current one is drawn;
-// the draws themselves run redundantly on all lanes (uniform control flow).
+// month's record; the draws themselves run redundantly on all lanes (uniform control
+// flow).  The serial month-to-month path touches only registers and LDS: the censored
+// month list and its per-series censoring mask sit in LDS (Tm), and the next month's
+// record is prefetched from global memory into the other half of a register ping-pong
+// pair while the current month is drawn, so no global-load round trip (and no vmcnt(0)
+// wait on the prefetch) lands between two months.
 template <int NS>
 __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState cs, RngArgs ra) {
   extern __shared__ double sm[];
@@ -492,13 +496,20 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
   const Rng rng = ra.make(c);
   const int ncol = 2 * p * NS;
   const int head = elb_cond_head(NS);
-  double* Sl = sm;           // T x NS (t-major)
-  double* Ul = sm + T * NS;  // this pass's uniforms, T x NS (t-major)
+  double* Sl = sm;                      // T x NS (t-major)
+  double* Ul = sm + T * NS;             // this pass's uniforms, T x NS (t-major)
+  int* Tm = (int*)(sm + 2 * T * NS);    // censored months: t | (censored-series mask << 16)
   double* Sc = e.Scur + (size_t)c * e.elbTmax * NS;
   const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * NS;
   const int* cl = e.cens + (size_t)s * e.elbTmax;
   const double* recs = e.cond + (size_t)c * e.elbTmax * e.condStride;
   for (int q = lane; q < T * NS; q += 64) Sl[q] = Sc[q];
+  for (int q = lane; q < nc; q += 64) {
+    const int t = cl[q];
+    int m = 0;
+    for (int a = 0; a < NS; ++a) m |= sN[t * NS + a] ? (1 << a) : 0;
+    Tm[q] = t | (m << 16);
+  }
   __syncthreads();
   // column geometry of this lane
   const int c0 = lane, c1 = lane + 64;
@@ -506,22 +517,25 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
   const int kk0 = c0 / NS, sp0 = c0 % NS, kk1 = c1 / NS, sp1 = c1 % NS;
   const int off0 = (kk0 < p) ? -(kk0 + 1) : (kk0 - p + 1);
   const int off1 = (kk1 < p) ? -(kk1 + 1) : (kk1 - p + 1);
-  auto load_rec = [&](int ci, double* hd, double* g0, double* g1) {
+  constexpr int kHd = NS + NS * (NS - 1) + NS;
+  struct Rec {
+    double hd[kHd], g0[NS], g1[NS];
+  };
+  // branch-free loads (clamped column, zeroed by select) so that the compiler's wait
+  // counting sees the prefetch as straight-line code and waits only for the older month
+  const int c0l = h0 ? c0 : 0, c1l = h1 ? c1 : 0;
+  auto load_rec = [&](int ci, Rec& r_) {
     const double* r = recs + (size_t)ci * e.condStride;
-    for (int q = 0; q < elb_cond_head(NS) - NS * NS; ++q) hd[q] = r[q];
+    for (int q = 0; q < kHd; ++q) r_.hd[q] = r[q];
     for (int a = 0; a < NS; ++a) {
-      g0[a] = h0 ? r[head + c0 * NS + a] : 0.0;
-      g1[a] = h1 ? r[head + c1 * NS + a] : 0.0;
+      r_.g0[a] = r[head + c0l * NS + a];
+      r_.g1[a] = r[head + c1l * NS + a];
     }
   };
-  constexpr int kHd = NS + NS * (NS - 1) + NS;
-  double hd[kHd], g0[NS], g1[NS];
-  double hdn[kHd], g0n[NS], g1n[NS];
-  load_rec(0, hd, g0, g1);
-  for (int n = 0; n < e.passes; ++n) {
-    // the pass's uniforms rand(Ns, elbT) (gibbsdrawShadowrates.m:173, page n) are data
-    // independent: all lanes draw them up front (Philox pairs in parallel, or the CRN
-    // page), so no generator sits on the serial month-to-month path below
+  // the pass's uniforms rand(Ns, elbT) (gibbsdrawShadowrates.m:173, page n) are data
+  // independent: all lanes draw them up front (Philox pairs in parallel, or the CRN
+  // page), so no generator sits on the serial month-to-month path
+  auto uniforms = [&](int n) {
     if (rng.crn) {
       for (int q = lane; q < T * NS; q += 64) Ul[q] = rng.uniform(CCMM_RNG_ELB, (uint32_t)(q + T * NS * n));
     } else {
@@ -536,46 +550,54 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
       }
     }
     __syncthreads();
-    for (int ci = 0; ci < nc; ++ci) {
-      const int t = cl[ci];
-      // prefetch next month's record (wraps to month 0 of the next pass)
-      const int cn = (ci + 1 < nc) ? ci + 1 : 0;
-      load_rec(cn, hdn, g0n, g1n);
-      double u[NS];
-      for (int a = 0; a < NS; ++a) u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
-      // Spost = a_t + Σ G S(neighbours)
-      const int tn0 = t + off0, tn1 = t + off1;
-      const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
-      const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
-      double sp[NS];
-      for (int a = 0; a < NS; ++a) sp[a] = fma(g0[a], v0, g1[a] * v1);
-      for (int a = 0; a < NS; ++a) sp[a] = hd[a] + wave_sum_dpp(sp[a]);
-      // conditional draws in index order (gibbsdrawShadowrates.m:206-218)
-      const double* beta = hd + NS;
-      const double* so = beta + NS * (NS - 1);
-      double cur[NS];
-      for (int a = 0; a < NS; ++a) cur[a] = Sl[t * NS + a];
-      for (int a = 0; a < NS; ++a) {
-        if (!sN[t * NS + a]) continue;
-        double mu = sp[a];
-        int y = 0;
-        for (int b = 0; b < NS; ++b) {
-          if (b == a) continue;
-          mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
-          ++y;
-        }
-        uint8_t fl;
-        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a], fl);
-        if (e.flags && lane == 0)  // drawTruncNormal.m branch taken (oracle.draw_trunc_normal flags)
-          e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
+  };
+  // month g of the flattened (pass, month) sequence: draw from rc, prefetch month g + 1
+  // into rn; tm = Tm entry of month g, returns month g + 1's
+  const int G = e.passes * nc;
+  auto month = [&](int g, int tm, const Rec& rc, Rec& rn) -> int {
+    const int n = g / nc, ci = g - n * nc;
+    if (ci == 0) uniforms(n);
+    const int cn = (ci + 1 < nc) ? ci + 1 : 0;  // wraps to month 0 of the next pass
+    load_rec(cn, rn);  // past the last month: a harmless reload of month 0
+    const int tmn = Tm[cn];
+    const int t = tm & 0xffff, msk = tm >> 16;
+    double u[NS];
+    for (int a = 0; a < NS; ++a) u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
+    // Spost = a_t + Σ G S(neighbours)
+    const int tn0 = t + off0, tn1 = t + off1;
+    const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
+    const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
+    double sp[NS];
+    for (int a = 0; a < NS; ++a) sp[a] = fma(h0 ? rc.g0[a] : 0.0, v0, (h1 ? rc.g1[a] : 0.0) * v1);
+    for (int a = 0; a < NS; ++a) sp[a] = rc.hd[a] + wave_sum_dpp(sp[a]);
+    // conditional draws in index order (gibbsdrawShadowrates.m:206-218)
+    const double* beta = rc.hd + NS;
+    const double* so = beta + NS * (NS - 1);
+    double cur[NS];
+    for (int a = 0; a < NS; ++a) cur[a] = Sl[t * NS + a];
+    for (int a = 0; a < NS; ++a) {
+      if (!((msk >> a) & 1)) continue;
+      double mu = sp[a];
+      int y = 0;
+      for (int b = 0; b < NS; ++b) {
+        if (b == a) continue;
+        mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
+        ++y;
       }
-      for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
-      for (int q = 0; q < kHd; ++q) hd[q] = hdn[q];
-      for (int a = 0; a < NS; ++a) {
-        g0[a] = g0n[a];
-        g1[a] = g1n[a];
-      }
+      uint8_t fl;
+      cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a], fl);
+      if (e.flags && lane == 0)  // drawTruncNormal.m branch taken (oracle.draw_trunc_normal flags)
+        e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
     }
+    for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
+    return tmn;
+  };
+  Rec ra_, rb_;
+  load_rec(0, ra_);
+  int tm = Tm[0];
+  for (int g = 0; g < G; g += 2) {
+    tm = month(g, tm, ra_, rb_);
+    if (g + 1 < G) tm = month(g + 1, tm, rb_, ra_);
   }
   __syncthreads();
   for (int q = lane; q < T * NS; q += 64) Sc[q] = Sl[q];
