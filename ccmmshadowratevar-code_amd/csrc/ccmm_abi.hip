@@ -1020,9 +1020,22 @@ struct ccmm_chains {
     const size_t lds_g = gl_lds_bytes(lagNT, drows, ldd, d.TP);
     const size_t lds_s = sl_lds_bytes(lagNT, drows, ldd, d.TP, d.N);
     const int nmax = d.N <= 8 ? 8 : (d.N <= 20 ? 20 : 32);
+    std::unique_lock<std::mutex> lk;
+    PhaseLock* L = nullptr;
+    if (mfma_lock > 0) {  // same phase lock as run_cta_big
+      L = &phase_lock(ctx->device, mfma_lock);
+      lk = std::unique_lock<std::mutex>(L->m);
+      if (L->last) HIPCHECK(hipStreamWaitEvent(ctx->stream, L->last, 0));
+      if (!mfma_ev) HIPCHECK(hipEventCreateWithFlags(&mfma_ev, hipEventDisableTiming));
+    }
     launch(KID_GRAMLAG, [&] {
       HIPCHECK(lag_launch_gram(lagNT, ctx->stream, lds_g, d, Tslot.p, ls, cs, iVdiag.p));
     });
+    if (L) {
+      HIPCHECK(hipEventRecord(mfma_ev, ctx->stream));
+      L->last = mfma_ev;
+      lk.unlock();
+    }
     launch(KID_SOLVELAG, [&] {
       HIPCHECK(lag_launch_solve(lagNT, nmax, ctx->stream, lds_s, d, Tslot.p, iVb.p, xsel(), ls, cs, ra));
     });

@@ -139,13 +139,26 @@ __device__ __forceinline__ void gl_syrk(const GlArgs& g, dbl4 (&acc)[gl_tpw(NT)]
   bs1 = 0.0;
   csum = 0.0;
   const int nks = (g.mode & 1) ? 0 : (g.T + 3) >> 2;
-  for (int ks = 0; ks < nks; ++ks) {
+  // software pipeline over k-steps: step ks scales its raw D values into the MFMA operands,
+  // then issues the LDS loads of step ks + 1 into the freed registers before its 15 MFMAs,
+  // so those loads complete under ~15 x 64 MFMA cycles instead of stalling the next step
+  // (scheduling barriers keep LLVM from sinking them next to their use)
+  double raw[NT], sw = 0.0;
+  auto load = [&](int ks) {
     const int t = 4 * ks + lq;
-    const double sw = g.swl[t];
+    sw = g.swl[t];
     const double* row = g.Dl + t * g.ldd;
+#pragma unroll
+    for (int b = 0; b < NT; ++b) raw[b] = row[off[b]];
+  };
+  if (nks > 0) load(0);
+  for (int ks = 0; ks < nks; ++ks) {
     double frag[NT];
 #pragma unroll
-    for (int b = 0; b < NT; ++b) frag[b] = row[off[b]] * sw;
+    for (int b = 0; b < NT; ++b) frag[b] = raw[b] * sw;
+    const double swc = sw;
+    load(ks + 1 < nks ? ks + 1 : ks);  // past the end: a harmless reload
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {
       if (W + kGlWaves * k < NTILE) {
@@ -155,9 +168,10 @@ __device__ __forceinline__ void gl_syrk(const GlArgs& g, dbl4 (&acc)[gl_tpw(NT)]
       }
     }
     // intercept row b = X~' w: wave W accumulates lag tiles W and W + 8
-    if (W < NT) bs0 = fma(frag[W < NT ? W : 0], sw, bs0);
-    if (W + kGlWaves < NT) bs1 = fma(frag[W + kGlWaves < NT ? W + kGlWaves : 0], sw, bs1);
-    csum = fma(sw, sw, csum);
+    if (W < NT) bs0 = fma(frag[W < NT ? W : 0], swc, bs0);
+    if (W + kGlWaves < NT) bs1 = fma(frag[W + kGlWaves < NT ? W + kGlWaves : 0], swc, bs1);
+    csum = fma(swc, swc, csum);
+    __builtin_amdgcn_sched_barrier(0);
   }
   bs0 += __shfl_xor(bs0, 16);
   bs0 += __shfl_xor(bs0, 32);
