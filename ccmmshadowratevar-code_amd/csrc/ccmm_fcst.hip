@@ -336,15 +336,16 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
     int head = 0;
     __syncthreads();
     for (int hh = 0; hh < H; ++hh) {
-      // SV path (mcmcVAR.m:302-312) and structural shock w = sv .* z
+      // SV path (mcmcVAR.m:302-312) and structural shock w = sv .* z.  Lane j draws the
+      // SV normal j of this horizon once (into dev, free until the scores), then every
+      // lane forms its row of sqrtPHI * z in the same j order as before
+      const int col = hh + job * H;
+      if (active && !mean_path && lane < N)
+        dev[lane] = svz ? svz[(size_t)col * N + lane] : rng.normal(CCMM_RNG_FCST, (uint32_t)(col * N + lane));
+      __builtin_amdgcn_wave_barrier();
       if (active && !mean_path && lane < N) {
         double shock = 0.0;
-        const int col = hh + job * H;
-        for (int j = 0; j < N; ++j) {
-          const double zz = svz ? svz[(size_t)col * N + j]
-                                : rng.normal(CCMM_RNG_FCST, (uint32_t)(col * N + j));
-          shock += sqrtPHI[lane + j * N] * zz;
-        }
+        for (int j = 0; j < N; ++j) shock += sqrtPHI[lane + j * N] * dev[j];
         logsv += shock;
         const double sv = exp(logsv * 0.5);
         const size_t zi = ((size_t)job * H + hh) * N + lane;
