@@ -280,9 +280,11 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   const int N = a.N, K = a.K, p = a.p, H = a.H, Nd = a.Nd;
   const int nw = blockDim.x >> 6;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // LDS: PAI K x N | per wave: ring_l[p*N] ring_c[p*N] w[N] sv[N] mu[N] dev[N] order[N] M[32*32]
+  // LDS: PAI K x N | per wave: ring_l[p*N] ring_c[p*N] w[N] sv[N] mu[N] dev[N] order[N]
+  // sel[N] + cens[N] M[32*32] (the score index lists live in LDS: as private arrays their
+  // data-dependent indexing put them in scratch memory on the serial score path)
   double* sPAI = sm;
-  const int per_wave = 2 * p * N + 5 * N + kFcstMaxN * kFcstMaxN;
+  const int per_wave = 2 * p * N + 6 * N + kFcstMaxN * kFcstMaxN;
   double* base = sm + (size_t)K * N + (size_t)wave * per_wave;
   double* ringl = base;
   double* ringc = ringl + p * N;
@@ -291,7 +293,9 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   double* mu = sv1 + N;
   double* dev = mu + N;
   int* order = (int*)(dev + N);
-  double* M = dev + 2 * N;
+  int* sel = (int*)(dev + 2 * N);              // N ints
+  uint8_t* cens = (uint8_t*)(sel + N);         // N bytes (same N-double slot)
+  double* M = dev + 3 * N;
 
   const int sl = a.slot ? a.slot[c] : 0;
   const double* PAIc = a.PAI + (size_t)c * a.ldPAI * N;
@@ -423,11 +427,9 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         }
         sc[0] = score_gauss(M, N, dev, ld);
       }
-      uint8_t cens[kFcstMaxN];
       // (2) censored full vector (ndxYIELDS censorable); the block-hybrid fcstLogscoreDraws
       if (natelb > 0) {
         for (int i = 0; i < N; ++i) { order[i] = i; cens[i] = a.ndxYields[i]; }
-        int sel[kFcstMaxN];
         for (int i = 0; i < N; ++i) sel[i] = i;
         sc[1] = score_censored(invA, sv1, mu, y, sel, cens, N, N, a.elb, M, dev, order, a.gl,
                                &unsupported, lane);
@@ -436,7 +438,6 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
       }
       // (3) macro block
       {
-        int sel[kFcstMaxN];
         int q = 0;
         for (int i = 0; i < N; ++i) if (!a.ndxYields[i]) sel[q++] = i;
         if (gram_rows_chol(invA, sv1, sel, nx, N, M)) {
@@ -448,7 +449,6 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
       }
       // (4) yields block: every yield censorable
       {
-        int sel[kFcstMaxN];
         int q = 0;
         for (int i = 0; i < N; ++i) if (a.ndxYields[i]) { sel[q] = i; cens[q] = 1; ++q; }
         if (natelb > 0) {
@@ -528,7 +528,7 @@ __global__ void k_fcst_accum(int N, int H, int Nd, int cap, int m, const double*
 }
 
 inline size_t fcst_lds_bytes(int N, int p, int K, int nw) {
-  const size_t per_wave = 2 * (size_t)p * N + 5 * (size_t)N + kFcstMaxN * kFcstMaxN;
+  const size_t per_wave = 2 * (size_t)p * N + 6 * (size_t)N + kFcstMaxN * kFcstMaxN;
   return ((size_t)K * N + (size_t)nw * per_wave) * sizeof(double);
 }
 
