@@ -283,15 +283,18 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   // LDS: PAI K x N | per wave: ring_l[p*N] ring_c[p*N] w[N] sv[N] mu[N] dev[N] order[N]
   // sel[N] + cens[N] M[32*32] (the score index lists live in LDS: as private arrays their
   // data-dependent indexing put them in scratch memory on the serial score path)
+  // (after PAI: muY[N] and the yield flags, shared by all waves of the chain)
   double* sPAI = sm;
+  double* smu = sm + (size_t)K * N;
+  int* syl = (int*)(smu + N);
   const int per_wave = 2 * p * N + 6 * N + kFcstMaxN * kFcstMaxN;
-  double* base = sm + (size_t)K * N + (size_t)wave * per_wave;
+  double* base = sm + (size_t)K * N + 2 * N + (size_t)wave * per_wave;
   double* ringl = base;
   double* ringc = ringl + p * N;
   double* w = ringc + p * N;
   double* sv1 = w + N;
-  double* mu = sv1 + N;
-  double* dev = mu + N;
+  const double* mu = smu;  // muY: one per chain (the per-wave slot sv1 + N is unused)
+  double* dev = sv1 + 2 * N;
   int* order = (int*)(dev + N);
   int* sel = (int*)(dev + 2 * N);              // N ints
   uint8_t* cens = (uint8_t*)(sel + N);         // N bytes (same N-double slot)
@@ -319,6 +322,21 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   rng.chain = a.ids ? a.ids[c] : (uint32_t)c;
   rng.sweep = a.sweep;
   const int nsv = N * H * Nd;
+  if (threadIdx.x < N) syl[threadIdx.x] = a.ndxYields[threadIdx.x];
+  __syncthreads();
+  // muY = fcstA(ndxfcstY, :) * Xjumpoff (mcmcVAR.m:326-328; block hybrid :577-580: the
+  // actual-rate equations read the yields' actual-rate lags), the same for every draw of
+  // the chain: lane i of wave 0 once, instead of every wave serially per draw
+  if (threadIdx.x < N) {
+    const int i = threadIdx.x;
+    const bool act = a.bh && a.actual[i];
+    double s = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const double xv = (act && k > 0 && syl[(k - 1) % N]) ? Xj[K + k - 1] : Xj[k];
+      s += sPAI[(size_t)i * K + k] * xv;
+    }
+    smu[i] = s;
+  }
   __syncthreads();
 
   const int njobs = a.bh ? Nd : Nd + 1;  // job Nd = zero-shock mean path (linear model)
@@ -399,17 +417,6 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
     // of the wave runs the same scalar algebra (uniform control flow, identical LDS
     // writes); the trivariate mvncdf quadrature spreads its nodes over the lanes
     if (active && !mean_path) {
-      for (int i = 0; i < N; ++i) {
-        // muY = fcstA(ndxfcstY, :) * Xjumpoff
-        const bool act = a.bh && a.actual[i];
-        double s = 0.0;
-        for (int k = 0; k < K; ++k) {
-          double xv = Xj[k];
-          if (act && k > 0 && a.ndxYields[(k - 1) % N]) xv = Xj[K + k - 1];
-          s += sPAI[(size_t)i * K + k] * xv;
-        }
-        mu[i] = s;
-      }
       int nx = 0, ni = 0, natelb = 0;
       for (int i = 0; i < N; ++i) {
         if (a.ndxYields[i]) { ++ni; natelb += (y[i] <= a.elb); } else ++nx;
@@ -529,7 +536,7 @@ __global__ void k_fcst_accum(int N, int H, int Nd, int cap, int m, const double*
 
 inline size_t fcst_lds_bytes(int N, int p, int K, int nw) {
   const size_t per_wave = 2 * (size_t)p * N + 6 * (size_t)N + kFcstMaxN * kFcstMaxN;
-  return ((size_t)K * N + (size_t)nw * per_wave) * sizeof(double);
+  return ((size_t)K * N + 2 * (size_t)N + (size_t)nw * per_wave) * sizeof(double);
 }
 
 }  // namespace ccmm
