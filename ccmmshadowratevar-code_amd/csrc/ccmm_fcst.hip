@@ -18,6 +18,11 @@ namespace ccmm {
 constexpr int kFcstMaxN = 32;
 constexpr int kFcstMaxWaves = 8;
 
+// LDS shared by the waves of a chain (doubles): PAI | muY | yield flags | invA | yrealized
+__host__ __device__ inline size_t fcst_shared_doubles(int N, int K) {
+  return (size_t)K * N + 3 * (size_t)N + (size_t)N * N;
+}
+
 struct GLNodes {  // Gauss-Legendre half rules (negative nodes) for n = 6, 12, 20 (Genz BVN)
   double x[3][10];
   double w[3][10];
@@ -285,10 +290,13 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   // data-dependent indexing put them in scratch memory on the serial score path)
   // (after PAI: muY[N] and the yield flags, shared by all waves of the chain)
   double* sPAI = sm;
+  // invA and yrealized staged too: the score algebra walks them in serial loops
   double* smu = sm + (size_t)K * N;
   int* syl = (int*)(smu + N);
+  double* sinvA = smu + 2 * N;
+  double* sy = sinvA + N * N;
   const int per_wave = 2 * p * N + 6 * N + kFcstMaxN * kFcstMaxN;
-  double* base = sm + (size_t)K * N + 2 * N + (size_t)wave * per_wave;
+  double* base = sm + fcst_shared_doubles(N, K) + (size_t)wave * per_wave;
   double* ringl = base;
   double* ringc = ringl + p * N;
   double* w = ringc + p * N;
@@ -307,9 +315,13 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
     sPAI[e] = PAIc[(size_t)j * a.ldPAI + k];
   }
   const double* Xj = a.Xj + (size_t)c * a.ldXj;
-  const double* invA = a.invA + (size_t)c * N * N;
+  const double* invAg = a.invA + (size_t)c * N * N;
   const double* sqrtPHI = a.sqrtPHI + (size_t)c * N * N;
-  const double* y = a.yreal + (size_t)sl * a.ldY;
+  const double* yg = a.yreal + (size_t)sl * a.ldY;
+  for (int e = threadIdx.x; e < N * N; e += blockDim.x) sinvA[e] = invAg[e];
+  if (threadIdx.x < N) sy[threadIdx.x] = yg[threadIdx.x];
+  const double* invA = sinvA;
+  const double* y = sy;
   const int tsv = a.svT ? a.svT[sl] - 1 : 0;
   const double* svz = a.svz ? a.svz + (size_t)c * a.crnStride : nullptr;
   const double* zc = a.z ? a.z + (size_t)c * a.crnStride : nullptr;
@@ -536,7 +548,7 @@ __global__ void k_fcst_accum(int N, int H, int Nd, int cap, int m, const double*
 
 inline size_t fcst_lds_bytes(int N, int p, int K, int nw) {
   const size_t per_wave = 2 * (size_t)p * N + 6 * (size_t)N + kFcstMaxN * kFcstMaxN;
-  return ((size_t)K * N + 2 * (size_t)N + (size_t)nw * per_wave) * sizeof(double);
+  return (fcst_shared_doubles(N, K) + (size_t)nw * per_wave) * sizeof(double);
 }
 
 }  // namespace ccmm
