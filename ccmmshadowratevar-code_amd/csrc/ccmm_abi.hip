@@ -844,9 +844,18 @@ struct ccmm_chains {
 
   void run_resid() {
     ChainState cs = view();
+    const int nb = d.N <= 8 ? 8 : (d.N <= 20 ? 20 : 32);
+    const size_t lds = (size_t)d.K * nb * sizeof(double);
     launch(KID_RESID, [&] {
-      hipLaunchKernelGGL(k_resid, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0, ctx->stream, d,
-                         Tslot.p, xsel(), cs);
+      if (d.N <= 32 && lds <= 64 * 1024) {  // one pass per design slab (k_resid_multi)
+        const dim3 g((d.TP + 255) / 256, d.B);
+        if (nb == 8) hipLaunchKernelGGL(k_resid_multi<8>, g, dim3(256), lds, ctx->stream, d, Tslot.p, xsel(), cs);
+        else if (nb == 20) hipLaunchKernelGGL(k_resid_multi<20>, g, dim3(256), lds, ctx->stream, d, Tslot.p, xsel(), cs);
+        else hipLaunchKernelGGL(k_resid_multi<32>, g, dim3(256), lds, ctx->stream, d, Tslot.p, xsel(), cs);
+      } else {
+        hipLaunchKernelGGL(k_resid, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0, ctx->stream, d,
+                           Tslot.p, xsel(), cs);
+      }
     });
     resid_valid = true;
   }

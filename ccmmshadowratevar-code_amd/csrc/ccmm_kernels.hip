@@ -41,6 +41,57 @@ __global__ void k_resid(Dims d, const int* __restrict__ Tslot, XSel xs, ChainSta
   E[t] = Y[(size_t)j * d.TP + t] - acc;
 }
 
+// E = Y - X PAI for all N equations of chain c in one pass over each distinct design slab
+// (the block-hybrid and hybrid models give equations of one chain a shared shadow-rate or
+// actual-rate slab): thread per t, the chain's PAI masked to the slab's equations in LDS
+// (row a = NB coefficients, read as broadcasts), NB accumulators per thread.  k_resid reads
+// the KP x TP slab once per equation, N times the bytes.  Same fma order over a per
+// equation as k_resid (other slabs' equations add exact zeros), so E is bit-identical.
+template <int NB>
+__global__ __launch_bounds__(256) void k_resid_multi(Dims d, const int* __restrict__ Tslot, XSel xs,
+                                                     ChainState cs) {
+  extern __shared__ double spai[];  // K x NB
+  const int c = blockIdx.y;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int N = d.N, K = d.K;
+  const int T = Tslot[cs.slot[c]];
+  const int* idx = xs.idx + (size_t)c * N;
+  const double* pai = cs.PAI + (size_t)c * N * d.KP;
+  double acc[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) acc[j] = 0.0;
+  const unsigned full = (N >= 32) ? 0xffffffffu : ((1u << N) - 1u);
+  unsigned done = 0;
+  while (done != full) {
+    const int s = idx[__builtin_ctz(~done & full)];
+    unsigned m = 0;
+    for (int j = 0; j < N; ++j) m |= (idx[j] == s) ? (1u << j) : 0u;
+    __syncthreads();  // the previous slab's readers are done with spai
+    for (int q = threadIdx.x; q < K * NB; q += 256) {
+      const int a = q / NB, j = q - a * NB;
+      spai[q] = (j < N && ((m >> j) & 1u)) ? pai[(size_t)j * d.KP + a] : 0.0;
+    }
+    __syncthreads();
+    if (t < T) {
+      const double* X = xs.pool + (size_t)s * d.KP * d.TP + t;
+      for (int a = 0; a < K; ++a) {
+        const double x = X[(size_t)a * d.TP];
+        const double* row = spai + a * NB;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = fma(x, row[j], acc[j]);
+      }
+    }
+    done |= m;
+  }
+  if (t < d.TP) {
+    const double* Y = xs.ypool + (size_t)xs.yidx[c] * N * d.TP;
+    double* E = cs.E + (size_t)c * N * d.TP;
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      if (j < N) E[(size_t)j * d.TP + t] = (t < T) ? Y[(size_t)j * d.TP + t] - acc[j] : 0.0;
+  }
+}
+
 // ============================================================== CTA weights
 // w_t^(j) = sum_{i>=j} A(i,j)^2 / sqrtht(t,i)^2 : the diagonal of kron(A(j:N,j),X)./lambda's
 // Gram (CTA.m:66-73).  Padded rows get weight 0.
