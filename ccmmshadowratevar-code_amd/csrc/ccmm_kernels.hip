@@ -700,14 +700,32 @@ __global__ __launch_bounds__(256) void k_phi(Dims d, const int* __restrict__ Tsl
   for (int e = tid; e < N * N; e += blockDim.x) {
     const int r = e / N, col = e % N;
     if (col > r) continue;
-    double a = 0.0;
+    // four independent partial sums: the T-long dot products are serial fma chains on
+    // one thread each, so their latency, not the fma count, sets the kernel time
     const double* er = etaw + (size_t)r * lde;
     const double* ec = etaw + (size_t)col * lde;
-    for (int t = 0; t < T; ++t) a = fma(er[t], ec[t], a);
-    Lpost[r * NS + col] = sP[r + col * N] + a;
-    double b = 0.0;
-    for (int q = 0; q < TZ; ++q) b = fma(Z[r + (size_t)N * q], Z[col + (size_t)N * q], b);
-    Rz[r * NS + col] = b;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int t = 0;
+    for (; t + 3 < T; t += 4) {
+      a0 = fma(er[t], ec[t], a0);
+      a1 = fma(er[t + 1], ec[t + 1], a1);
+      a2 = fma(er[t + 2], ec[t + 2], a2);
+      a3 = fma(er[t + 3], ec[t + 3], a3);
+    }
+    for (; t < T; ++t) a0 = fma(er[t], ec[t], a0);
+    Lpost[r * NS + col] = sP[r + col * N] + ((a0 + a1) + (a2 + a3));
+    const double* zr = Z + r;
+    const double* zc = Z + col;
+    double b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
+    int q = 0;
+    for (; q + 3 < TZ; q += 4) {
+      b0 = fma(zr[(size_t)N * q], zc[(size_t)N * q], b0);
+      b1 = fma(zr[(size_t)N * (q + 1)], zc[(size_t)N * (q + 1)], b1);
+      b2 = fma(zr[(size_t)N * (q + 2)], zc[(size_t)N * (q + 2)], b2);
+      b3 = fma(zr[(size_t)N * (q + 3)], zc[(size_t)N * (q + 3)], b3);
+    }
+    for (; q < TZ; ++q) b0 = fma(zr[(size_t)N * q], zc[(size_t)N * q], b0);
+    Rz[r * NS + col] = (b0 + b1) + (b2 + b3);
   }
   __syncthreads();
   int bad = 0;
