@@ -176,38 +176,50 @@ __device__ double tvn_cdf(const double* x, const double* M, const GLNodes& gl, i
   return wave_sum(acc) * 0.39894228040143267794;
 }
 
-// in-place lower Cholesky of an n x n LDS matrix (ld = kFcstMaxN); false if not SPD
-__device__ bool chol_lds(double* M, int n) {
+// in-place lower Cholesky of an n x n LDS matrix (ld = kFcstMaxN); false if not SPD.
+// Called by all 64 lanes of a wave with identical arguments: lane r computes row j + 1 + r
+// of column j (n <= 32: one pass), every entry with the same operation order as the
+// serial column-by-column form, so the factor is bit-identical to it.
+__device__ bool chol_lds(double* M, int n, int lane) {
   for (int j = 0; j < n; ++j) {
     double s = M[j + j * kFcstMaxN];
     for (int k = 0; k < j; ++k) s -= M[j + k * kFcstMaxN] * M[j + k * kFcstMaxN];
     if (!(s > 0.0)) return false;
     const double dj = sqrt(s);
-    M[j + j * kFcstMaxN] = dj;
-    for (int i = j + 1; i < n; ++i) {
-      double v = M[i + j * kFcstMaxN];
+    const int i = j + 1 + lane;
+    double v = 0.0;
+    if (i < n) {
+      v = M[i + j * kFcstMaxN];
       for (int k = 0; k < j; ++k) v -= M[i + k * kFcstMaxN] * M[j + k * kFcstMaxN];
-      M[i + j * kFcstMaxN] = v / dj;
+      v = v / dj;
     }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) M[j + j * kFcstMaxN] = dj;
+    if (i < n) M[i + j * kFcstMaxN] = v;
+    __builtin_amdgcn_wave_barrier();
   }
   return true;
 }
 
 // Omega = S(rows) S(rows)' for the index list rows[0..n) of S = invA diag(sv) (lower
 // triangular): M = chol(Omega, 'lower') (the chol(sqrtOmega(ndx,:)*sqrtOmega(ndx,:)')
-// of mcmcVAR.m:342,347 and logscoreGaussianCensored.m:54-56)
+// of mcmcVAR.m:342,347 and logscoreGaussianCensored.m:54-56).  Lanes split the Gram
+// entries (same k order per entry as the serial loop).
 __device__ bool gram_rows_chol(const double* invA, const double* sv, const int* rows, int n,
-                               int N, double* M) {
-  for (int a = 0; a < n; ++a)
-    for (int b = 0; b <= a; ++b) {
-      const int ra = rows[a], rb = rows[b];
-      const int kmax = ra < rb ? ra : rb;
-      double s = 0.0;
-      for (int k = 0; k <= kmax; ++k) s += invA[ra + k * N] * invA[rb + k * N] * sv[k] * sv[k];
-      M[a + b * kFcstMaxN] = s;
-      M[b + a * kFcstMaxN] = s;
-    }
-  return chol_lds(M, n);
+                               int N, double* M, int lane) {
+  __builtin_amdgcn_wave_barrier();
+  for (int e = lane; e < n * n; e += 64) {
+    const int a = e / n, b = e - a * n;
+    if (b > a) continue;
+    const int ra = rows[a], rb = rows[b];
+    const int kmax = ra < rb ? ra : rb;
+    double s = 0.0;
+    for (int k = 0; k <= kmax; ++k) s += invA[ra + k * N] * invA[rb + k * N] * sv[k] * sv[k];
+    M[a + b * kFcstMaxN] = s;
+    M[b + a * kFcstMaxN] = s;
+  }
+  __builtin_amdgcn_wave_barrier();
+  return chol_lds(M, n, lane);
 }
 
 // logscoreGaussian.m:15-20 with lower-triangular L (ld kFcstMaxN), dev = y - mu (overwritten)
@@ -243,7 +255,7 @@ __device__ double score_censored(const double* invA, const double* sv, const dou
   for (int i = 0; i < n; ++i)
     if (cens[i] && y[sel[i]] <= elb) { order[noff + nat] = sel[i]; ++nat; }
   if (nat > 3) { *unsupported = true; return NAN; }
-  if (!gram_rows_chol(invA, sv, order, n, N, M)) return NAN;
+  if (!gram_rows_chol(invA, sv, order, n, N, M, lane)) return NAN;
   double llf1 = 0.0;
   double y21[3], yat[3];
   for (int a = 0; a < nat; ++a) { y21[a] = mu[order[noff + a]]; yat[a] = y[order[noff + a]]; }
@@ -459,7 +471,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
       {
         int q = 0;
         for (int i = 0; i < N; ++i) if (!a.ndxYields[i]) sel[q++] = i;
-        if (gram_rows_chol(invA, sv1, sel, nx, N, M)) {
+        if (gram_rows_chol(invA, sv1, sel, nx, N, M, lane)) {
           for (int i = 0; i < nx; ++i) dev[i] = y[sel[i]] - mu[sel[i]];
           sc[2] = score_gauss(M, nx, dev, logdet_chol(M, nx));
         } else {
@@ -473,7 +485,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         if (natelb > 0) {
           sc[3] = score_censored(invA, sv1, mu, y, sel, cens, ni, N, a.elb, M, dev, order, a.gl,
                                  &unsupported, lane);
-        } else if (gram_rows_chol(invA, sv1, sel, ni, N, M)) {
+        } else if (gram_rows_chol(invA, sv1, sel, ni, N, M, lane)) {
           for (int i = 0; i < ni; ++i) dev[i] = y[sel[i]] - mu[sel[i]];
           sc[3] = score_gauss(M, ni, dev, logdet_chol(M, ni));
         } else {
