@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--hy-chains", default="256,1024", help="chains per GPU of the hybrid lines")
     ap.add_argument("--oos-steps", type=int, default=3,
                     help="timed kept sweeps (with forecasts) of the OOS line (configs[3]); 0 = skip")
-    ap.add_argument("--oos-chains", default="1,8", help="chains per vintage of the OOS lines")
+    ap.add_argument("--oos-chains", default="1,8,32", help="chains per vintage of the OOS lines")
     ap.add_argument("--s120-steps", type=int, default=2,
                     help="timed sweeps of the S120 stress line (configs[4], N=120); 0 = skip")
     ap.add_argument("--s120-warmup", type=int, default=1)
@@ -77,9 +77,31 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` outside a torch.distributed launcher: start N rank processes
+    (one per GPU, torch.distributed.run, rendezvous on 127.0.0.1) as CHILDREN of this
+    process, which never touches the GPU, and exit with their status.  Rank 0 prints the
+    JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + sys.argv[1:]
+    _progress(f"launching {n} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        _progress(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; reporting the launched world")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -148,8 +170,8 @@ def main():
         elapsed = float(t.item())
     draws = ch.get_draws()
     assert np.all(np.isfinite(draws["PAI_all"])), "non-finite draws"
-    fc = bench_predictive(ctx, ch, m, d, B) if (rank == 0 and not args.no_fcst) else None
     ch.close()
+    fc = bench_predictive(pkg, ctx, d, B) if (rank == 0 and not args.no_fcst) else None
     # secondary lines (configs[2], configs[3]) run on every rank: own barrier/max-reduction
     bh = None
     _progress("secondary lines")
@@ -169,8 +191,8 @@ def main():
         girf = bench_girf(pkg, ctx, d, args.girf_draws, rank, barrier, dist)
     oos = None
     if args.oos_steps > 0:
-        oos = [bench_oos(pkg, ctx, d, int(c), args, rank, barrier, dist)
-               for c in args.oos_chains.split(",") if c.strip()]
+        oos = [bench_oos(pkg, ctx, d, int(c), args, rank, barrier, dist, floor=(i == 0))
+               for i, c in enumerate(x for x in args.oos_chains.split(",") if x.strip())]
 
     if rank != 0:
         if dist is not None:
@@ -272,56 +294,68 @@ def main():
         dist.destroy_process_group()
 
 
-def bench_predictive(ctx, ch, m, d, B, H=48, Nd=10, reps=3):
-    """Predictive density of one kept draw for every chain (mcmcVAR.m:298-381) through
-    the block-level C-ABI ccmm_fcst (host buffers in and out, so PCIe-inclusive; the
-    kernel time k_fcst is in the rocprofv3 stats).  Not part of a sweep."""
-    st = ch.get_state()
-    yields = np.zeros(m.N, bool)
-    yields[[i for i, c in enumerate(d["ncode"]) if c in
-            ("FEDFUNDS", "TB6MS", "GS1", "GS5", "GS10", "BAA")]] = True
-    y1 = m.data[-1]  # realized values: the jump-off month itself (synthetic stand-in)
-    Xj = np.repeat(m.Xjumpoff[:, None], B, axis=1)
-    args = (st["PAI"], st["invA"], st["h"][-1], st["sqrtPHI"], Xj, y1, yields, 0.25, H, Nd)
-    ctx.fcst(*args, seed=5, sweep=0)  # warm-up
-    t0 = time.perf_counter()
-    for r in range(reps):
-        out = ctx.fcst(*args, seed=5, sweep=r + 1)
-    ms = (time.perf_counter() - t0) * 1e3 / reps
-    assert np.all(np.isfinite(out[3][0]))
-    return {"workload": f"ccmm_fcst: {B} chains x {Nd} draws x {H} horizons, linear + censored "
-                        "paths, RB mean, 4 log scores", "ms_per_call": round(ms, 3),
-            "chain_draws_per_s": round(B / (ms * 1e-3), 1), "boundary": "host buffers (PCIe-inclusive)"}
-
-
-def bench_oos(pkg, ctx, d, C, args, rank, barrier, dist, H=48, Nd=10):
-    """BASELINE.json configs[3] (goVARshadowrateBlockHybrid quasi-real-time OOS): all 164
-    vintages (jump-offs after 2008-12: T = 587..750, elbT = 2..165) x C chains as ONE
-    device-resident chain set per GPU (vintages sharded over ranks longest-processing-time
-    first), ELB Gibbs (101 passes) every sweep.  Timed: kept sweeps, each storing the draw
-    and simulating the predictive density on the device (10 draws x 48 horizons per kept
-    draw and chain, mcmcVARshadowrateBlockHybrid.m:550-625) plus the one-step log scores;
-    then plain (burn-in) sweeps.  value = units x sweeps / time summed over ranks (fixed
-    total work: strong scaling).  The projected OOS wall time is 1000 burn-in + 1000 kept
-    sweeps per unit at these rates."""
-    _progress(f"bench_oos {locals().get('B', locals().get('C'))}")
+def bench_predictive(pkg, ctx, d, B, H=48, Nd=10, steps=5):
+    """Predictive density of every kept draw (mcmcVAR.m:298-381, logscoreGaussian.m,
+    logscoreGaussianCensored.m) on a real vintage: jump-off 2022-07 (thisT = Tdata - 1), so
+    yrealized(:,1) is the 2022-08 data row (goVARshadowrateBlockHybrid.m:267-283), B chains
+    of the linear model, Nd = 10 draws x 48 horizons per kept draw.  Device-resident: the
+    forecast block runs inside the chain set after each stored sweep (ccmm_chains_set_fcst);
+    the rate is B / (k_fcst launch time, HIP events on the set's stream).  The block-level
+    ccmm_fcst call (host buffers in and out) is timed beside it as the PCIe-inclusive rate.
+    Not part of a sweep."""
     import time as _t
+    _progress(f"bench_predictive {B}")
     p = 12
-    S = pkg.samplers
-    ndxS, ndxO, ndxY = pkg.model.setShadowYields(d["ncode"], 0.25)
     mpm = pkg.model.setMinnesotaMean(d["ncode"])
-    Tj = [int(t) for t in (np.flatnonzero(d["ydates"] > S.datenum(2008, 12, 1)) + 1)]
-    world = dist.get_world_size() if dist is not None else 1
-    N, K = d["data"].shape[1], d["data"].shape[1] * p + 1
-    e0 = pkg.model.elbT0_of(d["data"], ndxS, 0.25, p)
-    costs = [pkg.distributed.unit_cost(t - p, K, N, n_cens=max(0, t - (e0 + 1 + p) + 1)) for t in Tj]
-    mine = pkg.distributed.lpt_assign(costs, world)[rank]
-    units = S._bh_units(d["data"], d["ydates"], [Tj[v] for v in mine], p, 12, ndxS, ndxO, mpm,
-                        0.25, e0, True, H)
-    ids = np.array([v * C + c for v in mine for c in range(C)], dtype=np.uint32)
-    steps = args.oos_steps
+    thisT = len(d["ydates"]) - 1
+    m = pkg.model.build_var(thisT, p, 12, d["data"], d["ydates"], mpm, True)
+    ndxS, ndxO, ndxY = pkg.model.setShadowYields(d["ncode"], 0.25)
+    yields = np.zeros(m.N, bool)
+    yields[ndxY] = True
+    yreal = pkg.samplers.realized_values(d["data"], thisT, H, ndxS, 0.25)
+    ch = pkg.Chains(ctx, N=m.N, p=p, T=m.T, B=B, crn=False, store_capacity=steps + 2, seed=424242)
+    ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    ch.set_fcst(H, Nd, yields, keep_paths=False)
+    ch.set_fcst_slot(0, yreal[:, 0])
+    st = pkg.model.initial_state(m, B)
+    ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+    ch.sweep(3, store=False)
+    ch.sweep(1, store=True)
+    ch.get_fcst()
+    ch.profile(True)
+    ch.sweep(steps, store=True)
+    ctx.synchronize()
+    kt = ch.kernel_times()
+    fc = ch.get_fcst()
+    assert np.all(np.isfinite(fc["scores"][:, :, 0, :])), "non-finite log scores"
+    kms = kt["k_fcst"][0] / kt["k_fcst"][1]
+    # the block-level call on the last state (PCIe-inclusive)
+    stt = ch.get_state()
+    ch.close()
+    Xj = np.repeat(m.Xjumpoff[:, None], B, axis=1)
+    args = (stt["PAI"], stt["invA"], stt["h"][m.T - 1], stt["sqrtPHI"], Xj, yreal[:, 0], yields, 0.25, H, Nd)
+    ctx.fcst(*args, seed=5, sweep=0)
+    t0 = _t.perf_counter()
+    for r in range(3):
+        ctx.fcst(*args, seed=5, sweep=r + 1)
+    ms_host = (_t.perf_counter() - t0) * 1e3 / 3
+    return {"workload": f"predictive density: {B} chains (linear, jump-off 2022-07, realized 2022-08) x "
+                        f"{Nd} draws x {H} horizons per kept draw, linear + censored paths, RB mean, "
+                        "4 one-step log scores",
+            "value": round(B / (kms * 1e-3), 1), "unit": "chain-draws/s (device-resident, k_fcst)",
+            "k_fcst_ms": round(kms, 4), "launches": int(kt["k_fcst"][1]),
+            "ccmm_fcst_ms_per_call_pcie": round(ms_host, 3),
+            "ccmm_fcst_chain_draws_per_s_pcie": round(B / (ms_host * 1e-3), 1),
+            "mean_logscore": round(float(np.mean(fc["scores"][:, :, 0, :])), 4)}
+
+
+def _oos_timed(S, ctx, units, C, ids, steps, barrier, H, Nd, profile):
+    """Time one OOS chain set through the reference's three ELB phases: Gibbs burn-in
+    sweeps, PS burn-in sweeps, kept sweeps (PS + stored draw + predictive density).
+    Returns (seconds per phase for `steps` sweeps, kernel times, PS stats, status)."""
+    import time as _t
     ch, _, _ = S._bh_chain_set(ctx, units, C, seed=1012023, ids=ids, store_capacity=steps + 1,
-                                gibbsburn=100, ELBbound=0.25, ndxYIELDS=ndxY, fcstNhorizons=H, Nd=Nd)
+                                gibbsburn=100, ELBbound=0.25, ndxYIELDS=_OOS_NDXY[0], fcstNhorizons=H, Nd=Nd)
     # the reference's ELB schedule (mcmcVARshadowrateBlockHybrid.m:433-466): Gibbs for
     # m < MCMCburnin/2, then 1000 PS proposals with the Gibbs draw as fallback
     ch.set_elb_ps(1000, 2 + steps)
@@ -338,16 +372,57 @@ def bench_oos(pkg, ctx, d, C, args, rank, barrier, dist, H=48, Nd=10):
 
     el_gibbs = timed(False)                       # m = 2 .. steps + 1: Gibbs burn-in
     el_burn = timed(False)                        # PS burn-in
-    if not args.no_profile:
+    if profile:
         ch.profile(True)
     el_kept = timed(True)                         # PS + stored draw + predictive density
-    kt = ch.kernel_times() if not args.no_profile else {}
+    kt = ch.kernel_times() if profile else {}
     fc = ch.get_fcst()
     assert np.all(np.isfinite(fc["fYsum"])), "non-finite forecasts"
     ch.profile(False)
     ps = ch.get_ps()
     st = ch.get_status()
+    B = ch.B
     ch.close()
+    return (el_gibbs, el_burn, el_kept), kt, ps, st, B
+
+
+_OOS_NDXY = [None]
+
+
+def bench_oos(pkg, ctx, d, C, args, rank, barrier, dist, H=48, Nd=10, floor=False):
+    """BASELINE.json configs[3] (goVARshadowrateBlockHybrid quasi-real-time OOS): all 164
+    vintages (jump-offs after 2008-12: T = 587..750, elbT = 2..165) x C chains as ONE
+    device-resident chain set per GPU (vintages sharded over ranks longest-processing-time
+    first), ELB Gibbs (101 passes) every sweep.  Timed: kept sweeps, each storing the draw
+    and simulating the predictive density on the device (10 draws x 48 horizons per kept
+    draw and chain, mcmcVARshadowrateBlockHybrid.m:550-625) plus the one-step log scores;
+    then plain (burn-in) sweeps.  value = units x sweeps / time summed over ranks (fixed
+    total work: strong scaling).  The projected OOS wall time is 1000 burn-in + 1000 kept
+    sweeps per unit at these rates.
+
+    floor=True also times the longest vintage alone (1 chain, T = 750, elbT = 165): the
+    per-sweep latency no number of GPUs can go below, because one rank always holds that
+    unit.  The expected N-GPU wall time of the line is max(floor run, 1-GPU run / N)."""
+    _progress(f"bench_oos C={C}")
+    p = 12
+    S = pkg.samplers
+    ndxS, ndxO, ndxY = pkg.model.setShadowYields(d["ncode"], 0.25)
+    _OOS_NDXY[0] = ndxY
+    mpm = pkg.model.setMinnesotaMean(d["ncode"])
+    Tj = [int(t) for t in (np.flatnonzero(d["ydates"] > S.datenum(2008, 12, 1)) + 1)]
+    world = dist.get_world_size() if dist is not None else 1
+    N, K = d["data"].shape[1], d["data"].shape[1] * p + 1
+    e0 = pkg.model.elbT0_of(d["data"], ndxS, 0.25, p)
+    startELB = e0 + 1 + p
+    costs = [pkg.distributed.unit_cost(t - p, K, N, n_cens=pkg.distributed.censored_months(
+        d["data"], ndxS, 0.25, startELB, t)) for t in Tj]
+    mine = pkg.distributed.lpt_assign(costs, world)[rank]
+    units = S._bh_units(d["data"], d["ydates"], [Tj[v] for v in mine], p, 12, ndxS, ndxO, mpm,
+                        0.25, e0, True, H)
+    ids = np.array([v * C + c for v in mine for c in range(C)], dtype=np.uint32)
+    steps = args.oos_steps
+    (el_gibbs, el_burn, el_kept), kt, ps, st, B = _oos_timed(S, ctx, units, C, ids, steps, barrier, H, Nd,
+                                                              not args.no_profile)
     if dist is not None:
         import torch
         tt = torch.tensor([el_kept, el_burn, el_gibbs], dtype=torch.float64, device=f"cuda:{ctx.device}")
@@ -357,8 +432,9 @@ def bench_oos(pkg, ctx, d, C, args, rank, barrier, dist, H=48, Nd=10):
     kept = units_total * steps / el_kept
     burn = units_total * steps / el_burn
     gibbs = units_total * steps / el_gibbs
-    n_ps = 2 * steps * ch.B
+    n_ps = 2 * steps * B
     acc = int(ps["countAccept"].sum() + ps["countAcceptBurnin"].sum())
+    proj = 500 * units_total / gibbs + 500 * units_total / burn + 1000 * units_total / kept
     res = {"workload": f"configs[3]: goVARshadowrateBlockHybrid OOS, {len(Tj)} vintages x {C} "
                        f"chain(s) = {units_total} units (T = 587..750, elbT = 2..165), one "
                        f"device-resident chain set per GPU, vintages LPT-sharded over {world} "
@@ -371,9 +447,23 @@ def bench_oos(pkg, ctx, d, C, args, rank, barrier, dist, H=48, Nd=10):
            "ms_per_burnin_gibbs_step": round(1e3 * el_gibbs / steps, 3), "steps": steps,
            "ps_accept_rate": round(acc / max(n_ps, 1), 4),
            "forecast": f"{Nd} draws x {H} horizons per kept draw and chain + 4 one-step scores",
-           "projected_full_run_s": round(500 * units_total / gibbs + 500 * units_total / burn +
-                                         1000 * units_total / kept, 1),
+           "projected_full_run_s": round(proj, 1),
            "flagged_units": int(np.count_nonzero(st)), "scaling": "strong"}
+    if floor and rank == 0:
+        # the longest vintage alone: the per-rank latency floor of any sharding
+        last = len(Tj) - 1
+        u1 = S._bh_units(d["data"], d["ydates"], [Tj[last]], p, 12, ndxS, ndxO, mpm, 0.25, e0, True, H)
+        (fg, fb, fk), _, _, _, _ = _oos_timed(S, ctx, u1, 1, np.array([last * C], np.uint32), steps,
+                                              lambda: ctx.synchronize(), H, Nd, False)
+        floor_s = (500 * fg + 500 * fb + 1000 * fk) / steps
+        res["per_rank_floor"] = {
+            "unit": f"vintage thisT = {Tj[last]} (T = {Tj[last] - p}, elbT = {Tj[last] - p - e0}), 1 chain",
+            "ms_per_gibbs_step": round(1e3 * fg / steps, 3), "ms_per_ps_step": round(1e3 * fb / steps, 3),
+            "ms_per_kept_step": round(1e3 * fk / steps, 3), "full_run_s": round(floor_s, 1),
+            "expected_full_run_s": {str(n): round(max(floor_s, proj * world / n), 1) for n in (1, 2, 4, 8)},
+            "note": "expected N-GPU wall time = max(longest vintage alone, this line's 1-GPU time / N): "
+                    "LPT puts the longest vintage on some rank, whose sweep cannot run faster than "
+                    "that unit's own latency"}
     if kt:
         res["kernel_ms_per_sweep"] = {k: round(v[0] / v[1], 4) for k, v in kt.items() if v[1]}
     return res
@@ -740,8 +830,31 @@ def _cpu_line(kind, budget_s, workers, sample):
     value = sum(n / el for n, el in res)
     nsw = sum(n for n, _ in res)
     return {"value": round(value, 4), "unit": "sweeps/s", "cores": workers, "kind": "port",
+            "scope": f"per-GPU share of the host: {workers} of its cores",
+            "per_core": round(value / workers, 4),
             "sample": f"{nsw} sweeps: {workers} single-thread processes (parfor-style, one chain "
                       f"each) x ~{budget_s:.0f} s, {sample}"}
+
+
+def _physical_cores():
+    """Physical cores of the host (sockets x cores per socket from /proc/cpuinfo)."""
+    phys = set()
+    try:
+        cur = {}
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if ":" in line:
+                    k, v = (x.strip() for x in line.split(":", 1))
+                    cur[k] = v
+                elif cur:
+                    phys.add((cur.get("physical id"), cur.get("core id")))
+                    cur = {}
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        return None
+    phys.discard((None, None))
+    return len(phys) or None
 
 
 def cpu_baseline(budget_s, workers=0):
@@ -776,6 +889,17 @@ def cpu_baseline(budget_s, workers=0):
           f"logical CPUs visible"
     lin = _cpu_line("linear-kron", budget_s, workers,
                     "oracle/ccmm_oracle.py linear sweep as written (kron CTA, explicit inverse), " + env)
+    # all host cores: the box allots a GPU job 16 of its CPUs, so the
+    # whole-host line is the measured single-thread rate x the physical core count
+    # (parfor workers are independent single-thread chains; no shared state to contend on
+    # beyond memory bandwidth, which a 750 x 241 working set does not stress)
+    ncore = _physical_cores()
+    if ncore:
+        lin["all_host_cores"] = {
+            "value": round(lin["per_core"] * ncore, 3), "unit": "sweeps/s", "cores": ncore,
+            "kind": "port", "cpu": cpu, "blas": blas,
+            "method": f"projected: measured per-core rate of the {workers}-process line x {ncore} "
+                      "physical cores (one single-thread parfor worker per core)"}
     lin["lines"] = {
         "linear_syrk": _cpu_line("linear-syrk", budget_s, workers,
                                  "linear sweep, algorithmic CTA (weighted SYRK + Cholesky + "

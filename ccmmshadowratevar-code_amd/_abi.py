@@ -106,6 +106,7 @@ _SIGS = {
                             _dp, _dp, _dp, _dp, _u8p, C.c_double, _dp, _dp, C.c_uint64,
                             C.c_int, _dp, _dp, _dp, _dp, _ip]),
     "ccmm_selftest_mfma_f64": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
+    "ccmm_selftest_mfma_f64_acc": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp]),
 }
 
 _lib = None
@@ -361,6 +362,16 @@ class Context:
         D = np.zeros((16, 16), order="F")
         _check(self.lib.ccmm_selftest_mfma_f64(self.handle, _ptr(_f(A16x4)), _ptr(_f(B4x16)),
                                                _ptr(D)), "ccmm_selftest_mfma_f64")
+        return D
+
+    def selftest_mfma_f64_acc(self, A, B, Cacc):
+        """D = C + A B per probe: A 16 x 4 x P, B 4 x 16 x P, C 16 x 16 x P (one MFMA each)."""
+        A, B, Cacc = _f(A), _f(B), _f(Cacc)
+        P = A.shape[2]
+        assert A.shape == (16, 4, P) and B.shape == (4, 16, P) and Cacc.shape == (16, 16, P)
+        D = np.zeros((16, 16, P), order="F")
+        _check(self.lib.ccmm_selftest_mfma_f64_acc(self.handle, P, _ptr(A), _ptr(B), _ptr(Cacc), _ptr(D)),
+               "ccmm_selftest_mfma_f64_acc")
         return D
 
 

@@ -2872,4 +2872,25 @@ int ccmm_selftest_mfma_f64(ccmm_ctx* ctx, const double* A16x4, const double* B4x
   });
 }
 
+int ccmm_selftest_mfma_f64_acc(ccmm_ctx* ctx, int nprobe, const double* A16x4, const double* B4x16,
+                               const double* C16x16, double* D16x16) {
+  return guarded([&] {
+    require(ctx && A16x4 && B4x16 && C16x16 && D16x16 && nprobe > 0 && nprobe <= (1 << 20), "bad argument");
+    HIPCHECK(hipSetDevice(ctx->device));
+    DBuf<double> a, b, cc, dd;
+    a.alloc((size_t)64 * nprobe);
+    b.alloc((size_t)64 * nprobe);
+    cc.alloc((size_t)256 * nprobe);
+    dd.alloc((size_t)256 * nprobe);
+    HIPCHECK(hipMemcpy(a.p, A16x4, (size_t)64 * nprobe * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(b.p, B4x16, (size_t)64 * nprobe * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(cc.p, C16x16, (size_t)256 * nprobe * sizeof(double), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_mfma_selftest_acc, dim3(nprobe), dim3(64), 0, ctx->stream, a.p, b.p, cc.p, dd.p, nprobe);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    HIPCHECK(hipMemcpy(D16x16, dd.p, (size_t)256 * nprobe * sizeof(double), hipMemcpyDeviceToHost));
+    return 0;
+  });
+}
+
 }  // extern "C"

@@ -460,7 +460,7 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
 #pragma unroll 16
         for (int k = 0; k < 64; ++k) a4[k & 3] = fma(Ls[lane * kBSLd + k], yv[r0 + k], a4[k & 3]);
         const double yi = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         yv[r0 + lane] = yi;
       }
       __syncthreads();
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
       if (wave == 0) {
         const double ri = yv[r0 + lane] - part[lane];
         part[64 + lane] = ri;
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 16
         for (int k = 0; k < 64; ++k) a4[k & 3] = fma(Ls[k * kBSLd + lane], part[64 + k], a4[k & 3]);

@@ -193,10 +193,10 @@ __device__ bool chol_lds(double* M, int n, int lane) {
       for (int k = 0; k < j; ++k) v -= M[i + k * kFcstMaxN] * M[j + k * kFcstMaxN];
       v = v / dj;
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     if (lane == 0) M[j + j * kFcstMaxN] = dj;
     if (i < n) M[i + j * kFcstMaxN] = v;
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
   }
   return true;
 }
@@ -207,7 +207,7 @@ __device__ bool chol_lds(double* M, int n, int lane) {
 // entries (same k order per entry as the serial loop).
 __device__ bool gram_rows_chol(const double* invA, const double* sv, const int* rows, int n,
                                int N, double* M, int lane) {
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   for (int e = lane; e < n * n; e += 64) {
     const int a = e / n, b = e - a * n;
     if (b > a) continue;
@@ -218,7 +218,7 @@ __device__ bool gram_rows_chol(const double* invA, const double* sv, const int* 
     M[a + b * kFcstMaxN] = s;
     M[b + a * kFcstMaxN] = s;
   }
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   return chol_lds(M, n, lane);
 }
 
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
       const int col = hh + job * H;
       if (active && !mean_path && lane < N)
         dev[lane] = svz ? svz[(size_t)col * N + lane] : rng.normal(CCMM_RNG_FCST, (uint32_t)(col * N + lane));
-      __builtin_amdgcn_wave_barrier();
+      wave_lds_sync();
       if (active && !mean_path && lane < N) {
         double shock = 0.0;
         for (int j = 0; j < N; ++j) shock += sqrtPHI[lane + j * N] * dev[j];

@@ -149,6 +149,15 @@ struct RngArgs {
   }
 };
 
+// Hand-off of LDS data between the lanes of one wave: wavefront-scope release/acquire
+// fences around the wave barrier, so that the compiler may not move or forward the LDS
+// stores and loads across it (the barrier alone only orders instruction scheduling).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -854,4 +854,22 @@ __global__ void k_mfma_selftest(const double* A, const double* B, double* D) {
   for (int r = 0; r < 4; ++r) D[((l >> 4) + 4 * r) + 16 * (l & 15)] = acc[r];  // column-major 16x16
 }
 
+// D = C + A B with a caller-given accumulator: probes of the instruction's internal
+// association and rounding (tools/probe_mfma_order.py, tests/test_gpu_mfma_order.py)
+__global__ void k_mfma_selftest_acc(const double* A, const double* B, const double* C, double* D, int nprobe) {
+  const int l = threadIdx.x;
+  const size_t pr = blockIdx.x;
+  if ((int)pr >= nprobe) return;
+  A += pr * 64;
+  B += pr * 64;
+  C += pr * 256;
+  D += pr * 256;
+  dbl4 acc;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r] = C[((l >> 4) + 4 * r) + 16 * (l & 15)];
+  acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(l & 15) + 16 * (l >> 4)], B[(l >> 4) + 4 * (l & 15)], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) D[((l >> 4) + 4 * r) + 16 * (l & 15)] = acc[r];
+}
+
 }  // namespace ccmm

@@ -88,7 +88,7 @@ __device__ __forceinline__ int gl_factor_inv(const double* Dg, double* Ws, int l
 #pragma unroll
     for (int m = 0; m < 16; ++m) Ws[lane * kGlLd + m] = (m < lane) ? row[m] : ((m == lane) ? rdiag : 0.0);
   }
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   // lane c < 16: column c of L^-1,  x_i = (delta_ic - sum_{m<i} L_im x_m) / L_ii
   const int c = lane;
   double x[16];
@@ -106,12 +106,12 @@ __device__ __forceinline__ int gl_factor_inv(const double* Dg, double* Ws, int l
     }
     x[i] = (i >= c) ? (s0 + s1) * Ws[ro + i] : 0.0;
   }
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   if (lane < 16) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) Ws[i * kGlLd + c] = x[i];
   }
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   return bad;
 }
 
@@ -258,7 +258,7 @@ __device__ __forceinline__ int gram_lag_factor(const GlArgs& g, double* sm, int 
         own = true;
       }
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     if (own && !(g.mode & 256)) bad |= gl_factor_inv(Ws, LinvB, lane);
   }
   for (int p = 0; p < (do_chol ? NT : 0); ++p) {
@@ -303,7 +303,7 @@ __device__ __forceinline__ int gram_lag_factor(const GlArgs& g, double* sm, int 
           own = true;
         }
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_lds_sync();
       if (own && !(g.mode & 256)) bad |= gl_factor_inv(Ws, LinvB, lane);
 #pragma unroll
       for (int k = 0; k < TPW; ++k) {

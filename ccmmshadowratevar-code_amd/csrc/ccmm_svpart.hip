@@ -62,7 +62,7 @@ __device__ __forceinline__ double sv_rsqrt(double d) {
 // LDS hand-off between the lanes of one wave: its LDS operations complete in order,
 // so only the compiler has to be kept from moving accesses across this point
 __device__ __forceinline__ void sv_wave_sync() {
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   asm volatile("" ::: "memory");
 }
 

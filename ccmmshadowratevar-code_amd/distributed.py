@@ -48,6 +48,19 @@ def unit_cost(T, K, N, n_cens=0, Nstate=None, Ny=None, passes=101):
     return float(f)
 
 
+def censored_months(data, ndxS, elb, startELB, thisT):
+    """Censored months of one vintage: rows startELB..thisT (1-based, the vintage's ELB
+    window, goVARshadowrateBlockHybrid.m:131-134) in which some shadow-rate series sits at
+    or below the ELB (mcmcVARshadowrateBlockHybrid.m:163-171).  The ELB Gibbs passes cost
+    one conditional draw per censored cell, so this (not the window length) drives the
+    vintage's ELB cost; after the 2015 lift-off the window grows while it does not."""
+    d = np.asarray(data, float)[:, np.asarray(ndxS, int)]
+    lo, hi = max(int(startELB) - 1, 0), int(thisT)
+    if hi <= lo:
+        return 0
+    return int(np.count_nonzero(np.any(d[lo:hi] <= elb, axis=1)))
+
+
 def lpt_assign(costs, world_size):
     """Longest-processing-time-first assignment of units to ranks.
     Returns a list (per rank) of unit indices, each sorted ascending."""

@@ -661,7 +661,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
     size = dist.get_world_size() if dist is not None else 1
     device = _rank_device(dist, device)
     K = N * p + 1
-    costs = [dm.unit_cost(t - p, K, N, n_cens=max(0, t - startELB + 1)) * C for t in Tjumpoffs]
+    costs = [dm.unit_cost(t - p, K, N, n_cens=dm.censored_months(data0, ndxSHADOWRATE, ELBbound, startELB, t)) * C
+             for t in Tjumpoffs]
     assignment = dm.lpt_assign(costs, size)
     mine = assignment[rank]
     t0 = time.perf_counter()

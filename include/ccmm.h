@@ -396,6 +396,11 @@ int ccmm_fcst(ccmm_ctx* ctx, int B, int N, int p, int H, int Nd, const double* P
 /* D16x16 = A16x4 * B4x16 computed by one v_mfma_f64_16x16x4_f64 with the operand
  * and accumulator lane maps the CTA SYRK kernel relies on (all column-major). */
 int ccmm_selftest_mfma_f64(ccmm_ctx* ctx, const double* A16x4, const double* B4x16, double* D16x16);
+/* nprobe independent D = C + A B (one v_mfma_f64_16x16x4_f64 each, caller-given accumulator),
+ * probe q at A16x4 + 64 q, B4x16 + 64 q, C16x16 / D16x16 + 256 q: measures the instruction's
+ * internal summation order and rounding points (tools/probe_mfma_order.py). */
+int ccmm_selftest_mfma_f64_acc(ccmm_ctx* ctx, int nprobe, const double* A16x4, const double* B4x16,
+                               const double* C16x16, double* D16x16);
 
 #ifdef __cplusplus
 }

@@ -296,6 +296,39 @@ def cta_syrk(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z):
     return PAI, 0
 
 
+def cta_sys_syrk(Y, Xs, N, K, T, A, sqrtht, iVdiag, iVb, PAI, z, return_sd=False):
+    """CTAsys.m:57-108 in the algorithmic (weighted-SYRK) form, for systems where the
+    as-written kron form is out of reach (S120: K = 1441, N = 120, X_j up to 1 GB).
+    Xs: list of N designs (T x K each; equations sharing a slab may share the array).
+    XPAI (CTAsys.m:67-73: X_jj PAI(:,jj) of every other equation, with the columns < j
+    already redrawn) is kept up to date column by column instead of recomputed per j:
+    the same values.  Per equation: G = X_j' diag(w) X_j + diag(iV_j), rhs = iVb_j + X_j' v
+    (SURVEY.md §3.4 identity), Cholesky, two triangular solves (CTA.m:95-96 with
+    Vchol = L^-T).  return_sd: posterior sd per coefficient (sqrt diag G^-1)."""
+    PAI = np.array(PAI, dtype=float, copy=True)
+    sd = np.zeros((K, N))
+    ih2 = 1.0 / sqrtht ** 2
+    XPAI = np.column_stack([Xs[jj] @ PAI[:, jj] for jj in range(N)])
+    for j in range(N):
+        E = Y - XPAI
+        E[:, j] = Y[:, j]
+        w = ih2[:, j:] @ (A[j:, j] ** 2)
+        v = ((E @ A[j:, :].T) * ih2[:, j:]) @ A[j:, j]
+        Xj = Xs[j]
+        G = Xj.T @ (Xj * w[:, None])
+        G[np.diag_indices(K)] += iVdiag[:, j]
+        L = np.linalg.cholesky(G)
+        y = solve_triangular(L, iVb[:, j] + Xj.T @ v, lower=True)
+        PAI[:, j] = solve_triangular(L.T, y + z[:, j], lower=False)
+        XPAI[:, j] = Xj @ PAI[:, j]
+        if return_sd:
+            Li = solve_triangular(L, np.eye(K), lower=True)
+            sd[:, j] = np.sqrt(np.einsum("ik,ik->k", Li, Li))
+    if return_sd:
+        return PAI, 0, sd
+    return PAI, 0
+
+
 def cta_post_moments_syrk(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, j):
     """Algebraic (weighted-SYRK) form of equation j's posterior precision and rhs,
     used only by tests to cross-check the kron form (SURVEY.md §3.4 identity)."""

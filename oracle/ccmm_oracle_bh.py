@@ -194,7 +194,7 @@ def bh_init_state(bs: BHSetup):
     return st
 
 
-def bh_sweep(st, bs: BHSetup, crn, return_flags=False, elb_impl="qr", use_ps=False):
+def bh_sweep(st, bs: BHSetup, crn, return_flags=False, elb_impl="qr", use_ps=False, cta_form="kron"):
     """One sweep of mcmcVARshadowrateBlockHybrid.m:322-523: the Gibbs ELB branch
     (m < MCMCburnin/2, :435-437), or with use_ps the acceptance-sampling branch
     (:438-466: PS proposals crn["zPS"], the first accepted, else the Gibbs draw).
@@ -203,18 +203,26 @@ def bh_sweep(st, bs: BHSetup, crn, return_flags=False, elb_impl="qr", use_ps=Fal
     conditionals in the residual form of elb_fast.gibbsdraw_shadowrates_stable
     (accurate when the shadow companion matrix is explosive, where the as-written
     Ytilde = Y - Y0 cancels catastrophically); "both" = stable, with the as-written
-    draw in out["shadowrate_qr"]."""
+    draw in out["shadowrate_qr"].
+
+    cta_form: "kron" = CTAsys.m as written; "syrk" = O.cta_sys_syrk (the same posterior in
+    the weighted-SYRK form; S120-sized systems)."""
     lin = bs.lin
     N, K, T = lin.N, lin.K, lin.T
     Y, X = st["Y"], st["X"]
-    XX = np.empty((T, K, N))
-    XX[:, :, bs.actualrateBlock] = bs.Xactual[:, :, None]
-    XX[:, :, ~bs.actualrateBlock] = X[:, :, None]
-    PAI, status = O.cta_sys(Y, XX, N, K, T, st["A"], st["sqrtht"], lin.iVdiag, lin.iVb, st["PAI"],
-                            crn["zPAI"])
+    Xs = [bs.Xactual if bs.actualrateBlock[j] else X for j in range(N)]
+    if cta_form == "kron":
+        XX = np.empty((T, K, N))
+        XX[:, :, bs.actualrateBlock] = bs.Xactual[:, :, None]
+        XX[:, :, ~bs.actualrateBlock] = X[:, :, None]
+        PAI, status = O.cta_sys(Y, XX, N, K, T, st["A"], st["sqrtht"], lin.iVdiag, lin.iVb, st["PAI"],
+                                crn["zPAI"])
+    else:
+        PAI, status = O.cta_sys_syrk(Y, Xs, N, K, T, st["A"], st["sqrtht"], lin.iVdiag, lin.iVb, st["PAI"],
+                                     crn["zPAI"])
     RESID = np.empty((T, N))
     for jj in range(N):
-        RESID[:, jj] = Y[:, jj] - XX[:, :, jj] @ PAI[:, jj]
+        RESID[:, jj] = Y[:, jj] - Xs[jj] @ PAI[:, jj]
     A, invA = O.a_step(RESID, st["sqrtht"], crn["zA"])
     logy2 = np.log((RESID @ A.T) ** 2 + lin.logy2offset)
     h, h0, shocks, kai = O.sv_ksc_corrsqrt(logy2.T, st["h"].T, st["sqrtPHI"], lin.Vol_0mean,

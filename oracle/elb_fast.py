@@ -201,16 +201,26 @@ def elb_conditionals_stable(Yb, e0, ndxS, sNaN, p, C, Psi, SVol):
         for l in range(1, min(p, t) + 1):
             eps[:, t] -= Ph(l) @ Yb[:, t - l]
 
+    cache = {}
+
     def solve(t, eps_at):
-        """eps_at(τ) = residual vector of month τ (t <= τ <= t + kmax)."""
+        """eps_at(τ) = residual vector of month τ (t <= τ <= t + kmax).  P_t, Ω_t and the
+        products B_k' Λ_{t+k} depend on t only: formed once per month (same operations)."""
         kmax = min(p, T - 1 - t)
-        P = Lam[t][np.ix_(S, S)].copy()
+        if t not in cache:
+            P = Lam[t][np.ix_(S, S)].copy()
+            Ms = []
+            for k in range(1, kmax + 1):
+                Bk = Phi[:, (k - 1) * Ny + S]
+                Mk = Bk.T @ Lam[t + k]
+                P += Mk @ Bk
+                Ms.append(Mk)
+            cache.clear()
+            cache[t] = (np.linalg.inv(P), Ms)
+        Om, Ms = cache[t]
         g = -(Lam[t] @ eps_at(t))[S]
         for k in range(1, kmax + 1):
-            Bk = Phi[:, (k - 1) * Ny + S]
-            P += Bk.T @ Lam[t + k] @ Bk
-            g += Bk.T @ Lam[t + k] @ eps_at(t + k)
-        Om = np.linalg.inv(P)
+            g += Ms[k - 1] @ eps_at(t + k)
         return Om @ g, Om
 
     def unit_eps(q, tp):

@@ -1,0 +1,118 @@
+"""Generate the real-data MCSE fixtures (tests/golden/mcse_real_{linear,bh}.npz): posterior
+moments from ONE long oracle chain on the reference's own data file fredblockMD20-2022-09.csv
+at the 2022-08 jump-off (N = 20, p = 12, T = 750, K = 241), with Geweke numerical standard
+errors as Diagnostics.m:134-300 computes them (oracle/ccmm_oracle_stats.momentg).
+
+  linear  BASELINE configs[1]: mcmcVAR.m sweeps (oracle.linear_sweep, CTA in
+          the weighted-SYRK form: the same posterior as CTA.m), reference initialisation
+          (mcmcVAR.m:197-206), BURN burn-in + KEEP kept sweeps.
+  bh      BASELINE configs[2] (C3): mcmcVARshadowrateBlockHybrid.m sweeps at ELB = 0.25 with the
+          reference's ELB schedule (:433-466): the Gibbs sampler (gibbsdrawShadowrates, 101
+          passes) for m < MCMCburnin / 2, then 1000 PS proposals, accept-first, Gibbs fallback.
+          CTAsys in the SYRK form, ELB conditionals in the stable residual form.
+
+Quantities (a subset, so that 4.5 combined standard errors is a sharp bar): the intercept
+and own first-lag coefficient of every equation, the first-lag coefficient of FEDFUNDS in
+every equation, the subdiagonal of A, the diagonal of PHI, sqrtht at three months; bh adds the
+shadow rates of 24 censored cells spread over the window.  Used by tests/test_gpu_mcse_real.py.
+
+Run: python tools/make_mcse_real_fixture.py linear|bh [--keep 2000] [--burn 1000]
+(CPU; linear ~15 min, bh ~1-2 h single-threaded)."""
+import argparse
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import numpy as np
+
+from oracle import ccmm_oracle as oracle
+from oracle.ccmm_oracle_stats import momentg
+
+TSEL = (0, 374, 749)
+NCELLS = 24
+
+
+def selection(N, p, ncode):
+    """Row/column indices into PAI (K x N) of the selected coefficients."""
+    ff = list(ncode).index("FEDFUNDS")
+    rows, cols = [], []
+    for j in range(N):
+        rows += [0, 1 + j, 1 + ff]       # intercept, own lag 1, FEDFUNDS lag 1
+        cols += [j, j, j]
+    return np.array(rows), np.array(cols)
+
+
+def quantities(PAI, A, PHI, sqrtht, sel, shadow=None, cells=None):
+    r, c = sel
+    N = A.shape[0]
+    q = [PAI[r, c], A[np.arange(1, N), np.arange(N - 1)], np.diag(PHI), sqrtht[list(TSEL), :].ravel(order="F")]
+    if shadow is not None:
+        q.append(shadow.ravel(order="F")[cells])
+    return np.concatenate(q)
+
+
+def censored_cells(sNaN):
+    """NCELLS censored cells (column-major index into Ns x elbT) spread over the window."""
+    idx = np.flatnonzero(sNaN.ravel(order="F"))
+    return idx[np.linspace(0, idx.size - 1, NCELLS).round().astype(int)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("kind", choices=["linear", "bh"])
+    ap.add_argument("--burn", type=int, default=1000)
+    ap.add_argument("--keep", type=int, default=2000)
+    ap.add_argument("--seed", type=int, default=20243)
+    ap.add_argument("--nproposals", type=int, default=1000)
+    args = ap.parse_args()
+    fred = oracle.load_fred_csv(ROOT / "tests/golden/data/fredblockMD20-2022-09.csv")
+    mpm = oracle.set_minnesota_mean(fred["ncode"])
+    thisT = len(fred["ydates"])
+    rng = np.random.default_rng(args.seed)
+    sel = selection(20, 12, fred["ncode"])
+    draws = []
+    t0 = time.time()
+    acc = 0
+    cells = None
+    if args.kind == "linear":
+        su = oracle.var_setup(thisT, 12, 12, fred["data"], fred["ydates"], mpm, True)
+        st = oracle.init_state(su)
+        for m in range(args.burn + args.keep):
+            st = oracle.linear_sweep(st, su, oracle.draw_crn(rng, su.N, su.K, su.T, su.dPHI), cta_form="syrk")
+            if m >= args.burn:
+                draws.append(quantities(st["PAI"], st["A"], st["PHI"], st["sqrtht"], sel))
+            if m % 100 == 0:
+                print(m, f"{time.time() - t0:.0f}s", flush=True)
+    else:
+        from oracle import ccmm_oracle_bh as bh
+        ndxS, ndxO, _ = oracle.set_shadow_yields(fred["ncode"], 0.25)
+        e0 = oracle.elb_t0(fred["data"], ndxS, 0.25, 12)
+        bs = bh.bh_setup(thisT, 12, 12, fred["data"], fred["ydates"], ndxS, ndxO, mpm, 0.25, e0)
+        cells = censored_cells(bs.sNaN)
+        st = bh.bh_init_state(bs)
+        ps_from = -(-args.burn // 2)                          # m >= MCMCburnin / 2 (1-based m)
+        for m in range(args.burn + args.keep):
+            use_ps = (m + 1) >= ps_from
+            crn = bh.bh_draw_crn(rng, bs, args.nproposals if use_ps else 0)
+            st = bh.bh_sweep(st, bs, crn, elb_impl="stable", use_ps=use_ps, cta_form="syrk")
+            acc += bool(st.get("ps_accept", 0))
+            if m >= args.burn:
+                draws.append(quantities(st["PAI"], st["A"], st["PHI"], st["sqrtht"], sel,
+                                        st["shadowrate"], cells))
+            if m % 50 == 0:
+                print(m, f"{time.time() - t0:.0f}s", "accepted", acc, flush=True)
+    D = np.array(draws)
+    mg = momentg(D)
+    out = ROOT / "tests" / "golden" / f"mcse_real_{args.kind}.npz"
+    extra = {} if cells is None else dict(cells=cells, accept=acc)
+    np.savez(out, pmean=mg["pmean"], pstd=mg["pstd"], nse=mg["nse"], nse1=mg["nse1"], nse2=mg["nse2"],
+             nse3=mg["nse3"], burn=args.burn, keep=args.keep, seed=args.seed, tsel=np.array(TSEL),
+             sel_rows=sel[0], sel_cols=sel[1], nproposals=args.nproposals, **extra)
+    print("wrote", out, "nvar", D.shape[1], "seconds", round(time.time() - t0),
+          "min rne3", float(np.min(mg["rne3"])))
+
+
+if __name__ == "__main__":
+    main()
