@@ -53,6 +53,8 @@ _SIGS = {
     "ccmm_synchronize": (C.c_int, [C.c_void_p]),
     "ccmm_cta": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _dp, C.c_int, _dp,
                            C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _ip]),
+    "ccmm_cta_aswitching": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _dp, C.c_int, _dp,
+                                      C.c_int, C.c_int, _dp, _dp, _u8p, _dp, _dp, _dp, _dp, _dp, _ip]),
     "ccmm_astep": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp]),
     "ccmm_sv_ksc": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp,
                               _dp, _dp, _dp, _dp, _i8p]),
@@ -90,9 +92,13 @@ _SIGS = {
     "ccmm_chains_set_elb_model": (C.c_int, [C.c_void_p, _ip, _u8p]),
     "ccmm_chains_set_elb_slot": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p]),
     "ccmm_chains_get_shadowrate": (C.c_int, [C.c_void_p, _dp]),
+    "ccmm_chains_get_cta_gram": (C.c_int, [C.c_void_p, _dp]),
     "ccmm_chains_set_elb_ps": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "ccmm_draw_summaries": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, C.c_int, _dp, _dp, _dp,
                                       _dp, _dp, _dp]),
+    "ccmm_girf_hybrid": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp,
+                                   _dp, _u8p, _u8p, C.c_double, _u8p, C.c_double, C.c_double, _dp, _dp,
+                                   C.c_uint64, _dp]),
     "ccmm_girf": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp,
                             _dp, C.c_int, _u8p, _u8p, C.c_double, _u8p, C.c_double, C.c_double, _dp,
                             _dp, C.c_uint64, _dp]),
@@ -206,6 +212,31 @@ class Context:
                                _ptr(_f(iVb)), _ptr(PAI), _ptr(_f(z)) if z is not None else None,
                                status.ctypes.data_as(_ip))
         _check(rc, "ccmm_cta")
+        return PAI, status
+
+    def cta_aswitching(self, Y, X, A, Aelb, atELB, sqrtht, iVdiag, iVb, PAI, z=None, y_per_chain=False,
+                       x_per_chain=False):
+        """Batched CTAsysAswitching draw: as ``cta`` plus Aelb N x N x B and atELB (T bools,
+        shared by the chains): the months at the ELB use Aelb (CTAsysAswitching.m:61-80)."""
+        A = _f(A)
+        N = A.shape[0]
+        B = A.shape[2] if A.ndim == 3 else 1
+        PAI = _f(PAI).copy(order="F")
+        K = PAI.shape[0]
+        T = np.asarray(Y).shape[0]
+        Xf = _f(X)
+        if x_per_chain:
+            nx = Xf.shape[2] if Xf.ndim == 4 else 1
+        else:
+            nx = Xf.shape[2] if Xf.ndim == 3 else 1
+        at = np.ascontiguousarray(np.asarray(atELB, bool).ravel(), dtype=np.uint8)
+        assert at.size == T, "atELB must hold T entries"
+        status = np.zeros(B, dtype=np.int32)
+        rc = self.lib.ccmm_cta_aswitching(self.handle, B, T, N, K, _ptr(_f(Y)), int(y_per_chain), _ptr(Xf), nx,
+                                          int(x_per_chain), _ptr(A), _ptr(_f(Aelb)), at.ctypes.data_as(_u8p),
+                                          _ptr(_f(sqrtht)), _ptr(_f(iVdiag)), _ptr(_f(iVb)), _ptr(PAI),
+                                          _ptr(_f(z)) if z is not None else None, status.ctypes.data_as(_ip))
+        _check(rc, "ccmm_cta_aswitching")
         return PAI, status
 
     def astep(self, RESID, sqrtht, z=None):
@@ -338,18 +369,31 @@ class Context:
         return out
 
     def girf(self, PAI, invA, sqrtPHI, SV0, Xjumpoff, H, nsim, shock11, *, bh=False, actual=None,
-             ndxYields=None, elb=0.25, cumcode=None, np_=12, z=None, svz=None, seed=1012023):
+             ndxYields=None, elb=0.25, cumcode=None, np_=12, z=None, svz=None, seed=1012023,
+             hybrid=False, ndxShadow=None, p=None):
         """Generalized impulse responses (ccmm_girf): PAI K x N x M, invA / sqrtPHI N x N x M,
         SV0 N x M, Xjumpoff (K [+ Ny p]) x M; z, svz N x H x nsim x M or None (Philox).
+        hybrid=True (ccmm_girf_hybrid, generateGIRF2hybrid): PAI (K + Ns p) x N x M with the
+        lag order ``p``, ring = ndxShadow, output floored for ndxYields.
         Returns N x H x 3 x M (baseline, +shock, -shock mean paths)."""
         PAI = _f(PAI)
-        K, N, M = PAI.shape
-        p = (K - 1) // N
+        Kx, N, M = PAI.shape
         u8 = lambda m: None if m is None else np.ascontiguousarray(np.asarray(m, bool), dtype=np.uint8)
         act, yl, cc = u8(actual), u8(ndxYields), u8(cumcode)
         out = np.zeros((N, int(H), 3, M), order="F")
         zz = None if z is None else _f(z)
         sz = None if svz is None else _f(svz)
+        if hybrid:
+            sh = u8(ndxShadow)
+            p = int(p) if p is not None else (Kx - 1) // (N + int(sh.sum()))
+            _check(self.lib.ccmm_girf_hybrid(self.handle, M, N, p, int(H), int(nsim), _ptr(PAI), _ptr(_f(invA)),
+                                             _ptr(_f(sqrtPHI)), _ptr(_f(SV0)), _ptr(_f(Xjumpoff)),
+                                             sh.ctypes.data_as(_u8p), yl.ctypes.data_as(_u8p), float(elb),
+                                             None if cc is None else cc.ctypes.data_as(_u8p), float(np_),
+                                             float(shock11), _ptr(zz), _ptr(sz), int(seed), _ptr(out)),
+                   "ccmm_girf_hybrid")
+            return out
+        p = (Kx - 1) // N
         _check(self.lib.ccmm_girf(self.handle, M, N, p, int(H), int(nsim), _ptr(PAI), _ptr(_f(invA)),
                                   _ptr(_f(sqrtPHI)), _ptr(_f(SV0)), _ptr(_f(Xjumpoff)), int(bool(bh)),
                                   None if act is None else act.ctypes.data_as(_u8p),
@@ -469,6 +513,13 @@ class Chains:
         k = np.zeros((self.T, self.N, self.B), dtype=np.int8, order="F")
         _check(self.lib.ccmm_chains_get_kai(self.handle, k.ctypes.data_as(_i8p)), "ccmm_chains_get_kai")
         return k
+
+    def get_cta_gram(self):
+        """The device's weighted Gram of every CTA system at the current state, K x K x N x B
+        ([c b'; b M], no prior; lag-structured path only)."""
+        G = np.zeros((self.K, self.K, self.N, self.B), order="F")
+        _check(self.lib.ccmm_chains_get_cta_gram(self.handle, _ptr(G)), "ccmm_chains_get_cta_gram")
+        return G
 
     def record_elb_flags(self, enable=True):
         _check(self.lib.ccmm_chains_record_elb_flags(self.handle, int(bool(enable))),

@@ -278,6 +278,7 @@ struct ccmm_chains {
   // kernel variants (A/B): CCMM_OLD_SOLVE=1 selects the first-generation solve kernel
   bool use_solve2 = std::getenv("CCMM_OLD_SOLVE") == nullptr;
   bool use_fused = std::getenv("CCMM_OLD_CHOL") == nullptr;
+  bool gc18 = std::getenv("CCMM_GC18") != nullptr;
   // timing-only ablation of k_gram_chol (results invalid): 1 = no SYRK, 2 = no Cholesky
   int gc_mode = std::getenv("CCMM_GC_MODE") ? std::atoi(std::getenv("CCMM_GC_MODE")) : 0;
   std::vector<bool> have_slot;
@@ -385,8 +386,14 @@ struct ccmm_chains {
     cs.svw = svw.p;
     cs.Zphi = Zphi.p;
     cs.status = status.p;
+    cs.Aelb = aswitch ? AelbD.p : nullptr;
+    cs.atELB = aswitch ? atELBD.p : nullptr;
     return cs;
   }
+  // CTAsysAswitching (block-level drop-in only): second A matrix for the months at the ELB
+  bool aswitch = false;
+  DBuf<double> AelbD;
+  DBuf<uint8_t> atELBD;
   XSel xsel() const { return XSel{Xpool.p, xidx.p, Ypool.p, yidx.p}; }
 
   int64_t crn_off[kRngBlocks] = {};
@@ -425,7 +432,10 @@ struct ccmm_chains {
     require(d.KP <= kBigMaxKP, "this build supports K <= 1536");
     // KP > 256: the register-tiled fused Gram + Cholesky (k_gram_chol) stops at 16 tiles; the
     // large path beats the generic SYRK + Cholesky there (hybrid model K = 277: 32 vs 41 ms)
-    big = d.KP > 256 || cf.N > kMaxNSmall || std::getenv("CCMM_FORCE_BIG") != nullptr;
+    // 256 < K <= 288 (the hybrid model, K = 277): the fused kernel with 18 tiles (k_gram_chol<18>)
+    // (experimental, CCMM_GC18=1: k_gram_chol<18> spills at 8 waves; the large path is the default)
+    big = (d.KP > 256 && (cf.K > 288 || !use_fused || !gc18)) || cf.N > kMaxNSmall ||
+          std::getenv("CCMM_FORCE_BIG") != nullptr;
     nslabX = nX;
     nslabY = nY;
     const size_t B = cf.B, N = cf.N, KP = d.KP, TP = d.TP;
@@ -838,8 +848,20 @@ struct ccmm_chains {
   }
 
   void ensure_cta() {
-    G.alloc((size_t)d.nmat * d.KP * d.KP);
+    if (!G.p) {
+      G.alloc((size_t)d.nmat * d.KP * d.KP);
+      // the fused NT = 18 path (256 < K <= 288, KP = 320) never writes rows / columns past 288:
+      // they stay zero for k_cta_solve2's 64-row blocks
+      HIPCHECK(hipMemsetAsync(G.p, 0, G.n * sizeof(double), ctx->stream));
+    }
     rdiag.alloc((size_t)d.nmat * d.KP);
+  }
+  // fused register-tiled Gram + Cholesky: KP <= 256 (16 tiles), or 256 < K <= 288 (18 tiles)
+  int fused_nt() const {
+    if (!use_fused) return 0;
+    if (d.KP <= 256) return d.KP / 16;
+    if (d.K <= 288 && gc18) return 18;
+    return 0;
   }
 
   void run_resid() {
@@ -872,15 +894,16 @@ struct ccmm_chains {
       run_cta_lag(ra, cs);
       return;
     }
-    const bool fused = use_fused && d.KP <= 256;
+    const int fnt = fused_nt();
+    const bool fused = fnt > 0;
     launch(KID_WEIGHTS, [&] {
       hipLaunchKernelGGL(k_cta_weights, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0,
                          ctx->stream, d, Tslot.p, cs, fused ? 1 : 0);
     });
     if (fused) {
-      const size_t lds = (size_t)std::max(2 * kGcTC * kGcLdz, 17 * 16 * kGcLdp) * sizeof(double);
+      const size_t lds = (size_t)std::max(2 * kGcTC * gc_ldz(fnt), (fnt + 1) * 16 * kGcLdp) * sizeof(double);
       launch(KID_GRAMCHOL, [&] {
-        switch (d.KP / 16) {
+        switch (fnt) {
 #define CASE_GC(NT)                                                                           \
   case NT:                                                                                    \
     HIPCHECK(hipFuncSetAttribute((const void*)k_gram_chol<NT>,                                \
@@ -892,6 +915,7 @@ struct ccmm_chains {
           CASE_GC(8)
           CASE_GC(12)
           CASE_GC(16)
+          CASE_GC(18)
 #undef CASE_GC
           default:
             throw ArgError("k_gram_chol: unsupported KP");
@@ -914,7 +938,7 @@ struct ccmm_chains {
     }
     const size_t lds_solve = (size_t)(d.TP + d.KP) * sizeof(double);
     const size_t lds_solve2 =
-        (size_t)(d.TP + 2 * d.KP + 64 * kSolveLd + d.N * d.N) * sizeof(double);
+        (size_t)(d.TP + 2 * d.KP + 64 * kSolveLd + 2 * d.N * d.N) * sizeof(double);
     launch(KID_SOLVE, [&] {
       if (use_solve2) {
         if (d.N <= 8)
@@ -1017,6 +1041,43 @@ struct ccmm_chains {
       HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
                               nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 4 & big_mask));
     });
+  }
+
+  // Parity export: the lag path's weighted Gram of every (chain, equation) system at the current
+  // state, [c b'; b M] (K x K, without the prior), decoded from the kernel's tile slots
+  void export_cta_gram(double* out) {
+    require(lag_active(), "ccmm_chains_get_cta_gram: the lag-structured CTA path is not active");
+    ensure_cta();
+    ChainState cs = view();
+    hipLaunchKernelGGL(k_cta_weights, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0, ctx->stream, d,
+                       Tslot.p, cs, 1);
+    HIPCHECK(hipGetLastError());
+    LagSel ls = lagsel();
+    ls.mode = 8;
+    const size_t lds_g = gl_lds_bytes(lagNT, drows, ldd, d.TP);
+    HIPCHECK(lag_launch_gram(lagNT, ctx->stream, lds_g, d, Tslot.p, ls, cs, iVdiag.p));
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    const int NT = lagNT, NTILE = gl_ntile(NT), K = d.K, KL = K - 1;
+    std::vector<double> o((size_t)gl_out_len(NT));
+    for (int mat = 0; mat < d.nmat; ++mat) {
+      HIPCHECK(hipMemcpy(o.data(), G.p + (size_t)mat * d.KP * d.KP, o.size() * sizeof(double),
+                         hipMemcpyDeviceToHost));
+      double* Gm = out + (size_t)mat * K * K;
+      Gm[0] = o[(size_t)NTILE * 256];
+      for (int a = 0; a < KL; ++a) Gm[1 + a] = Gm[(size_t)(1 + a) * K] = o[(size_t)NTILE * 256 + 1 + a];
+      for (int gi = 0; gi < NTILE; ++gi) {
+        const int ti = gl_ti(NT, gi), tj = gl_tj(NT, gi);
+        for (int r = 0; r < 4; ++r)
+          for (int lane = 0; lane < 64; ++lane) {
+            const int row = 16 * tj + (lane >> 4) + 4 * r, col = 16 * ti + (lane & 15);  // upper tile (tj, ti)
+            if (row < KL && col < KL) {
+              const double v = o[(size_t)gi * 256 + 64 * r + lane];
+              Gm[(size_t)(1 + row) + (size_t)(1 + col) * K] = v;
+              Gm[(size_t)(1 + col) + (size_t)(1 + row) * K] = v;
+            }
+          }
+      }
+    }
   }
 
   // CTA on the lag structure: sqrt weights -> Gram + Cholesky + inverse -> sequential solve
@@ -1342,17 +1403,21 @@ struct ccmm_chains {
 
   void set_fcst(int H, int Nd, const uint8_t* ndxYields, int keep) {
     const int N = cfg.N, p = cfg.p;
-    require(!hybrid, "predictive density of the hybrid model is not built (block-hybrid and linear only)");
-    require(cfg.p >= 1 && cfg.K == N * p + 1, "predictive density needs K = N*p + 1");
+    require(cfg.p >= 1 && (cfg.K == N * p + 1 || (hybrid && cfg.K == N * p + 1 + cfg.Ns * p)),
+            "predictive density needs K = N*p + 1 (hybrid: + Ns*p)");
+    require(!hybrid || cfg.Ns <= 4, "hybrid predictive density: Ns <= 4");
     require(N <= kFcstMaxN, "predictive density supports N <= 32");
     require(H >= 1 && Nd >= 1, "H and Nd must be >= 1");
     require(cfg.store_capacity > 0, "predictive density needs store_capacity > 0 (one record per kept draw)");
     int nwx = 0;
     for (int i = 0; i < N; ++i) nwx += ndxYields[i] ? 0 : 1;
     require(nwx > 0 && nwx < N, "need at least one macro series and one yield");
-    if (bh)
+    if (bh && !hybrid)
       for (int i = 0; i < N; ++i)
         require(!(hActual[i] && ndxYields[i]), "a yield cannot be in the actual-rate block");
+    if (hybrid)
+      for (int a = 0; a < cfg.Ns; ++a)
+        require(ndxYields[hNdxS[a]], "the shadow-rate variables must be yields (ndxYIELDS)");
     fH = H;
     fNd = Nd;
     fKeep = keep ? 1 : 0;
@@ -1378,7 +1443,7 @@ struct ccmm_chains {
       fPaths.alloc(B * cap * Nd * HN);
       fPathsC.alloc(B * cap * Nd * HN);
     }
-    int nw = std::min((fcst_bh ? Nd : Nd + 1), kFcstMaxWaves);
+    int nw = std::min(((fcst_bh || hybrid) ? Nd : Nd + 1), kFcstMaxWaves);
     while (nw > 1 && fcst_lds_bytes(N, p, cfg.K, nw) > 160 * 1024) --nw;
     require(fcst_lds_bytes(N, p, cfg.K, nw) <= 160 * 1024, "forecast state does not fit LDS");
     fnw = nw;
@@ -1479,7 +1544,12 @@ struct ccmm_chains {
     const int N = d.N, B = d.B, H = fH, Nd = fNd;
     ChainState cs = view();
     FcstArgs a{};
-    a.B = B; a.N = N; a.p = cfg.p; a.K = cfg.K; a.H = H; a.Nd = Nd; a.bh = fcst_bh ? 1 : 0;
+    a.B = B; a.N = N; a.p = cfg.p; a.H = H; a.Nd = Nd;
+    a.bh = hybrid ? 2 : (fcst_bh ? 1 : 0);
+    a.K = N * cfg.p + 1;
+    a.Kx = cfg.K;
+    a.Ns = hybrid ? cfg.Ns : 0;
+    a.ndxS = hybrid ? dNdxS.p : nullptr;
     a.PAI = PAI.p; a.ldPAI = d.KP; a.invA = invA.p; a.logSV = h.p; a.ldSV = d.TP;
     a.svT = Tslot.p; a.slot = slot.p; a.sqrtPHI = sqrtPHI.p; a.Xj = fXj.p; a.ldXj = fldXj;
     a.yreal = fYreal.p; a.ldY = N; a.ndxYields = fYields.p; a.actual = fcst_bh ? dActual.p : nullptr;
@@ -1496,13 +1566,14 @@ struct ccmm_chains {
     const size_t lds = fcst_lds_bytes(N, cfg.p, cfg.K, fnw);
     const XSel xs = xsel();
     launch(KID_FCST, [&] {
-      hipLaunchKernelGGL(k_fcst_jumpoff, dim3(B), dim3(256), 0, ctx->stream, N, cfg.p, cfg.K, d.TP,
-                         Tslot.p, slot.p, xs.ypool, xs.yidx, fldXj, fXj.p);
+      hipLaunchKernelGGL(k_fcst_jumpoff, dim3(B), dim3(256), 0, ctx->stream, N, cfg.p, N * cfg.p + 1, d.TP,
+                         Tslot.p, slot.p, xs.ypool, xs.yidx, fldXj, fXj.p, hybrid ? cfg.Ns : 0,
+                         hybrid ? dNdxS.p : nullptr, cfg.elb);
       HIPCHECK(hipFuncSetAttribute((const void*)k_fcst, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds));
       hipLaunchKernelGGL(k_fcst, dim3(B), dim3(64 * fnw), lds, ctx->stream, a);
       hipLaunchKernelGGL(k_fcst_accum, dim3(B), dim3(256), 0, ctx->stream, N, H, Nd,
-                         cfg.store_capacity, fstored, fY.p, fYc.p, fcst_bh ? nullptr : fYhat.p, fSc.p,
+                         cfg.store_capacity, fstored, fY.p, fYc.p, (fcst_bh || hybrid) ? nullptr : fYhat.p, fSc.p,
                          fYsum.p, fYcsum.p, fYhatsum.p, fScStore.p, fKeep ? fPaths.p : nullptr,
                          fKeep ? fPathsC.p : nullptr);
     });
@@ -1551,7 +1622,8 @@ struct ccmm_chains {
     // inputs of every flagged chain to the host, the redraws in parallel, PAI back
     struct Job {
       int c, T, fl = 0;
-      std::vector<double> Y, A, sh, ivd, ivb, pai, z;
+      std::vector<double> Y, A, Ae, sh, ivd, ivb, pai, z;
+      std::vector<uint8_t> at;
       std::vector<std::vector<double>> X;
       std::vector<const double*> Xs;
     };
@@ -1563,6 +1635,10 @@ struct ccmm_chains {
       jb.T = hT[s];
       dl(Ypool.p + (size_t)hyi[c] * N * TP, (size_t)N * TP, jb.Y);
       dl(A.p + (size_t)c * N * N, (size_t)N * N, jb.A);
+      if (aswitch) {
+        dl(AelbD.p + (size_t)c * N * N, (size_t)N * N, jb.Ae);
+        dl(atELBD.p + (size_t)c * TP, (size_t)TP, jb.at);
+      }
       dl(sqrtht.p + (size_t)c * N * TP, (size_t)N * TP, jb.sh);
       dl(iVdiag.p + (size_t)s * N * KP, (size_t)N * KP, jb.ivd);
       dl(iVb.p + (size_t)s * N * KP, (size_t)N * KP, jb.ivb);
@@ -1599,7 +1675,8 @@ struct ccmm_chains {
         for (size_t q; (q = next++) < jobs.size();) {
           Job& jb = jobs[q];
           jb.fl = host_cta_chain(N, K, jb.T, jb.Y.data(), TP, jb.Xs.data(), TP, jb.A.data(), jb.sh.data(), TP,
-                                 jb.ivd.data(), jb.ivb.data(), KP, jb.pai.data(), jb.z.data(), force_qr);
+                                 jb.ivd.data(), jb.ivb.data(), KP, jb.pai.data(), jb.z.data(), force_qr,
+                                 aswitch ? jb.Ae.data() : nullptr, aswitch ? jb.at.data() : nullptr);
         }
       };
       const unsigned nth = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
@@ -1714,18 +1791,31 @@ static ccmm_chain_config block_cfg(int B, int T, int N, int K) {
   return cf;
 }
 
-int ccmm_cta(ccmm_ctx* ctx, int B, int T, int N, int K, const double* Y, int y_per_chain,
-             const double* X, int nx, int x_per_chain, const double* A, const double* sqrtht,
-             const double* iVdiag, const double* iVb, double* PAI, const double* z, int* status) {
+static int cta_impl(ccmm_ctx* ctx, int B, int T, int N, int K, const double* Y, int y_per_chain,
+                    const double* X, int nx, int x_per_chain, const double* A, const double* Aelb,
+                    const uint8_t* atELB, const double* sqrtht, const double* iVdiag, const double* iVb,
+                    double* PAI, const double* z, int* status) {
   return guarded([&] {
     require(ctx && Y && X && A && sqrtht && iVdiag && iVb && PAI, "null argument");
     require(nx == 1 || nx == N, "nx must be 1 (CTA) or N (CTAsys)");
+    require((Aelb == nullptr) == (atELB == nullptr), "Aelb and atELB go together");
     HIPCHECK(hipSetDevice(ctx->device));
     ccmm_chains ch;
     ccmm_chain_config cf = block_cfg(B, T, N, K);
     cf.p = 0;  // K free-form for the block call
     const int nX = nx * (x_per_chain ? B : 1), nY = y_per_chain ? B : 1;
     ch.init(ctx, cf, nX, nY);
+    if (Aelb) {
+      require(!ch.big && ch.use_solve2, "CTAsysAswitching: supported for K <= 256 and N <= 32");
+      ch.aswitch = true;
+      ch.AelbD.alloc((size_t)B * N * N);
+      HIPCHECK(hipMemcpy(ch.AelbD.p, Aelb, (size_t)B * N * N * sizeof(double), hipMemcpyHostToDevice));
+      std::vector<uint8_t> at((size_t)B * ch.d.TP, 0);
+      for (int c = 0; c < B; ++c)
+        for (int t = 0; t < T; ++t) at[(size_t)c * ch.d.TP + t] = atELB[t] ? 1 : 0;
+      ch.atELBD.alloc(at.size());
+      HIPCHECK(hipMemcpy(ch.atELBD.p, at.data(), at.size(), hipMemcpyHostToDevice));
+    }
     for (int q = 0; q < nX; ++q) ch.upload_X(q, T, X + (size_t)q * T * K);
     ch.upload_TN(ch.Ypool.p, nY, T, Y, 0.0);
     std::vector<int> xi((size_t)B * N), yi(B);
@@ -1770,6 +1860,25 @@ int ccmm_cta(ccmm_ctx* ctx, int B, int T, int N, int K, const double* Y, int y_p
     }
     return 0;
   });
+}
+
+int ccmm_cta(ccmm_ctx* ctx, int B, int T, int N, int K, const double* Y, int y_per_chain,
+             const double* X, int nx, int x_per_chain, const double* A, const double* sqrtht,
+             const double* iVdiag, const double* iVb, double* PAI, const double* z, int* status) {
+  return cta_impl(ctx, B, T, N, K, Y, y_per_chain, X, nx, x_per_chain, A, nullptr, nullptr, sqrtht, iVdiag,
+                  iVb, PAI, z, status);
+}
+
+int ccmm_cta_aswitching(ccmm_ctx* ctx, int B, int T, int N, int K, const double* Y, int y_per_chain,
+                        const double* X, int nx, int x_per_chain, const double* A, const double* Aelb,
+                        const uint8_t* atELB, const double* sqrtht, const double* iVdiag, const double* iVb,
+                        double* PAI, const double* z, int* status) {
+  if (!Aelb || !atELB) {
+    g_err = "null argument";
+    return CCMM_ERR_ARG;
+  }
+  return cta_impl(ctx, B, T, N, K, Y, y_per_chain, X, nx, x_per_chain, A, Aelb, atELB, sqrtht, iVdiag, iVb,
+                  PAI, z, status);
 }
 
 int ccmm_astep(ccmm_ctx* ctx, int B, int T, int N, const double* RESID, const double* sqrtht,
@@ -2639,34 +2748,39 @@ int ccmm_chains_summaries(ccmm_chains* ch, int source, int slot, const uint8_t* 
   });
 }
 
-int ccmm_girf(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const double* PAI, const double* invA,
-              const double* sqrtPHI, const double* SV0, const double* Xjumpoff, int bh, const uint8_t* actual,
-              const uint8_t* ndxYields, double elb, const uint8_t* cumcode, double np_, double shock11,
-              const double* z, const double* svz, uint64_t seed, double* yhat) {
+// bh: 0 linear, 1 block hybrid (ring = ndxYields, actual = actualrateBlock), 2 hybrid (ring =
+// ring_vars = ndxSHADOWRATE, PAI (K + Ns p) x N x M); the output floor is ndxYields in both
+static int girf_impl(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const double* PAI, const double* invA,
+                     const double* sqrtPHI, const double* SV0, const double* Xjumpoff, int bh, const uint8_t* actual,
+                     const uint8_t* ring_vars, const uint8_t* ndxYields, double elb, const uint8_t* cumcode,
+                     double np_, double shock11, const double* z, const double* svz, uint64_t seed, double* yhat) {
   return guarded([&] {
     require(ctx && PAI && invA && sqrtPHI && SV0 && Xjumpoff && yhat, "null argument");
     require(M >= 1 && N >= 1 && N <= 32 && p >= 1 && H >= 1 && nsim >= 1, "bad dimensions (N <= 32)");
-    require(!bh || (actual && ndxYields), "block hybrid needs actual and ndxYields");
+    require(bh != 1 || (actual && ndxYields), "block hybrid needs actual and ndxYields");
+    require(bh != 2 || (ring_vars && ndxYields), "hybrid needs ndxShadow and ndxYields");
     require((z == nullptr) == (svz == nullptr), "z and svz: both or neither");
     HIPCHECK(hipSetDevice(ctx->device));
     const int K = N * p + 1;
     std::vector<int> yi;
     if (bh)
       for (int i = 0; i < N; ++i)
-        if (ndxYields[i]) yi.push_back(i);
+        if (ring_vars[i]) yi.push_back(i);
     const int Ny = (int)yi.size();
+    require(bh == 0 || Ny >= 1, "no ring variables");
     const int ldX = K + Ny * p;
+    const int ldP = (bh == 2) ? ldX : K;
     require((K + Ny * p + N + 3) / 4 <= 96, "state too large for the GIRF kernel (K + Ny p + N <= 384)");
     const size_t nch = (size_t)(nsim + 3) / 4;
     DBuf<double> dPAI, dA, dS, dSV, dX, dZ, dSZ, dPart, dOut;
-    DBuf<uint8_t> dAct, dCum;
+    DBuf<uint8_t> dAct, dCum, dFl;
     DBuf<int> dY;
     auto up = [&](auto& buf, const auto* src, size_t n) {
       buf.alloc(n);
       HIPCHECK(hipMemcpy(buf.p, src, n * sizeof(src[0]), hipMemcpyHostToDevice));
     };
-    // PAI K x N x M column-major == [M][N][K]
-    up(dPAI, PAI, (size_t)K * N * M);
+    // PAI ldP x N x M column-major == [M][N][ldP]
+    up(dPAI, PAI, (size_t)ldP * N * M);
     up(dA, invA, (size_t)N * N * M);
     up(dS, sqrtPHI, (size_t)N * N * M);
     up(dSV, SV0, (size_t)N * M);
@@ -2675,23 +2789,50 @@ int ccmm_girf(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const double*
       up(dZ, z, (size_t)N * H * nsim * M);
       up(dSZ, svz, (size_t)N * H * nsim * M);
     }
+    if (bh == 1) up(dAct, actual, (size_t)N);
     if (bh) {
-      up(dAct, actual, (size_t)N);
       up(dY, yi.data(), yi.size());
+      up(dFl, ndxYields, (size_t)N);
     }
     if (cumcode) up(dCum, cumcode, (size_t)N);
     dPart.alloc((size_t)M * 3 * nch * H * N);
     dOut.alloc((size_t)M * 3 * H * N);
     GirfArgs a{};
-    a.M = M; a.N = N; a.p = p; a.H = H; a.nsim = nsim; a.bh = bh ? 1 : 0; a.Ny = Ny;
+    a.M = M; a.N = N; a.p = p; a.H = H; a.nsim = nsim; a.bh = bh; a.Ny = Ny;
     a.PAI = dPAI.p; a.invA = dA.p; a.sqrtPHI = dS.p; a.SV0 = dSV.p; a.Xj = dX.p; a.ldX = ldX;
-    a.actual = bh ? dAct.p : nullptr; a.yidx = bh ? dY.p : nullptr; a.elb = elb; a.shock11 = shock11;
+    a.actual = bh == 1 ? dAct.p : nullptr; a.yidx = bh ? dY.p : nullptr; a.yfloor = bh ? dFl.p : nullptr;
+    a.elb = elb; a.shock11 = shock11;
     a.z = z ? dZ.p : nullptr; a.svz = z ? dSZ.p : nullptr; a.seed = seed;
     a.cumcode = cumcode ? dCum.p : nullptr; a.np_ = np_; a.part = dPart.p; a.out = dOut.p;
     a.force_generic = std::getenv("CCMM_GIRF_GENERIC") != nullptr ? 1 : 0;  // A/B of the specialised kernel
     HIPCHECK(girf_launch(ctx->stream, a));
     HIPCHECK(hipStreamSynchronize(ctx->stream));
     HIPCHECK(hipMemcpy(yhat, dOut.p, dOut.n * sizeof(double), hipMemcpyDeviceToHost));
+    return 0;
+  });
+}
+
+int ccmm_girf(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const double* PAI, const double* invA,
+              const double* sqrtPHI, const double* SV0, const double* Xjumpoff, int bh, const uint8_t* actual,
+              const uint8_t* ndxYields, double elb, const uint8_t* cumcode, double np_, double shock11,
+              const double* z, const double* svz, uint64_t seed, double* yhat) {
+  return girf_impl(ctx, M, N, p, H, nsim, PAI, invA, sqrtPHI, SV0, Xjumpoff, bh ? 1 : 0, actual, ndxYields,
+                   ndxYields, elb, cumcode, np_, shock11, z, svz, seed, yhat);
+}
+
+int ccmm_girf_hybrid(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const double* PAI, const double* invA,
+                     const double* sqrtPHI, const double* SV0, const double* Xjumpoff, const uint8_t* ndxShadow,
+                     const uint8_t* ndxYields, double elb, const uint8_t* cumcode, double np_, double shock11,
+                     const double* z, const double* svz, uint64_t seed, double* yhat) {
+  return girf_impl(ctx, M, N, p, H, nsim, PAI, invA, sqrtPHI, SV0, Xjumpoff, 2, nullptr, ndxShadow, ndxYields,
+                   elb, cumcode, np_, shock11, z, svz, seed, yhat);
+}
+
+int ccmm_chains_get_cta_gram(ccmm_chains* ch, double* G) {
+  return guarded([&] {
+    require(ch && G, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    ch->export_cta_gram(G);
     return 0;
   });
 }
@@ -2823,7 +2964,7 @@ int ccmm_fcst(ccmm_ctx* ctx, int B, int N, int p, int H, int Nd, const double* P
     dst.alloc(B);
     HIPCHECK(hipMemsetAsync(dst.p, 0, B * sizeof(int), ctx->stream));
     FcstArgs a{};
-    a.B = B; a.N = N; a.p = p; a.K = K; a.H = H; a.Nd = Nd; a.bh = 0;
+    a.B = B; a.N = N; a.p = p; a.K = K; a.Kx = K; a.H = H; a.Nd = Nd; a.bh = 0;
     a.PAI = dPAI.p; a.ldPAI = K; a.invA = dinvA.p; a.logSV = dlog.p; a.ldSV = 1;
     a.svT = nullptr; a.slot = nullptr; a.sqrtPHI = dsq.p; a.Xj = dXj.p; a.ldXj = K;
     a.yreal = dy.p; a.ldY = 0; a.ndxYields = dmask.p; a.actual = nullptr; a.elb = elb;

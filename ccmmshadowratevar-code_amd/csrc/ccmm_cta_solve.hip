@@ -29,6 +29,7 @@ __global__ __launch_bounds__(256) void k_cta_solve2(Dims d, const int* __restric
   double* rdl = yv + KP;                // KP
   double* Ls = rdl + KP;                // 64 x kSolveLd
   double* Al = Ls + 64 * kSolveLd;      // N x N (column-major A)
+  double* Ael = Al + N * N;             // N x N Aelb (CTAsysAswitching), when cs.Aelb
   const int c = blockIdx.x;
   const int s = cs.slot[c];
   const int T = Tslot[s];
@@ -38,6 +39,8 @@ __global__ __launch_bounds__(256) void k_cta_solve2(Dims d, const int* __restric
   const double* Y = xs.ypool + (size_t)xs.yidx[c] * N * TP;
   double* E = cs.E + (size_t)c * N * TP;
   for (int q = tid; q < N * N; q += 256) Al[q] = cs.A[(size_t)c * N * N + q];
+  if (cs.Aelb)
+    for (int q = tid; q < N * N; q += 256) Ael[q] = cs.Aelb[(size_t)c * N * N + q];
   __syncthreads();
 
   for (int j = 0; j < N; ++j) {
@@ -57,13 +60,14 @@ __global__ __launch_bounds__(256) void k_cta_solve2(Dims d, const int* __restric
           }
         }
         E[(size_t)j * TP + t] = Y[(size_t)j * TP + t];
+        const double* Am = (cs.atELB && cs.atELB[(size_t)c * TP + t]) ? Ael : Al;  // CTAsysAswitching.m:76-77
 #pragma unroll
         for (int i = 0; i < NMAX; ++i) {
           if (i >= j && i < N) {
             double ea = 0.0;
 #pragma unroll
-            for (int k = 0; k <= i; ++k) ea = fma(e[k], Al[i + k * N], ea);
-            acc += Al[i + j * N] * (ea * ih[i]) * ih[i];
+            for (int k = 0; k <= i; ++k) ea = fma(e[k], Am[i + k * N], ea);
+            acc += Am[i + j * N] * (ea * ih[i]) * ih[i];
           }
         }
       } else {

@@ -30,8 +30,13 @@ struct GLNodes {  // Gauss-Legendre half rules (negative nodes) for n = 6, 12, 2
 
 struct FcstArgs {
   int B, N, p, K, H, Nd;
-  int bh;                 // block-hybrid companion (mcmcVARshadowrateBlockHybrid.m:147-159,566-625)
-  const double* PAI;      // [B][N][ldPAI]  (K x N column-major per chain, ld K or KP)
+  int bh;                 // 1: block-hybrid companion (mcmcVARshadowrateBlockHybrid.m:147-159,566-625);
+                          // 2: hybrid (mcmcVARhybridGibbs.m:160-172,566-635): PAI has Kx = K + Ns p
+                          //    rows, the last Ns p multiply the Ns actual-rate lags max(shadow, ELB)
+  int Kx;                 // rows of PAI used (K, or K + Ns p for the hybrid model)
+  int Ns;                 // hybrid: shadow-rate variables
+  const int* ndxS;        // hybrid: [Ns] their indices
+  const double* PAI;      // [B][N][ldPAI]  (Kx x N column-major per chain, ld Kx or KP)
   int ldPAI;
   const double* invA;     // [B][N][N]
   const double* logSV;    // logSV0(c, i) = logSV[(c N + i) ldSV + (svT ? svT[slot c] - 1 : 0)]
@@ -40,7 +45,8 @@ struct FcstArgs {
   const int* slot;        // [B] data slot of chain c, or nullptr (slot 0)
   const double* sqrtPHI;  // [B][N][N]
   const double* Xj;       // [B][ldXj] Xjumpoff: K states [1, y(T), .., y(T-p+1)]; block hybrid:
-  int ldXj;               //   then p blocks of N actual-data lags Xj[K + l N + i] (:88-96,511-520)
+  int ldXj;               //   then p blocks of N actual-data lags Xj[K + l N + i] (:88-96,511-520);
+                          //   hybrid: p blocks of Ns floored actual rates Xj[K + l Ns + s] (:111-121)
   const double* yreal;    // yrealized(:,1) of chain c at yreal + slot(c) * ldY
   int ldY;
   const uint8_t* ndxYields;  // [N]
@@ -297,18 +303,18 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   const int N = a.N, K = a.K, p = a.p, H = a.H, Nd = a.Nd;
   const int nw = blockDim.x >> 6;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // LDS: PAI K x N | per wave: ring_l[p*N] ring_c[p*N] w[N] sv[N] mu[N] dev[N] order[N]
+  // LDS: PAI Kx x N | per wave: ring_l[p*N] ring_c[p*N] w[N] sv[N] mu[N] dev[N] order[N]
   // sel[N] + cens[N] M[32*32] (the score index lists live in LDS: as private arrays their
   // data-dependent indexing put them in scratch memory on the serial score path)
   // (after PAI: muY[N] and the yield flags, shared by all waves of the chain)
   double* sPAI = sm;
   // invA and yrealized staged too: the score algebra walks them in serial loops
-  double* smu = sm + (size_t)K * N;
+  double* smu = sm + (size_t)a.Kx * N;
   int* syl = (int*)(smu + N);
   double* sinvA = smu + 2 * N;
   double* sy = sinvA + N * N;
   const int per_wave = 2 * p * N + 6 * N + kFcstMaxN * kFcstMaxN;
-  double* base = sm + fcst_shared_doubles(N, K) + (size_t)wave * per_wave;
+  double* base = sm + fcst_shared_doubles(N, a.Kx) + (size_t)wave * per_wave;
   double* ringl = base;
   double* ringc = ringl + p * N;
   double* w = ringc + p * N;
@@ -321,9 +327,11 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   double* M = dev + 3 * N;
 
   const int sl = a.slot ? a.slot[c] : 0;
+  const int Kx = a.Kx;
+  const bool hy = a.bh == 2;
   const double* PAIc = a.PAI + (size_t)c * a.ldPAI * N;
-  for (int e = threadIdx.x; e < K * N; e += blockDim.x) {
-    const int j = e / K, k = e - j * K;
+  for (int e = threadIdx.x; e < Kx * N; e += blockDim.x) {
+    const int j = e / Kx, k = e - j * Kx;
     sPAI[e] = PAIc[(size_t)j * a.ldPAI + k];
   }
   const double* Xj = a.Xj + (size_t)c * a.ldXj;
@@ -334,10 +342,13 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   if (threadIdx.x < N) sy[threadIdx.x] = yg[threadIdx.x];
   const double* invA = sinvA;
   const double* y = sy;
+  int hs[4] = {-1, -1, -1, -1};  // hybrid: indices of the shadow-rate variables
+  if (hy)
+    for (int q = 0; q < a.Ns && q < 4; ++q) hs[q] = a.ndxS[q];
   const int tsv = a.svT ? a.svT[sl] - 1 : 0;
   const double* svz = a.svz ? a.svz + (size_t)c * a.crnStride : nullptr;
   const double* zc = a.z ? a.z + (size_t)c * a.crnStride : nullptr;
-  const bool isact = a.bh && lane < N && a.actual[lane];
+  const bool isact = a.bh == 1 && lane < N && a.actual[lane];
   const bool isyield = lane < N && a.ndxYields[lane];
   const bool isrec = lane < N && (a.recFloor ? a.recFloor[lane] : a.ndxYields[lane]);
   Rng rng;
@@ -353,12 +364,13 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   // the chain: lane i of wave 0 once, instead of every wave serially per draw
   if (threadIdx.x < N) {
     const int i = threadIdx.x;
-    const bool act = a.bh && a.actual[i];
+    const bool act = a.bh == 1 && a.actual[i];
     double s = 0.0;
     for (int k = 0; k < K; ++k) {
       const double xv = (act && k > 0 && syl[(k - 1) % N]) ? Xj[K + k - 1] : Xj[k];
-      s += sPAI[(size_t)i * K + k] * xv;
+      s += sPAI[(size_t)i * Kx + k] * xv;
     }
+    for (int k = K; k < Kx; ++k) s += sPAI[(size_t)i * Kx + k] * Xj[k];  // hybrid: actual-rate lags (:592-594)
     smu[i] = s;
   }
   __syncthreads();
@@ -375,8 +387,14 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         const int l = e / N, j = e - l * N;  // lag l+1 goes to slot (-l) mod p
         const int slot = (l == 0) ? 0 : p - l;
         ringl[slot * N + j] = Xj[1 + e];
-        // block hybrid: yields carry their actual-rate lags (Xjumpoff(K+1:end), :93-96)
-        ringc[slot * N + j] = (a.bh && a.ndxYields[j]) ? Xj[K + e] : Xj[1 + e];
+        // block hybrid: yields carry their actual-rate lags (Xjumpoff(K+1:end), :93-96);
+        // hybrid: the shadow-rate variables carry theirs (Xjumpoff(Kshadow+1:end), :111-121)
+        double cv = Xj[1 + e];
+        if (a.bh == 1 && a.ndxYields[j]) cv = Xj[K + e];
+        if (hy)
+          for (int q = 0; q < a.Ns && q < 4; ++q)
+            if (hs[q] == j) cv = Xj[K + l * a.Ns + q];
+        ringc[slot * N + j] = cv;
       }
     double logsv = (lane < N) ? a.logSV[((size_t)c * N + lane) * a.ldSV + tsv] : 0.0;
     int head = 0;
@@ -405,7 +423,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         double nu = 0.0;
         if (!mean_path)
           for (int j = 0; j <= lane; ++j) nu += invA[lane + j * N] * w[j];  // invA unit lower
-        const double* col = sPAI + (size_t)lane * K;
+        const double* col = sPAI + (size_t)lane * Kx;
         double sl2 = Xj[0] * col[0], sc = sl2;  // constant state stays 1 (fcstA(1,1) = 1)
         for (int l = 0; l < p; ++l) {
           int slot = head - l;
@@ -414,8 +432,13 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
           const double* rc = ringc + slot * N;
           const double* pc = col + 1 + l * N;
           for (int j = 0; j < N; ++j) { sl2 += pc[j] * rl[j]; sc += pc[j] * rc[j]; }
+          if (hy)  // fcstA(ndxfcstY, Kshadow+1:end) on the actual-rate ring (:626)
+            for (int q = 0; q < a.Ns && q < 4; ++q) sl2 += col[K + l * a.Ns + q] * rc[hs[q]];
         }
-        if (a.bh) {
+        if (hy) {
+          yl = sl2 + nu;
+          yc = (isyield && yl < a.elb) ? a.elb : yl;  // yields floored (:707-711); ring: max(shadow, ELB) (:634)
+        } else if (a.bh) {
           yl = (isact ? sc : sl2) + nu;               // fcstA * fcstX0 + fcstB * shocks (:615)
           yc = (isyield && yl < a.elb) ? a.elb : yl;  // actual rate max(shadow, ELB) (:623)
         } else {
@@ -505,9 +528,12 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
 // mcmcVARshadowrateBlockHybrid.m:511-520): [1, y(T), ..., y(T-p+1)] from the chain's Y
 // slab (block hybrid: the shadow-rate data), then p blocks of N lags of the slot's
 // actual data (the block-hybrid actual-rate states, data(Nobs-(l-1), ndxYIELDS)).
+// Hybrid (Ns > 0): the tail holds p blocks of the Ns shadow-rate variables' actual data floored at
+// the ELB, XjumpoffActualYieldLags (mcmcVARhybridGibbs.m:111-121, 536).
 __global__ void k_fcst_jumpoff(int N, int p, int K, int TP, const int* __restrict__ Tslot,
                                const int* __restrict__ slot, const double* __restrict__ ypool,
-                               const int* __restrict__ yidx, int ldXj, double* __restrict__ Xj) {
+                               const int* __restrict__ yidx, int ldXj, double* __restrict__ Xj, int Ns,
+                               const int* __restrict__ ndxS, double elb) {
   const int c = blockIdx.x;
   const int s = slot[c];
   const int T = Tslot[s];
@@ -518,6 +544,13 @@ __global__ void k_fcst_jumpoff(int N, int p, int K, int TP, const int* __restric
     if (e > 0 && e < K) {
       const int q = e - 1, l = q / N, i = q - l * N;
       v = Ych[(size_t)i * TP + T - 1 - l];
+    } else if (e >= K && Ns > 0) {
+      const int q = e - K, l = q / Ns, si = q - l * Ns;
+      v = 0.0;
+      if (l < p) {
+        const double yv = Ysl[(size_t)ndxS[si] * TP + T - 1 - l];
+        v = yv < elb ? elb : yv;
+      }
     } else if (e >= K) {
       const int q = e - K, l = q / N, i = q - l * N;
       v = Ysl[(size_t)i * TP + T - 1 - l];

@@ -8,6 +8,8 @@ namespace ccmm {
 
 struct GirfArgs {
   int M, N, p, H, nsim, bh, Ny;  // MCMC draws, variables, lags, horizons, shock paths, model
+                                 // (bh: 0 linear, 1 block hybrid, 2 hybrid: the ring holds the Ny
+                                 // shadow-rate variables and PAI has K + Ny p rows per equation)
   const double* PAI;             // device [M][N][K]
   const double* invA;            // device [M][N][N]
   const double* sqrtPHI;         // device [M][N][N] lower Cholesky of PHI
@@ -15,7 +17,8 @@ struct GirfArgs {
   const double* Xj;              // device [M][ldX] Xjumpoff
   int ldX;
   const uint8_t* actual;         // device [N] actualrateBlock (block hybrid) or null
-  const int* yidx;               // device [Ny] yield variables (block hybrid) or null
+  const int* yidx;               // device [Ny] ring variables (block hybrid: yields; hybrid: shadow rates)
+  const uint8_t* yfloor;         // device [N] variables floored at the ELB in the output (ndxYIELDS) or null
   double elb, shock11;
   const double* z;               // device [M][nsim][H][N] or null (Philox)
   const double* svz;             // device [M][nsim][H][N] or null

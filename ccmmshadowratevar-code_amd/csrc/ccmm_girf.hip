@@ -1,5 +1,6 @@
 // Generalized impulse responses by antithetic simulation (generateGIRF2linear.m,
-// generateGIRF2blockhybrid.m:199-259, simVAR / simVARshadowrateBlockHybrid, antitheticSim):
+// generateGIRF2blockhybrid.m:199-259, generateGIRF2hybrid.m:191-251, simVAR /
+// simVARshadowrateBlockHybrid / simVARhybrid, antitheticSim):
 // per MCMC draw, nsim shock paths x 4 antithetic shock sets x 3 scenarios (no shock,
 // +shock11, -shock11 on variable 1 at horizon 1), each simulated over H horizons, averaged.
 //
@@ -26,14 +27,16 @@ constexpr int kGS = 16;  // simulations per workgroup: 4 paths x 4 antithetic sh
 
 struct GirfDev {
   int M, N, p, H, nsim, bh, Ny, KX, KT, nchunk;
-  const double* PAI;      // [M][N][K]
+  int ldP;                // rows of PAI per equation: K (linear, block hybrid), K + Ny p (hybrid)
+  const double* PAI;      // [M][N][ldP]
   const double* invA;     // [M][N][N]
   const double* sqrtPHI;  // [M][N][N] lower
   const double* SV0;      // [M][N]
   const double* Xj;       // [M][ldX] Xjumpoff (block hybrid: K + p Ny states)
   int ldX;
   const uint8_t* actual;  // [N] (block hybrid)
-  const int* yidx;        // [Ny] yield variables (block hybrid)
+  const int* yidx;        // [Ny] ring variables (block hybrid: yields, hybrid: shadow rates)
+  const uint8_t* yfloor;  // [N] floored at the ELB in the output (ndxYIELDS), bh != 0
   double elb, shock11;
   const double* z;        // [M][nsim][H][N] or nullptr (Philox)
   const double* svz;      // [M][nsim][H][N] or nullptr
@@ -69,7 +72,8 @@ __global__ __launch_bounds__(128) void k_girf(GirfDev g) {
   double* ybuf = logsv + 4 * N;              // [N][kGS]
   double* nrm = ybuf + N * kGS;              // [2][4][N]: svz, z of this horizon
   int* rowtab = (int*)(nrm + 8 * N);         // [p][nks * 4]: state row of coordinate k at head
-  const double* PAI = g.PAI + (size_t)mm * N * K;
+  const int ldP = g.ldP;
+  const double* PAI = g.PAI + (size_t)mm * N * ldP;
   const double* invA = g.invA + (size_t)mm * N * N;
   const double* sqP = g.sqrtPHI + (size_t)mm * N * N;
   const double* SV0 = g.SV0 + (size_t)mm * N;
@@ -79,19 +83,21 @@ __global__ __launch_bounds__(128) void k_girf(GirfDev g) {
   double af[KS];
   {
     const int eq = 16 * et + (lane & 15);
-    const bool act = g.bh && eq < N && g.actual[eq];
+    const bool act = g.bh == 1 && eq < N && g.actual[eq];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int k = 4 * ks + (lane >> 4);
       double v = 0.0;
       if (eq < N && ks < nks) {
         if (k < K) {
-          v = PAI[(size_t)eq * K + k];
+          v = PAI[(size_t)eq * ldP + k];
           if (act && k > 0)
             for (int y = 0; y < g.Ny; ++y) v = (g.yidx[y] == (k - 1) % N) ? 0.0 : v;
         } else if (k < g.KX) {
           const int q = k - K, l = q / g.Ny, y = q - l * g.Ny;
-          v = act ? PAI[(size_t)eq * K + 1 + l * N + g.yidx[y]] : 0.0;
+          // hybrid (generateGIRF2hybrid.m:226-227): the PAI rows of the actual-rate lags;
+          // block hybrid (generateGIRF2blockhybrid.m:226-234): PAIactual of the yield lags
+          v = (g.bh == 2) ? PAI[(size_t)eq * ldP + K + q] : (act ? PAI[(size_t)eq * ldP + 1 + l * N + g.yidx[y]] : 0.0);
         } else if (k < g.KX + N) {
           v = invA[eq + (size_t)(k - g.KX) * N];
         }
@@ -182,13 +188,12 @@ __global__ __launch_bounds__(128) void k_girf(GirfDev g) {
       if (eq < N) {
         X[(size_t)(1 + nh * N + eq) * kGS + sim] = y;
         double yo = y;
-        if (g.bh)
+        if (g.bh) {
+          const double ya = y < g.elb ? g.elb : y;
           for (int q = 0; q < g.Ny; ++q)
-            if (g.yidx[q] == eq) {
-              const double ya = y < g.elb ? g.elb : y;
-              X[(size_t)(1 + Np + nh * g.Ny + q) * kGS + sim] = ya;
-              yo = ya;  // yields floored at the ELB in the output (:386-390)
-            }
+            if (g.yidx[q] == eq) X[(size_t)(1 + Np + nh * g.Ny + q) * kGS + sim] = ya;
+          if (g.yfloor[eq]) yo = ya;  // yields floored at the ELB in the output (:386-390)
+        }
         ybuf[eq * kGS + sim] = yo;
       }
     }
@@ -223,7 +228,8 @@ __global__ __launch_bounds__(128) void k_girf_fast(GirfDev g) {
   double* logsv = X + KR * kGS;              // [4][N]
   double* ybuf = logsv + 4 * N;              // [N][kGS]
   double* nrm = ybuf + N * kGS;              // [2][4][N]
-  const double* PAI = g.PAI + (size_t)mm * N * K;
+  const int ldP = g.ldP;
+  const double* PAI = g.PAI + (size_t)mm * N * ldP;
   const double* invA = g.invA + (size_t)mm * N * N;
   const double* sqP = g.sqrtPHI + (size_t)mm * N * N;
   const double* SV0 = g.SV0 + (size_t)mm * N;
@@ -232,7 +238,7 @@ __global__ __launch_bounds__(128) void k_girf_fast(GirfDev g) {
   double af[KS];
   {
     const int eq = 16 * et + (lane & 15);
-    const bool act = g.bh && eq < N && g.actual[eq];
+    const bool act = g.bh == 1 && eq < N && g.actual[eq];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int k = 4 * ks + lq;
@@ -241,17 +247,19 @@ __global__ __launch_bounds__(128) void k_girf_fast(GirfDev g) {
         if (k < LAGR) {
           const int l = k / N4, j = k - l * N4;
           if (j < N) {
-            v = PAI[(size_t)eq * K + 1 + l * N + j];
+            v = PAI[(size_t)eq * ldP + 1 + l * N + j];
             if (act)
               for (int y = 0; y < g.Ny; ++y) v = (g.yidx[y] == j) ? 0.0 : v;
           }
         } else if (k < SHR) {
           const int q = k - LAGR, l = q / NYD, jy = q - l * NYD;
-          if (jy < g.Ny && act) v = PAI[(size_t)eq * K + 1 + l * N + g.yidx[jy]];
+          if (jy < g.Ny)
+            v = (g.bh == 2) ? PAI[(size_t)eq * ldP + K + l * g.Ny + jy]
+                            : (act ? PAI[(size_t)eq * ldP + 1 + l * N + g.yidx[jy]] : 0.0);
         } else if (k < CR) {
           if (k - SHR < N) v = invA[eq + (size_t)(k - SHR) * N];
         } else if (k == CR) {
-          v = PAI[(size_t)eq * K];
+          v = PAI[(size_t)eq * ldP];
         }
       }
       af[ks] = v;
@@ -345,13 +353,12 @@ __global__ __launch_bounds__(128) void k_girf_fast(GirfDev g) {
       if (eq < N) {
         X[(size_t)(nh * N4 + eq) * kGS + sim] = y;
         double yo = y;
-        if (g.bh)
+        if (g.bh) {
+          const double ya = y < g.elb ? g.elb : y;
           for (int q = 0; q < g.Ny; ++q)
-            if (g.yidx[q] == eq) {
-              const double ya = y < g.elb ? g.elb : y;
-              X[(size_t)(LAGR + nh * NYD + q) * kGS + sim] = ya;
-              yo = ya;
-            }
+            if (g.yidx[q] == eq) X[(size_t)(LAGR + nh * NYD + q) * kGS + sim] = ya;
+          if (g.yfloor[eq]) yo = ya;
+        }
         ybuf[eq * kGS + sim] = yo;
       }
     }
@@ -397,6 +404,8 @@ hipError_t girf_launch(hipStream_t st, const GirfArgs& a) {
   g.M = a.M; g.N = a.N; g.p = a.p; g.H = a.H; g.nsim = a.nsim; g.bh = a.bh; g.Ny = a.bh ? a.Ny : 0;
   const int K = 1 + a.N * a.p;
   g.KX = K + g.Ny * a.p;
+  g.ldP = (a.bh == 2) ? g.KX : K;
+  g.yfloor = a.yfloor;
   g.KT = g.KX + a.N;
   g.nchunk = (a.nsim + 3) / 4;
   g.PAI = a.PAI; g.invA = a.invA; g.sqrtPHI = a.sqrtPHI; g.SV0 = a.SV0; g.Xj = a.Xj; g.ldX = a.ldX;
@@ -421,6 +430,7 @@ hipError_t girf_launch(hipStream_t st, const GirfArgs& a) {
     return hipGetLastError();
   };
   if (!a.force_generic && a.p == 12 && N4 == 20 && NY4 == 8) e = go_fast(k_girf_fast<12, 20, 8>);
+  else if (!a.force_generic && a.p == 12 && N4 == 20 && NY4 == 4) e = go_fast(k_girf_fast<12, 20, 4>);
   else if (!a.force_generic && a.p == 12 && N4 == 20 && NY4 == 0) e = go_fast(k_girf_fast<12, 20, 0>);
   else if (nks <= 32) e = go(k_girf<32>);
   else if (nks <= 64) e = go(k_girf<64>);

@@ -3,7 +3,8 @@
 //   G = X' diag(w) X + diag(iV_j)      (SYRK on v_mfma_f64_16x16x4_f64)
 //   L = chol(G)                        (right-looking, 16-wide panels, in registers)
 //
-// The lower triangle of G (KP = 16*NT <= 256, NT(NT+1)/2 tiles of 16 x 16) never
+// The lower triangle of G (16*NT <= 288, NT(NT+1)/2 tiles of 16 x 16; NT = 18 serves the hybrid
+// model's K = 277 inside a KP = 320 system buffer, the rows past 16*NT staying zero) never
 // leaves the register file: 8 waves, wave W owns tiles g = W + 8k of the
 // column-major enumeration of the lower tiles, one dbl4 MFMA accumulator per tile
 // (lane l holds G[ti*16 + (l>>4) + 4r][tj*16 + (l&15)], r = 0..3).  The body is
@@ -30,8 +31,10 @@ namespace ccmm {
 
 constexpr int kGcWaves = 8;
 constexpr int kGcTC = 16;     // t rows per SYRK chunk
-constexpr int kGcLdz = 272;   // LDS row stride (doubles) of a Z chunk: rows 32 banks apart
 constexpr int kGcLdp = 17;    // LDS row stride of a 16 x 16 panel tile
+// LDS row stride (doubles) of a Z chunk: 16 NT + 16, rows 32 banks apart (272 at NT = 16)
+__host__ __device__ constexpr int gc_ldz(int NT) { return 16 * NT + 16; }
+constexpr int kGcLdz = gc_ldz(16);
 
 // column-major enumeration of the lower tiles of an NT x NT tile grid
 __host__ __device__ constexpr int gc_tj(int NT, int g) {
@@ -75,8 +78,9 @@ __device__ __forceinline__ int gram_chol_body(const GcArgs& g, double* sm, int t
   for (int k = 0; k < TPW; ++k) acc[k] = dbl4{0.0, 0.0, 0.0, 0.0};
 
   // ------------------------------------------------------------ SYRK
+  constexpr int LDZ = gc_ldz(NT);
   double* Z0 = sm;
-  double* Z1 = sm + kGcTC * kGcLdz;
+  double* Z1 = sm + kGcTC * LDZ;
   constexpr int NLOAD = (kGcTC * 16 * NT + 511) / 512;
   const int nch = (g.mode & 1) ? 0 : (g.T + kGcTC - 1) / kGcTC;
   double vals[NLOAD];
@@ -94,7 +98,7 @@ __device__ __forceinline__ int gram_chol_body(const GcArgs& g, double* sm, int t
     for (int q = 0; q < NLOAD; ++q) {
       const int e = tid + 512 * q;
       const int t = e & 15, a = e >> 4;
-      if (a < 16 * NT) Z[t * kGcLdz + a] = vals[q];
+      if (a < 16 * NT) Z[t * LDZ + a] = vals[q];
     }
   };
   if (nch > 0) {
@@ -109,7 +113,7 @@ __device__ __forceinline__ int gram_chol_body(const GcArgs& g, double* sm, int t
     if (more) load_chunk(ch + 1);
 #pragma unroll
     for (int kk = 0; kk < kGcTC / 4; ++kk) {
-      const double* zr = Zc + (kk * 4 + lq) * kGcLdz + lr;
+      const double* zr = Zc + (kk * 4 + lq) * LDZ + lr;
       double frag[NT];
 #pragma unroll
       for (int b = 0; b < NT; ++b) frag[b] = zr[16 * b];

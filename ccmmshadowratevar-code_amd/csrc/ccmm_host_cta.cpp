@@ -18,6 +18,7 @@
 // R(k, k) < 0 in both and R is unique.  (Hence the QR draw equals the Cholesky draw with
 // z -> -z: same posterior, evaluated without squaring the condition number.)
 #include <cmath>
+#include <cstdint>
 #include <vector>
 
 namespace ccmm {
@@ -79,11 +80,19 @@ std::vector<double> qr_lower(std::vector<double>& M, int m, int n) {
 // Y(t, i) at Y[i * ldy + t]; equation i's design X_i(t, k) at Xs[i][k * ldx + t];
 // A column-major N x N (unit lower); sqrtht(t, i) at sqrtht[i * ldh + t];
 // iVdiag / iVb / PAI: row j = equation j, (j, k) at [j * ldk + k]; z(k, j) at z[k + K * j].
+// Aelb / atELB (CTAsysAswitching.m:61-92, optional): months t with atELB[t] != 0 use Aelb in
+// place of A in the residual map and the weights.
 // Returns bit 0: the QR branch ran for some equation; bit 1: a QR factor was singular.
 int host_cta_chain(int N, int K, int T, const double* Y, int ldy, const double* const* Xs, int ldx,
-                   const double* A, const double* sqrtht, int ldh, const double* iVdiag,
-                   const double* iVb, int ldk, double* PAI, const double* z, bool force_qr) {
+                   const double* A0, const double* sqrtht, int ldh, const double* iVdiag,
+                   const double* iVb, int ldk, double* PAI, const double* z, bool force_qr,
+                   const double* Aelb, const uint8_t* atELB) {
   int flags = 0;
+  const double* A = A0;
+  auto At = [&](int t) { return (Aelb && atELB && atELB[t]) ? Aelb : A0; };
+  if (Aelb)
+    for (int q = 0; q < N * N; ++q)
+      if (!std::isfinite(Aelb[q])) return 2;
   // a chain whose state is not finite is not redrawn (the QR branch cannot repair it)
   for (int i = 0; i < N; ++i)
     for (int t = 0; t < T; ++t)
@@ -106,7 +115,8 @@ int host_cta_chain(int N, int K, int T, const double* Y, int ldy, const double* 
     for (int t = 0; t < T; ++t) {
       const double dlt = col[t] - E[(size_t)i * T + t];
       E[(size_t)i * T + t] = col[t];
-      for (int r = i; r < N; ++r) EA[(size_t)r * T + t] += dlt * A[r + (size_t)i * N];
+      const double* Am = At(t);
+      for (int r = i; r < N; ++r) EA[(size_t)r * T + t] += dlt * Am[r + (size_t)i * N];
     }
   };
   for (int i = 0; i < N; ++i) set_col(i);
@@ -118,9 +128,10 @@ int host_cta_chain(int N, int K, int T, const double* Y, int ldy, const double* 
     // w2 and u(t) = sum_{i >= j} A(i, j) ytil_i(t) / lambda_i(t), ytil_i = EA(:, i) / lambda_i
     for (int t = 0; t < T; ++t) {
       double a = 0.0, b = 0.0;
+      const double* Am = At(t);
       for (int i = j; i < N; ++i) {
         const double lam = sqrtht[(size_t)i * ldh + t];
-        const double aij = A[i + (size_t)j * N];
+        const double aij = Am[i + (size_t)j * N];
         a += aij * aij / (lam * lam);
         b += aij * EA[(size_t)i * T + t] / (lam * lam);
       }

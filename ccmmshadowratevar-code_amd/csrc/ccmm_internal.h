@@ -115,6 +115,10 @@ struct ChainState {
   double* svw;       // [B][TP+1][N]
   double* Zphi;      // [B][N][TZ]  IW normals scratch
   int* status;       // [B]
+  // CTAsysAswitching (CTAsysAswitching.m:61-92): months with atELB[c][t] != 0 use the
+  // second A matrix Aelb in the CTA weights and residual map; nullptr = CTA / CTAsys
+  const double* Aelb;      // [B][N][N]
+  const uint8_t* atELB;    // [B][TP]
 };
 
 // ---------------------------------------------------------------- shared device helpers
@@ -202,6 +206,7 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
 // host CTA draw of one chain with the QR branch of CTA.m:80-92 (ccmm_host_cta.cpp)
 int host_cta_chain(int N, int K, int T, const double* Y, int ldy, const double* const* Xs, int ldx,
                    const double* A, const double* sqrtht, int ldh, const double* iVdiag,
-                   const double* iVb, int ldk, double* PAI, const double* z, bool force_qr);
+                   const double* iVb, int ldk, double* PAI, const double* z, bool force_qr,
+                   const double* Aelb = nullptr, const uint8_t* atELB = nullptr);
 
 }  // namespace ccmm

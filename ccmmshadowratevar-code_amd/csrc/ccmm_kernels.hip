@@ -102,7 +102,8 @@ __global__ void k_cta_weights(Dims d, const int* __restrict__ Tslot, ChainState 
   const int T = Tslot[cs.slot[c]];
   double w = 0.0;
   if (t < T) {
-    const double* A = cs.A + (size_t)c * d.N * d.N;
+    const bool elbm = cs.atELB && cs.atELB[(size_t)c * d.TP + t];  // CTAsysAswitching.m:68-80
+    const double* A = (elbm ? cs.Aelb : cs.A) + (size_t)c * d.N * d.N;
     const double* sh = cs.sqrtht + (size_t)c * d.N * d.TP;
     for (int i = j; i < d.N; ++i) {
       const double a = A[i + j * d.N] / sh[(size_t)i * d.TP + t];

@@ -14,7 +14,8 @@ struct LagSel {
   int ldd, rows, p;     // row stride (odd), rows per slab (TP + p), lag order
   int mode;             // timing-only ablation (CCMM_LAG_MODE, results invalid): gram 1 no SYRK,
                         // 2 no Cholesky, 4 no inverse; solve 16 no v, 32 no X'v, 64 no Linv
-                        // matvecs, 128 no X x
+                        // matvecs, 128 no X x.  gram 8: write the raw SYRK stage (Gram tiles,
+                        // b, c) and stop (ccmm_chains_get_cta_gram, parity tests)
 };
 
 constexpr int kGlWaves = 8;

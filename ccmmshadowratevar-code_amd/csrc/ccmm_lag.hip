@@ -199,6 +199,23 @@ __device__ __forceinline__ int gram_lag_factor(const GlArgs& g, double* sm, int 
     sti[k] = gi < NTILE ? gl_ti(NT, gi) : 0;
     stj[k] = gi < NTILE ? gl_tj(NT, gi) : 0;
   }
+  if (g.mode & 8) {  // parity export (ccmm_chains_get_cta_gram): the SYRK stage as it stands
+    double* o = g.out;
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) {
+      const int gi = W + kGlWaves * k;
+      if (gi < NTILE) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[gi * 256 + 64 * r + lane] = acc[k][r];
+      }
+    }
+    if (lq == 0) {
+      if (W < NT) o[NTILE * 256 + 1 + 16 * W + lr] = bs0;
+      if (W + kGlWaves < NT) o[NTILE * 256 + 1 + 16 * (W + kGlWaves) + lr] = bs1;
+    }
+    if (W == 0 && lane == 0) o[NTILE * 256] = csum;
+    return 0;
+  }
   __syncthreads();  // D no longer needed: the LDS is reused below
 
   double* lvec = sm;              // KL   b, then l = b / L00

@@ -6,7 +6,7 @@
 ``goVAR*`` parfor over vintages/chains becomes one GPU launch sequence).
 ``mcmcVARshadowrateBlockHybrid`` mirrors the block-hybrid shadow-rate sampler
 (outputs 1-13: draws and the predictive density).  ``goVARshadowrateBlockHybrid_batch``
-is the quasi-real-time OOS run over all vintages as one device batch per GPU.  ``CTA``/``CTAsys``/``drawTruncNormal`` mirror the L2 functions.
+is the quasi-real-time OOS run over all vintages as one device batch per GPU.  ``CTA``/``CTAsys``/``CTAsysAswitching``/``drawTruncNormal`` mirror the L2 functions.
 
 Every numerical step goes through ``libccmm.so``; there is no CPU fallback.
 """
@@ -293,7 +293,10 @@ def mcmcVARhybridGibbs(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateWeigh
                        gibbsburn=100, Nproposals=1000, elb_ps=True, stats=None):
     """mcmcVARhybridGibbs.m:1-14, outputs PAI_all (M x K x N, K = 1 + N p + Ns p),
     PHI_all, invA_all, sqrtht_all, shadowrate_all (M x Nshadowrates x elbT),
-    missingrate_all (NaN: it is the first PS proposal, :486).
+    missingrate_all (NaN: it is the first PS proposal, :486); with fcstNdraws the predictive
+    density of every kept draw simulated on the device (:566-635) and outputs 7-13 (:703-751):
+    fcstYdraws (yields floored at the ELB), fcstYhat, fcstShadowrateDraws, fcstShadowrateHat,
+    fcstLogscoreDraws, fcstLogscoreXdraws, fcstLogscoreIdraws.
 
     The shadow rates are drawn by accept-first PS proposals at every sweep with the Gibbs
     sampler as fallback (:458-483), the proposal sampler restated from the absent
@@ -306,8 +309,14 @@ def mcmcVARhybridGibbs(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateWeigh
         raise NotImplementedError("doELBsampling=false / doELBsampleAlternate=true need the "
                                   "missing-data sampler VARTVPSVprecisionsamplerNaN (absent "
                                   "em-matlabbox); out of scope")
-    if fcstNdraws or IRF1scale is not None:
-        raise NotImplementedError("predictive density / IRF outputs are a later row (SURVEY §8f)")
+    if IRF1scale is not None:
+        raise NotImplementedError("in-sampler IRF outputs: use samplers.generateGIRF(hybrid=True)")
+    doPredictiveDensity = bool(fcstNdraws)
+    if doPredictiveDensity:
+        if fcstNdraws % MCMCdraws:
+            raise ValueError("fcstNdraws must be multiple of MCMCdraws")
+        if yrealized is None or fcstNhorizons is None:
+            raise ValueError("predictive density needs yrealized and fcstNhorizons")
     hm = build_hybrid(thisT, p, np_, data0, ydates0, ndxSHADOWRATE, minnesotaPriorMean, ELBbound,
                       elbT0, doRATSprior)
     if hm.warn_elbT0:
@@ -324,6 +333,14 @@ def mcmcVARhybridGibbs(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateWeigh
     ch.set_elb_slot(0, hm.elbT0, hm.sNaN)
     if elb_ps and Nproposals:
         ch.set_elb_ps(Nproposals, 1)                   # every sweep (:458)
+    N = m.N
+    ndxYIELDS = np.union1d(hm.ndxS, np.asarray(ndxOTHERYIELDS, int))
+    if doPredictiveDensity:
+        H, Nd = int(fcstNhorizons), fcstNdraws // MCMCdraws
+        yields = np.zeros(N, bool)
+        yields[ndxYIELDS] = True
+        ch.set_fcst(H, Nd, yields, keep_paths=True)
+        ch.set_fcst_slot(0, np.asarray(yrealized, float).reshape(N, -1, order="F")[:, 0])
     st = initial_state(m, B)
     ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
     _run_chain_set(ch, burn, MCMCdraws, doprogress)
@@ -331,11 +348,18 @@ def mcmcVARhybridGibbs(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateWeigh
         ps = ch.get_ps()
         stats.update(countELBaccept=ps["countAccept"] + ps["countAcceptBurnin"],
                      stackAccept=ps["stackAccept"])
+    fc = ch.get_fcst(paths=True) if doPredictiveDensity else None
     out = ch.get_draws()
     ch.close()
     sr = out.get("shadowrate_all", np.full((MCMCdraws, len(hm.ndxS), 0, B), np.nan))
     res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"], sr,
            np.full((MCMCdraws, len(hm.ndxS), hm.elbT, B), np.nan)]
+    if doPredictiveDensity:
+        fYu = fc["paths"].reshape(N, H, fcstNdraws, B, order="F")          # uncensored simulation
+        fSd = fYu[ndxYIELDS].copy()                                         # fcstShadowrateDraws (:704)
+        fYd = fc["paths_censored"].reshape(N, H, fcstNdraws, B, order="F")  # yields floored (:707-711)
+        sc = [fc["scores"][:, :, k, :].reshape(fcstNdraws, B, order="F") for k in (1, 2, 3)]
+        res += [fYd, fYd.mean(axis=2), fSd, fSd.mean(axis=2), sc[0], sc[1], sc[2]]
     if B == 1:
         res = [a[..., 0] for a in res]
     return tuple(res)
@@ -361,6 +385,19 @@ def CTAsys(Y, X, N, K, T, A_, sqrtht, iV, iVb_prior, PAI, rndStream=None, *, dev
                                  np.asarray(iVb_prior).reshape(K, N, order="F"),
                                  np.asarray(PAI)[..., None],
                                  None if rndStream is None else np.asarray(rndStream)[..., None])
+    return out[..., 0]
+
+
+def CTAsysAswitching(Y, X, N, K, T, A_, Aelb_, atELB, sqrtht, iV, iVb_prior, PAI, rndStream=None, *, device=0):
+    """CTAsysAswitching.m:1 signature (the Aelb model's coefficient block): X is T x K x N, the
+    months with atELB true use Aelb_ instead of A_ (CTAsysAswitching.m:61-80)."""
+    iVd = np.diag(iV) if np.ndim(iV) == 2 else np.asarray(iV)
+    out, _ = context(device).cta_aswitching(Y, X, np.asarray(A_)[..., None], np.asarray(Aelb_)[..., None],
+                                            atELB, np.asarray(sqrtht)[..., None],
+                                            iVd.reshape(K, N, order="F"),
+                                            np.asarray(iVb_prior).reshape(K, N, order="F"),
+                                            np.asarray(PAI)[..., None],
+                                            None if rndStream is None else np.asarray(rndStream)[..., None])
     return out[..., 0]
 
 
@@ -539,20 +576,24 @@ def matlab_prctile(x, pct, axis=0):
 
 
 def _bh_units(data0, ydates0, Tjumpoffs, p, np_, ndxSHADOWRATE, ndxOTHERYIELDS,
-              minnesotaPriorMean, ELBbound, elbT0, doRATSprior, fcstNhorizons):
-    """Host setup of every vintage (mcmcVARshadowrateBlockHybrid.m:30-295) and its
-    yrealized (goVARshadowrateBlockHybrid.m:267-283)."""
+              minnesotaPriorMean, ELBbound, elbT0, doRATSprior, fcstNhorizons, model="blockhybrid"):
+    """Host setup of every vintage (mcmcVARshadowrateBlockHybrid.m:30-295; model="hybrid":
+    mcmcVARhybridGibbs.m:33-339) and its yrealized (goVARshadowrateBlockHybrid.m:267-283)."""
     out = []
     for thisT in Tjumpoffs:
-        bm = build_bh(int(thisT), p, np_, data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS,
-                      minnesotaPriorMean, ELBbound, elbT0, doRATSprior)
+        if model == "hybrid":
+            bm = build_hybrid(int(thisT), p, np_, data0, ydates0, ndxSHADOWRATE, minnesotaPriorMean,
+                              ELBbound, elbT0, doRATSprior)
+        else:
+            bm = build_bh(int(thisT), p, np_, data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS,
+                          minnesotaPriorMean, ELBbound, elbT0, doRATSprior)
         yr = realized_values(data0, int(thisT), fcstNhorizons, ndxSHADOWRATE, ELBbound)
         out.append((int(thisT), bm, yr))
     return out
 
 
 def _bh_chain_set(ctx, units, C, *, seed, ids, store_capacity, gibbsburn, ELBbound, ndxYIELDS,
-                  fcstNhorizons=None, Nd=None, keep_paths=False):
+                  fcstNhorizons=None, Nd=None, keep_paths=False, model="blockhybrid"):
     """One device-resident chain set holding every unit (vintage) as a data slot with C
     chains each (the parfor over vintages as one batch), reference initialisation per
     chain (:308-317), predictive density on every stored sweep."""
@@ -561,13 +602,15 @@ def _bh_chain_set(ctx, units, C, *, seed, ids, store_capacity, gibbsburn, ELBbou
     Tmax = max(u[1].var.T for u in units)
     elbTmax = max(max(u[1].elbT for u in units), 1)
     B = C * len(units)
+    hybrid = model == "hybrid"
     ch = _abi.Chains(ctx, N=N, p=p, T=Tmax, B=B, ndata=len(units), crn=False,
-                     store_capacity=store_capacity, seed=int(seed), model=_abi.MODEL_BLOCKHYBRID,
+                     store_capacity=store_capacity, seed=int(seed),
+                     model=_abi.MODEL_HYBRID if hybrid else _abi.MODEL_BLOCKHYBRID,
                      Ns=len(bm0.ndxS), elbTmax=elbTmax, elb_gibbsburn=gibbsburn, elb=ELBbound)
     for s, (_, bm, _) in enumerate(units):
         m = bm.var
         ch.set_data(s, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
-    ch.set_elb_model(bm0.ndxS, bm0.actual_block)
+    ch.set_elb_model(bm0.ndxS, None if hybrid else bm0.actual_block)
     yields = np.zeros(N, bool)
     yields[np.asarray(ndxYIELDS, int)] = True
     if fcstNhorizons:
@@ -601,7 +644,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                                      gibbsburn=100, rndStream=1012023, dist=None, device=None,
                                      chunk=50, max_retries=2, keep_draws=False, progress=False,
                                      Nproposals=1000, elb_ps=True, postprocess=False, cumcode=None,
-                                     setQuantiles=None, maxlambda=False):
+                                     setQuantiles=None, maxlambda=False, model="blockhybrid"):
     """The quasi-real-time OOS run of goVARshadowrateBlockHybrid.m:126-517 for the block-
     hybrid shadow-rate VAR, as ONE device-resident chain set per rank: every vintage
     thisT in Tjumpoffs (default: ydates > 2008-12, :127) is a data slot of the set with
@@ -634,7 +677,11 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
     cumulated forms fcstYcum* (cumsum over horizons for ``cumcode``), fcstShadowYmedian /
     fcstShadowYquantiles, PAImedian / PAIquantiles, the score draws fcstYmvlogscore*Draws;
     setQuantiles default goVARshadowrateBlockHybrid.m:141.  maxlambda=True adds
-    drawsMaxVARroot (max |eig| of each draw's companion matrix, :382-392, host LAPACK)."""
+    drawsMaxVARroot (max |eig| of each draw's companion matrix, :382-392, host LAPACK).
+
+    model="hybrid" runs goVARhybrid.m instead (goVARhybrid_batch): mcmcVARhybridGibbs per
+    vintage (K = N p + 1 + Ns p, PS proposals at every sweep, :458), modellabel ELBhybrid; the
+    max-root block is commented out in that driver (:383-430), so maxlambda is refused."""
     import time
     from . import distributed as dm
     data0 = np.asarray(data0, float)
@@ -660,14 +707,18 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
     rank = dist.get_rank() if dist is not None else 0
     size = dist.get_world_size() if dist is not None else 1
     device = _rank_device(dist, device)
-    K = N * p + 1
+    hybrid = model == "hybrid"
+    if hybrid and maxlambda:
+        raise ValueError("goVARhybrid.m computes no max VAR roots (:383-430 commented out)")
+    K = N * p + 1 + (ndxSHADOWRATE.size * p if hybrid else 0)
     costs = [dm.unit_cost(t - p, K, N, n_cens=dm.censored_months(data0, ndxSHADOWRATE, ELBbound, startELB, t)) * C
              for t in Tjumpoffs]
     assignment = dm.lpt_assign(costs, size)
     mine = assignment[rank]
     t0 = time.perf_counter()
     units = _bh_units(data0, ydates0, [Tjumpoffs[v] for v in mine], p, np_, ndxSHADOWRATE,
-                      ndxOTHERYIELDS, minnesotaPriorMean, ELBbound, elbT0, doRATSprior, H) if mine else []
+                      ndxOTHERYIELDS, minnesotaPriorMean, ELBbound, elbT0, doRATSprior, H,
+                      model=model) if mine else []
     t_setup = time.perf_counter() - t0
     ctx = context(device)
     Ns = ndxSHADOWRATE.size
@@ -688,9 +739,10 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                                           store_capacity=MCMCdraws if postprocess else chunk,
                                           gibbsburn=gibbsburn, ELBbound=ELBbound,
                                           ndxYIELDS=ndxYIELDS, fcstNhorizons=H, Nd=Nd,
-                                          keep_paths=postprocess)
+                                          keep_paths=postprocess, model=model)
         if elb_ps and Nproposals and ch.elbTmax:
-            ch.set_elb_ps(Nproposals, max(1, -(-burn // 2)))  # m >= MCMCburnin * .5 (:435)
+            # block hybrid: m >= MCMCburnin * .5 (:435); hybrid: every sweep (mcmcVARhybridGibbs.m:458)
+            ch.set_elb_ps(Nproposals, 1 if hybrid else max(1, -(-burn // 2)))
         B = ch.B
         done = 0
         while done < burn:
@@ -698,7 +750,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
             ch.sweep(n, store=False)
             done += n
             if progress:
-                print(f"[rank {rank}] burn-in {done}/{burn}", flush=True)
+                print(f"[rank {rank}] burn-in {done}/{burn} ({time.perf_counter() - t1:.1f} s)", flush=True)
         scores = np.empty((Nd, MCMCdraws, 4, B))
         fYsum = np.zeros((N, H, B))
         fYcsum = np.zeros((N, H, B))
@@ -727,7 +779,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                     PAIdraws[done:done + n] = P
             done += n
             if progress:
-                print(f"[rank {rank}] kept {done}/{MCMCdraws}", flush=True)
+                print(f"[rank {rank}] kept {done}/{MCMCdraws} ({time.perf_counter() - t1:.1f} s)", flush=True)
         if postprocess:
             # goVARshadowrateBlockHybrid.m:349-480 on the device, per vintage (data slot)
             for k, i in enumerate(vidx):
@@ -740,6 +792,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                 sh = ch.summaries(0, k, rows=yields, pct=pct)                   # shadowratedraws
                 pa = ch.summaries(2, k, pct=pct)                                # PAI_all
                 post[i] = dict(yd=yd, yc=yc, sh=sh, pa=pa, ycr=ycr)
+                if progress and (k % 8 == 7 or k == len(vidx) - 1):
+                    print(f"[rank {rank}] device summaries {k + 1}/{len(vidx)} vintages", flush=True)
             fc = ch.get_fcst()
             scores[:] = fc["scores"]
             fYsum[:] = fc["fYsum"]
@@ -810,6 +864,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                 if maxlambda:
                     r["drawsMaxVARroot"] = max_var_roots(np.moveaxis(P, 3, 1).reshape(-1, K, N), N, p)
             res[mine[i]] = r
+            if progress and (k % 4 == 3 or k == len(vidx) - 1):
+                print(f"[rank {rank}] results {k + 1}/{len(vidx)} vintages", flush=True)
         return res, failed
 
     t1 = time.perf_counter()
@@ -902,6 +958,14 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
     return out
 
 
+def goVARhybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS, minnesotaPriorMean, **kw):
+    """goVARhybrid.m (the quasi-real-time OOS run of the hybrid shadow-rate VAR,
+    mcmcVARhybridGibbs per vintage, parfor at :258) as one device-resident chain set per rank;
+    same arguments and outputs as goVARshadowrateBlockHybrid_batch (PAI* over K = N p + 1 + Ns p)."""
+    return goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS, minnesotaPriorMean,
+                                            model="hybrid", **kw)
+
+
 # ---------------------------------------------------------------------------------------
 # Generalized impulse responses (generateGIRF2linear.m / generateGIRF2blockhybrid.m)
 
@@ -916,8 +980,10 @@ def _ivech(v, N):
 def generateGIRF(data, ydates, irfDate, PAI_all, invA_all, PHI_all, sqrtht_all, *, p=12, np_=12,
                  cumcode=None, shock11=1.0, irfNdraws=1000, irfHorizon=120, blockhybrid=False,
                  ndxSHADOWRATE=None, ndxOTHERYIELDS=None, ELBbound=0.25, shadowrate_all=None,
-                 elbT0=None, seed=1012023, device=0):
-    """The GIRF simulation of generateGIRF2linear.m / generateGIRF2blockhybrid.m:176-283 for
+                 elbT0=None, seed=1012023, device=0, hybrid=False):
+    """The GIRF simulation of generateGIRF2linear.m / generateGIRF2blockhybrid.m:176-283 /
+    generateGIRF2hybrid.m:168-275 (hybrid=True: PAI_all M x (K + Ns p) x N, the actual-rate
+    lags of the Ns shadow-rate variables in the state, simVARhybrid) for
     one irfDate and shock scale (shock11 = IRF1scale * shocksize) over the M kept draws,
     on the device (ccmm_girf): returns fcstYhat / fcstYhat1plus / fcstYhat1minus (medians over
     the draws of the simulated mean paths), IRF1plus / IRF1minus (medians of +shock - base and
@@ -926,34 +992,50 @@ def generateGIRF(data, ydates, irfDate, PAI_all, invA_all, PHI_all, sqrtht_all, 
     p+1..), shadowrate_all M x Ns x elbT (block hybrid); indices 0-based."""
     data = np.asarray(data, float)
     ydates = np.asarray(ydates, float)
-    M, K, N = PAI_all.shape
+    M, Kx, N = PAI_all.shape
+    K = 1 + N * p
     t0 = int(np.flatnonzero(ydates == irfDate)[0])               # ndxIRFT0 - 1 (0-based)
     cum = np.zeros(N, bool) if cumcode is None else np.asarray(cumcode, bool)
-    if blockhybrid:
+    shadow = None
+    if hybrid:                                                    # generateGIRF2hybrid.m:64-75
+        yields = np.zeros(N, bool)
+        yields[np.union1d(ndxSHADOWRATE, ndxOTHERYIELDS)] = True
+        yidx = np.asarray(ndxSHADOWRATE, int)                     # the actual-rate ring
+        shadow = np.zeros(N, bool)
+        shadow[yidx] = True
+        actual = None
+        ns = K + yidx.size * p
+        if Kx != ns:
+            raise ValueError("hybrid PAI_all must have K + Nshadowrates p rows")
+        blockhybrid_ring = True
+    elif blockhybrid:
         yidx = np.union1d(ndxSHADOWRATE, ndxOTHERYIELDS)
         yields = np.zeros(N, bool)
         yields[yidx] = True
         actual = ~yields
         ns = K + yidx.size * p
+        blockhybrid_ring = True
     else:
         yields = actual = None
         ns = K
+        blockhybrid_ring = False
     Xj = np.zeros((ns, M))
     for mm in range(M):
         thisData = data[:t0 + 1].copy()                           # jumpoffData (:198-201)
-        if blockhybrid and shadowrate_all is not None and t0 + 1 - elbT0 - p > 0:
+        if blockhybrid_ring and shadowrate_all is not None and t0 + 1 - elbT0 - p > 0:
             n = t0 + 1 - elbT0 - p                                # (:166-172, 207-209)
             thisData[p + elbT0:t0 + 1, ndxSHADOWRATE] = shadowrate_all[mm, :, :n].T
         Xj[0, mm] = 1.0
         for l in range(p):
             Xj[1 + l * N:1 + (l + 1) * N, mm] = thisData[t0 - l, :N]
-            if blockhybrid:                                       # (:215-218)
+            if blockhybrid_ring:                                  # (:215-218; hybrid :211-214)
                 Xj[K + l * yidx.size:K + (l + 1) * yidx.size, mm] = thisData[t0 - l, yidx]
     SV0 = np.asarray(sqrtht_all, float)[:, t0 - p, :].T          # SVjumpoffDraws (:164)
     sqrtPHI = np.stack([np.linalg.cholesky(_ivech(PHI_all[m], N)) for m in range(M)], -1)
     out = context(device).girf(np.moveaxis(PAI_all, 0, -1), np.moveaxis(invA_all, 0, -1), sqrtPHI, SV0,
                                Xj, irfHorizon, irfNdraws, shock11, bh=blockhybrid, actual=actual,
-                               ndxYields=yields, elb=ELBbound, cumcode=cum, np_=np_, seed=seed)
+                               ndxYields=yields, elb=ELBbound, cumcode=cum, np_=np_, seed=seed,
+                               hybrid=hybrid, ndxShadow=shadow, p=p)
     base, plus, minus = out[:, :, 0, :], out[:, :, 1, :], out[:, :, 2, :]
     prc70 = np.array([_normcdf(-1), _normcdf(1)]) * 100
     ctx = context(device)

@@ -105,6 +105,19 @@ int ccmm_cta(ccmm_ctx* ctx, int B, int T, int N, int K,
              const double* iVdiag, const double* iVb,
              double* PAI, const double* z, int* status);
 
+/* CTAsysAswitching.m:1-123 (the Aelb shadow-rate model's coefficient block): as ccmm_cta with
+ * CTAsys designs, but the months with atELB[t] != 0 use the second A matrix Aelb in the residual
+ * map and the weights (CTAsysAswitching.m:61-80: kron(Aelb_(j:N,j), XatELB) stacked over
+ * kron(A_(j:N,j), XawayELB)).  Aelb N x N x B, atELB T bytes (logical, shared by the chains).
+ * The QR branch (:82-93) is the host fallback of ccmm_cta with the same two-matrix map.
+ * Supports N <= 32, K <= 256. */
+int ccmm_cta_aswitching(ccmm_ctx* ctx, int B, int T, int N, int K,
+                        const double* Y, int y_per_chain,
+                        const double* X, int nx, int x_per_chain,
+                        const double* A, const double* Aelb, const uint8_t* atELB,
+                        const double* sqrtht, const double* iVdiag, const double* iVb,
+                        double* PAI, const double* z, int* status);
+
 /* A-matrix draw, flat prior (mcmcVAR.m:236-254 == mcmcVARshadowrateBlockHybrid.m:354-372).
  *   RESID T x N x B, sqrtht T x N x B, z (N(N-1)/2) x B or NULL
  *   A out N x N x B (unit lower), invA out N x N x B (A_\I, mcmcVAR.m:254) */
@@ -317,6 +330,11 @@ int ccmm_chains_set_elb_ps(ccmm_chains* ch, int nproposals, int ps_from_m);
  * (ndxAccept of each stored draw, 0 = no proposal accepted or Gibbs sweep; M = stored draws;
  * call before ccmm_chains_get_draws, which resets the store).  Any pointer may be NULL. */
 int ccmm_chains_get_ps(ccmm_chains* ch, int* countAccept, int* countAcceptBurnin, int* stackAccept);
+/* Parity diagnostic: the device's weighted Gram of every CTA system at the chain set's current
+ * state (A, sqrtht, X), K x K x N x B: [c b'; b M] with c = sum_t w_t, b = X~' w, M = X~' diag(w) X~
+ * (CTA.m:73 without the prior), exactly as the lag-structured coefficient kernel forms it before
+ * the factorisation.  Only when that path is active (linear / block-hybrid models, N <= 32). */
+int ccmm_chains_get_cta_gram(ccmm_chains* ch, double* G);
 /* Current shadow rates, Ns x elbTmax x B (the last sweep's draw). */
 int ccmm_chains_get_shadowrate(ccmm_chains* ch, double* shadowrate);
 /* Current per-chain data: X T x K x B, Y T x N x B (block-hybrid: the chain's
@@ -369,6 +387,17 @@ int ccmm_girf(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const double*
               const double* sqrtPHI, const double* SV0, const double* Xjumpoff, int bh, const uint8_t* actual,
               const uint8_t* ndxYields, double elb, const uint8_t* cumcode, double np_, double shock11,
               const double* z, const double* svz, uint64_t seed, double* yhat);
+
+/* generateGIRF2hybrid.m:176-259 (simVARhybrid, :361-386): the hybrid model's GIRFs.  The state
+ * holds [1, p lags of y, p lags of the Ns actual (shadow-rate) variables]; the companion rows are
+ * the full hybrid PAI (:226-227: fcstA(ndxfcstY,:) = PAIdraws), the actual-rate states are
+ * max(shadow, ELB) (:373-375) and the output floors ndxYields (:378-381).
+ *   PAI (K + Ns p) x N x M (K = N p + 1), Xjumpoff (K + Ns p) x M, ndxShadow / ndxYields N bytes;
+ *   the rest as ccmm_girf. */
+int ccmm_girf_hybrid(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const double* PAI, const double* invA,
+                     const double* sqrtPHI, const double* SV0, const double* Xjumpoff, const uint8_t* ndxShadow,
+                     const uint8_t* ndxYields, double elb, const uint8_t* cumcode, double np_, double shock11,
+                     const double* z, const double* svz, uint64_t seed, double* yhat);
 
 /* ------------------------------------------------------------ diagnostics */
 

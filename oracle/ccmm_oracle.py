@@ -276,6 +276,32 @@ def cta_sys(Y, XX, N, K, T, A, sqrtht, iVdiag, iVb, PAI, z, return_sd=False, for
     return PAI, status
 
 
+def cta_sys_aswitching(Y, XX, N, K, T, A, Aelb, atELB, sqrtht, iVdiag, iVb, PAI, z, return_sd=False,
+                       force_qr=False):
+    """CTAsysAswitching.m:57-110 as written: per equation the kron-materialised designs of the
+    months at the ELB (Aelb) stacked over those away from it (A), explicit inverse."""
+    PAI = np.array(PAI, dtype=float, copy=True)
+    at = np.asarray(atELB, bool)
+    sd = np.zeros((K, N))
+    status = 0
+    for j in range(N):
+        XPAI = np.empty((T, N))
+        for jj in range(N):
+            XPAI[:, jj] = 0.0 if jj == j else XX[:, :, jj] @ PAI[:, jj]
+        lam_at = sqrtht[at, j:].ravel(order="F")
+        lam_aw = sqrtht[~at, j:].ravel(order="F")
+        YX = Y - XPAI
+        Yj = np.concatenate([(YX[at] @ Aelb[j:, :].T).ravel(order="F") / lam_at,
+                             (YX[~at] @ A[j:, :].T).ravel(order="F") / lam_aw])
+        Xj = np.vstack([np.kron(Aelb[j:, j][:, None], XX[at, :, j]) / lam_at[:, None],
+                        np.kron(A[j:, j][:, None], XX[~at, :, j]) / lam_aw[:, None]])
+        PAI[:, j], s, sd[:, j] = _cta_post(Xj, Yj, iVdiag[:, j], iVb[:, j], z[:, j], K, force_qr)
+        status |= s
+    if return_sd:
+        return PAI, status, sd
+    return PAI, status
+
+
 def cta_syrk(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z):
     """CTA.m:57-98 in the algorithmic form the device uses: per equation
     the weighted Gram X' diag(w) X + diag(iV_j) (no kron materialisation), Cholesky and
@@ -576,12 +602,17 @@ def vech_lower(M):
 # One linear BVAR-SV sweep (mcmcVAR.m:211-274)
 # --------------------------------------------------------------------------
 def linear_sweep(st, su: Setup, crn, cta_form="kron", force_qr=False):
-    """cta_form: "kron" = CTA.m as written; "syrk" = the algorithmic form (cta_syrk).
+    """cta_form: "kron" = CTA.m as written; "syrk" = the algorithmic form (cta_syrk); "mirror" =
+    the device's operation order up to the factorisation (oracle/cta_mirror.py).
     force_qr: every equation takes CTA.m's QR branch (kron form only)."""
     N, K, T = su.N, su.K, su.T
     if cta_form == "kron":
         PAI, status = cta(su.Y, su.X, N, K, st["A"], st["sqrtht"], su.iVdiag, su.iVb, st["PAI"],
                           crn["zPAI"], force_qr=force_qr)
+    elif cta_form == "mirror":
+        from . import cta_mirror
+        PAI = cta_mirror.cta(su.Y, su.X, N, K, st["A"], st["sqrtht"], su.iVdiag, su.iVb, st["PAI"], crn["zPAI"])
+        status = 0
     else:
         PAI, status = cta_syrk(su.Y, su.X, N, K, st["A"], st["sqrtht"], su.iVdiag, su.iVb,
                                st["PAI"], crn["zPAI"])

@@ -258,3 +258,73 @@ def fcst_draw_bh(PAI, invA, logSV0, sqrtPHI, Xjumpoff, yrealized, ndxYields, act
             x = xd
             x[ndxfcstActual] = np.maximum(x[ndxfcstShadow], elb)
     return fY, scores
+
+
+def hybrid_jumpoff(Y, data, p, ndxSHADOWRATE, elb):
+    """Xjumpoff of mcmcVARhybridGibbs.m:111-121, 531-536 (Nstates = Kshadow + Ns p):
+    [1, Y(end), ..., Y(end-p+1)] of the chain's (shadow-rate) Y, then
+    XjumpoffActualYieldLags = data(Nobs-(l-1), ndxSHADOWRATE) floored at the ELB."""
+    T, N = Y.shape
+    s = np.asarray(ndxSHADOWRATE, int)
+    x = [np.ones(1)] + [Y[T - l] for l in range(1, p + 1)]
+    x += [np.maximum(data[data.shape[0] - l, s], elb) for l in range(1, p + 1)]
+    return np.concatenate(x)
+
+
+def fcst_draw_hybrid(PAI, invA, logSV0, sqrtPHI, Xjumpoff, yrealized, ndxYields, ndxSHADOWRATE, elb, svz, z):
+    """One kept draw of mcmcVARhybridGibbs.m:566-635 as written: the dense companion on
+    Nstates = Kshadow + Ns p states (:160-172) with fcstA(ndxfcstY, :) = PAI' (:587), the
+    simulation with the actual-rate states max(shadow, ELB) (:623-635) and the one-step scores
+    (:590-620).  PAI (Kshadow + Ns p) x N.  Returns fcstY N x H x Nd (uncensored; the yields
+    are floored afterwards, :707-711) and scores 3 x Nd = (fcstLogscoreDraws,
+    fcstLogscoreXdraws, fcstLogscoreIdraws)."""
+    Kx, N = PAI.shape
+    s = np.asarray(ndxSHADOWRATE, int)
+    Ns = s.size
+    p = (Kx - 1) // (N + Ns)
+    K = 1 + N * p
+    H, Nd = z.shape[1], z.shape[2]
+    ndxYields = np.asarray(ndxYields, bool)
+    Nstates = K + Ns * p
+    fcstA = np.zeros((Nstates, Nstates))
+    fcstA[0, 0] = 1.0
+    fcstA[1 + N:K, 1:K - N] = np.eye(N * (p - 1))
+    fcstA[K + Ns:, K:K + Ns * (p - 1)] = np.eye(Ns * (p - 1))
+    ndxfcstActual = K + np.arange(Ns)
+    ndxfcstShadow = 1 + s
+    ndxfcstY = 1 + np.arange(N)
+    fcstB = np.zeros((Nstates, N))
+    fcstB[ndxfcstY, :] = np.eye(N)
+    fcstA[ndxfcstY, :] = PAI.T
+    logSVshocks = (sqrtPHI @ svz).reshape(N, H, Nd, order="F")
+    logSV = logSV0[:, None, None] + np.cumsum(logSVshocks, axis=1)
+    fcstSVdraws = np.exp(logSV * 0.5)
+    nushocks = fcstSVdraws * z
+    ndxYx = ~ndxYields
+    yNatELB = int(np.sum(yrealized[ndxYields] <= elb))
+    fY = np.empty((N, H, Nd))
+    scores = np.empty((3, Nd))
+    for nn in range(Nd):
+        muY = (fcstA @ Xjumpoff)[ndxfcstY]
+        sqrtOmegaY = invA @ np.diag(fcstSVdraws[:, 0, nn])
+        if yNatELB > 0:
+            scores[0, nn] = logscore_gaussian_censored(muY, sqrtOmegaY, yrealized, elb, ndxYields)
+        else:
+            scores[0, nn] = logscore_gaussian(muY, sqrtOmegaY, yrealized, np.sum(logSV[:, 0, nn]))
+        Sx = sqrtOmegaY[ndxYx, :]
+        Lx = np.linalg.cholesky(Sx @ Sx.T)
+        scores[1, nn] = logscore_gaussian(muY[ndxYx], Lx, yrealized[ndxYx], 2 * np.sum(np.log(np.diag(Lx))))
+        Si = sqrtOmegaY[ndxYields, :]
+        Li = np.linalg.cholesky(Si @ Si.T)
+        if yNatELB > 0:
+            scores[2, nn] = logscore_gaussian_censored(muY[ndxYields], Li, yrealized[ndxYields], elb)
+        else:
+            scores[2, nn] = logscore_gaussian(muY[ndxYields], Li, yrealized[ndxYields])
+        x = Xjumpoff.copy()
+        theseShocks = invA @ nushocks[:, :, nn]
+        for hh in range(H):
+            xd = fcstA @ x + fcstB @ theseShocks[:, hh]
+            fY[:, hh, nn] = xd[ndxfcstY]
+            x = xd
+            x[ndxfcstActual] = np.maximum(x[ndxfcstShadow], elb)
+    return fY, scores

@@ -14,6 +14,20 @@ from __future__ import annotations
 import numpy as np
 
 
+def companion_hybrid(PAI, N, p, shadow):
+    """fcstA of generateGIRF2hybrid.m:178-185, 226-227: Nstates = K + p Ns, the companion rows
+    are the hybrid PAI itself ((K + Ns p) x N), a shift for the Ns actual-rate lags."""
+    K = 1 + N * p
+    Ns = int(np.count_nonzero(shadow))
+    ns = K + p * Ns
+    A = np.zeros((ns, ns))
+    A[0, 0] = 1.0
+    A[1 + N:K, 1:K - N] = np.eye(N * (p - 1))
+    A[K + Ns:, K:ns - Ns] = np.eye(Ns * (p - 1))
+    A[1:1 + N, :] = PAI.T
+    return A
+
+
 def companion(PAI, N, p, bh=False, actual=None, yields=None):
     """fcstA (generateGIRF2blockhybrid.m:183-189, 226-234): K states [1, y lags] and for the
     block hybrid p blocks of the Ny actual-rate lags."""
@@ -42,12 +56,23 @@ def companion(PAI, N, p, bh=False, actual=None, yields=None):
 
 
 def girf_draw(PAI, invA, sqrtPHI, SV0, Xjumpoff, z, svz, shock11, cumcode, np_, bh=False,
-              actual=None, yields=None, elb=0.25):
+              actual=None, yields=None, elb=0.25, shadow=None, p=None):
     """One MCMC draw.  z, svz: N x H x nsim (zdraws; fcstSVdraws reshaped).  Returns
-    (yhat_base, yhat_plus, yhat_minus), each N x H."""
+    (yhat_base, yhat_plus, yhat_minus), each N x H.  shadow (N bools) selects the hybrid model
+    (generateGIRF2hybrid.m, simVARhybrid :361-386): PAI (K + Ns p) x N, the actual-rate ring
+    holds the shadow-rate variables, the output floors ``yields``."""
     N, H, nsim = z.shape
-    p = (PAI.shape[0] - 1) // N
-    A = companion(PAI, N, p, bh, actual, yields)
+    hybrid = shadow is not None
+    if hybrid:
+        Ns = int(np.count_nonzero(shadow))
+        p = (PAI.shape[0] - 1) // (N + Ns) if p is None else p
+        A = companion_hybrid(PAI, N, p, shadow)
+        ring = np.flatnonzero(shadow)
+        bh = True
+    else:
+        p = (PAI.shape[0] - 1) // N
+        A = companion(PAI, N, p, bh, actual, yields)
+        ring = np.flatnonzero(yields) if bh else np.array([], int)
     ns = A.shape[0]
     yidx = np.flatnonzero(yields) if bh else np.array([], int)
     K = 1 + N * p
@@ -65,7 +90,7 @@ def girf_draw(PAI, invA, sqrtPHI, SV0, Xjumpoff, z, svz, shock11, cumcode, np_, 
                 out[:, h, nn] = xn[1:1 + N]
                 x = xn
                 if bh:
-                    x[K:K + yidx.size] = np.maximum(x[1 + yidx], elb)
+                    x[K:K + ring.size] = np.maximum(x[1 + ring], elb)
         if bh:
             yy = out[yidx]
             yy[yy < elb] = elb

@@ -1,0 +1,95 @@
+"""CTA in the device's operation order -- TEST INFRASTRUCTURE ONLY (the checker of
+tests/test_gpu_mirror.py; never imported by the product).
+
+ccmm_oracle.cta / cta_syrk restate CTA.m:57-98 (as written / algorithmic); at the conditioning
+of the real data (cond(iV_post) ~ 1e9 with smooth volatility) a mere change of summation order
+moves a draw by ~1e-8 posterior sd, so those forms cannot pin the device to the
+1e-9 of the north star.  This form evaluates the same posterior with the device's weights,
+weighted Gram (v_mfma_f64_16x16x4_f64: fused multiply-adds in k order, measured by
+tools/probe_mfma_order.py), residuals and right-hand side operation for operation
+(oracle/cta_lag_mirror.c), and factors the posterior precision with LAPACK: the remaining
+difference to the device is the Cholesky / triangular-solve order only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+from scipy.linalg import cholesky, solve_triangular
+
+_HERE = Path(__file__).resolve().parent
+_LIB = None
+_dp = C.POINTER(C.c_double)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        so = _HERE / "libccmm_mirror.so"
+        if not so.exists() or so.stat().st_mtime < (_HERE / "cta_lag_mirror.c").stat().st_mtime:
+            subprocess.run(["make", "-C", str(_HERE)], check=True, capture_output=True)
+        _LIB = C.CDLL(str(so))
+        for name, args in (("ccmm_mirror_weights", [C.c_int, C.c_int, C.c_int, _dp, _dp, _dp]),
+                           ("ccmm_mirror_gram", [C.c_int, C.c_int, _dp, _dp, _dp]),
+                           ("ccmm_mirror_resid", [C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp]),
+                           ("ccmm_mirror_v", [C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp]),
+                           ("ccmm_mirror_rhs", [C.c_int, C.c_int, _dp, _dp, _dp, _dp]),
+                           ("ccmm_mirror_resid_update", [C.c_int, C.c_int, _dp, _dp, _dp, _dp])):
+            f = getattr(_LIB, name)
+            f.argtypes = args
+            f.restype = None
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(_dp)
+
+
+def _F(a):
+    return np.asfortranarray(np.asarray(a, dtype=np.float64))
+
+
+def weights(A, sqrtht, j):
+    T, N = sqrtht.shape
+    sw = np.zeros(T)
+    A, sh = _F(A), _F(sqrtht)
+    lib().ccmm_mirror_weights(T, N, j, _p(A), _p(sh), _p(sw))
+    return sw
+
+
+def gram(X, sw):
+    """[c b'; b M] of the device SYRK stage (no prior), K x K."""
+    T, K = X.shape
+    X = _F(X)
+    G = np.zeros((K, K), order="F")
+    lib().ccmm_mirror_gram(T, K, _p(X), _p(np.ascontiguousarray(sw)), _p(G))
+    return G
+
+
+def cta(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z):
+    """CTA.m:57-98 (CTA: one design) with the device's arithmetic up to the factorisation."""
+    T = Y.shape[0]
+    Y, X, A, sh = _F(Y), _F(X), _F(A), _F(sqrtht)
+    PAI = _F(PAI).copy(order="F")
+    E = np.zeros((T, N), order="F")
+    L_ = lib()
+    L_.ccmm_mirror_resid(T, K, N, _p(Y), _p(X), _p(PAI), _p(E))
+    v = np.zeros(T)
+    rhs = np.zeros(K)
+    for j in range(N):
+        sw = weights(A, sh, j)
+        G = gram(X, sw)
+        G[np.diag_indices(K)] += iVdiag[:, j]
+        L_.ccmm_mirror_v(T, N, j, _p(A), _p(sh), _p(Y), _p(E), _p(v))
+        ivb = np.ascontiguousarray(iVb[:, j], dtype=np.float64)
+        L_.ccmm_mirror_rhs(T, K, _p(X), _p(v), _p(ivb), _p(rhs))
+        Lc = cholesky(G, lower=True)
+        x = solve_triangular(Lc.T, solve_triangular(Lc, rhs, lower=True) + z[:, j], lower=False)
+        PAI[:, j] = x
+        xj = np.ascontiguousarray(x)
+        Ej = np.zeros(T)
+        L_.ccmm_mirror_resid_update(T, K, _p(X), _p(np.ascontiguousarray(Y[:, j])), _p(xj), _p(Ej))
+        E[:, j] = Ej
+    return np.array(PAI)

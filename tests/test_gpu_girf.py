@@ -131,3 +131,43 @@ def test_girf_reference_shape_crn(ctx, gi, bh):
         for sc in range(3):
             err = np.max(np.abs(got[:, :, sc, m] - want[sc]) / np.maximum(np.abs(want[sc]), 1.0))
             assert err < 1e-12, (m, sc, err)
+
+
+def _hybrid_draws(rng, N, p, M, Ns):
+    """Hybrid PAI (K + Ns p) x N x M: the linear draws plus small coefficients on the Ns p
+    actual-rate lags (Xffrlags, mcmcVARhybridGibbs.m:74-84)."""
+    PAI, invA, sqrtPHI, SV0, _ = _draws(rng, N, p, M, False, 0)
+    K = 1 + N * p
+    PAIh = np.concatenate([PAI, 0.05 * rng.standard_normal((Ns * p, N, M))], axis=0)
+    Xj = np.zeros((K + Ns * p, M))
+    Xj[0] = 1.0
+    Xj[1:] = 0.3 * rng.standard_normal((K + Ns * p - 1, M)) + 0.2
+    return PAIh, invA, sqrtPHI, SV0, Xj
+
+
+@pytest.mark.parametrize("N,p,yidx,sidx", [(5, 2, [2, 3, 4], [2, 3]),
+                                            (20, 12, [14, 15, 16, 17, 18, 19], [14, 15, 16])])
+def test_girf_hybrid_crn(ctx, gi, N, p, yidx, sidx):
+    """generateGIRF2hybrid.m (simVARhybrid, :361-386) against the oracle on common random numbers:
+    the state carries the Ns shadow-rate variables' actual-rate lags, the companion rows are the
+    full hybrid PAI, the output floors every yield.  N = 20, p = 12, Ns = 3 runs the specialised
+    kernel (ring padded to 4 rows), the toy shape the table-driven one."""
+    rng = np.random.default_rng(40 + N)
+    H, nsim, M = 14, 5, 2
+    yields = np.zeros(N, bool)
+    yields[yidx] = True
+    shadow = np.zeros(N, bool)
+    shadow[sidx] = True
+    PAI, invA, sqrtPHI, SV0, Xj = _hybrid_draws(rng, N, p, M, int(shadow.sum()))
+    z = rng.standard_normal((N, H, nsim, M))
+    svz = rng.standard_normal((N, H, nsim, M))
+    cum = np.zeros(N, bool)
+    cum[0] = True
+    got = ctx.girf(PAI, invA, sqrtPHI, SV0, Xj, H, nsim, 0.3, hybrid=True, ndxShadow=shadow, ndxYields=yields,
+                   elb=0.25, cumcode=cum, np_=12, z=z, svz=svz, p=p)
+    for m in range(M):
+        want = gi.girf_draw(PAI[..., m], invA[..., m], sqrtPHI[..., m], SV0[:, m], Xj[:, m], z[..., m],
+                            svz[..., m], 0.3, cum, 12, yields=yields, elb=0.25, shadow=shadow, p=p)
+        for sc in range(3):
+            err = np.max(np.abs(got[:, :, sc, m] - want[sc]) / np.maximum(np.abs(want[sc]), 1.0))
+            assert err < 1e-12, (m, sc, err)

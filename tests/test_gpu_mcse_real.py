@@ -1,0 +1,106 @@
+"""Monte Carlo parity on the reference's own data (fredblockMD20-2022-09, 2022-08 jump-off,
+N = 20, p = 12, T = 750, K = 241): posterior means from 128 Philox device chains against ONE
+long oracle chain committed as tests/golden/mcse_real_{linear,bh}.npz (tools/
+make_mcse_real_fixture.py: 1000 burn-in + 2000 kept sweeps, Geweke NSE with the 15 % taper of
+Diagnostics.m:134-300).
+
+  linear  configs[1] / SURVEY §8d C2: mcmcVAR.m sweeps from the reference initialisation.
+  bh      configs[2] / C3: mcmcVARshadowrateBlockHybrid.m at ELB 0.25 with the reference's ELB
+          schedule (Gibbs for m < MCMCburnin / 2 = 500, then 1000 PS proposals, accept-first,
+          Gibbs fallback; ~3 % of proposals sets accepted on this window), so the Gibbs-fallback
+          regime of the real run has a posterior-level check.
+
+Quantities: intercepts, own and FEDFUNDS first-lag coefficients of every equation, the
+subdiagonal of A, diag(PHI), sqrtht at three months (+ 24 censored shadow-rate cells for bh).
+Each must agree within 4.5 combined standard errors: the device chains are independent, so
+their estimate's standard error is the spread of the 128 chain means / sqrt(128).  A different
+generator stream makes this the test that the device samples the same posterior."""
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _fixture(kind):
+    path = ROOT / "tests" / "golden" / f"mcse_real_{kind}.npz"
+    if not path.exists():
+        pytest.fail(f"{path.name} missing: run tools/make_mcse_real_fixture.py {kind}")
+    return np.load(path)
+
+
+def _vech_diag_index(N):
+    """Positions of PHI's diagonal in PHI_all = PHI_((tril(PHI_))~=0) (column-major vech)."""
+    off, out = 0, []
+    for j in range(N):
+        out.append(off)
+        off += N - j
+    return np.array(out)
+
+
+def _run(pkg, ctx, oracle, fred, g, kind, B=128, burn=1000, keep=500, chunk=25):
+    mpm = oracle.set_minnesota_mean(fred["ncode"])
+    thisT = len(fred["ydates"])
+    rows, cols, tsel = g["sel_rows"], g["sel_cols"], list(g["tsel"])
+    if kind == "linear":
+        m = pkg.model.build_var(thisT, 12, 12, fred["data"], fred["ydates"], mpm, True)
+        ch = pkg.Chains(ctx, N=m.N, p=12, T=m.T, B=B, crn=False, store_capacity=chunk, seed=31337)
+    else:
+        ndxS, ndxO, _ = pkg.model.setShadowYields(fred["ncode"], 0.25)
+        e0 = pkg.model.elbT0_of(fred["data"], ndxS, 0.25, 12)
+        bm = pkg.model.build_bh(thisT, 12, 12, fred["data"], fred["ydates"], ndxS, ndxO, mpm, 0.25, e0, True)
+        m = bm.var
+        ch = pkg.Chains(ctx, N=m.N, p=12, T=m.T, B=B, crn=False, store_capacity=chunk, seed=31337,
+                        model=pkg.MODEL_BLOCKHYBRID, Ns=len(bm.ndxS), elbTmax=bm.elbT, elb_gibbsburn=100,
+                        elb=0.25)
+    ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    if kind == "bh":
+        ch.set_elb_model(bm.ndxS, bm.actual_block)
+        ch.set_elb_slot(0, bm.elbT0, bm.sNaN)
+        ch.set_elb_ps(1000, -(-burn // 2))                  # m >= MCMCburnin / 2 (:435)
+    st = pkg.model.initial_state(m, B)
+    ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+    ch.sweep(burn)
+    N = m.N
+    dix = _vech_diag_index(N)
+    sums = None
+    for done in range(0, keep, chunk):
+        ch.sweep(chunk, store=True)
+        d = ch.get_draws()
+        P = d["PAI_all"][:, rows, cols, :]                                  # M x nsel x B
+        A = np.linalg.inv(np.moveaxis(d["invA_all"], 3, 1))                 # M x B x N x N
+        asub = np.moveaxis(A[:, :, np.arange(1, N), np.arange(N - 1)], 1, 2)
+        phi = d["PHI_all"][:, dix, :]
+        sq = d["sqrtht_all"][:, tsel, :, :].reshape(chunk, len(tsel) * N, B, order="F")
+        parts = [P, asub, phi, sq]
+        if kind == "bh":
+            sr = d["shadowrate_all"].reshape(chunk, -1, B, order="F")[:, g["cells"], :]
+            parts.append(sr)
+        Q = np.concatenate(parts, axis=1)                                   # M x nq x B
+        s = Q.sum(axis=0)
+        sums = s if sums is None else sums + s
+    status = ch.get_status()
+    acc = None
+    if kind == "bh":
+        ps = ch.get_ps()
+        acc = float((ps["countAccept"].sum() + ps["countAcceptBurnin"].sum()) / (B * (burn + keep - burn // 2)))
+    ch.close()
+    assert not np.any(status & ~1), status
+    return sums / keep, acc                                                # nq x B chain means
+
+
+@pytest.mark.parametrize("kind", ["linear", "bh"])
+def test_real_data_posterior_means_within_mcse(pkg, ctx, oracle, fred, kind):
+    g = _fixture(kind)
+    means, acc = _run(pkg, ctx, oracle, fred, g, kind)
+    B = means.shape[1]
+    m_gpu = means.mean(axis=1)
+    nse_gpu = means.std(axis=1, ddof=1) / np.sqrt(B)
+    z = (m_gpu - g["pmean"]) / np.sqrt(g["nse3"] ** 2 + nse_gpu ** 2)
+    print(f"{kind}: {z.size} quantities, max |z| {np.abs(z).max():.2f}, median |z| {np.median(np.abs(z)):.2f}"
+          + ("" if acc is None else f", device PS accept rate {acc:.3f}, oracle {float(g['accept']) / 2500:.3f}"))
+    for q in np.argsort(-np.abs(z))[:5]:
+        print(f"  q{q}: gpu {m_gpu[q]:.5f} +- {nse_gpu[q]:.5f}  oracle {g['pmean'][q]:.5f} +- {g['nse3'][q]:.5f}"
+              f"  z {z[q]:.2f}")
+    assert np.abs(z).max() < 4.5, np.round(z, 2)
