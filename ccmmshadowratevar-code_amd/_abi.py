@@ -105,6 +105,7 @@ _SIGS = {
     "ccmm_chains_summaries": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, _u8p, _dp, C.c_int, _dp,
                                         _dp, _dp, _dp, _dp, _dp]),
     "ccmm_chains_get_ps": (C.c_int, [C.c_void_p, _ip, _ip, _ip]),
+    "ccmm_chains_get_ps_mean": (C.c_int, [C.c_void_p, _dp]),
     "ccmm_chains_get_xy": (C.c_int, [C.c_void_p, _dp, _dp]),
     "ccmm_chains_profile": (C.c_int, [C.c_void_p, C.c_int]),
     "ccmm_chains_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _dp, _i64p, C.c_char_p, C.c_int]),
@@ -681,6 +682,13 @@ class Chains:
         _check(self.lib.ccmm_chains_get_ps(self.handle, ca.ctypes.data_as(_ip), cb.ctypes.data_as(_ip),
                                            st.ctypes.data_as(_ip)), "ccmm_chains_get_ps")
         return dict(countAccept=ca, countAcceptBurnin=cb, stackAccept=st[:M])
+
+    def get_ps_mean(self):
+        """The last PS sweep's conditional mean of the censored cells (P^-1 b), Ns x elbTmax x B,
+        NaN elsewhere (ccmm_chains_get_ps_mean)."""
+        out = np.zeros((self.Ns, self.elbTmax, self.B), order="F")
+        _check(self.lib.ccmm_chains_get_ps_mean(self.handle, _ptr(out)), "ccmm_chains_get_ps_mean")
+        return out
 
     def summaries(self, source, slot, rows=None, cumcode=None, realized=None, pct=()):
         """Device summaries of the kept draws of data slot ``slot`` (ccmm_chains_summaries):

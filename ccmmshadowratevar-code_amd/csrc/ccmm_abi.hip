@@ -553,6 +553,12 @@ struct ccmm_chains {
   }
   int lag_mode = std::getenv("CCMM_LAG_MODE") ? std::atoi(std::getenv("CCMM_LAG_MODE")) : 0;
   int sv_mode = std::getenv("CCMM_SV_MODE") ? std::atoi(std::getenv("CCMM_SV_MODE")) : 0;
+  // passes of the ELB step in flight (k_elb_gibbs_wf): 1 (sequential k_elb_gibbs), 4 or 8
+  int elb_waves = [] {
+    const char* v = std::getenv("CCMM_ELB_WAVES");
+    const int w = v ? std::atoi(v) : 8;
+    return (w == 1 || w == 4) ? w : 8;
+  }();
   // timing-only ablation of k_elb_gibbs (results invalid): 1 no truncnorm, 2 no uniforms
   int elb_mode = std::getenv("CCMM_ELB_MODE") ? std::atoi(std::getenv("CCMM_ELB_MODE")) : 0;
   LagSel lagsel() const { return LagSel{Dpool.p, xidx.p, dColmap.p, ldd, drows, cfg.p, lag_mode}; }
@@ -1374,24 +1380,46 @@ struct ccmm_chains {
       }
     });
     if (ps) run_ps(ra, e, kept);
-    const size_t lds_gibbs =  // S | uniforms | month list
-        (size_t)2 * e.elbTmax * Ns * sizeof(double) + (size_t)e.elbTmax * sizeof(int);
+    // Gibbs passes: elb_waves passes in flight (k_elb_gibbs_wf, bit-identical draws), or the
+    // one-wave sequential kernel (CCMM_ELB_WAVES=1)
+    auto gibbs_lds = [&](int w) {
+      return w == 1 ? (size_t)2 * e.elbTmax * Ns * sizeof(double) + (size_t)e.elbTmax * sizeof(int)
+                    : (size_t)(1 + w) * e.elbTmax * Ns * sizeof(double) + (size_t)2 * e.elbTmax * sizeof(int) +
+                          (size_t)2 * w * sizeof(int);
+    };
+    int W = elb_waves;
+    while (W > 1 && gibbs_lds(W) > 160 * 1024) W = (W == 8) ? 4 : 1;  // long ELB windows
+    const size_t lds_gibbs = gibbs_lds(W);
     launch(KID_ELBGIBBS, [&] {
-      switch (Ns) {
+#define GIBBS_K(NS, WW)                                                                                     \
+  do {                                                                                                      \
+    HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs_wf<NS, WW>,                                       \
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gibbs));              \
+    hipLaunchKernelGGL((k_elb_gibbs_wf<NS, WW>), dim3(d.B), dim3(64 * WW), lds_gibbs, ctx->stream, d, e, cs, \
+                       ra);                                                                                 \
+  } while (0)
 #define CASE_NS(NS)                                                                            \
   case NS:                                                                                     \
-    HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs<NS>,                                 \
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gibbs)); \
-    hipLaunchKernelGGL(k_elb_gibbs<NS>, dim3(d.B), dim3(64), lds_gibbs, ctx->stream, d, e, cs, ra); \
+    if (W == 1) {                                                                              \
+      HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs<NS>,                               \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gibbs)); \
+      hipLaunchKernelGGL(k_elb_gibbs<NS>, dim3(d.B), dim3(64), lds_gibbs, ctx->stream, d, e, cs, ra); \
+    } else if (W == 4) {                                                                       \
+      GIBBS_K(NS, 4);                                                                          \
+    } else {                                                                                   \
+      GIBBS_K(NS, 8);                                                                          \
+    }                                                                                          \
     break;
+      switch (Ns) {
         CASE_NS(1)
         CASE_NS(2)
         CASE_NS(3)
         CASE_NS(4)
-#undef CASE_NS
         default:
           throw ArgError("Ns must be in [1, 4]");
       }
+#undef CASE_NS
+#undef GIBBS_K
     });
     const int nrb = e.elbTmax * Ns * (p + 1);
     launch(KID_ELBREBUILD, [&] {
@@ -2691,6 +2719,35 @@ int ccmm_chains_get_ps(ccmm_chains* ch, int* countAccept, int* countAcceptBurnin
       if (ch->sAccept.p) HIPCHECK(hipMemcpy(buf.data(), ch->sAccept.p, buf.size() * sizeof(int), hipMemcpyDeviceToHost));
       for (size_t c = 0; c < B; ++c)
         for (size_t m = 0; m < M; ++m) stackAccept[m + M * c] = buf[c * cap + m];
+    }
+    return 0;
+  });
+}
+
+int ccmm_chains_get_ps_mean(ccmm_chains* ch, double* mean) {
+  return guarded([&] {
+    require(ch && mean, "null argument");
+    require(ch->ps_np > 0 && ch->psL.p, "ccmm_chains_set_elb_ps was not called or no PS sweep ran");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    const size_t B = ch->cfg.B, nmax = ch->ps_nmax, W = ch->psW, per = (size_t)ch->cfg.Ns * ch->cfg.elbTmax;
+    std::vector<double> L(B * nmax * W), yb(B * nmax);
+    std::vector<int> cell(B * nmax), n(B);
+    HIPCHECK(hipMemcpy(L.data(), ch->psL.p, L.size() * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(yb.data(), ch->psY.p, yb.size() * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(cell.data(), ch->psCell.p, cell.size() * sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(n.data(), ch->psN.p, n.size() * sizeof(int), hipMemcpyDeviceToHost));
+    for (size_t c = 0; c < B; ++c) {
+      double* o = mean + c * per;
+      for (size_t q = 0; q < per; ++q) o[q] = std::nan("");
+      const double* Lc = L.data() + c * nmax * W;
+      std::vector<double> x(n[c], 0.0);
+      for (int i = n[c] - 1; i >= 0; --i) {  // x = L'^-1 ybar, band storage L(i + j, i) at [i][j]
+        double v = yb[c * nmax + i];
+        for (size_t j = 1; j < W && i + (int)j < n[c]; ++j) v -= Lc[(size_t)i * W + j] * x[i + j];
+        x[i] = v / Lc[(size_t)i * W];
+        o[cell[c * nmax + i]] = x[i];
+      }
     }
     return 0;
   });

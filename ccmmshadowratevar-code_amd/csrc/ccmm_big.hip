@@ -221,52 +221,134 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
       }
     }
     __syncthreads();
-    // ---- 2. factor the diagonal block (wave 0, lane = row; readlane broadcasts), invert it
-    if (wave == 0 && !(skip & 2)) {
-      double row[kBT];
-      double mydiag = 1.0;
+    // ---- 2. factor the diagonal block and invert it, as a 4 x 4 grid of 16 x 16 tiles:
+    //         right-looking over tile columns q, the 16 x 16 tile (q, q) factored and inverted
+    //         by wave 0 (lane = row, readlane broadcasts), the tiles below it scaled by
+    //         L_qq^-T and the trailing tiles updated on MFMA by all waves; then the inverse's
+    //         off-diagonal tiles Li_rq = -L_rr^-1 sum_k L_rk Li_kq by distance r - q on MFMA
+    if (!(skip & 2)) {
+      for (int e = tid; e < kBT * kBT; e += 256) {
+        const int i = e & 63, k = e >> 6;
+        Lk[i * kLiLd + k] = (k <= i) ? A[(size_t)(kcol + k) * KP + kcol + i] : 0.0;
+        Li[i * kLiLd + k] = 0.0;
+      }
+      __syncthreads();
+      for (int q = 0; q < 4; ++q) {
+        if (wave == 0) {
+          double* Tq = Lk + 16 * q * kLiLd + 16 * q;
+          double row[16];
+          double mydiag = 1.0;
 #pragma unroll
-      for (int m = 0; m < kBT; ++m) row[m] = (m <= lane) ? A[(size_t)(kcol + m) * KP + kcol + lane] : 0.0;
+          for (int m = 0; m < 16; ++m) row[m] = (lane < 16 && m <= lane) ? Tq[lane * kLiLd + m] : 0.0;
 #pragma unroll
-      for (int kk = 0; kk < kBT; ++kk) {
-        double dkk = readlane_d(row[kk], kk);
-        if (!(dkk > 0.0)) {
-          bad = 1;
-          dkk = 1.0;
+          for (int kk = 0; kk < 16; ++kk) {
+            double dkk = readlane_d(row[kk], kk);
+            if (!(dkk > 0.0)) {
+              bad = 1;
+              dkk = 1.0;
+            }
+            const double piv = sqrt(dkk);
+            const double rp = 1.0 / piv;
+            if (lane == kk) {
+              row[kk] = piv;
+              mydiag = piv;
+            }
+            if (lane > kk) row[kk] *= rp;
+            const double lik = row[kk];
+#pragma unroll
+            for (int m = kk + 1; m < 16; ++m) {
+              const double lmk = readlane_d(lik, m);
+              if (lane >= m) row[m] = fma(-lik, lmk, row[m]);
+            }
+          }
+          if (lane < 16) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) Tq[lane * kLiLd + m] = (m <= lane) ? row[m] : 0.0;
+            rd[kcol + 16 * q + lane] = 1.0 / mydiag;
+          }
+          wave_lds_sync();
+          // column c = lane of L_qq^-1 by forward substitution
+          if (lane < 16) {
+            double* Lq = Li + 16 * q * kLiLd + 16 * q;
+            const int c = lane;
+            double x[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              double s0 = (i == c) ? 1.0 : 0.0, s1 = 0.0;
+#pragma unroll
+              for (int m = 0; m < i; m += 2) {
+                s0 = fma(-Tq[i * kLiLd + m], x[m], s0);
+                if (m + 1 < i) s1 = fma(-Tq[i * kLiLd + m + 1], x[m + 1], s1);
+              }
+              x[i] = (i >= c) ? (s0 + s1) / Tq[i * kLiLd + i] : 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) Lq[i * kLiLd + c] = x[i];
+          }
         }
-        const double piv = sqrt(dkk);
-        const double rp = 1.0 / piv;
-        if (lane == kk) {
-          row[kk] = piv;
-          mydiag = piv;
-        }
-        if (lane > kk) row[kk] *= rp;
-        const double lik = row[kk];
+        __syncthreads();
+        // tiles below: L_rq = A_rq L_qq^-T  (A operand A_rq(i, k), B operand Linv_qq(j, k))
+        if (wave < 3 - q) {
+          const int r = q + 1 + wave;
+          dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int m = kk + 1; m < kBT; ++m) {
-          const double lmk = readlane_d(lik, m);
-          if (lane >= m) row[m] = fma(-lik, lmk, row[m]);
+          for (int kk = 0; kk < 4; ++kk) {
+            const double a = Lk[(16 * r + lr) * kLiLd + 16 * q + 4 * kk + lk];
+            const double b = Li[(16 * q + lr) * kLiLd + 16 * q + 4 * kk + lk];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) Lk[(16 * r + lk + 4 * r4) * kLiLd + 16 * q + lr] = acc[r4];
+        }
+        __syncthreads();
+        // trailing tiles A_rs -= L_rq L_sq'  (q < s <= r <= 3)
+        if (q < 3) {
+          int pr = 0;
+          for (int r = q + 1; r < 4; ++r)
+            for (int s2 = q + 1; s2 <= r; ++s2, ++pr) {
+              if ((pr & 3) != wave) continue;
+              dbl4 acc;
+#pragma unroll
+              for (int r4 = 0; r4 < 4; ++r4) acc[r4] = Lk[(16 * r + lk + 4 * r4) * kLiLd + 16 * s2 + lr];
+#pragma unroll
+              for (int kk = 0; kk < 4; ++kk) {
+                const double a = Lk[(16 * r + lr) * kLiLd + 16 * q + 4 * kk + lk];
+                const double b = Lk[(16 * s2 + lr) * kLiLd + 16 * q + 4 * kk + lk];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a, b, acc, 0, 0, 0);
+              }
+#pragma unroll
+              for (int r4 = 0; r4 < 4; ++r4) Lk[(16 * r + lk + 4 * r4) * kLiLd + 16 * s2 + lr] = acc[r4];
+            }
+          __syncthreads();
         }
       }
+      // inverse tiles below the diagonal, by distance (each wave one tile per distance)
+      for (int dist = 1; dist < 4; ++dist) {
+        if (wave < 4 - dist) {
+          const int qq = wave, r = wave + dist;
+          dbl4 sacc = dbl4{0.0, 0.0, 0.0, 0.0};  // S = sum_k L_rk Li_kq, k = q .. r - 1
+          for (int kt = qq; kt < r; ++kt) {
 #pragma unroll
-      for (int m = 0; m < kBT; ++m) {
-        const double v = (m <= lane) ? row[m] : 0.0;
-        Lk[lane * kLiLd + m] = v;
-        if (m <= lane) A[(size_t)(kcol + m) * KP + kcol + lane] = v;
-      }
-      rd[kcol + lane] = 1.0 / mydiag;
-      // column `lane` of L_kk^{-1} by forward substitution, kept in LDS
-      for (int i = 0; i < kBT; ++i) {
-        double s0 = (i == lane) ? 1.0 : 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-        int k = lane;
-        for (; k + 3 < i; k += 4) {  // four independent LDS read / FMA chains
-          s0 = fma(-Lk[i * kLiLd + k], Li[k * kLiLd + lane], s0);
-          s1 = fma(-Lk[i * kLiLd + k + 1], Li[(k + 1) * kLiLd + lane], s1);
-          s2 = fma(-Lk[i * kLiLd + k + 2], Li[(k + 2) * kLiLd + lane], s2);
-          s3 = fma(-Lk[i * kLiLd + k + 3], Li[(k + 3) * kLiLd + lane], s3);
+            for (int kk = 0; kk < 4; ++kk) {
+              const double a = Lk[(16 * r + lr) * kLiLd + 16 * kt + 4 * kk + lk];
+              const double b = Li[(16 * kt + 4 * kk + lk) * kLiLd + 16 * qq + lr];
+              sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, sacc, 0, 0, 0);
+            }
+          }
+          dbl4 x = dbl4{0.0, 0.0, 0.0, 0.0};  // -Linv_rr S: the accumulator is the B operand
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const double a = Li[(16 * r + lr) * kLiLd + 16 * r + 4 * kk + lk];
+            x = __builtin_amdgcn_mfma_f64_16x16x4f64(-a, sacc[kk], x, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) Li[(16 * r + lk + 4 * r4) * kLiLd + 16 * qq + lr] = x[r4];
         }
-        for (; k < i; ++k) s0 = fma(-Lk[i * kLiLd + k], Li[k * kLiLd + lane], s0);
-        Li[i * kLiLd + lane] = (i >= lane) ? ((s0 + s1) + (s2 + s3)) / Lk[i * kLiLd + i] : 0.0;
+        __syncthreads();
+      }
+      for (int e = tid; e < kBT * kBT; e += 256) {
+        const int i = e & 63, k = e >> 6;
+        if (k <= i) A[(size_t)(kcol + k) * KP + kcol + i] = Lk[i * kLiLd + k];
       }
     }
     __syncthreads();

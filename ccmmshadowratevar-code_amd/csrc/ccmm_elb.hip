@@ -603,6 +603,154 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
   for (int q = lane; q < T * NS; q += 64) Sc[q] = Sl[q];
 }
 
+// ---------------------------------------------------------------- Gibbs passes, wavefront
+// The same draws as k_elb_gibbs, with W passes in flight at once (one wave each).  Pass n
+// at censored month i reads the cells of months within p of t_i: the past ones as drawn
+// by pass n, the future ones and its own as drawn by pass n - 1.  So pass n may draw i
+// as soon as pass n - 1 has drawn every month up to reach(i) = max{j : t_j <= t_i + p}
+// (and pass n + 1 may then only touch months whose whole neighbourhood pass n has left):
+// the sequential order's reads are reproduced exactly, every cell sees the values it
+// sees in k_elb_gibbs, and the draws, flags and uniforms are bit-identical.  Steps run in
+// lock-step (one barrier each); progress counters are double-buffered by step parity so a
+// wave reads only what its predecessor published before the last barrier.  Within a step
+// the active months of different passes are more than p calendar months apart, so their
+// reads and writes of Sl never overlap.
+template <int NS, int W>
+__global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, ChainState cs, RngArgs ra) {
+  extern __shared__ double sm[];
+  const int c = blockIdx.x;
+  const int s = cs.slot[c];
+  const int p = e.p;
+  const int T = e.elbT[s], nc = e.ncens[s];
+  if (nc == 0) return;
+  if (e.psFlag && e.psFlag[c] > 0) return;  // a PS proposal was accepted (:453-454)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Rng rng = ra.make(c);
+  const int ncol = 2 * p * NS;
+  const int head = elb_cond_head(NS);
+  const int pg = e.elbTmax * NS;
+  double* Sl = sm;                              // T x NS (t-major), shared by all passes
+  double* Ul = sm + (size_t)pg * (1 + wave);    // this wave's pass uniforms, T x NS
+  int* Tm = (int*)(sm + (size_t)pg * (1 + W));  // censored months: t | (mask << 16)
+  int* reach = Tm + e.elbTmax;                  // reach(i)
+  int* prog = reach + e.elbTmax;                // [2][W] next draw of each wave, n nc + i
+  double* Sc = e.Scur + (size_t)c * e.elbTmax * NS;
+  const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * NS;
+  const int* cl = e.cens + (size_t)s * e.elbTmax;
+  const double* recs = e.cond + (size_t)c * e.elbTmax * e.condStride;
+  const int P = e.passes;
+  const int done_all = P * nc;
+  for (int q = tid; q < T * NS; q += 64 * W) Sl[q] = Sc[q];
+  for (int q = tid; q < nc; q += 64 * W) {
+    const int t = cl[q];
+    int m = 0;
+    for (int a = 0; a < NS; ++a) m |= sN[t * NS + a] ? (1 << a) : 0;
+    Tm[q] = t | (m << 16);
+    int j = q;
+    while (j + 1 < nc && cl[j + 1] <= t + p) ++j;
+    reach[q] = j;
+  }
+  if (tid < 2 * W) {
+    const int w = tid % W;
+    prog[tid] = (w < P) ? w * nc : done_all;
+  }
+  __syncthreads();
+  const int c0 = lane, c1 = lane + 64;
+  const bool h0 = c0 < ncol, h1 = c1 < ncol;
+  const int kk0 = c0 / NS, sp0 = c0 % NS, kk1 = c1 / NS, sp1 = c1 % NS;
+  const int off0 = (kk0 < p) ? -(kk0 + 1) : (kk0 - p + 1);
+  const int off1 = (kk1 < p) ? -(kk1 + 1) : (kk1 - p + 1);
+  constexpr int kHd = NS + NS * (NS - 1) + NS;
+  struct Rec {
+    double hd[kHd], g0[NS], g1[NS];
+  };
+  const int c0l = h0 ? c0 : 0, c1l = h1 ? c1 : 0;
+  auto load_rec = [&](int ci, Rec& r_) {
+    const double* r = recs + (size_t)ci * e.condStride;
+    for (int q = 0; q < kHd; ++q) r_.hd[q] = r[q];
+    for (int a = 0; a < NS; ++a) {
+      r_.g0[a] = r[head + c0l * NS + a];
+      r_.g1[a] = r[head + c1l * NS + a];
+    }
+  };
+  // pass n's uniforms rand(Ns, elbT) (gibbsdrawShadowrates.m:173, page n), drawn by this wave
+  auto uniforms = [&](int n) {
+    if (rng.crn) {
+      for (int q = lane; q < T * NS; q += 64) Ul[q] = rng.uniform(CCMM_RNG_ELB, (uint32_t)(q + T * NS * n));
+    } else {
+      const uint32_t base = (uint32_t)(T * NS * n);
+      for (int q = 2 * lane; q < T * NS + 1; q += 128) {
+        const uint32_t i0 = base + (uint32_t)q - ((base + (uint32_t)q) & 1u);
+        const u32x4 r = rng.raw(CCMM_RNG_ELB, i0 >> 1);
+        const int q0 = (int)(i0 - base), q1 = q0 + 1;
+        if (q0 >= 0 && q0 < T * NS) Ul[q0] = u01(r.x, r.y);
+        if (q1 >= 0 && q1 < T * NS) Ul[q1] = u01(r.z, r.w);
+      }
+    }
+    wave_lds_sync();
+  };
+  int n = wave, i = 0;
+  Rec rc, rn;
+  load_rec(0, rc);
+  int tm = Tm[0];
+  for (int step = 0;; ++step) {
+    const int* prd = prog + ((step + 1) & 1) * W;  // published before the last barrier
+    int* pwr = prog + (step & 1) * W;
+    bool fin = true;
+#pragma unroll
+    for (int w = 0; w < W; ++w) fin &= prd[w] >= done_all;
+    if (fin) break;
+    bool can = n < P;
+    if (can && n > 0) can = prd[(wave + W - 1) % W] >= (n - 1) * nc + reach[i] + 1;
+    if (can) {
+      if (i == 0) uniforms(n);
+      int nn = n, ni = i + 1;
+      if (ni == nc) {
+        nn = n + W;
+        ni = 0;
+      }
+      load_rec(ni, rn);  // this wave's next month (a harmless reload past its last pass)
+      const int tmn = Tm[ni];
+      const int t = tm & 0xffff, msk = tm >> 16;
+      double u[NS];
+      for (int a = 0; a < NS; ++a) u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
+      const int tn0 = t + off0, tn1 = t + off1;
+      const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
+      const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
+      double sp[NS];
+      for (int a = 0; a < NS; ++a) sp[a] = fma(h0 ? rc.g0[a] : 0.0, v0, (h1 ? rc.g1[a] : 0.0) * v1);
+      for (int a = 0; a < NS; ++a) sp[a] = rc.hd[a] + wave_sum_dpp(sp[a]);
+      const double* beta = rc.hd + NS;
+      const double* so = beta + NS * (NS - 1);
+      double cur[NS];
+      for (int a = 0; a < NS; ++a) cur[a] = Sl[t * NS + a];
+      for (int a = 0; a < NS; ++a) {
+        if (!((msk >> a) & 1)) continue;
+        double mu = sp[a];
+        int y = 0;
+        for (int b = 0; b < NS; ++b) {
+          if (b == a) continue;
+          mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
+          ++y;
+        }
+        uint8_t fl;
+        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a], fl);
+        if (e.flags && lane == 0)
+          e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
+      }
+      for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
+      rc = rn;
+      tm = tmn;
+      n = nn;
+      i = ni;
+    }
+    if (lane == 0) pwr[wave] = (n < P) ? n * nc + i : done_all;
+    __syncthreads();
+  }
+  for (int q = tid; q < T * NS; q += 64 * W) Sc[q] = Sl[q];
+}
+
 // ---------------------------------------------------------------- rebuild X, Y (per chain)
 // shadowYdata(p+elbT0+1:end, ndxS) = shadowrate'; X(t, 1+(l-1)N+s) = Y(t-l, s) (:501-509)
 __global__ void k_elb_rebuild(Dims d, ElbDev e, XSel xs, ChainState cs, int xslab0, double* dpool,

@@ -195,6 +195,21 @@ __device__ __forceinline__ double dpp_d(double v) {
   return r.d;
 }
 
+// v + v[lane ^ 16] and v + v[lane ^ 32] by the gfx950 row swaps (VALU, no LDS round trip):
+// a swap of a register with itself leaves the two partners in the two results
+__device__ __forceinline__ double xsum16(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+}
+__device__ __forceinline__ double xsum32(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+}
+
 __device__ __forceinline__ double wave_sum_dpp(double v) {
   v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]

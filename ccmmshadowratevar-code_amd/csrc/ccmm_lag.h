@@ -13,8 +13,8 @@ struct LagSel {
   const int* colmap;    // [16*NT] offset of lag column a relative to row t (doubles)
   int ldd, rows, p;     // row stride (odd), rows per slab (TP + p), lag order
   int mode;             // timing-only ablation (CCMM_LAG_MODE, results invalid): gram 1 no SYRK,
-                        // 2 no Cholesky, 4 no inverse; solve 16 no v, 32 no X'v, 64 no Linv
-                        // matvecs, 128 no X x.  gram 8: write the raw SYRK stage (Gram tiles,
+                        // 2 no Cholesky; solve 16 no v, 32 no X'v, 64 no triangular
+                        // substitutions, 128 no X x.  gram 8: write the raw SYRK stage (Gram tiles,
                         // b, c) and stop (ccmm_chains_get_cta_gram, parity tests)
 };
 
@@ -47,17 +47,14 @@ __host__ __device__ constexpr int gl_out_len(int NT) { return gl_ntile(NT) * 256
 // LDS of k_gram_chol_lag: max(SYRK stage, factor stage)
 inline size_t gl_lds_bytes(int NT, int rows, int ldd, int TP) {
   const size_t syrk = (size_t)rows * ldd + TP + 4;
-  const size_t fac = 16 * NT + 8 + 64 + 2 * kGlTile + 2 * (size_t)NT * kGlTile + kGlWaves * kGlTile +
-                     (size_t)gl_ntile(NT) * 16;
+  const size_t fac = 16 * NT + 8 + 64 + 2 * kGlTile + 2 * (size_t)NT * kGlTile + kGlWaves * kGlTile;
   return std::max(syrk, fac) * sizeof(double);
 }
 
 constexpr int kSlThreads = 512;
 
-// LDS of k_cta_solve_lag: D | union{v + X'v partials, tile partials} | rl | xl | A | red | colmap
-__host__ __device__ inline int sl_union(int NT, int TP) {
-  return (TP + 512 > gl_ntile(NT) * 16) ? TP + 512 : gl_ntile(NT) * 16;
-}
+// LDS of k_cta_solve_lag: D | v + X'v partials | rl | xl | A | red | colmap
+__host__ __device__ inline int sl_union(int NT, int TP) { return TP + 512; }
 inline size_t sl_lds_bytes(int NT, int rows, int ldd, int TP, int N) {
   const size_t n = (size_t)rows * ldd + sl_union(NT, TP) + 256 + 256 + N * N + 16;
   return n * sizeof(double) + 16 * NT * sizeof(int);

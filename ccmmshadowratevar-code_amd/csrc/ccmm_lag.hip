@@ -16,17 +16,20 @@
 //                                   l = b / L00, M <- M + diag(iV~) - l l'
 //                                   (the first step of right-looking Cholesky)
 //       L~ = chol(M)                right-looking, 16-wide panels, trailing update on MFMA
-//       Linv = inv(L)               right-looking blocked inversion on MFMA (CTA.m:77
-//                                   forms the same explicit inverse, Vchol = (L \ I)')
-//     output per system (doubles): NTILE tiles of Linv~ (row-major 16 x 16, tile
-//     g = column-major enumeration of the lower tiles), then [256]:
-//       [0] = 1 / L00, [1 + a] = Linv(1 + a, 0) = -(Linv~ l)_a / L00
+//     output per system (doubles): NTILE tiles in the slot layout (tile g = column-major
+//     enumeration of the lower tiles) of the block factorisation L~ = L_u D, D = diag(L~_pp),
+//     L_u unit block lower with blocks M_ip = L~_ip L~_pp^-1: the diagonal slots hold
+//     U~_pp^-1 = L~_pp^-T (the inverses the panel steps form anyway), the others M_ip'; then
+//     [256]: [0] = 1 / L00, [1 + a] = L(1 + a, 0)
 //
 //   k_cta_solve_lag  per chain, equations j = 1..N in order (CTA.m:60-97):
 //       v_t = sum_{i>=j} A(i,j) [E_t A(i,:)'] / sqrtht(t,i)^2        thread per t
 //       rhs = iVb_j + X' v                                          D in LDS
-//       PAI(:,j) = Linv' (Linv rhs + z_j)   (CTA.m:95-96: V rhs + Vc z with
-//                                            V = Vc Vc', Vc = Linv')
+//       PAI(:,j) = L' \ (L \ rhs + z_j)   (CTA.m:95-96: V rhs + Vc z with V = Vc Vc',
+//                                          Vc = Vchol = inv(L)'), block substitutions with
+//                                          L_u on the register-resident tiles (one barrier
+//                                          per block step) and the D blocks in parallel: the
+//                                          explicit inverse CTA.m:77 forms is never needed
 //       E(:,j) = Y(:,j) - X PAI(:,j)                                D in LDS
 //
 // Padded lag columns (a >= Np) map to a spare zero column of D, so they carry zero
@@ -223,7 +226,6 @@ __device__ __forceinline__ int gram_lag_factor(const GlArgs& g, double* sm, int 
   double* Dg = misc + 8;          // diagonal tile of the current panel
   double* Pn0 = Dg + kGlTile;     // 2 x NT tiles: panel rows; (inverse) U column / Z row
   double* Ws = Pn0 + 2 * NT * kGlTile + W * kGlTile;  // this wave's L_pp^-1
-  double* part = Pn0 + 2 * NT * kGlTile + kGlWaves * kGlTile;  // NTILE x 16
 
   if (lq == 0) {
     if (W < NT) lvec[16 * W + lr] = bs0;
@@ -295,9 +297,15 @@ __device__ __forceinline__ int gram_lag_factor(const GlArgs& g, double* sm, int 
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk)
             cc = __builtin_amdgcn_mfma_f64_16x16x4f64(LinvB[lr * kGlLd + 4 * kk + lq], acc[k][kk], cc, 0, 0, 0);
-          acc[k] = cc;
 #pragma unroll
           for (int r = 0; r < 4; ++r) Pn[ti * kGlTile + (lq + 4 * r) * kGlLd + lr] = cc[r];
+          // stored form: M'_pi = U_pp^-1 U_pi = (L_ip L_pp^-1)', the block of the unit block
+          // factor (k_cta_solve_lag: one barrier per block step); off the panel's critical path
+          dbl4 mm = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+            mm = __builtin_amdgcn_mfma_f64_16x16x4f64(LinvB[(4 * kk + lq) * kGlLd + lr], cc[kk], mm, 0, 0, 0);
+          acc[k] = mm;
         }
       }
     }
@@ -337,95 +345,14 @@ __device__ __forceinline__ int gram_lag_factor(const GlArgs& g, double* sm, int 
     }
   }
 
-  __syncthreads();
-
-  // ------------------------------------------------------------ Z = U^-1 (= Linv~')
-  // block back substitution from the bottom tile row:  at step p
-  //   Z_pj = U_pp^-1 B_pj (j > p), Z_pp = U_pp^-1;   B_ij -= U_ip Z_pj (i < p, j >= p)
-  // upper tile (a, b) lives in slot (ti = b, tj = a); slot (i, j) holds U_ij until
-  // step j, then B_ij, then (after step i) Z_ij.
-  for (int p = ((g.mode & 4) ? -1 : NT - 1); p >= 0; --p) {
-    const int lr = gl_opaque(lr0), lq = gl_opaque(lq0);
-    double* XD = Dg;                                  // U_pp^-1
-    double* LP = Pn0 + (p & 1) * NT * kGlTile;        // U_ip, i < p (slot i)
-    double* XR = Pn0 + ((p + 1) & 1) * NT * kGlTile;  // Z_pj, j >= p (slot j)
-    // (1) U_pp^-1 and column p of U -> LDS
-#pragma unroll
-    for (int k = 0; k < TPW; ++k) {
-      const int gi = W + kGlWaves * k;
-      if (gi < NTILE && sti[k] == p) {
-        const int tj = stj[k];
-        double* dst = (tj == p) ? XD : LP + tj * kGlTile;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dst[(lq + 4 * r) * kGlLd + lr] = acc[k][r];
-      }
-    }
-    __syncthreads();
-    // (2) row p: Z_pj = U_pp^-1 B_pj (j > p); Z_pp -> XR as well
-#pragma unroll
-    for (int k = 0; k < TPW; ++k) {
-      const int gi = W + kGlWaves * k;
-      if (gi < NTILE && stj[k] == p) {
-        const int ti = sti[k];
-        if (ti > p) {
-          dbl4 cc = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk)
-            cc = __builtin_amdgcn_mfma_f64_16x16x4f64(XD[lr * kGlLd + 4 * kk + lq], acc[k][kk], cc, 0, 0, 0);
-          acc[k] = cc;
-        }
-        double* dst = XR + ti * kGlTile;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dst[(lq + 4 * r) * kGlLd + lr] = acc[k][r];
-      }
-    }
-    __syncthreads();
-    // (3) rows above: B_ij -= U_ip Z_pj (j > p);  B_ip = -U_ip Z_pp
-#pragma unroll
-    for (int k = 0; k < TPW; ++k) {
-      const int gi = W + kGlWaves * k;
-      if (gi < NTILE && stj[k] < p && sti[k] >= p) {
-        const int ti = sti[k], tj = stj[k];
-        const double* Ua = LP + tj * kGlTile;
-        const double* Zb = XR + ti * kGlTile;
-        dbl4 cc = (ti == p) ? dbl4{0.0, 0.0, 0.0, 0.0} : acc[k];
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-          cc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Ua[lr * kGlLd + 4 * kk + lq], Zb[(4 * kk + lq) * kGlLd + lr],
-                                                    cc, 0, 0, 0);
-        acc[k] = cc;
-      }
-    }
-    // the next step writes XD and the other LP parity after its first barrier; XR of
-    // step p-1 is this LP buffer, written only after that barrier
-    __syncthreads();
-  }
-
-  // ------------------------------------------------------------ intercept column of Linv
-  //   Linv(1+a, 0) = -(Linv~ l)_a / L00; slot element (lq+4r, lr) = Linv~(16 ti + lr, 16 tj + lq + 4r)
-#pragma unroll
-  for (int k = 0; k < TPW; ++k) {
-    const int gi = W + kGlWaves * k;
-    if (gi < NTILE) {
-      const int tj = stj[k];
-      double v = 0.0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v = fma(acc[k][r], lvec[16 * tj + lq + 4 * r], v);
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      if (lq == 0) part[gi * 16 + lr] = v;
-    }
-  }
-  __syncthreads();
+  // ------------------------------------------------------------ intercept column of L
+  //   L(1+a, 0) = l_a (lvec, already b / L00); [0] = 1 / L00
   double* o = g.out;
-  if (tid < KL) {
-    const int ti = tid >> 4, rr = tid & 15;
-    double sacc = 0.0;
-    for (int tj = 0; tj <= ti; ++tj) sacc += part[gl_tile(NT, ti, tj) * 16 + rr];
-    o[NTILE * 256 + 1 + tid] = -sacc * rL00;
-  }
+  if (tid < KL) o[NTILE * 256 + 1 + tid] = lvec[tid];
   if (tid == 0) o[NTILE * 256] = rL00;
-  // ------------------------------------------------------------ Linv~ tiles -> HBM in slot layout
+  // ------------------------------------------------------------ factor tiles -> HBM in slot layout
+  //   off-diagonal slots U~_{tj,ti} = L~_{ti,tj}', diagonal slots U~_pp^-1 (the solve's
+  //   blocked substitutions, k_cta_solve_lag)
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
     const int gi = W + kGlWaves * k;
@@ -485,10 +412,10 @@ __global__ __launch_bounds__(512, 1) void k_gram_chol_lag(Dims d, const int* __r
 }
 
 // ================================================================== sequential solve
-// The Linv~ tiles of the current equation live in registers in the slot layout of
+// The factor tiles of the current equation live in registers in the slot layout of
 // k_gram_chol_lag (wave W holds slots W + 8k; element (lq + 4r, lr) of slot (ti, tj) =
-// Linv~(16 ti + lr, 16 tj + lq + 4r)): one coalesced HBM read per system, issued after
-// the v_t loads so that it overlaps the X'v product.
+// M'_{tj,ti}(lq + 4r, lr), U~_pp^-1 on the diagonal): one coalesced HBM read per system,
+// issued after the v_t loads so that it overlaps the X'v product.
 template <int NT, int NMAX>
 __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int* __restrict__ Tslot,
                                                               const double* __restrict__ iVb, XSel xs, LagSel ls,
@@ -502,7 +429,6 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
   double* Dl = sm;
   double* vl = Dl + rows * ldd;      // TP            phases 1-2
   double* part = vl + TP;            // 2 x 256       phase 2
-  double* tp = vl;                   // NTILE x 16    phases 3-4 (tile partials)
   double* rl = vl + sl_union(NT, TP);  // 256  rhs, then c = y + z  (K-space)
   double* xl = rl + 256;             // 256  y, then x            (K-space)
   double* Al = xl + 256;             // N x N
@@ -531,12 +457,12 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
 
   for (int j = 0; j < N; ++j) {
     // per-equation opaque lane ids: no lane-derived address is hoisted out of the
-    // equation loop next to the 120 Linv registers (see gl_opaque)
+    // equation loop next to the 120 factor registers (see gl_opaque)
     const int lane = gl_opaque(lane0), lr = lane & 15, lq = lane >> 4;
     const int mat = c * N + j;
     const int slab = ls.idx[mat];
     const double* Lo = cs.G + (size_t)mat * KP * KP;
-    const double* Lv = Lo + NTILE * 256;  // [0] 1/L00, [1+a] Linv(1+a,0)
+    const double* Lv = Lo + NTILE * 256;  // [0] 1/L00, [1+a] L(1+a,0)
     if (slab != cur) {
       __syncthreads();
       const double* src = ls.dpool + (size_t)slab * rows * ldd;
@@ -552,7 +478,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
         for (int k = 0; k < NMAX; ++k) {
           if (k < N) {
             e[k] = (k == j) ? Y[(size_t)k * TP + t] : E[(size_t)k * TP + t];
-            w2[k] = ih2[(size_t)k * TP + t];
+            w2[k] = (k >= j) ? ih2[(size_t)k * TP + t] : 0.0;  // rows i >= j only
           }
         }
 #pragma unroll
@@ -568,7 +494,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       vl[t] = acc;
     }
     __syncthreads();
-    // Linv~ of this system -> registers (consumed in phases 3-4); issued after the
+    // factor tiles of this system -> registers (consumed in phases 3-4); issued after the
     // barrier so that they cannot be hoisted into the v_t loop (register pressure)
     dbl4 lt[TPW];
 #pragma unroll
@@ -610,75 +536,101 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       rl[kx] = part[tid] + part[256 + tid] + ivb[kx];
     }
     __syncthreads();
-    // ---- (3) y = Linv rhs: per slot, row 16 ti + lr of Linv~ against rhs block tj
-    if (!(ls.mode & 64)) {
+    // ---- (3) forward substitution L y = rhs (CTA.m:95's Vchol' rhs without the explicit
+    //         inverse): y_0 = rhs_0 / L00, r~ = rhs~ - l y_0, then L_u z = r~ by block steps
+    //         (after step p - 1, z_p = r~_p is final; the owners of the slots (i, p) below
+    //         take M_ip z_p off r~_i, one barrier), and y_p = L~_pp^-1 z_p for all p at once
+    if (tid < KL) rl[1 + tid] = fma(-Lv[1 + tid], rl[0] * Lv[0], rl[1 + tid]);
+    if (tid == KL) xl[0] = rl[0] * Lv[0];
+    __syncthreads();
+    // slot (ti, tj) times block tj of u, summed over the slot's rows: (M u)_ti (or U^-T u)
+    auto colsum = [&](const dbl4& t, const double* u) {
+      double v = t[0] * u[0];
+      v = fma(t[1], u[4], v);
+      v = fma(t[2], u[8], v);
+      v = fma(t[3], u[12], v);
+      return xsum32(xsum16(v));
+    };
+    const bool subst = !(ls.mode & 64);
+    for (int p = 0; p < (subst ? NT - 1 : 0); ++p) {
 #pragma unroll
       for (int k = 0; k < TPW; ++k) {
         const int gi = wave + kGlWaves * k;
-        if (gi < NTILE) {
-          const double* rv = rl + 1 + 16 * stj[k] + lq;
-          double v = lt[k][0] * rv[0];
-          v = fma(lt[k][1], rv[4], v);
-          v = fma(lt[k][2], rv[8], v);
-          v = fma(lt[k][3], rv[12], v);
-          v += __shfl_xor(v, 16);
-          v += __shfl_xor(v, 32);
-          if (lq == 0) tp[gi * 16 + lr] = v;
+        if (gi < NTILE && stj[k] == p && sti[k] > p) {
+          const double v = colsum(lt[k], rl + 1 + 16 * p + lq);
+          if (lq == 0) rl[1 + 16 * sti[k] + lr] -= v;
+        }
+      }
+      __syncthreads();
+    }
+    if (subst) {
+#pragma unroll
+      for (int k = 0; k < TPW; ++k) {
+        const int gi = wave + kGlWaves * k;
+        if (gi < NTILE && sti[k] == stj[k]) {
+          const double v = colsum(lt[k], rl + 1 + 16 * sti[k] + lq);
+          if (lq == 0) xl[1 + 16 * sti[k] + lr] = v;
         }
       }
     }
     __syncthreads();
-    if (tid < KL) {
-      const int ti = tid >> 4, rr = tid & 15;
-      double sacc = Lv[1 + tid] * rl[0];
-      for (int tj = 0; tj <= ti; ++tj) sacc += tp[gl_tile(NT, ti, tj) * 16 + rr];
-      xl[1 + tid] = sacc;
-    }
-    if (tid == KL) xl[0] = rl[0] * Lv[0];
-    __syncthreads();
-    // ---- (4) c = y + z_j (randn(K,N) of CTA.m:58, column j); x = Linv' c
+    // ---- (4) c = y + z_j (randn(K,N) of CTA.m:58, column j); back substitution L' x = c:
+    //         w_p = L~_pp^-T c~_p for all p at once, then L_u' x~ = w by block steps from the
+    //         bottom (x_p = w_p final; the owners of the slots (p, i) take M_pi' x_p off w_i),
+    //         and x_0 = (c_0 - l' x~) / L00
     if (tid <= KL) {
       const int kx = (tid == KL) ? 0 : 1 + tid;
       rl[kx] = xl[kx] + ((kx < K) ? rng.normal(CCMM_RNG_PAI, (uint32_t)(kx + K * j)) : 0.0);
     }
     __syncthreads();
-    if (!(ls.mode & 64)) {
-      // slot contribution to x(16 tj + lq + 4r) = sum_lr lt[r] c(16 ti + lr): four sums over
+    {
+      // slot times block ti of u, per slot row (lq + 4r) = sum_lr t[r] u(lr): four sums over
       // the 16 lanes of a row group, folded so that lane (lr & 3) == 0 ends with r = lr >> 2
       const bool b8 = lr & 8, b4 = lr & 4;
+      auto fold = [&](const dbl4& t, double cv) {
+        const double v0 = t[0] * cv, v1 = t[1] * cv, v2 = t[2] * cv, v3 = t[3] * cv;
+        double a = b8 ? v2 : v0, b = b8 ? v3 : v1;
+        a += __shfl_xor(b8 ? v0 : v2, 8);
+        b += __shfl_xor(b8 ? v1 : v3, 8);
+        double q = b4 ? b : a;
+        q += __shfl_xor(b4 ? a : b, 4);
+        q += dpp_d<0x4E>(q);  // xor 2 (quad_perm, no LDS round trip)
+        q += dpp_d<0xB1>(q);  // xor 1
+        return q;
+      };
+      if (subst) {
 #pragma unroll
-      for (int k = 0; k < TPW; ++k) {
-        const int gi = wave + kGlWaves * k;
-        if (gi < NTILE) {
-          const double cv = rl[1 + 16 * sti[k] + lr];
-          const double v0 = lt[k][0] * cv, v1 = lt[k][1] * cv, v2 = lt[k][2] * cv, v3 = lt[k][3] * cv;
-          double a = b8 ? v2 : v0, b = b8 ? v3 : v1;
-          a += __shfl_xor(b8 ? v0 : v2, 8);
-          b += __shfl_xor(b8 ? v1 : v3, 8);
-          double q = b4 ? b : a;
-          q += __shfl_xor(b4 ? a : b, 4);
-          q += dpp_d<0x4E>(q);  // xor 2 (quad_perm, no LDS round trip)
-          q += dpp_d<0xB1>(q);  // xor 1
-          if ((lr & 3) == 0) tp[gi * 16 + lq + 4 * (lr >> 2)] = q;
+        for (int k = 0; k < TPW; ++k) {
+          const int gi = wave + kGlWaves * k;
+          if (gi < NTILE && sti[k] == stj[k]) {
+            const double q = fold(lt[k], rl[1 + 16 * sti[k] + lr]);
+            if ((lr & 3) == 0) xl[1 + 16 * sti[k] + lq + 4 * (lr >> 2)] = q;
+          }
         }
       }
+      __syncthreads();
+      for (int p = (subst ? NT - 1 : 0); p >= 1; --p) {
+#pragma unroll
+        for (int k = 0; k < TPW; ++k) {
+          const int gi = wave + kGlWaves * k;
+          if (gi < NTILE && sti[k] == p && stj[k] < p) {
+            const double q = fold(lt[k], xl[1 + 16 * p + lr]);
+            if ((lr & 3) == 0) xl[1 + 16 * stj[k] + lq + 4 * (lr >> 2)] -= q;
+          }
+        }
+        __syncthreads();
+      }
     }
-    {  // x_0 = c_0 / L00 + sum_a Linv(1+a,0) c_{1+a}
-      double pr = (tid < KL) ? Lv[1 + tid] * rl[1 + tid] : 0.0;
+    {  // l' x~
+      double pr = (tid < KL) ? Lv[1 + tid] * xl[1 + tid] : 0.0;
       pr = wave_sum_dpp(pr);
       if (lane == 0) red[wave] = pr;
     }
     __syncthreads();
-    if (tid < KL) {
-      const int tj = tid >> 4, cc = tid & 15;
-      double sacc = 0.0;
-      for (int ti = tj; ti < NT; ++ti) sacc += tp[gl_tile(NT, ti, tj) * 16 + cc];
-      xl[1 + tid] = sacc;
-    }
     if (tid == KL) {
-      double sacc = rl[0] * Lv[0];
+      double sacc = 0.0;
       for (int w = 0; w < kSlThreads / 64; ++w) sacc += red[w];
-      xl[0] = sacc;
+      xl[0] = (rl[0] - sacc) * Lv[0];
     }
     __syncthreads();
     // ---- (5) PAI(:,j) = x; E(:,j) = Y(:,j) - X x

@@ -79,16 +79,12 @@ __global__ __launch_bounds__(64) void k_ps_chol(Dims d, ElbDev e, PsDev ps, Chai
     if (kp > p) return 0.0;
     return -x[Ns * Ns + Ns + ((kp - 1) * Ns + aj) * Ns + ai];
   };
-  // b(i): the PS linear term given the month's observed (uncensored) shadow rates
+  // b(i) = AA_m' (cc - AA_o y_o) of the censored cell: k_elb_cond's b_PS is the gradient at
+  // censored cells = 0 with every observed cell (the month's uncensored shadow rates included)
+  // at its value, so it is the whole linear term
   auto rhs = [&](int i) -> double {
     const int ci = info[i] >> 3, ai = info[i] & 7;
-    const int t = e.cens[(size_t)s * e.elbTmax + ci];
-    const double* x = recs + (size_t)ci * e.condStride + xo;
-    double v = x[Ns * Ns + ai];
-    for (int b = 0; b < Ns; ++b)
-      if (!e.sNaN[((size_t)s * e.elbTmax + t) * Ns + b])
-        v -= x[ai * Ns + b] * e.Yt[((size_t)c * e.elbTmax + t) * N + e.ndxS[b]];
-    return v;
+    return recs[(size_t)ci * e.condStride + xo + Ns * Ns + ai];
   };
   for (int q = lane; q < W * W; q += 64) {
     const int r = q / W, cc = q % W;

@@ -236,16 +236,31 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   // (Ct[i (i + 1) / 2 + m], m <= i), the diagonal as its reciprocal
   auto store_factor = [&](int t, const double (&sr)[NN], const double (&rps)[NN], double w)
                           __attribute__((always_inline)) {
-    double* Ct = Cg + (size_t)t * NN2;
     if (lane < NN) {
-      const int rb = PACK ? (ln * (ln + 1)) / 2 : ln * NN;
 #pragma unroll
-      for (int m = 0; m < NN; ++m) {
-        myC[lane * CLD + m] = sr[m];
-        if (!PACK || m <= ln) Ct[rb + m] = sr[m];
-      }
+      for (int m = 0; m < NN; ++m) myC[lane * CLD + m] = sr[m];
       myw[lane] = w;
       Wg[(size_t)t * NN + lane] = w;
+    }
+  };
+  // packed entry e -> its LDS offset row * CLD + col (rows of the lower triangle, or full rows)
+  auto unpack_at = [&](int e) __attribute__((always_inline)) -> int {
+    if (!PACK) return (e / NN) * CLD + (e % NN);
+    int r = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+    r += ((r + 1) * (r + 2)) / 2 <= e ? 1 : 0;
+    r -= (r * (r + 1)) / 2 > e ? 1 : 0;
+    return r * CLD + (e - (r * (r + 1)) / 2);
+  };
+  constexpr int NP = PACK ? NN * (NN + 1) / 2 : NN * NN;
+  constexpr int kST = (NP + 63) / 64;
+  // the factor of block t leaves the wave's LDS copy for HBM as kST coalesced 64-lane
+  // stores (after the sv_wave_sync that follows store_factor)
+  auto flush_factor = [&](int t) __attribute__((always_inline)) {
+    double* Ct = Cg + (size_t)t * NN2;
+#pragma unroll
+    for (int i = 0; i < kST; ++i) {
+      const int e = lane + 64 * i;
+      if (e < NP) Ct[e] = myC[unpack_at(e)];
     }
   };
 
@@ -285,6 +300,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
         store_factor(t, sr, rps, w);
       }
       sv_wave_sync();
+      flush_factor(t);
       // [X1 X2] = C^-1 [-Q  M_{t,left}], one right-hand column per lane (the diagonal
       // of myC holds 1 / C_kk)
       {
@@ -405,6 +421,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
         store_factor(sb, sr, rps, w);
       }
       sv_wave_sync();
+      flush_factor(sb);
       if (i + 1 < P - 1) {
         // X1 = C^-1 M_{sep i, sep i+1}: column `lane` of M is r[M + lane*NN + k]
         double x[NN];
@@ -444,14 +461,6 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
 #pragma unroll
   for (int m = 0; m < NN; ++m) qrow[m] = Ql[ln * NN + m];
   // C_t -> LDS (whole wave), then row / column / reciprocal diagonal per lane
-  auto unpack_at = [&](int e) __attribute__((always_inline)) -> int {  // packed e -> row*CLD + col
-    if (!PACK) return (e / NN) * CLD + (e % NN);
-    int r = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
-    r += ((r + 1) * (r + 2)) / 2 <= e ? 1 : 0;
-    r -= (r * (r + 1)) / 2 > e ? 1 : 0;
-    return r * CLD + (e - (r * (r + 1)) / 2);
-  };
-  constexpr int NP = PACK ? NN * (NN + 1) / 2 : NN * NN;
   auto load_factor = [&](int t, double (&lr)[NN], double (&lc)[NN], double (&rps)[NN])
                          __attribute__((always_inline)) {
     const double* Ct = Cg + (size_t)t * NN2;

@@ -793,7 +793,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                 pa = ch.summaries(2, k, pct=pct)                                # PAI_all
                 post[i] = dict(yd=yd, yc=yc, sh=sh, pa=pa, ycr=ycr)
                 if progress and (k % 8 == 7 or k == len(vidx) - 1):
-                    print(f"[rank {rank}] device summaries {k + 1}/{len(vidx)} vintages", flush=True)
+                    print(f"[rank {rank}] device summaries {k + 1}/{len(vidx)} vintages "
+                          f"({time.perf_counter() - t1:.1f} s)", flush=True)
             fc = ch.get_fcst()
             scores[:] = fc["scores"]
             fYsum[:] = fc["fYsum"]
@@ -865,7 +866,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                     r["drawsMaxVARroot"] = max_var_roots(np.moveaxis(P, 3, 1).reshape(-1, K, N), N, p)
             res[mine[i]] = r
             if progress and (k % 4 == 3 or k == len(vidx) - 1):
-                print(f"[rank {rank}] results {k + 1}/{len(vidx)} vintages", flush=True)
+                print(f"[rank {rank}] results {k + 1}/{len(vidx)} vintages ({time.perf_counter() - t1:.1f} s)",
+                      flush=True)
         return res, failed
 
     t1 = time.perf_counter()

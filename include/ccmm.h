@@ -330,6 +330,11 @@ int ccmm_chains_set_elb_ps(ccmm_chains* ch, int nproposals, int ps_from_m);
  * (ndxAccept of each stored draw, 0 = no proposal accepted or Gibbs sweep; M = stored draws;
  * call before ccmm_chains_get_draws, which resets the store).  Any pointer may be NULL. */
 int ccmm_chains_get_ps(ccmm_chains* ch, int* countAccept, int* countAcceptBurnin, int* stackAccept);
+/* Parity diagnostic of the PS branch: the conditional mean P^-1 b of the censored cells that
+ * the last PS sweep's proposals were drawn around (VARTVPSVprecisionsamplerNaN at z = 0,
+ * mcmcVARshadowrateBlockHybrid.m:439-441), Ns x elbTmax x B, NaN outside the censored cells
+ * (the device's banded factor, back-substituted on the host). */
+int ccmm_chains_get_ps_mean(ccmm_chains* ch, double* mean);
 /* Parity diagnostic: the device's weighted Gram of every CTA system at the chain set's current
  * state (A, sqrtht, X), K x K x N x B: [c b'; b M] with c = sum_t w_t, b = X~' w, M = X~' diag(w) X~
  * (CTA.m:73 without the prior), exactly as the lag-structured coefficient kernel forms it before

@@ -1,0 +1,59 @@
+"""The wavefront schedule of the ELB Gibbs passes (k_elb_gibbs_wf: up to 8 passes of
+gibbsdrawShadowrates.m in flight, one wave each) reproduces the sequential kernel
+(k_elb_gibbs, CCMM_ELB_WAVES=1) bit for bit: shadow rates, every drawTruncNormal branch flag
+and the whole chain state after several block-hybrid sweeps on the reference's data
+(fredblockMD20-2022-09, ELB 0.25, 2022-08 jump-off: 109 censored months), with Philox draws
+and with CRN-free reuse of the same seed.  Also a short censored window (2012-06 jump-off),
+where fewer passes fit in flight than there are waves."""
+import os
+from datetime import date
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(pkg, fred, waves, thisT, B=8, sweeps=3):
+    os.environ["CCMM_ELB_WAVES"] = str(waves)
+    try:
+        mpm = pkg.model.setMinnesotaMean(fred["ncode"])
+        ndxS, ndxO, _ = pkg.model.setShadowYields(fred["ncode"], 0.25)
+        e0 = pkg.model.elbT0_of(fred["data"], ndxS, 0.25, 12)
+        bm = pkg.model.build_bh(thisT, 12, 12, fred["data"], fred["ydates"], ndxS, ndxO, mpm, 0.25, e0, True)
+        m = bm.var
+        ctx = pkg.Context(0)
+        ch = pkg.Chains(ctx, N=m.N, p=12, T=m.T, B=B, crn=False, store_capacity=sweeps, seed=777,
+                        model=pkg.MODEL_BLOCKHYBRID, Ns=len(bm.ndxS), elbTmax=bm.elbT, elb_gibbsburn=100,
+                        elb=0.25)
+        ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+        ch.set_elb_model(bm.ndxS, bm.actual_block)
+        ch.set_elb_slot(0, bm.elbT0, bm.sNaN)
+        st = pkg.model.initial_state(m, B)
+        ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+        ch.record_elb_flags(True)
+        ch.sweep(sweeps, store=True)
+        out = dict(ch.get_state())
+        out["shadow"] = ch.get_shadowrate()
+        out["flags"] = ch.get_elb_flags()
+        out["status"] = ch.get_status()
+        ch.close()
+        return out, bm.elbT
+    finally:
+        os.environ.pop("CCMM_ELB_WAVES", None)
+
+
+@pytest.mark.parametrize("jump", ["last", "2012-06"])
+def test_wavefront_equals_sequential(pkg, fred, jump):
+    yd = np.asarray(fred["ydates"], float)            # MATLAB datenums
+    jun2012 = date(2012, 6, 1).toordinal() + 366
+    thisT = len(yd) if jump == "last" else int(np.nonzero(yd == jun2012)[0][0]) + 1
+    ref, elbT = _run(pkg, fred, 1, thisT)
+    assert not np.any(ref["status"] & ~1)
+    for w in (4, 8):
+        got, _ = _run(pkg, fred, w, thisT)
+        for k in ref:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=f"waves={w} {k}")
+    print(f"{jump}: elbT {elbT}, {int(np.count_nonzero(ref['flags']))} flagged draws, identical for 4 and 8 waves")

@@ -1,8 +1,9 @@
 """Monte Carlo parity on the reference's own data (fredblockMD20-2022-09, 2022-08 jump-off,
-N = 20, p = 12, T = 750, K = 241): posterior means from 128 Philox device chains against ONE
-long oracle chain committed as tests/golden/mcse_real_{linear,bh}.npz (tools/
-make_mcse_real_fixture.py: 1000 burn-in + 2000 kept sweeps, Geweke NSE with the 15 % taper of
-Diagnostics.m:134-300).
+N = 20, p = 12, T = 750, K = 241): posterior means from 128 Philox device chains against long
+oracle chains committed as tests/golden/mcse_real_{linear,bh}.npz (tools/
+make_mcse_real_fixture.py: 1000 burn-in + 2000 kept sweeps per chain, Geweke NSE with the 15 %
+taper of Diagnostics.m:134-300; bh pools independent chains), the device chains averaging
+the same window of sweeps.
 
   linear  configs[1] / SURVEY §8d C2: mcmcVAR.m sweeps from the reference initialisation.
   bh      configs[2] / C3: mcmcVARshadowrateBlockHybrid.m at ELB 0.25 with the reference's ELB
@@ -30,6 +31,12 @@ def _fixture(kind):
     return np.load(path)
 
 
+def _oracle_accept(g):
+    if "accept_rate" in g:
+        return float(g["accept_rate"])
+    return float(g["accept"]) / (int(g["burn"]) + int(g["keep"]) - int(g["burn"]) // 2)
+
+
 def _vech_diag_index(N):
     """Positions of PHI's diagonal in PHI_all = PHI_((tril(PHI_))~=0) (column-major vech)."""
     off, out = 0, []
@@ -39,7 +46,7 @@ def _vech_diag_index(N):
     return np.array(out)
 
 
-def _run(pkg, ctx, oracle, fred, g, kind, B=128, burn=1000, keep=500, chunk=25):
+def _run(pkg, ctx, oracle, fred, g, kind, B=128, burn=1000, keep=2000, chunk=50):
     mpm = oracle.set_minnesota_mean(fred["ncode"])
     thisT = len(fred["ydates"])
     rows, cols, tsel = g["sel_rows"], g["sel_cols"], list(g["tsel"])
@@ -93,13 +100,15 @@ def _run(pkg, ctx, oracle, fred, g, kind, B=128, burn=1000, keep=500, chunk=25):
 @pytest.mark.parametrize("kind", ["linear", "bh"])
 def test_real_data_posterior_means_within_mcse(pkg, ctx, oracle, fred, kind):
     g = _fixture(kind)
-    means, acc = _run(pkg, ctx, oracle, fred, g, kind)
+    # the oracle's kept window (sweeps burn .. burn + keep): slow directions (the intercepts of
+    # the bh model) still drift after 1000 sweeps, so both sides average the same window
+    means, acc = _run(pkg, ctx, oracle, fred, g, kind, burn=int(g["burn"]), keep=int(g["keep"]))
     B = means.shape[1]
     m_gpu = means.mean(axis=1)
     nse_gpu = means.std(axis=1, ddof=1) / np.sqrt(B)
     z = (m_gpu - g["pmean"]) / np.sqrt(g["nse3"] ** 2 + nse_gpu ** 2)
     print(f"{kind}: {z.size} quantities, max |z| {np.abs(z).max():.2f}, median |z| {np.median(np.abs(z)):.2f}"
-          + ("" if acc is None else f", device PS accept rate {acc:.3f}, oracle {float(g['accept']) / 2500:.3f}"))
+          + ("" if acc is None else f", device PS accept rate {acc:.3f}, oracle {_oracle_accept(g):.3f}"))
     for q in np.argsort(-np.abs(z))[:5]:
         print(f"  q{q}: gpu {m_gpu[q]:.5f} +- {nse_gpu[q]:.5f}  oracle {g['pmean'][q]:.5f} +- {g['nse3'][q]:.5f}"
               f"  z {z[q]:.2f}")

@@ -136,6 +136,44 @@ def test_ps_real_window(pkg, ctx, oracle, bh, fred):
     _check(oracle, bs, got, S, ps, want, 5e-6)
 
 
+def test_ps_mean_real_data(pkg, ctx, oracle, bh, fred):
+    """The proposals' centre P^-1 b on real data, where many censored months have series above
+    the ELB (observed cells of the month enter b through the residuals only): the device's
+    banded factor (ccmm_chains_get_ps_mean) against the oracle's dense precision sampler at
+    z = 0, at the chain's final state of a Philox sweep.  Independent of whether any proposal
+    is accepted (on this window the accept branch is rare from the reference start)."""
+    bs = _real_bs(bh, oracle, fred)
+    lin = bs.lin
+    partial = int(np.count_nonzero(np.any(bs.sNaN, axis=0) & ~np.all(bs.sNaN, axis=0)))
+    assert partial > 0, "the window has no partially censored month"
+    B = 2
+    ch = pkg.Chains(ctx, N=lin.N, p=lin.p, T=lin.T, B=B, crn=False, model=pkg.MODEL_BLOCKHYBRID,
+                    Ns=len(bs.ndxS), elbTmax=bs.elbT, elb_gibbsburn=bs.gibbsburn, elb=bs.ELB,
+                    store_capacity=2, seed=91)
+    ch.set_data(0, lin.Y, lin.X, lin.iVdiag, lin.iVb, lin.sPHI, lin.Vol_0mean, lin.Vol_0vcvsqrt)
+    ch.set_elb_model(bs.ndxS, bs.actualrateBlock)
+    ch.set_elb_slot(0, bs.elbT0, bs.sNaN)
+    ch.set_elb_ps(64, 1)
+    st = oracle.init_state(lin)
+    ch.set_state(*[np.repeat(st[k][..., None], B, -1) for k in ("PAI", "A", "sqrtht", "h",
+                                                                "sqrtPHI")])
+    ch.sweep(2, store=True)
+    got = ch.get_state()
+    mean = ch.get_ps_mean()
+    ch.close()
+    N = lin.N
+    for c in range(B):
+        args = bh.ps_inputs(bs, got["PAI"][..., c], got["A"][..., c], got["sqrtht"][..., c])
+        nmiss = int(np.count_nonzero(args[3]))
+        YY = bh.precision_sampler_nan(*args, np.zeros((nmiss, 1))).reshape(N, bs.elbT, order="F")
+        want = YY[bs.ndxS, :][bs.sNaN]
+        have = mean[:, :bs.elbT, c][bs.sNaN]
+        err = np.max(np.abs(have - want))
+        print(f"chain {c}: {nmiss} censored cells, {partial} partially censored months, "
+              f"max |mean diff| {err:.2e}, cells above the ELB at the mean {int(np.sum(want >= bs.ELB))}")
+        assert err < 1e-8, err
+
+
 def test_ps_philox_batch(pkg, ctx, oracle, bh, fred):
     """Philox stream, 32 chains, PS from the first sweep with the reference's 1000 proposals:
     status clean, censored cells below the ELB, acceptance bookkeeping consistent."""

@@ -17,7 +17,12 @@ every equation, the subdiagonal of A, the diagonal of PHI, sqrtht at three month
 shadow rates of 24 censored cells spread over the window.  Used by tests/test_gpu_mcse_real.py.
 
 Run: python tools/make_mcse_real_fixture.py linear|bh [--keep 2000] [--burn 1000]
-(CPU; linear ~15 min, bh ~1-2 h single-threaded)."""
+(CPU; linear ~15 min, bh ~1-2 h single-threaded).
+
+Several independent chains (the bh intercepts mix slowly: effective sample size ~30 per
+2000 draws, so one chain's spectral NSE is itself noisy): run each with its own seed and
+--part-out FILE (in parallel processes), then --merge FILE ... pools them: the mean of the
+chain means, NSE = sqrt(sum NSE_i^2) / nchains."""
 import argparse
 import sys
 import time
@@ -59,6 +64,30 @@ def censored_cells(sNaN):
     return idx[np.linspace(0, idx.size - 1, NCELLS).round().astype(int)]
 
 
+def merge(kind, files):
+    """Pool independent chains (each file one chain's moments) into the fixture."""
+    parts = [dict(np.load(f)) for f in files]
+    K = len(parts)
+    pm = np.array([q["pmean"] for q in parts])
+    ns = np.array([q["nse3"] for q in parts])
+    keep = int(parts[0]["keep"])
+    burn = int(parts[0]["burn"])
+    for q in parts:
+        assert int(q["keep"]) == keep and int(q["burn"]) == burn
+    extra = {}
+    if kind == "bh":
+        acc = sum(int(q["accept"]) for q in parts)
+        nps = K * (burn + keep - (burn // 2))
+        extra = dict(cells=parts[0]["cells"], accept=acc, accept_rate=acc / nps)
+    out = ROOT / "tests" / "golden" / f"mcse_real_{kind}.npz"
+    np.savez(out, pmean=pm.mean(axis=0), nse3=np.sqrt((ns ** 2).sum(axis=0)) / K, pmean_chains=pm,
+             nse3_chains=ns, seeds=np.array([int(q["seed"]) for q in parts]), nchains=K, burn=burn, keep=keep,
+             tsel=parts[0]["tsel"], sel_rows=parts[0]["sel_rows"], sel_cols=parts[0]["sel_cols"],
+             nproposals=parts[0]["nproposals"], **extra)
+    print("wrote", out, "chains", K, "spread of chain means / pooled NSE (max):",
+          float(np.max(pm.std(axis=0, ddof=1) / np.sqrt(K) / (np.sqrt((ns ** 2).sum(axis=0)) / K))))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("kind", choices=["linear", "bh"])
@@ -66,7 +95,11 @@ def main():
     ap.add_argument("--keep", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=20243)
     ap.add_argument("--nproposals", type=int, default=1000)
+    ap.add_argument("--part-out", default=None, help="write this chain's moments here")
+    ap.add_argument("--merge", nargs="+", default=None, help="pool chain files into the fixture")
     args = ap.parse_args()
+    if args.merge:
+        return merge(args.kind, args.merge)
     fred = oracle.load_fred_csv(ROOT / "tests/golden/data/fredblockMD20-2022-09.csv")
     mpm = oracle.set_minnesota_mean(fred["ncode"])
     thisT = len(fred["ydates"])
@@ -105,7 +138,7 @@ def main():
                 print(m, f"{time.time() - t0:.0f}s", "accepted", acc, flush=True)
     D = np.array(draws)
     mg = momentg(D)
-    out = ROOT / "tests" / "golden" / f"mcse_real_{args.kind}.npz"
+    out = Path(args.part_out) if args.part_out else ROOT / "tests" / "golden" / f"mcse_real_{args.kind}.npz"
     extra = {} if cells is None else dict(cells=cells, accept=acc)
     np.savez(out, pmean=mg["pmean"], pstd=mg["pstd"], nse=mg["nse"], nse1=mg["nse1"], nse2=mg["nse2"],
              nse3=mg["nse3"], burn=args.burn, keep=args.keep, seed=args.seed, tsel=np.array(TSEL),
