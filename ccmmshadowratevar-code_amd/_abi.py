@@ -44,6 +44,34 @@ class ChainConfig(C.Structure):
                 ("elb", C.c_double)]
 
 
+class Vintage(C.Structure):
+    """ccmm_vintage (include/ccmm.h)."""
+    _fields_ = [("T", C.c_int), ("Y", _dp), ("X", _dp), ("iVdiag", _dp), ("iVb", _dp), ("sPHI", _dp),
+                ("h0mean", _dp), ("h0vcvsqrt", _dp), ("PAI0", _dp), ("sqrtht0", _dp), ("h0init", _dp), ("elbT0", C.c_int),
+                ("sNaN", _u8p), ("yrealized", _dp), ("unit", C.c_uint32)]
+
+
+class BatchConfig(C.Structure):
+    """ccmm_batch_config (include/ccmm.h)."""
+    _fields_ = [("model", C.c_int), ("N", C.c_int), ("p", C.c_int), ("Ns", C.c_int), ("ndxS", _ip),
+                ("actual_block", _u8p), ("ndxYields", _u8p), ("nchains", C.c_int), ("MCMCdraws", C.c_int),
+                ("burnin", C.c_int), ("gibbsburn", C.c_int), ("Nproposals", C.c_int), ("fcstNdraws", C.c_int),
+                ("H", C.c_int), ("elb", C.c_double), ("seed", C.c_uint64), ("chunk", C.c_int),
+                ("max_retries", C.c_int), ("postprocess", C.c_int), ("nq", C.c_int), ("pct", _dp),
+                ("cumcode", _u8p)]
+
+
+BATCH_OUT_FIELDS = ("logscore", "fcstYhat", "fcstShadowYhat", "PAImean", "PAIstdev", "shadowrate_all",
+                    "countELBaccept", "attempts", "fcstYmedian", "fcstYcrps", "fcstYquantiles", "fcstYcummedian",
+                    "fcstYcumcrps", "fcstYcumquantiles", "fcstShadowYmedian", "fcstShadowYquantiles", "PAImedian",
+                    "PAIquantiles", "scoreDraws")
+
+
+class BatchOut(C.Structure):
+    """ccmm_batch_out (include/ccmm.h)."""
+    _fields_ = [(nm, _ip if nm in ("countELBaccept", "attempts") else _dp) for nm in BATCH_OUT_FIELDS]
+
+
 _SIGS = {
     "ccmm_abi_version": (C.c_int, []),
     "ccmm_last_error": (C.c_char_p, []),
@@ -93,6 +121,7 @@ _SIGS = {
     "ccmm_chains_set_elb_slot": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p]),
     "ccmm_chains_get_shadowrate": (C.c_int, [C.c_void_p, _dp]),
     "ccmm_chains_get_cta_gram": (C.c_int, [C.c_void_p, _dp]),
+    "ccmm_chains_get_cta_factor": (C.c_int, [C.c_void_p, _dp]),
     "ccmm_chains_set_elb_ps": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "ccmm_draw_summaries": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, C.c_int, _dp, _dp, _dp,
                                       _dp, _dp, _dp]),
@@ -112,6 +141,8 @@ _SIGS = {
     "ccmm_fcst": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp,
                             _dp, _dp, _dp, _dp, _u8p, C.c_double, _dp, _dp, C.c_uint64,
                             C.c_int, _dp, _dp, _dp, _dp, _ip]),
+    "ccmm_run_batch": (C.c_int, [C.c_void_p, C.POINTER(BatchConfig), C.c_int, C.POINTER(Vintage),
+                                 C.POINTER(BatchOut)]),
     "ccmm_selftest_mfma_f64": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
     "ccmm_selftest_mfma_f64_acc": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp]),
 }
@@ -403,6 +434,72 @@ class Context:
                                   _ptr(zz), _ptr(sz), int(seed), _ptr(out)), "ccmm_girf")
         return out
 
+    def run_batch(self, *, model, N, p, Ns, ndxS, actual_block, ndxYields, nchains, MCMCdraws, burnin,
+                  gibbsburn, Nproposals, fcstNdraws, H, elb, seed, chunk, max_retries, postprocess, pct,
+                  cumcode, vintages, want=None):
+        """ccmm_run_batch: the vintage loop as one device-resident chain set.  ``vintages``: list of
+        dicts with T, Y, X, iVdiag, iVb, sPHI, h0mean, h0vcvsqrt, PAI0, sqrtht0, h0init (optional),
+        elbT0, sNaN, yrealized (N x H), unit.  Returns the ccmm_batch_out arrays (MATLAB shapes, vintage last);
+        ``want``: names to fetch (default all that apply)."""
+        V = len(vintages)
+        shadow = model in (MODEL_BLOCKHYBRID, MODEL_HYBRID)
+        K = N * p + 1 + (Ns * p if model == MODEL_HYBRID else 0)
+        Ns_ = Ns if shadow else 0
+        pct = _f(np.asarray(pct, float).ravel())
+        nq = pct.size
+        C_ = int(nchains)
+        keep = []                                                  # host buffers alive across the call
+        def arr(a, dt=np.float64):
+            a = np.asfortranarray(np.asarray(a, dtype=dt))
+            keep.append(a)
+            return a
+        vs = (Vintage * max(V, 1))()
+        elbTall = 0
+        for i, u in enumerate(vintages):
+            T = int(u["T"])
+            e0 = int(u.get("elbT0", T))
+            if shadow:
+                elbTall = max(elbTall, T - e0)
+            sn = None
+            if shadow and T > e0:
+                sn = arr(np.asarray(u["sNaN"], bool), np.uint8).ctypes.data_as(_u8p)
+            vs[i] = Vintage(T, _ptr(arr(u["Y"])), _ptr(arr(u["X"])), _ptr(arr(u["iVdiag"])), _ptr(arr(u["iVb"])),
+                            _ptr(arr(u["sPHI"])), _ptr(arr(u["h0mean"])), _ptr(arr(u["h0vcvsqrt"])),
+                            _ptr(arr(u["PAI0"])), _ptr(arr(u["sqrtht0"])),
+                            _ptr(arr(u["h0init"])) if u.get("h0init") is not None else None, e0, sn,
+                            _ptr(arr(u["yrealized"])),
+                            int(u["unit"]))
+        u8 = lambda a: None if a is None else arr(np.asarray(a, bool), np.uint8).ctypes.data_as(_u8p)
+        nd = arr(np.asarray(ndxS if shadow else [0], np.int32), np.int32)
+        cfg = BatchConfig(model, N, p, Ns_, nd.ctypes.data_as(_ip), u8(actual_block), u8(ndxYields), C_,
+                          MCMCdraws, burnin, gibbsburn, Nproposals, fcstNdraws, H, elb, seed, chunk,
+                          max_retries, int(bool(postprocess)), nq, _ptr(pct) if nq else None, u8(cumcode))
+        Ny = int(np.count_nonzero(ndxYields))
+        shapes = dict(logscore=(4, V), fcstYhat=(N, H, V), fcstShadowYhat=(N, H, V), PAImean=(K, N, V),
+                      PAIstdev=(K, N, V), countELBaccept=(V,), attempts=(V,))
+        if shadow:
+            shapes["shadowrate_all"] = (MCMCdraws, Ns_, elbTall, C_, V)
+        if postprocess:
+            shapes.update(fcstYmedian=(N, H, V), fcstYcrps=(N, H, V), fcstYquantiles=(N, H, nq, V),
+                          fcstYcummedian=(N, H, V), fcstYcumcrps=(N, H, V), fcstYcumquantiles=(N, H, nq, V),
+                          fcstShadowYmedian=(Ny, H, V), fcstShadowYquantiles=(Ny, H, nq, V),
+                          PAImedian=(K, N, V), PAIquantiles=(K, N, nq, V), scoreDraws=(fcstNdraws * C_, 4, V))
+        out = {}
+        for nm, shp in shapes.items():
+            if want is not None and nm not in want and nm != "attempts":
+                continue
+            if nm in ("countELBaccept", "attempts"):
+                out[nm] = np.zeros(shp, np.int32)
+            else:
+                out[nm] = np.zeros(shp, order="F")
+        bo = BatchOut(*[None if nm not in out else
+                        (out[nm].ctypes.data_as(_ip) if out[nm].dtype == np.int32 else _ptr(out[nm]))
+                        for nm in BATCH_OUT_FIELDS])
+        rc = self.lib.ccmm_run_batch(self.handle, C.byref(cfg), V, vs, C.byref(bo))
+        if rc != CCMM_WARN_MVNCDF:
+            _check(rc, "ccmm_run_batch")
+        return out
+
     def selftest_mfma_f64(self, A16x4, B4x16):
         D = np.zeros((16, 16), order="F")
         _check(self.lib.ccmm_selftest_mfma_f64(self.handle, _ptr(_f(A16x4)), _ptr(_f(B4x16)),
@@ -521,6 +618,28 @@ class Chains:
         G = np.zeros((self.K, self.K, self.N, self.B), order="F")
         _check(self.lib.ccmm_chains_get_cta_gram(self.handle, _ptr(G)), "ccmm_chains_get_cta_gram")
         return G
+
+    def get_cta_factor(self):
+        """The device's CTA factor record of every system at the current state (ccmm_chains_get_cta_factor),
+        decoded: S (NT*NT*256 per system, slot (ti, tj) at ti + tj NT as 16 x 16 row-major, the layout of
+        oracle/cta_mirror.factor), l (16 NT), 1 / L00; arrays over (equation, chain)."""
+        NT = (self.K - 1 + 15) // 16
+        ntile = NT * (NT + 1) // 2
+        n = ntile * 256 + 256
+        raw = np.zeros((n, self.N, self.B), order="F")
+        _check(self.lib.ccmm_chains_get_cta_factor(self.handle, _ptr(raw)), "ccmm_chains_get_cta_factor")
+        S = np.zeros((NT * NT * 256, self.N, self.B))
+        lane = np.arange(64)
+        gi = 0
+        for tj in range(NT):
+            for ti in range(tj, NT):
+                for r in range(4):
+                    rows = (lane >> 4) + 4 * r
+                    cols = lane & 15
+                    base = (ti + tj * NT) * 256
+                    S[base + rows * 16 + cols] = raw[gi * 256 + 64 * r + lane]
+                gi += 1
+        return S, raw[ntile * 256 + 1:ntile * 256 + 1 + 16 * NT], raw[ntile * 256]
 
     def record_elb_flags(self, enable=True):
         _check(self.lib.ccmm_chains_record_elb_flags(self.handle, int(bool(enable))),

@@ -1086,6 +1086,26 @@ struct ccmm_chains {
     }
   }
 
+  // Parity export: the lag path's factor record of every (chain, equation) system at the current
+  // state as k_gram_chol_lag writes it (gl_out_len(NT) doubles per system: the factor tiles in
+  // slot layout, then [1 / L00, L(1 + a, 0)])
+  void export_cta_factor(double* out) {
+    require(lag_active(), "ccmm_chains_get_cta_factor: the lag-structured CTA path is not active");
+    ensure_cta();
+    ChainState cs = view();
+    hipLaunchKernelGGL(k_cta_weights, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0, ctx->stream, d,
+                       Tslot.p, cs, 1);
+    HIPCHECK(hipGetLastError());
+    const LagSel ls = lagsel();
+    const size_t lds_g = gl_lds_bytes(lagNT, drows, ldd, d.TP);
+    HIPCHECK(lag_launch_gram(lagNT, ctx->stream, lds_g, d, Tslot.p, ls, cs, iVdiag.p));
+    HIPCHECK(hipStreamSynchronize(ctx->stream));
+    const size_t n = (size_t)gl_out_len(lagNT);
+    for (int mat = 0; mat < d.nmat; ++mat)
+      HIPCHECK(hipMemcpy(out + (size_t)mat * n, G.p + (size_t)mat * d.KP * d.KP, n * sizeof(double),
+                         hipMemcpyDeviceToHost));
+  }
+
   // CTA on the lag structure: sqrt weights -> Gram + Cholesky + inverse -> sequential solve
   void run_cta_lag(const RngArgs& ra, const ChainState& cs) {
     launch(KID_WEIGHTS, [&] {
@@ -1751,6 +1771,11 @@ struct ccmm_chains {
     return CCMM_OK;
   }
 };
+
+namespace ccmm {
+// error message of the next ccmm_last_error() on this thread (host modules outside this unit)
+void set_last_error(const std::string& msg) { g_err = msg; }
+}  // namespace ccmm
 
 // ============================================================== C ABI
 extern "C" {
@@ -2890,6 +2915,15 @@ int ccmm_chains_get_cta_gram(ccmm_chains* ch, double* G) {
     require(ch && G, "null argument");
     HIPCHECK(hipSetDevice(ch->ctx->device));
     ch->export_cta_gram(G);
+    return 0;
+  });
+}
+
+int ccmm_chains_get_cta_factor(ccmm_chains* ch, double* F) {
+  return guarded([&] {
+    require(ch && F, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    ch->export_cta_factor(F);
     return 0;
   });
 }

@@ -48,17 +48,6 @@ struct GlArgs {
   const double* swl;   // LDS sqrt weights
 };
 
-// Per-wave factor + inverse of the SPD 16 x 16 tile Dg (row-major, ld kGlLd, lower
-// triangle read): Ws := L^-1 (lower, row-major, ld kGlLd).  Every wave runs this on
-// the same tile, so no barrier separates the factorisation from its consumers.
-__device__ __forceinline__ double gl_rsqrt(double d) {  // rsq estimate + 2 Newton steps
-  double r = __builtin_amdgcn_rsq(d);
-  const double hd = 0.5 * d;
-  r = r * fma(-hd * r, r, 1.5);
-  r = r * fma(-hd * r, r, 1.5);
-  return r;
-}
-
 // Opaque copy of a per-lane value: the factorisation loops below are inlined into the
 // panel loop, and without this LLVM hoists every lane-dependent constant they derive
 // (the δ_ic of the inverse, per-slot LDS addresses) out of that loop and spills them
@@ -68,6 +57,22 @@ __device__ __forceinline__ int gl_opaque(int v) {
   return v;
 }
 
+// 1 / sqrt(d) as a deterministic function of d's bits, so that the factor can be reproduced bit for
+// bit by a restatement (oracle/cta_lag_mirror.c): the integer seed 0x5fe6eb50c7b537a9 - (bits >> 1)
+// (relative error <= 3.5 %) and four Newton steps r <- r (1.5 - (d / 2) r^2) (error 1.8e-3, 4.6e-6,
+// 3e-11, then rounding).  The hardware v_rsq_f64 estimate is not reproducible off the device, and
+// the IEEE sqrt + division pair puts ~25 dependent instructions on the serial pivot path.
+__device__ __forceinline__ double gl_rsqrt_det(double d) {
+  const long long bits = __double_as_longlong(d);
+  double r = __longlong_as_double(0x5fe6eb50c7b537a9LL - (bits >> 1));
+  const double hd = 0.5 * d;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) r = r * fma(-(hd * r), r, 1.5);
+  return r;
+}
+
+// Per-wave factor + inverse of the SPD 16 x 16 tile Dg (row-major, ld kGlLd, lower
+// triangle read): Ws := L^-1 (lower, row-major, ld kGlLd).
 __device__ __forceinline__ int gl_factor_inv(const double* Dg, double* Ws, int lane_in) {
   const int lane = gl_opaque(lane_in);
   double row[16];
@@ -78,7 +83,7 @@ __device__ __forceinline__ int gl_factor_inv(const double* Dg, double* Ws, int l
   for (int kk = 0; kk < 16; ++kk) {
     double dkk = readlane_d(row[kk], kk);
     dmin = fmin(dmin, dkk);
-    const double rp = gl_rsqrt(fmax(dkk, 1e-300));
+    const double rp = gl_rsqrt_det(fmax(dkk, 1e-300));
     if (lane == kk) rdiag = rp;
     const double lik = (lane > kk) ? row[kk] * rp : 0.0;
     row[kk] = lik;

@@ -644,7 +644,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                                      gibbsburn=100, rndStream=1012023, dist=None, device=None,
                                      chunk=50, max_retries=2, keep_draws=False, progress=False,
                                      Nproposals=1000, elb_ps=True, postprocess=False, cumcode=None,
-                                     setQuantiles=None, maxlambda=False, model="blockhybrid"):
+                                     setQuantiles=None, maxlambda=False, model="blockhybrid",
+                                     engine="python"):
     """The quasi-real-time OOS run of goVARshadowrateBlockHybrid.m:126-517 for the block-
     hybrid shadow-rate VAR, as ONE device-resident chain set per rank: every vintage
     thisT in Tjumpoffs (default: ydates > 2008-12, :127) is a data slot of the set with
@@ -681,7 +682,12 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
 
     model="hybrid" runs goVARhybrid.m instead (goVARhybrid_batch): mcmcVARhybridGibbs per
     vintage (K = N p + 1 + Ns p, PS proposals at every sweep, :458), modellabel ELBhybrid; the
-    max-root block is commented out in that driver (:383-430), so maxlambda is refused."""
+    max-root block is commented out in that driver (:383-430), so maxlambda is refused.
+
+    engine="native" runs the rank's vintage loop (chain set, burn-in, kept sweeps, forecast
+    records, device summaries, retries) inside the library, ccmm_run_batch (include/ccmm.h): the
+    same Philox streams and the same per-vintage results (keep_draws / maxlambda not available
+    there)."""
     import time
     from . import distributed as dm
     data0 = np.asarray(data0, float)
@@ -874,6 +880,18 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
     local, retries = {}, []
     todo = list(range(len(mine)))
     attempt = 0
+    if engine == "native":
+        if keep_draws or maxlambda:
+            raise ValueError("engine='native' keeps no PAI draws (keep_draws / maxlambda)")
+        local, retries = _native_batch(ctx, units, mine, C=C, N=N, p=p, K=K, Ns=Ns, H=H, Nd=Nd,
+                                       MCMCdraws=MCMCdraws, burn=burn, gibbsburn=gibbsburn,
+                                       Nproposals=Nproposals if elb_ps else 0, ELBbound=ELBbound,
+                                       rndStream=rndStream, chunk=chunk, max_retries=max_retries,
+                                       postprocess=postprocess, pct=pct, cumcode=cumcode,
+                                       ndxYIELDS=ndxYIELDS, hybrid=hybrid)
+        todo = []
+    elif engine != "python":
+        raise ValueError(f"engine must be 'python' or 'native', not {engine!r}")
     while todo:
         res, failed = run(todo, attempt)
         local.update(res)
@@ -958,6 +976,67 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                         units_local=n_units, sweeps_local=n_units * (burn + MCMCdraws),
                         setup_s=t_setup, run_s=t_run, retries=retries)
     return out
+
+
+def _native_batch(ctx, units, mine, *, C, N, p, K, Ns, H, Nd, MCMCdraws, burn, gibbsburn, Nproposals,
+                  ELBbound, rndStream, chunk, max_retries, postprocess, pct, cumcode, ndxYIELDS, hybrid):
+    """The rank's vintage loop through ccmm_run_batch; returns the per-vintage result dicts of
+    goVARshadowrateBlockHybrid_batch (keyed by global vintage index) and the retried vintages."""
+    if not units:
+        return {}, []
+    yields = np.zeros(N, bool)
+    yields[np.asarray(ndxYIELDS, int)] = True
+    vins = []
+    for i, (thisT, bm, yr) in enumerate(units):
+        m = bm.var
+        st = initial_state(m, 1)
+        vins.append(dict(T=m.T, Y=m.Y, X=m.X, iVdiag=m.iVdiag, iVb=m.iVb, sPHI=m.sPHI, h0mean=m.Vol_0mean,
+                         h0vcvsqrt=m.Vol_0vcvsqrt, PAI0=st["PAI"][..., 0], sqrtht0=st["sqrtht"][..., 0], h0init=st["h"][..., 0],
+                         elbT0=bm.elbT0, sNaN=bm.sNaN, yrealized=yr, unit=mine[i]))
+    bm0 = units[0][1]
+    out = ctx.run_batch(model=_abi.MODEL_HYBRID if hybrid else _abi.MODEL_BLOCKHYBRID, N=N, p=p, Ns=Ns,
+                        ndxS=bm0.ndxS, actual_block=None if hybrid else bm0.actual_block, ndxYields=yields,
+                        nchains=C, MCMCdraws=MCMCdraws, burnin=burn, gibbsburn=gibbsburn, Nproposals=Nproposals,
+                        fcstNdraws=Nd * MCMCdraws, H=H, elb=ELBbound, seed=int(rndStream), chunk=chunk,
+                        max_retries=max_retries, postprocess=postprocess, pct=pct, cumcode=cumcode,
+                        vintages=vins)
+    res, retries = {}, []
+    nq = pct.size
+    Ny = int(np.count_nonzero(yields))
+    for i, (thisT, bm, yr) in enumerate(units):
+        a = int(out["attempts"][i])
+        if a > 1:
+            retries.append(mine[i])
+        if a > max_retries + 1:
+            res[mine[i]] = None
+            continue
+        r = dict(thisT=thisT, yrealized=yr,
+                 countELBaccept=None if Nproposals == 0 else int(out["countELBaccept"][i]),
+                 logscore=out["logscore"][1, i], logscoreX=out["logscore"][2, i], logscoreI=out["logscore"][3, i],
+                 fcstYhat=out["fcstYhat"][..., i].copy(), fcstShadowYhat=out["fcstShadowYhat"][yields][..., i].copy(),
+                 PAImean=out["PAImean"][..., i].copy(), PAIstdev=out["PAIstdev"][..., i].copy())
+        if postprocess:
+            ycr = np.array(yr, float)
+            yh = r["fcstYhat"].copy()
+            if cumcode is not None:
+                ycr[cumcode] = np.cumsum(ycr[cumcode], axis=1)
+                yh[cumcode] = np.cumsum(yh[cumcode], axis=1)
+            r.update(PAImedian=out["PAImedian"][..., i], PAIquantiles=out["PAIquantiles"][..., i],
+                     fcstYmedian=out["fcstYmedian"][..., i], fcstYcrps=out["fcstYcrps"][..., i],
+                     fcstYquantiles=out["fcstYquantiles"][..., i], fcstYcumrealized=ycr, fcstYcumhat=yh,
+                     fcstYcummedian=out["fcstYcummedian"][..., i], fcstYcumcrps=out["fcstYcumcrps"][..., i],
+                     fcstYcumquantiles=out["fcstYcumquantiles"][..., i],
+                     fcstShadowYmedian=out["fcstShadowYmedian"][..., i].reshape(Ny, H),
+                     fcstShadowYquantiles=out["fcstShadowYquantiles"][..., i].reshape(Ny, H, nq),
+                     fcstYmvlogscoreDraws=out["scoreDraws"][:, 1, i], fcstYmvlogscoreXdraws=out["scoreDraws"][:, 2, i],
+                     fcstYmvlogscoreIdraws=out["scoreDraws"][:, 3, i])
+        if bm.elbT > 0:
+            sh = out["shadowrate_all"][:, :, :bm.elbT, :, i]                 # M x Ns x elbT x C
+            sr = sh.transpose(2, 1, 0, 3).reshape(bm.elbT, Ns, -1)
+            r["shadowrateMid"] = np.median(sr, axis=2)
+            r["shadowrateTails"] = np.moveaxis(matlab_prctile(sr, [5, 25, 75, 95], axis=2), 0, 2)
+        res[mine[i]] = r
+    return res, [retries] if retries else []
 
 
 def goVARhybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS, minnesotaPriorMean, **kw):

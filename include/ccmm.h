@@ -340,6 +340,14 @@ int ccmm_chains_get_ps_mean(ccmm_chains* ch, double* mean);
  * (CTA.m:73 without the prior), exactly as the lag-structured coefficient kernel forms it before
  * the factorisation.  Only when that path is active (linear / block-hybrid models, N <= 32). */
 int ccmm_chains_get_cta_gram(ccmm_chains* ch, double* G);
+/* Parity diagnostic: the factor record of every CTA system at the current state as the lag-structured
+ * kernel writes it, (NT (NT + 1) / 2 * 256 + 256) doubles per system (NT = ceil((K - 1) / 16)), systems
+ * ordered (equation, chain): the 16 x 16 factor tiles in slot order (slot g = column-major enumeration of
+ * the lower tile pairs (ti, tj); element (row (lane >> 4) + 4 r, column lane & 15) at g 256 + 64 r + lane;
+ * off-diagonal slots the unit block factor's blocks, diagonal slots the inverses of the diagonal
+ * factor tiles, transposed), then [1 / L00, L(1 + a, 0) for a = 0..16 NT - 1].  Same path as
+ * ccmm_chains_get_cta_gram. */
+int ccmm_chains_get_cta_factor(ccmm_chains* ch, double* F);
 /* Current shadow rates, Ns x elbTmax x B (the last sweep's draw). */
 int ccmm_chains_get_shadowrate(ccmm_chains* ch, double* shadowrate);
 /* Current per-chain data: X T x K x B, Y T x N x B (block-hybrid: the chain's
@@ -373,6 +381,92 @@ int ccmm_draw_summaries(ccmm_ctx* ctx, int S, int n, const double* draws, const 
 int ccmm_chains_summaries(ccmm_chains* ch, int source, int slot, const uint8_t* rows, const uint8_t* cumcode,
                           const double* realized, int nq, const double* pct, double* mean, double* median,
                           double* quantiles, double* stdev, double* crps);
+
+/* ------------------------------------------------------------ batch run (the vintage loop)
+ * ccmm_run_batch replaces the parfor over vintages of goVARshadowrateBlockHybrid.m:258-517
+ * (goVARhybrid.m:258 for the hybrid model, goVAR.m:242 for the linear one) for the vintages
+ * handed to this process: ONE device-resident chain set holds every vintage as a data slot with
+ * `nchains` chains; each chain runs `burnin` + MCMCdraws sweeps (mcmcVARshadowrateBlockHybrid.m:
+ * 56-58, 306-689) and every kept sweep simulates fcstNdraws / MCMCdraws forecast paths on the
+ * device (:550-625).  The ELB step is the Gibbs sampler for m < ceil(burnin / 2) and the
+ * accept-first PS proposals after (:433-466; hybrid: PS at every sweep, mcmcVARhybridGibbs.m:458;
+ * Nproposals = 0: Gibbs every sweep).  Philox streams: chain c of vintage v is keyed by
+ * unit(v) * nchains + c (+ 1000003 per retry), so results do not depend on how vintages are
+ * sharded over processes.  Failure recovery (goVARshadowrateBlockHybrid.m:287-310): a vintage
+ * whose chains flagged a non-SPD pivot (ccmm_chains_get_status bits other than 1) is re-run from
+ * its initial state on fresh streams, up to max_retries times; after that its outputs are NaN.
+ * The setup of each vintage (data matrices, Minnesota prior, initial PREVdraw) is the caller's:
+ * the MATLAB driver's own code computes it (mcmcVARshadowrateBlockHybrid.m:30-295, :308-317). */
+typedef struct {
+  int T;                        /* VAR rows (thisT - p) */
+  const double* Y;              /* T x N (actual data, :62-72) */
+  const double* X;              /* T x K */
+  const double* iVdiag;         /* K x N (diagonal of iV, mcmcVAR.m:186) */
+  const double* iVb;            /* K x N */
+  const double* sPHI;           /* N x N */
+  const double* h0mean;         /* N     Vol_0mean */
+  const double* h0vcvsqrt;      /* N x N Vol_0vcvsqrt */
+  const double* PAI0;           /* K x N  PREVdraw.PAI at m == 0 (X\Y, :308) */
+  const double* sqrtht0;        /* T x N  PREVdraw.sqrtht at m == 0 (AR residuals, :313) */
+  const double* h0init;         /* T x N  PREVdraw.Vol_states at m == 0 (2 log(sqrtht0), :314), or NULL:
+                                   computed here */
+  int elbT0;                    /* shadow-rate models: first VAR row (0-based) of the ELB window */
+  const uint8_t* sNaN;          /* Ns x (T - elbT0) censored cells (may be NULL when T == elbT0) */
+  const double* yrealized;      /* N x H (goVARshadowrateBlockHybrid.m:267-283, floored at the ELB) */
+  uint32_t unit;                /* global vintage index (Philox stream key) */
+} ccmm_vintage;
+
+typedef struct {
+  int model;                    /* CCMM_MODEL_LINEAR, _BLOCKHYBRID or _HYBRID */
+  int N, p;                     /* K = N p + 1 (+ Ns p for the hybrid model) */
+  int Ns;                       /* shadow-rate models: number of shadow rates */
+  const int* ndxS;              /* Ns 0-based ndxSHADOWRATE */
+  const uint8_t* actual_block;  /* N bytes, actualrateBlock (block hybrid; NULL otherwise) */
+  const uint8_t* ndxYields;     /* N bytes, ndxYIELDS (forecast censoring) */
+  int nchains;                  /* chains per vintage */
+  int MCMCdraws;                /* kept sweeps per chain */
+  int burnin;                   /* burn-in sweeps per chain (the reference: MCMCdraws) */
+  int gibbsburn;                /* Gibbs passes per ELB step before the kept one (100) */
+  int Nproposals;               /* elb.Nproposals (1000); 0: Gibbs ELB step every sweep */
+  int fcstNdraws;               /* multiple of MCMCdraws (:123-126) */
+  int H;                        /* fcstNhorizons */
+  double elb;                   /* ELBbound */
+  uint64_t seed;                /* rndStream seed */
+  int chunk;                    /* sweeps per device call (host synchronisation points) */
+  int max_retries;
+  int postprocess;              /* keep every kept draw and path in HBM; device summaries */
+  int nq;                       /* number of quantiles (postprocess) */
+  const double* pct;            /* nq percentiles (setQuantiles) */
+  const uint8_t* cumcode;       /* N bytes or NULL: cumsum over horizons (:353-355) */
+} ccmm_batch_config;
+
+typedef struct {                /* V = number of vintages; any pointer may be NULL */
+  double* logscore;             /* 4 x V log mean exp over the fcstNdraws * nchains one-step score
+                                   draws (k as ccmm_chains_get_fcst: 1 = fcstYmvlogscore, 2 = X,
+                                   3 = I; :437-447) */
+  double* fcstYhat;             /* N x H x V mean censored path (:450) */
+  double* fcstShadowYhat;       /* N x H x V mean uncensored (shadow-rate) path */
+  double* PAImean;              /* K x N x V (:376) */
+  double* PAIstdev;             /* K x N x V std(., 1) (:377) */
+  double* shadowrate_all;       /* MCMCdraws x Ns x elbTmax x nchains x V kept shadow rates */
+  int* countELBaccept;          /* V (countAccept + countAcceptBurnin over the vintage's chains) */
+  int* attempts;                /* V: runs used (> max_retries + 1: failed, outputs NaN) */
+  /* postprocess != 0 (goVARshadowrateBlockHybrid.m:349-480) */
+  double* fcstYmedian;          /* N x H x V */
+  double* fcstYcrps;            /* N x H x V */
+  double* fcstYquantiles;       /* N x H x nq x V */
+  double* fcstYcummedian;       /* N x H x V (cumcode applied to paths and yrealized) */
+  double* fcstYcumcrps;         /* N x H x V */
+  double* fcstYcumquantiles;    /* N x H x nq x V */
+  double* fcstShadowYmedian;    /* Ny x H x V (rows ndxYields) */
+  double* fcstShadowYquantiles; /* Ny x H x nq x V */
+  double* PAImedian;            /* K x N x V */
+  double* PAIquantiles;         /* K x N x nq x V */
+  double* scoreDraws;           /* (fcstNdraws * nchains) x 4 x V, order (Nd, kept draw, chain) */
+} ccmm_batch_out;
+
+int ccmm_run_batch(ccmm_ctx* ctx, const ccmm_batch_config* cfg, int V, const ccmm_vintage* vintages,
+                   ccmm_batch_out* out);
 
 /* ------------------------------------------------------------ GIRF
  * Generalized impulse responses by antithetic simulation, batched over M MCMC draws

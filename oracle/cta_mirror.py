@@ -6,9 +6,10 @@ of the real data (cond(iV_post) ~ 1e9 with smooth volatility) a mere change of s
 moves a draw by ~1e-8 posterior sd, so those forms cannot pin the device to the
 1e-9 of the north star.  This form evaluates the same posterior with the device's weights,
 weighted Gram (v_mfma_f64_16x16x4_f64: fused multiply-adds in k order, measured by
-tools/probe_mfma_order.py), residuals and right-hand side operation for operation
-(oracle/cta_lag_mirror.c), and factors the posterior precision with LAPACK: the remaining
-difference to the device is the Cholesky / triangular-solve order only.
+tools/probe_mfma_order.py), residuals, right-hand side, intercept peel, tiled right-looking
+Cholesky with 16 x 16 diagonal-tile inverses, and the block substitutions of the unit block
+factor, operation for operation (oracle/cta_lag_mirror.c; ccmm_lag.hip).  factor="lapack" keeps
+the previous form (LAPACK Cholesky and triangular solves of the mirrored Gram) for comparison.
 """
 from __future__ import annotations
 
@@ -36,10 +37,13 @@ def lib():
                            ("ccmm_mirror_resid", [C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp]),
                            ("ccmm_mirror_v", [C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp]),
                            ("ccmm_mirror_rhs", [C.c_int, C.c_int, _dp, _dp, _dp, _dp]),
-                           ("ccmm_mirror_resid_update", [C.c_int, C.c_int, _dp, _dp, _dp, _dp])):
+                           ("ccmm_mirror_resid_update", [C.c_int, C.c_int, _dp, _dp, _dp, _dp]),
+                           ("ccmm_mirror_solve", [C.c_int, _dp, _dp, C.c_double, _dp, _dp, _dp])):
             f = getattr(_LIB, name)
             f.argtypes = args
             f.restype = None
+        _LIB.ccmm_mirror_factor.argtypes = [C.c_int, _dp, _dp, _dp, _dp, _dp]
+        _LIB.ccmm_mirror_factor.restype = C.c_int
     return _LIB
 
 
@@ -68,8 +72,32 @@ def gram(X, sw):
     return G
 
 
-def cta(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z):
-    """CTA.m:57-98 (CTA: one design) with the device's arithmetic up to the factorisation."""
+def factor(G, iv):
+    """Device-order factorisation of G + diag(iv) (G = [c b'; b M] from gram()): returns the
+    factor record (slots, l, 1 / L00) and the non-positive-pivot flag."""
+    K = G.shape[0]
+    NT = (K - 1 + 15) // 16
+    S = np.zeros(NT * NT * 256)
+    lv = np.zeros(16 * NT)
+    r = C.c_double(0.0)
+    bad = lib().ccmm_mirror_factor(K, _p(_F(G)), _p(np.ascontiguousarray(iv, dtype=np.float64)), _p(S), _p(lv),
+                                   C.byref(r))
+    return (S, lv, r.value), bool(bad)
+
+
+def solve(fac, rhs, z):
+    """x = L' \\ (L \\ rhs + z) in the device's substitution order."""
+    S, lv, rL00 = fac
+    K = rhs.size
+    x = np.zeros(K)
+    lib().ccmm_mirror_solve(K, _p(S), _p(lv), rL00, _p(np.ascontiguousarray(rhs, dtype=np.float64)),
+                            _p(np.ascontiguousarray(z, dtype=np.float64)), _p(x))
+    return x
+
+
+def cta(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z, factor_form="device"):
+    """CTA.m:57-98 (CTA: one design) with the device's arithmetic throughout (factor_form="lapack":
+    LAPACK Cholesky and solves of the mirrored Gram and right-hand side)."""
     T = Y.shape[0]
     Y, X, A, sh = _F(Y), _F(X), _F(A), _F(sqrtht)
     PAI = _F(PAI).copy(order="F")
@@ -81,12 +109,17 @@ def cta(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z):
     for j in range(N):
         sw = weights(A, sh, j)
         G = gram(X, sw)
-        G[np.diag_indices(K)] += iVdiag[:, j]
         L_.ccmm_mirror_v(T, N, j, _p(A), _p(sh), _p(Y), _p(E), _p(v))
         ivb = np.ascontiguousarray(iVb[:, j], dtype=np.float64)
         L_.ccmm_mirror_rhs(T, K, _p(X), _p(v), _p(ivb), _p(rhs))
-        Lc = cholesky(G, lower=True)
-        x = solve_triangular(Lc.T, solve_triangular(Lc, rhs, lower=True) + z[:, j], lower=False)
+        if factor_form == "lapack":
+            Gp = G.copy()
+            Gp[np.diag_indices(K)] += iVdiag[:, j]
+            Lc = cholesky(Gp, lower=True)
+            x = solve_triangular(Lc.T, solve_triangular(Lc, rhs, lower=True) + z[:, j], lower=False)
+        else:
+            fac, _ = factor(G, iVdiag[:, j])
+            x = solve(fac, rhs, z[:, j])
         PAI[:, j] = x
         xj = np.ascontiguousarray(x)
         Ej = np.zeros(T)

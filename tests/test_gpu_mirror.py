@@ -6,9 +6,13 @@ order is measured and restated, so that the remaining difference is the factoris
   * The lag-structured coefficient kernel's weighted Gram [c b'; b M] (ccmm_chains_get_cta_gram)
     equals the C restatement in that order (oracle/cta_lag_mirror.c) BIT FOR BIT, on the real
     data (fredblockMD20-2022-09, N = 20, p = 12, T = 750, K = 241).
-  * One CRN sweep on the real data against the oracle with CTA in that order
-    (oracle.linear_sweep(cta_form="mirror"): LAPACK Cholesky and solves): PAI, A, sqrtht and
-    sqrtPHI within 1e-9 (|Δ| / max(|x|, sd_post)); KSC indicators bit-exact."""
+  * The factor record the kernel writes (intercept peel, 16 x 16 diagonal-tile factors and
+    inverses with IEEE sqrt / division pivots, MFMA panel products and trailing updates; the
+    unit block factor's blocks) equals the C restatement BIT FOR BIT (ccmm_chains_get_cta_factor
+    vs oracle/cta_mirror.factor).
+  * One CRN sweep on the real data against the oracle with CTA in that order end to end
+    (oracle.linear_sweep(cta_form="mirror"): the mirrored factorisation and block substitutions):
+    PAI, A, sqrtht and sqrtPHI within 1e-9 (|Δ| / max(|x|, sd_post)); KSC indicators bit-exact."""
 import numpy as np
 import pytest
 
@@ -58,6 +62,30 @@ def test_cta_gram_bit_exact_real_data(pkg, ctx, oracle, fred):
             np.testing.assert_array_equal(got, want)
 
 
+def test_cta_factor_bit_exact_real_data(pkg, ctx, oracle, fred):
+    from oracle import cta_mirror
+    su, m = _real(pkg, oracle, fred)
+    B = 2
+    sts = [random_state(oracle, su, seed=400 + c) for c in range(B)]
+    ch = pkg.Chains(ctx, N=su.N, p=su.p, T=su.T, B=B, crn=True)
+    ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    ch.set_state(*[np.stack([s[k] for s in sts], -1) for k in ("PAI", "A", "sqrtht", "h", "sqrtPHI")])
+    S, lv, r = ch.get_cta_factor()
+    ch.close()
+    for c in range(B):
+        for j in (0, 7, su.N - 1):
+            sw = cta_mirror.weights(sts[c]["A"], sts[c]["sqrtht"], j)
+            (Sw, lw, rw), bad = cta_mirror.factor(cta_mirror.gram(su.X, sw), su.iVdiag[:, j])
+            assert not bad
+            nd = int(np.count_nonzero(S[:, j, c] != Sw))
+            rel = float(np.max(np.abs(S[:, j, c] - Sw) / np.maximum(np.abs(Sw), 1e-300)))
+            print("chain", c, "eq", j, "factor entries differing", nd, "of", Sw.size, "max rel", rel,
+                  "| l", int(np.count_nonzero(lv[:, j, c] != lw)), "| 1/L00", r[j, c] == rw)
+            np.testing.assert_array_equal(lv[:, j, c], lw)
+            assert r[j, c] == rw
+            np.testing.assert_array_equal(S[:, j, c], Sw)
+
+
 def test_linear_sweep_real_data_1e9(pkg, ctx, oracle, fred):
     su, m = _real(pkg, oracle, fred)
     B = 4
@@ -81,7 +109,8 @@ def test_linear_sweep_real_data_1e9(pkg, ctx, oracle, fred):
              "A": rel_err(got["A"][..., c], st["A"], oracle.a_step_sd(st["RESID"], sts[c]["sqrtht"])),
              "sqrtht": rel_err(got["sqrtht"][..., c], st["sqrtht"]),
              "sqrtPHI": rel_err(got["sqrtPHI"][..., c], st["sqrtPHI"], 1e-3)}
-        print("chain", c, {k: f"{v:.2e}" for k, v in e.items()})
+        print("chain", c, {k: f"{v:.2e}" for k, v in e.items()},
+              "PAI entries differing", int(np.count_nonzero(got["PAI"][..., c] != st["PAI"])))
         np.testing.assert_array_equal(kai[..., c], st["kai"])
         worst = max(worst, max(e.values()))
     assert worst < 1e-9, worst
