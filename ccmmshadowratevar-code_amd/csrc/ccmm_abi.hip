@@ -2783,7 +2783,7 @@ int ccmm_draw_summaries(ccmm_ctx* ctx, int S, int n, const double* draws, const 
                         double* crps) {
   return guarded([&] {
     require(ctx && draws, "null argument");
-    require(S >= 1 && n >= 1 && (size_t)S * n < (1ull << 31), "S x n must be in [1, 2^31)");
+    require(S >= 1 && n >= 1, "S and n must be positive");  // sorted in batches of < 2^31 items
     require(nq >= 0 && (nq == 0 || pct), "bad quantile list");
     HIPCHECK(hipSetDevice(ctx->device));
     DBuf<double> A, Bs, out;

@@ -59,20 +59,25 @@ __device__ __forceinline__ int gl_opaque(int v) {
 
 // 1 / sqrt(d) as a deterministic function of d's bits, so that the factor can be reproduced bit for
 // bit by a restatement (oracle/cta_lag_mirror.c): the integer seed 0x5fe6eb50c7b537a9 - (bits >> 1)
-// (relative error <= 3.5 %) and four Newton steps r <- r (1.5 - (d / 2) r^2) (error 1.8e-3, 4.6e-6,
-// 3e-11, then rounding).  The hardware v_rsq_f64 estimate is not reproducible off the device, and
-// the IEEE sqrt + division pair puts ~25 dependent instructions on the serial pivot path.
+// (relative error <= 3.5 %) and two fourth-order steps r <- r + r e (1/2 + e (3/8 + 5/16 e)),
+// e = 1 - d r^2 (error <= 1.4e-16 over the double range; five dependent operations per step, against
+// three per Newton step of which four would be needed).  The hardware v_rsq_f64 estimate is not
+// reproducible off the device, and the IEEE sqrt + division pair puts ~25 dependent instructions on
+// the serial pivot path.
 __device__ __forceinline__ double gl_rsqrt_det(double d) {
   const long long bits = __double_as_longlong(d);
   double r = __longlong_as_double(0x5fe6eb50c7b537a9LL - (bits >> 1));
-  const double hd = 0.5 * d;
 #pragma unroll
-  for (int it = 0; it < 4; ++it) r = r * fma(-(hd * r), r, 1.5);
+  for (int it = 0; it < 2; ++it) {
+    const double e = fma(-(d * r), r, 1.0);
+    const double q = fma(fma(0.3125, e, 0.375), e, 0.5);
+    r = fma(r * e, q, r);
+  }
   return r;
 }
 
 // Per-wave factor + inverse of the SPD 16 x 16 tile Dg (row-major, ld kGlLd, lower
-// triangle read): Ws := L^-1 (lower, row-major, ld kGlLd).
+// triangle read): Ws := L^-1 (lower, row-major, ld kGlLd).  Lane i < 16 holds row i.
 __device__ __forceinline__ int gl_factor_inv(const double* Dg, double* Ws, int lane_in) {
   const int lane = gl_opaque(lane_in);
   double row[16];
@@ -91,30 +96,21 @@ __device__ __forceinline__ int gl_factor_inv(const double* Dg, double* Ws, int l
     for (int m = kk + 1; m < 16; ++m) row[m] = fma(-lik, readlane_d(lik, m), row[m]);
   }
   const int bad = (dmin > 0.0) ? 0 : 1;
-  // L -> Ws, diagonal as its reciprocal
-  if (lane < 16) {
-#pragma unroll
-    for (int m = 0; m < 16; ++m) Ws[lane * kGlLd + m] = (m < lane) ? row[m] : ((m == lane) ? rdiag : 0.0);
-  }
-  wave_lds_sync();
-  // lane c < 16: column c of L^-1,  x_i = (delta_ic - sum_{m<i} L_im x_m) / L_ii
+  // lane c < 16: column c of L^-1,  x_i = (delta_ic - sum_{m<i} L_im x_m) / L_ii, with L_im and
+  // 1 / L_ii read from lane i's registers (row[m], rdiag) as scalars: no LDS round trip on the
+  // serial path of the 16 rows
   const int c = lane;
   double x[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    // row i's loads are issued after x[i-1] (opaque dependency): all 120 hoisted to the
-    // top they would spill next to the 120 accumulator registers
-    int ro = i * kGlLd;
-    if (i > 0) asm volatile("" : "+v"(ro) : "v"(x[i - 1]));
     double s0 = (i == c) ? 1.0 : 0.0, s1 = 0.0;
 #pragma unroll
     for (int m = 0; m < i; m += 2) {
-      s0 = fma(-Ws[ro + m], x[m], s0);
-      if (m + 1 < i) s1 = fma(-Ws[ro + m + 1], x[m + 1], s1);
+      s0 = fma(-readlane_d(row[m], i), x[m], s0);
+      if (m + 1 < i) s1 = fma(-readlane_d(row[m + 1], i), x[m + 1], s1);
     }
-    x[i] = (i >= c) ? (s0 + s1) * Ws[ro + i] : 0.0;
+    x[i] = (i >= c) ? (s0 + s1) * readlane_d(rdiag, i) : 0.0;
   }
-  wave_lds_sync();
   if (lane < 16) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) Ws[i * kGlLd + c] = x[i];
@@ -520,13 +516,32 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
       if (ls.mode & 32) {
       } else if (a < KL) {
+        // four strided chains (t mod 4); the loads of eight months are issued before their
+        // fused multiply-adds so that one LDS round trip serves eight products
         const double* col = Dl + cm[a];
         int t = t0;
-        for (; t + 3 < t1; t += 4) {
+        for (; t + 7 < t1; t += 8) {
+          double cv[8], vv[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            cv[u] = col[(t + u) * ldd];
+            vv[u] = vl[t + u];
+          }
+          p0 = fma(cv[0], vv[0], p0);
+          p1 = fma(cv[1], vv[1], p1);
+          p2 = fma(cv[2], vv[2], p2);
+          p3 = fma(cv[3], vv[3], p3);
+          p0 = fma(cv[4], vv[4], p0);
+          p1 = fma(cv[5], vv[5], p1);
+          p2 = fma(cv[6], vv[6], p2);
+          p3 = fma(cv[7], vv[7], p3);
+        }
+        if (t + 3 < t1) {
           p0 = fma(col[t * ldd], vl[t], p0);
           p1 = fma(col[(t + 1) * ldd], vl[t + 1], p1);
           p2 = fma(col[(t + 2) * ldd], vl[t + 2], p2);
           p3 = fma(col[(t + 3) * ldd], vl[t + 3], p3);
+          t += 4;
         }
         for (; t < t1; ++t) p0 = fma(col[t * ldd], vl[t], p0);
       } else if (a == KL) {
@@ -646,14 +661,35 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       if (t < T && !(ls.mode & 128)) {
         const double* rowp = Dl + t * ldd;
         double s0 = xl[0], s1 = 0.0, s2 = 0.0, s3 = 0.0;
-        int a = 0;
-        for (; a + 3 < KL; a += 4) {
-          s0 = fma(rowp[cm[a]], xl[1 + a], s0);
-          s1 = fma(rowp[cm[a + 1]], xl[2 + a], s1);
-          s2 = fma(rowp[cm[a + 2]], xl[3 + a], s2);
-          s3 = fma(rowp[cm[a + 3]], xl[4 + a], s3);
+        if ((N & 3) == 0) {
+          // lag l, variable k is column a = (l - 1) N + k at D row t + p - l: with N a multiple
+          // of four, a mod 4 = k mod 4, so the chains need no column table (no dependent LDS
+          // load per product); the padded columns a >= N p are zero data and are skipped
+          const int P = ls.p;
+          for (int l = 1; l <= P; ++l) {
+            const double* row = rowp + (P - l) * ldd;
+            const double* xa = xl + 1 + (l - 1) * N;
+#pragma unroll
+            for (int k = 0; k < NMAX; k += 4) {
+              if (k < N) {
+                const double d0 = row[k], d1 = row[k + 1], d2 = row[k + 2], d3 = row[k + 3];
+                s0 = fma(d0, xa[k], s0);
+                s1 = fma(d1, xa[k + 1], s1);
+                s2 = fma(d2, xa[k + 2], s2);
+                s3 = fma(d3, xa[k + 3], s3);
+              }
+            }
+          }
+        } else {
+          int a = 0;
+          for (; a + 3 < KL; a += 4) {
+            s0 = fma(rowp[cm[a]], xl[1 + a], s0);
+            s1 = fma(rowp[cm[a + 1]], xl[2 + a], s1);
+            s2 = fma(rowp[cm[a + 2]], xl[3 + a], s2);
+            s3 = fma(rowp[cm[a + 3]], xl[4 + a], s3);
+          }
+          for (; a < KL; ++a) s0 = fma(rowp[cm[a]], xl[1 + a], s0);
         }
-        for (; a < KL; ++a) s0 = fma(rowp[cm[a]], xl[1 + a], s0);
         o = Y[(size_t)j * TP + t] - ((s0 + s1) + (s2 + s3));
       }
       E[(size_t)j * TP + t] = o;

@@ -18,6 +18,9 @@
 // CRPS (crpsDraws, em-matlabbox, source absent): mean|x - y| - 1/n^2 sum_i (2i - n - 1) x_(i).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <climits>
+
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include "ccmm_post.h"
@@ -55,7 +58,7 @@ __device__ __forceinline__ double hazen_index(int n, double pc) {
 __global__ __launch_bounds__(256) void k_post_stats(int S, int n, const double* __restrict__ sorted,
                                                     const double* __restrict__ realized, int nq,
                                                     const double* __restrict__ pct, double* mean,
-                                                    double* median, double* quant, double* sd,
+                                                    double* median, double* quant, size_t ldq, double* sd,
                                                     double* crps) {
   __shared__ double red[256];
   const int s = blockIdx.x;
@@ -104,7 +107,7 @@ __global__ __launch_bounds__(256) void k_post_stats(int S, int n, const double* 
   // median: the middle value, or the mean of the middle pair (MATLAB median, numpy median)
   if (median && tid == 0) median[s] = (n & 1) ? x[n / 2] : (x[n / 2 - 1] + x[n / 2]) / 2.0;
   if (quant)
-    for (int q = tid; q < nq; q += 256) quant[(size_t)q * S + s] = pq(pct[q]);
+    for (int q = tid; q < nq; q += 256) quant[(size_t)q * ldq + s] = pq(pct[q]);
 }
 
 // forecast paths: chain c's record of kept draw m, forecast draw job, horizon h, variable i
@@ -159,28 +162,44 @@ __global__ void k_offsets(int S, int n, int* off) {
 
 }  // namespace
 
+// rocPRIM's segmented sort counts items in 32 bits: the series are sorted in batches of at most
+// INT_MAX items (each batch's segment offsets s n fit an int)
+static size_t series_per_sort(int S, int n) {
+  return std::max<size_t>(1, std::min<size_t>((size_t)S, (size_t)INT_MAX / (size_t)n));
+}
+
 size_t post_workspace_bytes(int S, int n) {
   size_t tb = 0;
+  if (S <= 0 || n <= 0) return 256;
+  const size_t per = series_per_sort(S, n);
   (void)rocprim::segmented_radix_sort_keys((void*)nullptr, tb, (const double*)nullptr, (double*)nullptr,
-                                           (unsigned int)((size_t)S * n), (unsigned int)S, (const int*)nullptr,
+                                           (unsigned int)(per * n), (unsigned int)per, (const int*)nullptr,
                                            (const int*)nullptr, 0, 64, (hipStream_t)0);
-  return tb + (size_t)(S + 1) * sizeof(int) + 256;
+  return tb + (per + 1) * sizeof(int) + 256;
 }
 
 hipError_t post_summaries(hipStream_t st, int S, int n, const double* draws, double* sorted, void* ws,
                           size_t ws_bytes, const double* realized, int nq, const double* pct, double* mean,
                           double* median, double* quant, double* sd, double* crps) {
   if (S <= 0 || n <= 0) return hipSuccess;
+  const size_t per = series_per_sort(S, n);
   int* off = (int*)ws;
-  void* tmp = (char*)ws + (((size_t)(S + 1) * sizeof(int) + 255) / 256) * 256;
+  void* tmp = (char*)ws + (((per + 1) * sizeof(int) + 255) / 256) * 256;
   size_t tb = ws_bytes - ((char*)tmp - (char*)ws);
-  hipLaunchKernelGGL(k_offsets, dim3((S + 256) / 256), dim3(256), 0, st, S, n, off);
-  PCHECK(hipGetLastError());
-  PCHECK(rocprim::segmented_radix_sort_keys(tmp, tb, draws, sorted, (unsigned int)((size_t)S * n),
-                                            (unsigned int)S, off, off + 1, 0, 64, st));
-  hipLaunchKernelGGL(k_post_stats, dim3(S), dim3(256), 0, st, S, n, sorted, realized, nq, pct, mean, median,
-                     quant, sd, crps);
-  return hipGetLastError();
+  auto at = [](double* p, size_t o) { return p ? p + o : nullptr; };
+  for (size_t s0 = 0; s0 < (size_t)S; s0 += per) {
+    const int Sc = (int)std::min(per, (size_t)S - s0);
+    hipLaunchKernelGGL(k_offsets, dim3((Sc + 256) / 256), dim3(256), 0, st, Sc, n, off);
+    PCHECK(hipGetLastError());
+    PCHECK(rocprim::segmented_radix_sort_keys(tmp, tb, draws + s0 * n, sorted + s0 * n,
+                                              (unsigned int)((size_t)Sc * n), (unsigned int)Sc, off, off + 1, 0, 64,
+                                              st));
+    hipLaunchKernelGGL(k_post_stats, dim3(Sc), dim3(256), 0, st, Sc, n, sorted + s0 * n,
+                       realized ? realized + s0 : nullptr, nq, pct, at(mean, s0), at(median, s0), at(quant, s0),
+                       (size_t)S, at(sd, s0), at(crps, s0));
+    PCHECK(hipGetLastError());
+  }
+  return hipSuccess;
 }
 
 hipError_t post_gather_fcst(hipStream_t st, const double* src, int chain0, int C, int M, int Nd, int H, int N,

@@ -148,21 +148,24 @@ void ccmm_mirror_resid_update(int T, int K, const double* X, const double* Yj, c
  * (tj, ti) of the symmetric matrix, i.e. M(16 tj + a, 16 ti + b).  Every v_mfma_f64_16x16x4_f64
  * is four fused multiply-adds in k order (measured), so a product of two 16 x 16 tiles is an fma
  * chain over m = 0..15 per entry.  Pivots: 1 / sqrt(d) by the device's deterministic integer-seed
- * Newton form (gl_rsqrt_det).  The intercept pivot L00 = sqrt(c + iv0), 1 / L00 uses the IEEE
+ * fourth-order iteration (gl_rsqrt_det).  The intercept pivot L00 = sqrt(c + iv0), 1 / L00 uses the IEEE
  * (correctly rounded) sqrt and division on both sides.
  * ------------------------------------------------------------------------------------------ */
 #define MT 16
 typedef double tile_t[MT][MT];
 
-/* gl_rsqrt_det: integer seed 0x5fe6eb50c7b537a9 - (bits >> 1), four Newton steps */
+/* gl_rsqrt_det: integer seed 0x5fe6eb50c7b537a9 - (bits >> 1), two fourth-order steps */
 static double rsqrt_det(double d) {
   long long bits;
   memcpy(&bits, &d, sizeof bits);
   bits = 0x5fe6eb50c7b537a9LL - (bits >> 1);
   double r;
   memcpy(&r, &bits, sizeof r);
-  const double hd = 0.5 * d;
-  for (int it = 0; it < 4; ++it) r = r * fma(-(hd * r), r, 1.5);
+  for (int it = 0; it < 2; ++it) {
+    const double e = fma(-(d * r), r, 1.0);
+    const double q = fma(fma(0.3125, e, 0.375), e, 0.5);
+    r = fma(r * e, q, r);
+  }
   return r;
 }
 
