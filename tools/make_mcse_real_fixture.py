@@ -22,7 +22,9 @@ Run: python tools/make_mcse_real_fixture.py linear|bh [--keep 2000] [--burn 1000
 Several independent chains (the bh intercepts mix slowly: effective sample size ~30 per
 2000 draws, so one chain's spectral NSE is itself noisy): run each with its own seed and
 --part-out FILE (in parallel processes), then --merge FILE ... pools them: the mean of the
-chain means, NSE = sqrt(sum NSE_i^2) / nchains."""
+chain means, NSE = sqrt(sum NSE_i^2) / nchains, plus the between-chain standard error.  The
+committed bh fixture pools seeds 20243 and 30001-30006 (their part files:
+tests/golden/mcse_bh_parts/)."""
 import argparse
 import sys
 import time
@@ -80,7 +82,11 @@ def merge(kind, files):
         nps = K * (burn + keep - (burn // 2))
         extra = dict(cells=parts[0]["cells"], accept=acc, accept_rate=acc / nps)
     out = ROOT / "tests" / "golden" / f"mcse_real_{kind}.npz"
+    # the spread of the independent chain means is an estimate of the pooled mean's standard
+    # error that does not lean on the spectral NSE (which underestimates the slowest directions,
+    # ESS ~30 per chain for the bh intercepts)
     np.savez(out, pmean=pm.mean(axis=0), nse3=np.sqrt((ns ** 2).sum(axis=0)) / K, pmean_chains=pm,
+             se_between=pm.std(axis=0, ddof=1) / np.sqrt(K),
              nse3_chains=ns, seeds=np.array([int(q["seed"]) for q in parts]), nchains=K, burn=burn, keep=keep,
              tsel=parts[0]["tsel"], sel_rows=parts[0]["sel_rows"], sel_cols=parts[0]["sel_cols"],
              nproposals=parts[0]["nproposals"], **extra)
