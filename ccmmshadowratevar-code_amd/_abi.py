@@ -135,6 +135,8 @@ _SIGS = {
                                         _dp, _dp, _dp, _dp, _dp]),
     "ccmm_chains_get_ps": (C.c_int, [C.c_void_p, _ip, _ip, _ip]),
     "ccmm_chains_get_ps_mean": (C.c_int, [C.c_void_p, _dp]),
+    "ccmm_chains_keep_missingrate": (C.c_int, [C.c_void_p, C.c_int]),
+    "ccmm_chains_get_missingrate": (C.c_int, [C.c_void_p, _dp]),
     "ccmm_chains_get_xy": (C.c_int, [C.c_void_p, _dp, _dp]),
     "ccmm_chains_profile": (C.c_int, [C.c_void_p, C.c_int]),
     "ccmm_chains_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _dp, _i64p, C.c_char_p, C.c_int]),
@@ -801,6 +803,17 @@ class Chains:
         _check(self.lib.ccmm_chains_get_ps(self.handle, ca.ctypes.data_as(_ip), cb.ctypes.data_as(_ip),
                                            st.ctypes.data_as(_ip)), "ccmm_chains_get_ps")
         return dict(countAccept=ca, countAcceptBurnin=cb, stackAccept=st[:M])
+
+    def keep_missingrate(self, enable=True):
+        """Keep proposal 1 of every stored PS sweep (missingrate_all, ccmm_chains_keep_missingrate)."""
+        _check(self.lib.ccmm_chains_keep_missingrate(self.handle, int(bool(enable))), "ccmm_chains_keep_missingrate")
+
+    def get_missingrate(self):
+        """missingrate_all of the stored draws, M x Ns x elbTmax x B (call before get_draws)."""
+        out = np.zeros((self.stored(), self.Ns, self.elbTmax, self.B), order="F")
+        if out.size:
+            _check(self.lib.ccmm_chains_get_missingrate(self.handle, _ptr(out)), "ccmm_chains_get_missingrate")
+        return out
 
     def get_ps_mean(self):
         """The last PS sweep's conditional mean of the censored cells (P^-1 b), Ns x elbTmax x B,

@@ -1245,6 +1245,15 @@ struct ccmm_chains {
         hipLaunchKernelGGL(k_elb_store, dim3(d.B), dim3(256), 0, ctx->stream, e, cs, sShadow.p,
                            cfg.store_capacity, stored);
       });
+      if (keep_first) {  // missingrate_all (mcmcVARshadowrate.m:498)
+        sMissing.alloc(B * cap * cfg.Ns * cfg.elbTmax);
+        ElbDev e2 = elb_view();
+        launch(KID_STORE, [&] {
+          hipLaunchKernelGGL(k_ps_first_store, dim3(d.B), dim3(256), 0, ctx->stream,
+                             (last_ps && psFirst.p) ? psFirst.p : nullptr, e2.elbT, cs.slot, sMissing.p,
+                             cfg.Ns * cfg.elbTmax, cfg.Ns, cfg.store_capacity, stored);
+        });
+      }
       if (ps_np > 0) {  // stackAccept (:457): ndxAccept of the stored sweep, 0 = none / Gibbs
         sAccept.alloc(B * cap);
         launch(KID_STORE, [&] {
@@ -1324,12 +1333,19 @@ struct ccmm_chains {
     ps.acc = psAcc.p;
     ps.flag = psFlag.p;
     ps.count = psCount.p;
+    ps.per = cfg.Ns * std::max(cfg.elbTmax, 1);
+    ps.first = keep_first ? psFirst.p : nullptr;
     return ps;
   }
+  // missingrate_all (mcmcVARshadowrate.m:435, 498; mcmcVARhybridGibbs.m:486): keep proposal 1 of
+  // every PS sweep in the draw store (ccmm_chains_keep_missingrate)
+  bool keep_first = false;
+  DBuf<double> psFirst, sMissing;
   int last_ps = 0;  // whether the last ELB step ran the PS branch (draw store bookkeeping)
 
   void run_ps(const RngArgs& ra, ElbDev& e, bool kept) {
     ChainState cs = view();
+    if (keep_first) psFirst.alloc((size_t)d.B * cfg.Ns * std::max(cfg.elbTmax, 1));
     const PsDev ps = ps_view();
     const size_t lds = (size_t)(psW * psW + 2 * psW) * sizeof(double) + (size_t)ps_nmax * sizeof(int);
     require(lds <= 160 * 1024, "PS branch: cell list does not fit LDS");
@@ -1337,6 +1353,10 @@ struct ccmm_chains {
       HIPCHECK(hipFuncSetAttribute((const void*)k_ps_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(k_ps_chol, dim3(d.B), dim3(64), lds, ctx->stream, d, e, ps, cs);
     });
+    if (ps.first) {  // proposal 1's uncensored cells are the window's data (the chain's current Y)
+      HIPCHECK(hipMemcpyAsync(psFirst.p, e.Scur, (size_t)d.B * ps.per * sizeof(double), hipMemcpyDeviceToDevice,
+                              ctx->stream));
+    }
     launch(KID_PSPROP, [&] {
       const dim3 g((ps_np + 255) / 256, d.B);
       switch (psW) {
@@ -2745,6 +2765,36 @@ int ccmm_chains_get_ps(ccmm_chains* ch, int* countAccept, int* countAcceptBurnin
       for (size_t c = 0; c < B; ++c)
         for (size_t m = 0; m < M; ++m) stackAccept[m + M * c] = buf[c * cap + m];
     }
+    return 0;
+  });
+}
+
+int ccmm_chains_keep_missingrate(ccmm_chains* ch, int enable) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    require(ch->bh, "chain set has no ELB step (shadow-rate models only)");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    require(ch->stored == 0, "ccmm_chains_keep_missingrate: call before storing draws");
+    ch->keep_first = enable != 0;
+    return 0;
+  });
+}
+
+int ccmm_chains_get_missingrate(ccmm_chains* ch, double* missingrate_all) {
+  return guarded([&] {
+    require(ch && missingrate_all, "null argument");
+    require(ch->keep_first, "ccmm_chains_keep_missingrate was not enabled");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    const size_t B = ch->cfg.B, cap = ch->cfg.store_capacity, M = ch->stored;
+    const size_t per = (size_t)ch->cfg.Ns * ch->cfg.elbTmax;
+    if (M == 0 || per == 0) return 0;
+    std::vector<double> buf(B * cap * per);
+    HIPCHECK(hipMemcpy(buf.data(), ch->sMissing.p, buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (size_t c = 0; c < B; ++c)
+      for (size_t m = 0; m < M; ++m)
+        for (size_t e = 0; e < per; ++e) missingrate_all[m + M * (e + per * c)] = buf[(c * cap + m) * per + e];
     return 0;
   });
 }

@@ -36,6 +36,9 @@ struct PsDev {
   int* acc;         // [B]           smallest accepted proposal (0-based), INT_MAX none
   int* flag;        // [B]           ndxAccept of this sweep (1-based), 0 none
   int* count;       // [B][2]        accepted sweeps: [0] burn-in, [1] kept (countELBaccept*)
+  double* first;    // [B][Ns elbTmax] proposal 1 over the window (shadowrateProposals(:,:,1), kept as
+                    //               missingrate, mcmcVARshadowrate.m:435); nullptr: not kept
+  int per;          // Ns elbTmax
 };
 
 // ---------------------------------------------------------------- banded Cholesky
@@ -167,8 +170,11 @@ __global__ __launch_bounds__(256) void k_ps_prop(ElbDev e, PsDev ps, RngArgs ra)
   __syncthreads();
   if (k < ps.NP) {
     const Rng rng = ra.make(c);
+    // proposal 1 also lands in its censored cells of `first` (whose other cells hold the window's data)
+    const bool keep = k == 0 && ps.first != nullptr;
     const bool ok = ps_backsub<W>(ps.L + (size_t)c * ps.nmax * W, ps.ybar + (size_t)c * ps.nmax, n, rng, k,
-                                  ps.elb, nullptr, nullptr);
+                                  ps.elb, keep ? ps.first + (size_t)c * ps.per : nullptr,
+                                  keep ? ps.cell + (size_t)c * ps.nmax : nullptr);
     if (ok) atomicMin(&kmin, k);
   }
   __syncthreads();
@@ -182,6 +188,8 @@ __global__ __launch_bounds__(64) void k_ps_apply(ElbDev e, PsDev ps, RngArgs ra,
   const int n = ps.n[c];
   const int kmin = ps.acc[c];
   ps.acc[c] = INT_MAX;
+  if (n == 0 && ps.first)  // no proposals this sweep (precision not positive definite)
+    for (int q = 0; q < ps.per; ++q) ps.first[(size_t)c * ps.per + q] = __builtin_nan("");
   if (n == 0 || kmin == INT_MAX) {
     ps.flag[c] = 0;
     return;
@@ -191,6 +199,17 @@ __global__ __launch_bounds__(64) void k_ps_apply(ElbDev e, PsDev ps, RngArgs ra,
                       e.Scur + (size_t)c * e.elbTmax * e.Ns, ps.cell + (size_t)c * ps.nmax);
   ps.flag[c] = kmin + 1;
   ps.count[2 * c + (kept ? 1 : 0)] += 1;
+}
+
+// missingrate_all(thisMCMCdraw,:,:) = missingrate (mcmcVARshadowrate.m:498): proposal 1 of a PS
+// sweep, NaN for a Gibbs sweep (:406) and beyond the vintage's window
+__global__ void k_ps_first_store(const double* first, const int* elbT, const int* slot, double* out, int per,
+                                 int Ns, int cap, int m) {
+  const int c = blockIdx.x;
+  const int T = elbT[slot[c]];
+  double* o = out + ((size_t)c * cap + m) * per;
+  for (int q = threadIdx.x; q < per; q += blockDim.x)
+    o[q] = (first && q / Ns < T) ? first[(size_t)c * per + q] : __builtin_nan("");
 }
 
 // stackAccept(thisMCMCdraw) = ndxAccept (:457), 0 when the sweep fell back to Gibbs

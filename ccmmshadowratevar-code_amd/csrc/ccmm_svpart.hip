@@ -638,15 +638,15 @@ static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const
   return hipGetLastError();
 }
 
-// block factors stored as full rows (default: phase A's row stores stay unpredicated, measured
-// 2.20 vs 2.62 ms at N = 20, B = 256) or packed lower triangles (mode bit 128: 0.55x the
-// factor traffic)
+// block factors stored as packed lower triangles (default: 0.55x the factor traffic of full rows,
+// and no register spills at NN = 20; measured 2.16 vs 2.19 ms at N = 20, B = 256 since the factor
+// leaves LDS by coalesced stores) or as full rows (mode bit 128, for comparison); same draws
 template <int NN, int NW>
 static hipError_t sv_launch_one(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
                                 const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
                                 int mode) {
-  if (mode & 128) return sv_launch_one_<NN, NW, true>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
-  return sv_launch_one_<NN, NW, false>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+  if (mode & 128) return sv_launch_one_<NN, NW, false>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+  return sv_launch_one_<NN, NW, true>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
 }
 
 hipError_t sv_launch_part(int N, hipStream_t st, Dims d, const int* Tslot, const double* V0inv,

@@ -124,7 +124,8 @@ def mcmcVARshadowrateBlockHybrid(thisT, MCMCdraws, p, np_, data0, ydates0, actua
                                  burnin=None, gibbsburn=100, Nproposals=1000, elb_ps=True,
                                  stats=None):
     """mcmcVARshadowrateBlockHybrid.m:1-14, outputs PAI_all, PHI_all, invA_all,
-    sqrtht_all, shadowrate_all (M x Nshadowrates x elbT), missingrate_all (NaN).
+    sqrtht_all, shadowrate_all (M x Nshadowrates x elbT), missingrate_all (NaN: the draw of the
+    doELBsampleAlternate branch, off in every reference driver, :470-478).
 
     The ELB step follows :433-466: the Gibbs sampler for m < MCMCburnin/2, then the
     acceptance-sampling branch (Nproposals draws of the precision sampler restated from
@@ -209,8 +210,8 @@ def mcmcVARshadowrate(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMe
     with YHAT0 = [] (Gibbs for m < MCMCburnin/2, then elb.Nproposals = 100 PS proposals,
     :397-436), and the linear model's predictive density whose censored recursion floors
     ndxOTHERYIELDS only (:539-546), chain set model CCMM_MODEL_SHADOWRATE.  Outputs 1-17:
-    PAI_all, PHI_all, invA_all, sqrtht_all, shadowrate_all, missingrate_all, fcstYdraws,
-    fcstYhat, fcstYcensorDraws, fcstYcensorHat, fcstShadowrateDraws, fcstShadowrateHat,
+    PAI_all, PHI_all, invA_all, sqrtht_all, shadowrate_all, missingrate_all (proposal 1 of the
+    sweep's PS draws, :435, 498; NaN for Gibbs sweeps), fcstYdraws, fcstYhat, fcstYcensorDraws, fcstYcensorHat, fcstShadowrateDraws, fcstShadowrateHat,
     fcstYhatRB, fcstLogscoreDraws, fcstLogscoreXdraws, fcstLogscoreIdraws, stackAccept
     (:630-700).  Indices 0-based."""
     if check_stationarity:
@@ -239,6 +240,7 @@ def mcmcVARshadowrate(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMe
     ch.set_elb_slot(0, bm.elbT0, bm.sNaN)
     if Nproposals:
         ch.set_elb_ps(Nproposals, max(1, -(-burn // 2)))      # m >= MCMCburnin * .5 (:403)
+        ch.keep_missingrate(True)                             # missingrate = proposal 1 (:435, 498)
     ndxY = np.union1d(bm.ndxS, bm.ndxO)
     yields = np.zeros(N, bool)
     yields[ndxY] = True
@@ -259,11 +261,12 @@ def mcmcVARshadowrate(thisT, MCMCdraws, p, np_, data0, ydates0, minnesotaPriorMe
         if stats is not None:
             stats.update(countELBaccept=ps["countAccept"], countELBacceptBurnin=ps["countAcceptBurnin"])
     fc = ch.get_fcst(paths=True) if doPredictiveDensity else None
+    miss = ch.get_missingrate() if Nproposals and bm.elbT else None
     out = ch.get_draws()
     ch.close()
     sr = out.get("shadowrate_all", np.full((MCMCdraws, len(bm.ndxS), 0, B), np.nan))
     res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"], sr,
-           np.full_like(sr, np.nan)]
+           miss[:, :, :bm.elbT] if miss is not None else np.full_like(sr, np.nan)]
     if doPredictiveDensity:
         fYd = fc["paths"].reshape(N, H, fcstNdraws, B, order="F").copy()
         fSd = fYd[ndxY].copy()                                # fcstShadowrateDraws (:640)
@@ -293,7 +296,8 @@ def mcmcVARhybridGibbs(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateWeigh
                        gibbsburn=100, Nproposals=1000, elb_ps=True, stats=None):
     """mcmcVARhybridGibbs.m:1-14, outputs PAI_all (M x K x N, K = 1 + N p + Ns p),
     PHI_all, invA_all, sqrtht_all, shadowrate_all (M x Nshadowrates x elbT),
-    missingrate_all (NaN: it is the first PS proposal, :486); with fcstNdraws the predictive
+    missingrate_all (proposal 1 of each sweep's PS draws, :486; NaN with elb_ps=False); with
+    fcstNdraws the predictive
     density of every kept draw simulated on the device (:566-635) and outputs 7-13 (:703-751):
     fcstYdraws (yields floored at the ELB), fcstYhat, fcstShadowrateDraws, fcstShadowrateHat,
     fcstLogscoreDraws, fcstLogscoreXdraws, fcstLogscoreIdraws.
@@ -333,6 +337,7 @@ def mcmcVARhybridGibbs(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateWeigh
     ch.set_elb_slot(0, hm.elbT0, hm.sNaN)
     if elb_ps and Nproposals:
         ch.set_elb_ps(Nproposals, 1)                   # every sweep (:458)
+        ch.keep_missingrate(True)                      # missingrate = proposal 1 (:486)
     N = m.N
     ndxYIELDS = np.union1d(hm.ndxS, np.asarray(ndxOTHERYIELDS, int))
     if doPredictiveDensity:
@@ -349,11 +354,12 @@ def mcmcVARhybridGibbs(thisT, MCMCdraws, p, np_, data0, ydates0, actualrateWeigh
         stats.update(countELBaccept=ps["countAccept"] + ps["countAcceptBurnin"],
                      stackAccept=ps["stackAccept"])
     fc = ch.get_fcst(paths=True) if doPredictiveDensity else None
+    miss = ch.get_missingrate() if elb_ps and Nproposals and hm.elbT else None
     out = ch.get_draws()
     ch.close()
     sr = out.get("shadowrate_all", np.full((MCMCdraws, len(hm.ndxS), 0, B), np.nan))
     res = [out["PAI_all"], out["PHI_all"], out["invA_all"], out["sqrtht_all"], sr,
-           np.full((MCMCdraws, len(hm.ndxS), hm.elbT, B), np.nan)]
+           miss[:, :, :hm.elbT] if miss is not None else np.full((MCMCdraws, len(hm.ndxS), hm.elbT, B), np.nan)]
     if doPredictiveDensity:
         fYu = fc["paths"].reshape(N, H, fcstNdraws, B, order="F")          # uncensored simulation
         fSd = fYu[ndxYIELDS].copy()                                         # fcstShadowrateDraws (:704)

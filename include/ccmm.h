@@ -330,6 +330,14 @@ int ccmm_chains_set_elb_ps(ccmm_chains* ch, int nproposals, int ps_from_m);
  * (ndxAccept of each stored draw, 0 = no proposal accepted or Gibbs sweep; M = stored draws;
  * call before ccmm_chains_get_draws, which resets the store).  Any pointer may be NULL. */
 int ccmm_chains_get_ps(ccmm_chains* ch, int* countAccept, int* countAcceptBurnin, int* stackAccept);
+/* missingrate_all (mcmcVARshadowrate.m:270, 435, 498; mcmcVARhybridGibbs.m:332, 486): with enable != 0
+ * every stored sweep also keeps proposal 1 of its PS branch (shadowrateProposals(:,:,1): the censored cells
+ * from the sampler, the others the window's data); a sweep that ran the Gibbs branch stores NaN (:406).
+ * Call before the first stored sweep.  get_missingrate: M x Ns x elbTmax x B, NaN beyond a vintage's
+ * window; call before ccmm_chains_get_draws (which resets the store).  The block-hybrid driver keeps
+ * missingrate NaN (doELBsampleAlternate = false, mcmcVARshadowrateBlockHybrid.m:470-478). */
+int ccmm_chains_keep_missingrate(ccmm_chains* ch, int enable);
+int ccmm_chains_get_missingrate(ccmm_chains* ch, double* missingrate_all);
 /* Parity diagnostic of the PS branch: the conditional mean P^-1 b of the censored cells that
  * the last PS sweep's proposals were drawn around (VARTVPSVprecisionsamplerNaN at z = 0,
  * mcmcVARshadowrateBlockHybrid.m:439-441), Ns x elbTmax x B, NaN outside the censored cells

@@ -178,15 +178,16 @@ def ps_shadowrate(bs: BHSetup, PAI, A, sqrtht, zPS):
     """Acceptance-sampling branch of the ELB step (m >= MCMCburnin/2,
     mcmcVARshadowrateBlockHybrid.m:438-460): Nproposals unconstrained draws of the
     censored cells, the first whose censored cells all lie below the ELB is accepted.
-    Returns (shadowrate Ns x elbT or None, ndxAccept 1-based or 0)."""
+    Returns (shadowrate Ns x elbT or None, ndxAccept 1-based or 0, the first proposal
+    shadowrateProposals(:,:,1), which mcmcVARshadowrate.m:435 keeps as missingrate)."""
     N = bs.lin.N
     YY = precision_sampler_nan(*ps_inputs(bs, PAI, A, sqrtht), zPS)
     YY = YY.reshape(N, bs.elbT, -1, order="F")
     props = YY[bs.ndxS, :, :]                                                        # :444
     for k in range(props.shape[2]):                                                  # :446-452
         if np.all(props[:, :, k][bs.sNaN] < bs.ELB):
-            return props[:, :, k], k + 1
-    return None, 0
+            return props[:, :, k], k + 1, props[:, :, 0]
+    return None, 0, props[:, :, 0]
 
 
 def bh_init_state(bs: BHSetup):
@@ -237,8 +238,9 @@ def bh_sweep(st, bs: BHSetup, crn, return_flags=False, elb_impl="qr", use_ps=Fal
         elbY = Y[bs.elbT0:, :].T
         flags = None
         if use_ps:
-            sr, k = ps_shadowrate(bs, PAI, A, sqrtht, crn["zPS"])
+            sr, k, first = ps_shadowrate(bs, PAI, A, sqrtht, crn["zPS"])
             out["ps_accept"] = k
+            out["missingrate"] = first    # shadowrateProposals(:,:,1), mcmcVARshadowrate.m:435
             if k:
                 Xn, Yn = rebuild_XY(bs, sr)
                 out.update(X=Xn, Y=Yn, shadowrate=sr, shadowrate_qr=sr, elb_flags=None,

@@ -111,7 +111,8 @@ def hybrid_draw_crn(rng, hs: HybridSetup, nproposals=0):
 def ps_shadowrate(hs: HybridSetup, PAI, A, sqrtht, zPS):
     """mcmcVARhybridGibbs.m:446-483: PS proposals from the precision sampler
     (ccmm_oracle_bh.precision_sampler_nan) with PAIshadow = PAI(1:Kshadow,:) and the
-    actual-rate lags' fit as intercept; returns (shadowrate or None, ndxAccept)."""
+    actual-rate lags' fit as intercept; returns (shadowrate or None, ndxAccept, the first proposal
+    shadowrateProposals(:,:,1) = missingrate, :486)."""
     from .ccmm_oracle_bh import precision_sampler_nan
     lin = hs.lin
     N, p, Ks = lin.N, lin.p, hs.Kshadow
@@ -129,8 +130,8 @@ def ps_shadowrate(hs: HybridSetup, PAI, A, sqrtht, zPS):
     props = YY[hs.ndxS, :, :]
     for k in range(props.shape[2]):                                                  # :466-471
         if np.all(props[:, :, k][hs.sNaN] < hs.ELB):
-            return props[:, :, k], k + 1
-    return None, 0
+            return props[:, :, k], k + 1, props[:, :, 0]
+    return None, 0, props[:, :, 0]
 
 
 def elb_state_space(hs: HybridSetup, PAI, invA, sqrtht):
@@ -185,8 +186,9 @@ def hybrid_sweep(st, hs: HybridSetup, crn, elb_impl="stable", use_ps=False):
         C, Psi, SVol, Yhatactual = elb_state_space(hs, PAI, invA, sqrtht)
         elbY = Y[hs.elbT0:, :].T
         if use_ps:
-            sr, k = ps_shadowrate(hs, PAI, A, sqrtht, crn["zPS"])
+            sr, k, first = ps_shadowrate(hs, PAI, A, sqrtht, crn["zPS"])
             out["ps_accept"] = k
+            out["missingrate"] = first    # shadowrateProposals(:,:,1), mcmcVARhybridGibbs.m:486
             if k:
                 Xn, Yn = rebuild_XY(hs, sr)
                 out.update(X=Xn, Y=Yn, shadowrate=sr)

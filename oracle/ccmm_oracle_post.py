@@ -45,7 +45,8 @@ def std1(x, axis=0):
 
 def crps_draws(y, draws, axis=-1):
     """crpsDraws(y, draws): CRPS of the empirical distribution of ``draws`` along ``axis``
-    at the realisation y (NaN y gives NaN)."""
+    at the realisation y (NaN y gives NaN).  PARITY UNPINNED: em-matlabbox's crpsDraws source is
+    absent; this is the declared estimator (1 / n^2 normalisation, Gneiting-Raftery eq. 21)."""
     x = np.sort(np.moveaxis(np.asarray(draws, float), axis, -1), axis=-1)
     n = x.shape[-1]
     y = np.asarray(y, float)[..., None]

@@ -4,7 +4,12 @@ ccmm_post.hip: gather, rocPRIM segmented sort, summary kernel) against the oracl
 
 Order statistics (median, quantiles) are compared bit for bit: the kernel reproduces
 numpy's index and interpolation arithmetic.  Sums (mean, std, CRPS) are reduced in a
-different order than numpy's pairwise summation: 1e-13 relative."""
+different order than numpy's pairwise summation: 1e-13 relative.
+
+CRPS parity is UNPINNED: crpsDraws lives in the absent em-matlabbox submodule, so the oracle's
+estimator (the CRPS of the draws' empirical distribution, mean|x - y| - sum_i (2i - n - 1) x_(i) / n^2,
+Gneiting-Raftery eq. 21) is a declared convention that the device matches; an estimator with
+1 / (n (n - 1)) would give different values and no reference output decides between them."""
 import numpy as np
 import pytest
 

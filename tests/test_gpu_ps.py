@@ -227,6 +227,7 @@ def test_ps_hybrid_toy(pkg, ctx, oracle, bh):
     ch.set_elb_model(hs.ndxS, None)
     ch.set_elb_slot(0, hs.elbT0, hs.sNaN)
     ch.set_elb_ps(NP, 1)
+    ch.keep_missingrate(True)
     ch.set_state(*[np.stack([s[k] for s in sts], -1) for k in ("PAI", "A", "sqrtht", "h", "sqrtPHI")])
 
     def flat(crn):
@@ -241,6 +242,7 @@ def test_ps_hybrid_toy(pkg, ctx, oracle, bh):
     got = ch.get_state()
     S = ch.get_shadowrate()
     ps = ch.get_ps()
+    miss = ch.get_missingrate()          # missingrate_all (mcmcVARhybridGibbs.m:486): proposal 1
     n_acc = 0
     for c in range(B):
         st = sts[c]
@@ -248,6 +250,8 @@ def test_ps_hybrid_toy(pkg, ctx, oracle, bh):
         for m in range(nsw):
             st = hy.hybrid_sweep(st, hs, crns[c][m], use_ps=True)
             acc.append(st["ps_accept"])
+            em = rel_err(miss[m, :, :hs.elbT, c], st["missingrate"], 0.1)
+            assert em < 1e-7, (c, m, em)
         n_acc += sum(1 for a in acc if a)
         assert list(ps["stackAccept"][:, c]) == acc, (c, ps["stackAccept"][:, c], acc)
         e = {"PAI": rel_err(got["PAI"][..., c], st["PAI"], 1e-2),
