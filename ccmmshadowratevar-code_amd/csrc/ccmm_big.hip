@@ -117,12 +117,13 @@ __global__ __launch_bounds__(256) void k_gram_big(Dims d, const int* __restrict_
 // diagonal block and its inverse instead (a union: 66.5 KB, two systems per CU).
 constexpr int kCK = 16;  // k columns per pipelined chunk of the update
 constexpr int kLiLd = 65;
-__global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict__ slotIV,
+__global__ __launch_bounds__(256, 2) void k_chol_big(Dims d, const int* __restrict__ slotIV,
                                                      const double* __restrict__ iVdiag, ChainState cs,
                                                      double* __restrict__ rdiag,
                                                      double* __restrict__ Dinv, int skip) {
   // skip: timing-only phase ablation (CCMM_CHOL_SKIP; results invalid): 1 update, 2 factor,
-  // 4 panel
+  // 4 panel; inside the factor phase 8 the 16 x 16 tile factor + inverse, 16 the inverse's
+  // off-diagonal tiles, 32 the trailing tile updates
   __shared__ double smu[2 * kBT * kLiLd];  // update: Bs[2][kCK][kBLd]; factor: Lk | Li
   double* Lk = smu;                        // Lk[i * kLiLd + k] = L_kk(i, k)
   double* Li = smu + kBT * kLiLd;          // Li[j * kLiLd + k] = (L_kk^{-1})(j, k)
@@ -133,12 +134,16 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
   double* A = cs.G + (size_t)mat * KP * KP;
   const double* iv = iVdiag + ((size_t)slotIV[c] * d.N + j) * KP;
   double* rd = rdiag + (size_t)mat * KP;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int lr = lane & 15, lk = lane >> 4;
-  for (int a = tid; a < KP; a += 256) A[(size_t)a * KP + a] += iv[a];
+  const int tid0 = threadIdx.x, wave = tid0 >> 6;
+  for (int a = tid0; a < KP; a += 256) A[(size_t)a * KP + a] += iv[a];
   __syncthreads();
   int bad = 0;
   for (int kb = 0; kb < nb; ++kb) {
+    // lane ids made opaque per block column: the fragment addresses derived from them are then
+    // recomputed where used instead of ~100 of them being hoisted out of this loop and spilled
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, lr = lane & 15, lk = lane >> 4;
     const int kcol = kb * kBT;
     const int nch = kcol / kCK;
     // ---- 1. update of block column kb, four row blocks at a time (one per wave)
@@ -153,13 +158,14 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
         for (int y = 0; y < 4; ++y)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            acc[x][y][r] = A[(size_t)(kcol + y * 16 + lr) * KP + irow + x * 16 + lk + 4 * r];
+            acc[x][y][r] = -A[(size_t)(kcol + y * 16 + lr) * KP + irow + x * 16 + lk + 4 * r];  // -C: the
+      // products add into the negated block (no negated copy of the A fragments), negated back on store
       if (nch > 0) {
-        double an[16], bv[4];
-        // chunk 0 -> registers -> LDS buffer 0
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-          an[q] = A[(size_t)((q >> 2) * 4 + lk) * KP + irow + (q & 3) * 16 + lr];
+        // the shared L(kb, k) chunk is double-buffered in LDS; each wave's own A fragments are
+        // loaded per chunk (a register prefetch of them would exceed the 256 registers that two
+        // systems per CU leave a wave: one system's serial tile factorisation then runs beside
+        // the other's MFMA update)
+        double bv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int e = tid + 256 * q;
@@ -172,15 +178,14 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
         }
         __syncthreads();
         for (int ch = 0; ch < nch; ++ch) {
+          const int kc = ch * kCK;
           double ac[16];
 #pragma unroll
-          for (int q = 0; q < 16; ++q) ac[q] = -an[q];
+          for (int q = 0; q < 16; ++q)
+            ac[q] = A[(size_t)(kc + (q >> 2) * 4 + lk) * KP + irow + (q & 3) * 16 + lr];
           const bool more = ch + 1 < nch;
           if (more) {
             const int k0 = (ch + 1) * kCK;
-#pragma unroll
-            for (int q = 0; q < 16; ++q)
-              an[q] = A[(size_t)(k0 + (q >> 2) * 4 + lk) * KP + irow + (q & 3) * 16 + lr];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int e = tid + 256 * q;
@@ -217,7 +222,7 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
           for (int y = 0; y < 4; ++y)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              A[(size_t)(kcol + y * 16 + lr) * KP + irow + x * 16 + lk + 4 * r] = acc[x][y][r];
+              A[(size_t)(kcol + y * 16 + lr) * KP + irow + x * 16 + lk + 4 * r] = -acc[x][y][r];
       }
     }
     __syncthreads();
@@ -234,10 +239,10 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
       }
       __syncthreads();
       for (int q = 0; q < 4; ++q) {
-        if (wave == 0) {
+        if (wave == 0 && !(skip & 8)) {
           double* Tq = Lk + 16 * q * kLiLd + 16 * q;
           double row[16];
-          double mydiag = 1.0;
+          double rdg = 1.0;  // 1 / L_ii of this lane's row
 #pragma unroll
           for (int m = 0; m < 16; ++m) row[m] = (lane < 16 && m <= lane) ? Tq[lane * kLiLd + m] : 0.0;
 #pragma unroll
@@ -247,11 +252,15 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
               bad = 1;
               dkk = 1.0;
             }
-            const double piv = sqrt(dkk);
-            const double rp = 1.0 / piv;
+            // 1 / sqrt(d): hardware estimate + two Newton steps (no IEEE sqrt / division on
+            // the serial pivot chain); L_kk = d / sqrt(d)
+            double rp = __builtin_amdgcn_rsq(dkk);
+            const double hd = 0.5 * dkk;
+            rp = rp * fma(-hd * rp, rp, 1.5);
+            rp = rp * fma(-hd * rp, rp, 1.5);
             if (lane == kk) {
-              row[kk] = piv;
-              mydiag = piv;
+              row[kk] = dkk * rp;
+              rdg = rp;
             }
             if (lane > kk) row[kk] *= rp;
             const double lik = row[kk];
@@ -264,12 +273,11 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
           if (lane < 16) {
 #pragma unroll
             for (int m = 0; m < 16; ++m) Tq[lane * kLiLd + m] = (m <= lane) ? row[m] : 0.0;
-            rd[kcol + 16 * q + lane] = 1.0 / mydiag;
+            rd[kcol + 16 * q + lane] = rdg;
           }
-          wave_lds_sync();
-          // column c = lane of L_qq^-1 by forward substitution
-          if (lane < 16) {
-            double* Lq = Li + 16 * q * kLiLd + 16 * q;
+          // column c = lane of L_qq^-1 by forward substitution, L_im and 1 / L_ii read from
+          // lane i's registers (no LDS round trip or division on the serial row chain)
+          {
             const int c = lane;
             double x[16];
 #pragma unroll
@@ -277,13 +285,16 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
               double s0 = (i == c) ? 1.0 : 0.0, s1 = 0.0;
 #pragma unroll
               for (int m = 0; m < i; m += 2) {
-                s0 = fma(-Tq[i * kLiLd + m], x[m], s0);
-                if (m + 1 < i) s1 = fma(-Tq[i * kLiLd + m + 1], x[m + 1], s1);
+                s0 = fma(-readlane_d(row[m], i), x[m], s0);
+                if (m + 1 < i) s1 = fma(-readlane_d(row[m + 1], i), x[m + 1], s1);
               }
-              x[i] = (i >= c) ? (s0 + s1) / Tq[i * kLiLd + i] : 0.0;
+              x[i] = (i >= c) ? (s0 + s1) * readlane_d(rdg, i) : 0.0;
             }
+            if (lane < 16) {
+              double* Lq = Li + 16 * q * kLiLd + 16 * q;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) Lq[i * kLiLd + c] = x[i];
+              for (int i = 0; i < 16; ++i) Lq[i * kLiLd + c] = x[i];
+            }
           }
         }
         __syncthreads();
@@ -302,7 +313,7 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
         }
         __syncthreads();
         // trailing tiles A_rs -= L_rq L_sq'  (q < s <= r <= 3)
-        if (q < 3) {
+        if (q < 3 && !(skip & 32)) {
           int pr = 0;
           for (int r = q + 1; r < 4; ++r)
             for (int s2 = q + 1; s2 <= r; ++s2, ++pr) {
@@ -323,7 +334,7 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
         }
       }
       // inverse tiles below the diagonal, by distance (each wave one tile per distance)
-      for (int dist = 1; dist < 4; ++dist) {
+      for (int dist = 1; dist < 4 && !(skip & 16); ++dist) {
         if (wave < 4 - dist) {
           const int qq = wave, r = wave + dist;
           dbl4 sacc = dbl4{0.0, 0.0, 0.0, 0.0};  // S = sum_k L_rk Li_kq, k = q .. r - 1
@@ -358,7 +369,7 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
       for (int e = tid; e < kBT * kBT; e += 256) Dk[e] = Li[(e >> 6) * kLiLd + (e & 63)];
     }
     // ---- 3. panel below: L(r, kb) = C(r, kb) L_kk^{-T} on MFMA, 64-row tiles per wave;
-    //         the tile's C fragments are loaded in two bursts of 32 per lane
+    //         the tile's C fragments are loaded in four bursts of 16 per lane
     for (int rt = kb + 1 + wave; rt < nb && !(skip & 4); rt += 4) {
       const int r0 = rt * kBT;
       dbl4 acc[4][4];
@@ -366,9 +377,9 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
       for (int x = 0; x < 4; ++x)
 #pragma unroll
         for (int y = 0; y < 4; ++y) acc[x][y] = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int half = 0; half < 4; ++half) {
-        double fa[16];
+#pragma unroll 1
+      for (int half = 0; half < 4; ++half) {  // not unrolled: the later bursts' loads would be
+        double fa[16];                        // hoisted and spill the accumulators
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int k = half * 16 + (q >> 2) * 4 + lk;
@@ -397,7 +408,7 @@ __global__ __launch_bounds__(256) void k_chol_big(Dims d, const int* __restrict_
     }
     __syncthreads();
   }
-  if (bad && lane == 0) atomicOr(&cs.status[c], 2);
+  if (bad && (tid0 & 63) == 0) atomicOr(&cs.status[c], 2);
 }
 
 // ============================================================== sequential solve (per chain)
