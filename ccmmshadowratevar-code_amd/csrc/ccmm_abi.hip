@@ -408,7 +408,7 @@ struct ccmm_chains {
     fcst_bh = bh && cf.model != CCMM_MODEL_SHADOWRATE;
     hybrid = cf.model == CCMM_MODEL_HYBRID;
     if (bh) {
-      require(cf.Ns >= 1 && cf.Ns <= kElbNsMax, "Ns must be in [1, 4]");
+      require(cf.Ns >= 1 && cf.Ns <= kElbNsMax, "Ns must be in [1, 5]");
       require(cf.elbTmax >= 0 && cf.elbTmax <= cf.T, "elbTmax must be in [0, T]");
       require(cf.elbTmax < 65536, "elbTmax must be < 65536");  // k_elb_gibbs month list
       require(cf.elb_gibbsburn >= 0, "elb_gibbsburn must be >= 0");
@@ -1297,8 +1297,8 @@ struct ccmm_chains {
         wmax = std::max(wmax, i - first + 1);
       }
     }
-    require(wmax <= kPsWMax, "PS branch: censored-cell band width exceeds 64 (Ns (p + 1) too large)");
-    psW = wmax <= 16 ? 16 : wmax <= 32 ? 32 : wmax <= 48 ? 48 : 64;
+    require(wmax <= kPsWMax, "PS branch: censored-cell band width exceeds 80 (Ns (p + 1) too large)");
+    psW = wmax <= 16 ? 16 : wmax <= 32 ? 32 : wmax <= 48 ? 48 : wmax <= 64 ? 64 : 80;
     ps_nmax = nmax;
     const size_t B = cfg.B;
     eEtPS.alloc(B * ET * cfg.N);
@@ -1369,6 +1369,7 @@ struct ccmm_chains {
         CASE_PSW(32)
         CASE_PSW(48)
         CASE_PSW(64)
+        CASE_PSW(80)
 #undef CASE_PSW
         default:
           throw ArgError("PS band width");
@@ -1414,9 +1415,10 @@ struct ccmm_chains {
         CASE_NSC(2)
         CASE_NSC(3)
         CASE_NSC(4)
+        CASE_NSC(5)
 #undef CASE_NSC
         default:
-          throw ArgError("Ns must be in [1, 4]");
+          throw ArgError("Ns must be in [1, 5]");
       }
     });
     if (ps) run_ps(ra, e, kept);
@@ -1455,8 +1457,9 @@ struct ccmm_chains {
         CASE_NS(2)
         CASE_NS(3)
         CASE_NS(4)
+        CASE_NS(5)
         default:
-          throw ArgError("Ns must be in [1, 4]");
+          throw ArgError("Ns must be in [1, 5]");
       }
 #undef CASE_NS
 #undef GIBBS_K
@@ -1473,7 +1476,7 @@ struct ccmm_chains {
     const int N = cfg.N, p = cfg.p;
     require(cfg.p >= 1 && (cfg.K == N * p + 1 || (hybrid && cfg.K == N * p + 1 + cfg.Ns * p)),
             "predictive density needs K = N*p + 1 (hybrid: + Ns*p)");
-    require(!hybrid || cfg.Ns <= 4, "hybrid predictive density: Ns <= 4");
+    require(!hybrid || cfg.Ns <= kElbNsMax, "hybrid predictive density: Ns <= 5");
     require(N <= kFcstMaxN, "predictive density supports N <= 32");
     require(H >= 1 && Nd >= 1, "H and Nd must be >= 1");
     require(cfg.store_capacity > 0, "predictive density needs store_capacity > 0 (one record per kept draw)");
@@ -2247,7 +2250,7 @@ int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p
       g_err = "dimension mismatch";
       return CCMM_ERR_DIM;
     }
-    require(Ns >= 1 && Ns <= 4, "Ns must be in [1, 4]");
+    require(Ns >= 1 && Ns <= kElbNsMax, "Ns must be in [1, 5]");
     HIPCHECK(hipSetDevice(ctx->device));
     const int K = Ny * p + 1, T = elbT, passes = burnin + Ndraws;
     ccmm_chain_config cf{};

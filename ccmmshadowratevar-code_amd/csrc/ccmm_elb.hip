@@ -25,7 +25,7 @@
 
 namespace ccmm {
 
-constexpr int kElbNsMax = 4;
+constexpr int kElbNsMax = 5;  // Ns = 5: the Krippner / Wu-Xia datasets at ELB > 0.25 (setShadowYields.m:1-5)
 constexpr int kElbColMax = 128;  // 2 p Ns neighbour columns, two per lane
 
 struct ElbDev {

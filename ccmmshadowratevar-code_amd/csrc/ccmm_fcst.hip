@@ -342,9 +342,9 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   if (threadIdx.x < N) sy[threadIdx.x] = yg[threadIdx.x];
   const double* invA = sinvA;
   const double* y = sy;
-  int hs[4] = {-1, -1, -1, -1};  // hybrid: indices of the shadow-rate variables
+  int hs[kElbNsMax] = {-1, -1, -1, -1, -1};  // hybrid: indices of the shadow-rate variables
   if (hy)
-    for (int q = 0; q < a.Ns && q < 4; ++q) hs[q] = a.ndxS[q];
+    for (int q = 0; q < a.Ns && q < kElbNsMax; ++q) hs[q] = a.ndxS[q];
   const int tsv = a.svT ? a.svT[sl] - 1 : 0;
   const double* svz = a.svz ? a.svz + (size_t)c * a.crnStride : nullptr;
   const double* zc = a.z ? a.z + (size_t)c * a.crnStride : nullptr;
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         double cv = Xj[1 + e];
         if (a.bh == 1 && a.ndxYields[j]) cv = Xj[K + e];
         if (hy)
-          for (int q = 0; q < a.Ns && q < 4; ++q)
+          for (int q = 0; q < a.Ns && q < kElbNsMax; ++q)
             if (hs[q] == j) cv = Xj[K + l * a.Ns + q];
         ringc[slot * N + j] = cv;
       }
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
           const double* pc = col + 1 + l * N;
           for (int j = 0; j < N; ++j) { sl2 += pc[j] * rl[j]; sc += pc[j] * rc[j]; }
           if (hy)  // fcstA(ndxfcstY, Kshadow+1:end) on the actual-rate ring (:626)
-            for (int q = 0; q < a.Ns && q < 4; ++q) sl2 += col[K + l * a.Ns + q] * rc[hs[q]];
+            for (int q = 0; q < a.Ns && q < kElbNsMax; ++q) sl2 += col[K + l * a.Ns + q] * rc[hs[q]];
         }
         if (hy) {
           yl = sl2 + nu;

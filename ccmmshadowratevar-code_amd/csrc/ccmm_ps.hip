@@ -24,7 +24,7 @@
 
 namespace ccmm {
 
-constexpr int kPsWMax = 64;  // band width limit: Ns (p + 1) <= 64 (Ns = 4 with p = 12: 52)
+constexpr int kPsWMax = 80;  // band width limit: Ns (p + 1) <= 80 (Ns = 5 with p = 12: 65)
 
 struct PsDev {
   int nmax, W, NP;  // max censored cells over slots, band width, proposals per sweep

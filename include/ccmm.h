@@ -188,7 +188,7 @@ typedef struct {
   double logy2offset;     /* getKSC7values offset (ext; this build declares 1e-3) */
   uint64_t seed;          /* Philox key */
   /* CCMM_MODEL_BLOCKHYBRID only (ignored otherwise) */
-  int Ns;                 /* number of shadow-rate variables, 1..4 (Nshadowrates) */
+  int Ns;                 /* number of shadow-rate variables, 1..5 (Nshadowrates; 5 with the Krippner / Wu-Xia data at ELB > 0.25) */
   int elbTmax;            /* max over data slots of elbT = T - elbT0 */
   int elb_gibbsburn;      /* Gibbs burn-in passes per sweep (gibbsdrawShadowrates call, :436: 100) */
   double elb;             /* ELBbound */
@@ -323,7 +323,7 @@ int ccmm_chains_set_elb_slot(ccmm_chains* ch, int slot, int elbT0, const uint8_t
  * gibbsdrawShadowrates serves the sweep (:462-463).  CRN mode appends randn(nmiss,
  * nproposals) (block CCMM_RNG_PS, nmiss x nproposals column-major, sized Ns elbTmax
  * nproposals) to every sweep's record.  nproposals = 0: Gibbs every sweep (default).
- * Requires Ns (p + 1) <= 64. */
+ * Requires Ns (p + 1) <= 80. */
 int ccmm_chains_set_elb_ps(ccmm_chains* ch, int nproposals, int ps_from_m);
 /* PS bookkeeping (:303-305, 453-460): countAccept / countAcceptBurnin B ints since set_state
  * (sweeps whose proposal was accepted after / during burn-in), stackAccept M x B ints
