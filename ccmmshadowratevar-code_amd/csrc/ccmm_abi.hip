@@ -1351,7 +1351,7 @@ struct ccmm_chains {
     require(lds <= 160 * 1024, "PS branch: cell list does not fit LDS");
     launch(KID_PSCHOL, [&] {
       HIPCHECK(hipFuncSetAttribute((const void*)k_ps_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(k_ps_chol, dim3(d.B), dim3(64), lds, ctx->stream, d, e, ps, cs);
+      hipLaunchKernelGGL(k_ps_chol, dim3(d.B), dim3(psW > 64 ? 128 : 64), lds, ctx->stream, d, e, ps, cs);
     });
     if (ps.first) {  // proposal 1's uncensored cells are the window's data (the chain's current Y)
       HIPCHECK(hipMemcpyAsync(psFirst.p, e.Scur, (size_t)d.B * ps.per * sizeof(double), hipMemcpyDeviceToDevice,

@@ -88,7 +88,7 @@ __device__ double bvnu(double dh, double dk, double r, const GLNodes& gl) {
       sn = sin(asr * (-gl.x[ng][i] + 1.0) * 0.5);
       bvn += gl.w[ng][i] * exp((sn * hk - hs) / (1.0 - sn * sn));
     }
-    return bvn * asr / (2.0 * twopi) + ncdf(-h) * ncdf(-k);
+    return fmax(0.0, fmin(1.0, bvn * asr / (2.0 * twopi) + ncdf(-h) * ncdf(-k)));
   }
   if (r < 0) { k = -k; hk = -hk; }
   if (ar < 1.0) {
@@ -114,10 +114,14 @@ __device__ double bvnu(double dh, double dk, double r, const GLNodes& gl) {
     }
     bvn = -bvn / twopi;
   }
-  if (r > 0) return bvn + ncdf(-fmax(h, k));
+  // the result clamped to [0, 1] as Genz's BVNU returns it (BVNU = MAX(0, MIN(1, BVN))) and
+  // MATLAB's bivariate mvncdf with it: far in the tails the cancellation below can leave a
+  // probability of order -1e-17, whose log would turn the draw's score (and the vintage's log
+  // mean exp) into NaN
+  if (r > 0) return fmax(0.0, fmin(1.0, bvn + ncdf(-fmax(h, k))));
   bvn = -bvn;
   if (k > h) bvn += ncdf(k) - ncdf(h);
-  return bvn;
+  return fmax(0.0, fmin(1.0, bvn));
 }
 
 // Trivariate normal P(X <= x), X ~ N(0, L L') with L lower 3x3 (ld kFcstMaxN at M):
@@ -179,7 +183,7 @@ __device__ double tvn_cdf(const double* x, const double* M, const GLNodes& gl, i
     const double h = (x[1] - l21 * z) / l22, k = (x[2] - l31 * z) / s3;
     acc += gl.w[2][i] * exp(-0.5 * z * z) * bvnu(-h, -k, rho, gl) * r;
   }
-  return wave_sum(acc) * 0.39894228040143267794;
+  return fmax(0.0, fmin(1.0, wave_sum(acc) * 0.39894228040143267794));  // Genz TVNU: MAX(0, MIN(1, TVN))
 }
 
 // in-place lower Cholesky of an n x n LDS matrix (ld = kFcstMaxN); false if not SPD.

@@ -42,11 +42,12 @@ struct PsDev {
 };
 
 // ---------------------------------------------------------------- banded Cholesky
-__global__ __launch_bounds__(64) void k_ps_chol(Dims d, ElbDev e, PsDev ps, ChainState cs) {
+// One thread per band row (64 threads, 128 for band widths above 64: Ns = 5 with p = 12)
+__global__ __launch_bounds__(128) void k_ps_chol(Dims d, ElbDev e, PsDev ps, ChainState cs) {
   extern __shared__ double sm[];
   const int c = blockIdx.x;
   const int s = cs.slot[c];
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x, nth = blockDim.x;
   const int Ns = e.Ns, p = e.p, N = d.N, W = ps.W;
   const int nc = e.ncens[s];
   double* win = sm;                 // W x W: A(row, col) at [(row % W) W + col % W]
@@ -65,7 +66,7 @@ __global__ __launch_bounds__(64) void k_ps_chol(Dims d, ElbDev e, PsDev ps, Chai
   }
   __syncthreads();
   const int n = sn;
-  for (int i = lane; i < n; i += 64) {
+  for (int i = lane; i < n; i += nth) {
     const int ci = info[i] >> 3, a = info[i] & 7;
     ps.cell[(size_t)c * ps.nmax + i] = e.cens[(size_t)s * e.elbTmax + ci] * Ns + a;
   }
@@ -89,7 +90,7 @@ __global__ __launch_bounds__(64) void k_ps_chol(Dims d, ElbDev e, PsDev ps, Chai
     const int ci = info[i] >> 3, ai = info[i] & 7;
     return recs[(size_t)ci * e.condStride + xo + Ns * Ns + ai];
   };
-  for (int q = lane; q < W * W; q += 64) {
+  for (int q = lane; q < W * W; q += nth) {
     const int r = q / W, cc = q % W;
     win[q] = (cc <= r && r < n) ? pentry(r, cc) : 0.0;
   }
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(64) void k_ps_chol(Dims d, ElbDev e, PsDev ps, Chai
   for (int k = 0; k < n; ++k) {
     const int r = lane;
     const double v = (r < W && k + r < n) ? win[((k + r) % W) * W + k % W] : 0.0;
-    const double dkk = readlane_d(v, 0);
+    const double dkk = win[(k % W) * W + k % W];  // row 0's v, read by every wave
     fail |= !(dkk > 0.0);
     const double lkk = sqrt(fabs(dkk) > 0.0 ? fabs(dkk) : 1.0);
     const double l = (r == 0) ? lkk : v / lkk;
