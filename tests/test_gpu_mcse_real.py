@@ -2,8 +2,9 @@
 N = 20, p = 12, T = 750, K = 241): posterior means from 128 Philox device chains against long
 oracle chains committed as tests/golden/mcse_real_{linear,bh}.npz (tools/
 make_mcse_real_fixture.py: 1000 burn-in + 2000 kept sweeps per chain, Geweke NSE with the 15 %
-taper of Diagnostics.m:134-300; bh pools seven independent chains, whose between-chain spread
-bounds the oracle's standard error from below), the device chains averaging the same window of
+taper of Diagnostics.m:134-300; each fixture pools seven independent chains, whose between-chain
+spread bounds the oracle's standard error from below: one linear chain's spectral NSE understates
+the spread of the seven chain means by up to 2.3x), the device chains averaging the same window of
 sweeps.
 
   linear  configs[1] / SURVEY §8d C2: mcmcVAR.m sweeps from the reference initialisation.

@@ -24,7 +24,8 @@ Several independent chains (the bh intercepts mix slowly: effective sample size 
 --part-out FILE (in parallel processes), then --merge FILE ... pools them: the mean of the
 chain means, NSE = sqrt(sum NSE_i^2) / nchains, plus the between-chain standard error.  The
 committed bh fixture pools seeds 20243 and 30001-30006 (their part files:
-tests/golden/mcse_bh_parts/)."""
+tests/golden/mcse_bh_parts/), the linear one seeds 20243 and 40001-40006
+(tests/golden/mcse_linear_parts/)."""
 import argparse
 import sys
 import time
