@@ -133,6 +133,8 @@ _SIGS = {
                             _dp, C.c_uint64, _dp]),
     "ccmm_chains_summaries": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, _u8p, _dp, C.c_int, _dp,
                                         _dp, _dp, _dp, _dp, _dp]),
+    "ccmm_chains_summaries_floor": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, _u8p, _u8p, C.c_double, _dp,
+                                              C.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
     "ccmm_chains_get_ps": (C.c_int, [C.c_void_p, _ip, _ip, _ip]),
     "ccmm_chains_get_ps_mean": (C.c_int, [C.c_void_p, _dp]),
     "ccmm_chains_keep_missingrate": (C.c_int, [C.c_void_p, C.c_int]),
@@ -822,9 +824,10 @@ class Chains:
         _check(self.lib.ccmm_chains_get_ps_mean(self.handle, _ptr(out)), "ccmm_chains_get_ps_mean")
         return out
 
-    def summaries(self, source, slot, rows=None, cumcode=None, realized=None, pct=()):
+    def summaries(self, source, slot, rows=None, cumcode=None, realized=None, pct=(), floor_rows=None, floor=0.0):
         """Device summaries of the kept draws of data slot ``slot`` (ccmm_chains_summaries):
-        source 0 paths / 1 censored paths (series = rows x H) / 2 PAI (K x N)."""
+        source 0 paths / 1 censored paths (series = rows x H) / 2 PAI (K x N).  floor_rows (N
+        bools): those variables' paths floored at ``floor`` first (ccmm_chains_summaries_floor)."""
         N = self.N
         if source in (0, 1):
             nr = N if rows is None else int(np.count_nonzero(rows))
@@ -841,6 +844,16 @@ class Chains:
             out["crps"] = np.zeros(S)
         rw = None if rows is None else np.ascontiguousarray(np.asarray(rows, bool), dtype=np.uint8)
         cc = None if cumcode is None else np.ascontiguousarray(np.asarray(cumcode, bool), dtype=np.uint8)
+        if floor_rows is not None:
+            fr = np.ascontiguousarray(np.asarray(floor_rows, bool), dtype=np.uint8)
+            assert fr.size == N
+            _check(self.lib.ccmm_chains_summaries_floor(
+                self.handle, int(source), int(slot), None if rw is None else rw.ctypes.data_as(_u8p),
+                None if cc is None else cc.ctypes.data_as(_u8p), fr.ctypes.data_as(_u8p), float(floor), _ptr(rz),
+                pct.size, _ptr(pct) if pct.size else None, _ptr(out["mean"]), _ptr(out["median"]),
+                _ptr(out["quantiles"]) if pct.size else None, _ptr(out["stdev"]), _ptr(out.get("crps"))),
+                "ccmm_chains_summaries_floor")
+            return out
         _check(self.lib.ccmm_chains_summaries(
             self.handle, int(source), int(slot), None if rw is None else rw.ctypes.data_as(_u8p),
             None if cc is None else cc.ctypes.data_as(_u8p), _ptr(rz), pct.size,

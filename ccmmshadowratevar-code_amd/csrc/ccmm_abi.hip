@@ -1537,9 +1537,10 @@ struct ccmm_chains {
   DBuf<double> postA, postB, postOut;
   DBuf<char> postWs;
   DBuf<int> postRows;
-  DBuf<uint8_t> postCum;
-  void summaries(int source, int sl, const uint8_t* rows, const uint8_t* cumcode, const double* realized, int nq,
-                 const double* pct, double* mean, double* median, double* quant, double* sdev, double* crps) {
+  DBuf<uint8_t> postCum, postFlo;
+  void summaries(int source, int sl, const uint8_t* rows, const uint8_t* cumcode, const uint8_t* flo, double fl,
+                 const double* realized, int nq, const double* pct, double* mean, double* median, double* quant,
+                 double* sdev, double* crps) {
     require(sl >= 0 && sl < cfg.ndata, "slot out of range");
     require(nq >= 0 && (nq == 0 || pct), "bad quantile list");
     std::vector<int> hs(cfg.B);
@@ -1569,12 +1570,17 @@ struct ccmm_chains {
         postCum.alloc(N);
         HIPCHECK(hipMemcpy(postCum.p, cumcode, N, hipMemcpyHostToDevice));
       }
+      if (flo) {
+        postFlo.alloc(N);
+        HIPCHECK(hipMemcpy(postFlo.p, flo, N, hipMemcpyHostToDevice));
+      }
       postA.alloc((size_t)S * n);
       HIPCHECK(post_gather_fcst(ctx->stream, source == 0 ? fPaths.p : fPathsC.p, c0, C, fstored, fNd, fH, N,
                                 cfg.store_capacity, postRows.p, (int)rl.size(), cumcode ? postCum.p : nullptr,
-                                postA.p));
+                                flo ? postFlo.p : nullptr, fl, postA.p));
     } else if (source == 2) {
       require(stored > 0 && sPAI.p, "no stored draws");
+      require(!flo, "a floor applies to forecast paths only");
       S = K * N;
       n = C * stored;
       postA.alloc((size_t)S * n);
@@ -2878,7 +2884,22 @@ int ccmm_chains_summaries(ccmm_chains* ch, int source, int slot, const uint8_t* 
     require(ch != nullptr, "null argument");
     HIPCHECK(hipSetDevice(ch->ctx->device));
     HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
-    ch->summaries(source, slot, rows, cumcode, realized, nq, pct, mean, median, quantiles, stdev, crps);
+    ch->summaries(source, slot, rows, cumcode, nullptr, 0.0, realized, nq, pct, mean, median, quantiles, stdev,
+                  crps);
+    return 0;
+  });
+}
+
+int ccmm_chains_summaries_floor(ccmm_chains* ch, int source, int slot, const uint8_t* rows, const uint8_t* cumcode,
+                                const uint8_t* floor_rows, double floor, const double* realized, int nq,
+                                const double* pct, double* mean, double* median, double* quantiles, double* stdev,
+                                double* crps) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+    ch->summaries(source, slot, rows, cumcode, floor_rows, floor, realized, nq, pct, mean, median, quantiles, stdev,
+                  crps);
     return 0;
   });
 }

@@ -386,10 +386,12 @@ __global__ __launch_bounds__(1024) void k_phi_big(Dims d, const int* __restrict_
 // with 16-wide panels, the inverse built row block by row block as the panels complete.
 //   panel i (rows p0 .. p0+15):
 //     wave 0: factor the diagonal block, invert it (Dv_i) and store Dv_i over it
-//     all:    L(r, panel) = S(r, panel) Dv_i' for the rows below;
-//             T = L(block i, 0:p0) Linv(0:p0, 0:p0)                   (2 x 2 tiles, Tb)
+//     all:    L(r, panel) = S(r, panel) Dv_i' for the blocks below;
+//             T = L(block i, 0:p0) Linv(0:p0, 0:p0)                   (Tb)
 //     all:    trailing update;  Linv(block i, 0:p0) = -Dv_i T
-// Only the lower triangle is read or written.  Tb: LDS scratch, kCB x 128 doubles.
+// The block products run on MFMA, one 16 x 16 block per wave.  Only the lower triangle is read
+// (the upper triangle of S may hold anything; diagonal blocks are masked).  Tb: LDS scratch,
+// kCB x 128 doubles.
 constexpr int kCB = 16;
 
 template <int NT>
@@ -446,86 +448,82 @@ __device__ void wg_chol_inv(double* S, int n, double* Tb, int* bad) {
           if (m <= lane) S[(p0 + lane) * kNL + p0 + m] = dv[m];
     }
     __syncthreads();
-    const double* Dv = S + p0 * kNL + p0;  // Dv(r, q) = Dv[r * kNL + q], q <= r
-    // (a) panel rows below: L(r, p0 + m) = sum_{q <= m} S(r, p0 + q) Dv(m, q)
-    for (int r = p0 + pw + tid; r < n; r += NT) {
-      double x[kCB];
+    // 16 x 16 blocks on v_mfma_f64_16x16x4 (A(lr, lq), B(lq, lr), D(lq + 4 r, lr)), one block task
+    // per wave round robin; Dv(r, q) = S(p0 + r, p0 + q), q <= r
+    const int lr = lane & 15, lq = lane >> 4;
+    const int NB = (n + 15) >> 4, pb = p0 >> 4;
+    // (a) L(I, pb) = S(I, pb) Dv', I > pb;  (b) T(J) = sum_{K=J}^{pb-1} L(pb, K) Linv(K, J), J < pb
+    const int na = NB - 1 - pb;
+    for (int task = wave; task < na + pb; task += NT / 64) {
+      dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+      if (task < na) {
+        const int I = pb + 1 + task, r = 16 * I + lr;
 #pragma unroll
-      for (int q = 0; q < kCB; ++q) x[q] = (q < pw) ? S[r * kNL + p0 + q] : 0.0;
-#pragma unroll
-      for (int m = 0; m < kCB; ++m) {
-        if (m < pw) {
-          double sacc = 0.0;
-#pragma unroll
-          for (int q = 0; q <= m; ++q) sacc = fma(x[q], Dv[m * kNL + q], sacc);
-          S[r * kNL + p0 + m] = sacc;
+        for (int kk = 0; kk < 4; ++kk) {
+          const int q = 4 * kk + lq;
+          const double x = (r < n && q < pw) ? S[r * kNL + p0 + q] : 0.0;
+          const double y = (q <= lr && lr < pw) ? S[(p0 + lr) * kNL + p0 + q] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
         }
-      }
-    }
-    // (b) T(r, j) = sum_{k = j}^{p0-1} L(p0 + r, k) Linv(k, j), 2 x 2 tiles over (r, j)
-    const int tr = (pw + 1) / 2, tc = p0 / 2;
-    for (int e = tid; e < tr * tc; e += NT) {
-      const int r0 = 2 * (e / tc), j0 = 2 * (e % tc);
-      const int ra = p0 + r0, rb = p0 + min(r0 + 1, pw - 1);
-      double t00 = 0.0, t01 = 0.0, t10 = 0.0, t11 = 0.0;
-      {  // k = j0: Linv(j0, j0 + 1) = 0
-        const double la = S[ra * kNL + j0], lb = S[rb * kNL + j0], v0 = S[j0 * kNL + j0];
-        t00 = la * v0;
-        t10 = lb * v0;
-      }
-      for (int k = j0 + 1; k < p0; ++k) {
-        const double la = S[ra * kNL + k], lb = S[rb * kNL + k];
-        const double v0 = S[k * kNL + j0], v1 = S[k * kNL + j0 + 1];
-        t00 = fma(la, v0, t00);
-        t01 = fma(la, v1, t01);
-        t10 = fma(lb, v0, t10);
-        t11 = fma(lb, v1, t11);
-      }
-      Tb[r0 * 128 + j0] = t00;
-      Tb[r0 * 128 + j0 + 1] = t01;
-      if (r0 + 1 < pw) {
-        Tb[(r0 + 1) * 128 + j0] = t10;
-        Tb[(r0 + 1) * 128 + j0 + 1] = t11;
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int row = 16 * I + lq + 4 * r4;
+          if (row < n && lr < pw) S[row * kNL + p0 + lr] = acc[r4];
+        }
+      } else {
+        const int J = task - na;
+        for (int K = J; K < pb; ++K)
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int q = 4 * kk + lq;
+            const double x = (lr < pw) ? S[(p0 + lr) * kNL + 16 * K + q] : 0.0;
+            const double y = (K > J || lr <= q) ? S[(16 * K + q) * kNL + 16 * J + lr] : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
+          }
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) Tb[(lq + 4 * r4) * 128 + 16 * J + lr] = acc[r4];
       }
     }
     __syncthreads();
-    // (c) trailing update, 4 x 4 tiles: S(i, j) -= L(i, panel) . L(j, panel)
-    const int r0 = p0 + pw, nr = n - r0;
-    const int mt = (nr + 3) / 4, ntile = mt * (mt + 1) / 2;
-    for (int tile = tid; tile < ntile; tile += NT) {
-      int ti = 0, tj = tile;
-      while (tj > ti) {
-        tj -= ti + 1;
-        ++ti;
-      }
-      const int a0 = r0 + 4 * ti, b0 = r0 + 4 * tj;
-      double acc[16];
+    // (c) S(I, I2) -= L(I, pb) L(I2, pb)', pb < I2 <= I;  (d) Linv(pb, J) = -Dv T(J), J < pb
+    const int mb = NB - 1 - pb, nc = mb * (mb + 1) / 2;
+    for (int task = wave; task < nc + pb; task += NT / 64) {
+      dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+      if (task < nc) {
+        int x0 = 0, y0 = task;
+        while (y0 > x0) {
+          y0 -= x0 + 1;
+          ++x0;
+        }
+        const int I = pb + 1 + x0, I2 = pb + 1 + y0;
+        const int ra = 16 * I + lr, rb = 16 * I2 + lr;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[e] = 0.0;
-      for (int m = 0; m < pw; ++m) {
-        double la[4], lb[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          la[i] = S[min(a0 + i, n - 1) * kNL + p0 + m];
-          lb[i] = S[min(b0 + i, n - 1) * kNL + p0 + m];
+        for (int kk = 0; kk < 4; ++kk) {
+          const int q = 4 * kk + lq;
+          const double x = (ra < n && q < pw) ? S[ra * kNL + p0 + q] : 0.0;
+          const double y = (rb < n && q < pw) ? S[rb * kNL + p0 + q] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int row = 16 * I + lq + 4 * r4;
+          if (row < n && rb < n) S[row * kNL + rb] -= acc[r4];
+        }
+      } else {
+        const int J = task - nc;
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) acc[i * 4 + jj] = fma(la[i], lb[jj], acc[i * 4 + jj]);
+        for (int kk = 0; kk < 4; ++kk) {
+          const int q = 4 * kk + lq;
+          const double x = (q <= lr && lr < pw) ? S[(p0 + lr) * kNL + p0 + q] : 0.0;
+          const double y = (q < pw) ? Tb[q * 128 + 16 * J + lr] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int row = p0 + lq + 4 * r4;
+          if (row < n) S[row * kNL + 16 * J + lr] = -acc[r4];
+        }
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-          if (a0 + i < n && b0 + jj <= a0 + i) S[(a0 + i) * kNL + b0 + jj] -= acc[i * 4 + jj];
-    }
-    // (d) Linv(p0 + r, j) = -sum_{q <= r} Dv(r, q) T(q, j), j < p0
-    for (int e = tid; e < pw * p0; e += NT) {
-      const int r = e / p0, j = e - r * p0;
-      double v = 0.0;
-      for (int q = 0; q <= r; ++q) v = fma(Dv[r * kNL + q], Tb[q * 128 + j], v);
-      S[(p0 + r) * kNL + j] = -v;
     }
     __syncthreads();
   }
@@ -534,7 +532,8 @@ __device__ void wg_chol_inv(double* S, int n, double* Tb, int* bad) {
 // ================================================================ SV (time-ordered sampler)
 // Per chain (kSvNT threads).  scratch per chain (row-major, ld N): Q = PHI^{-1}; Lt[t] =
 // L_t^{-1}; Mt[t] = M_t = L_{t-1}^{-1} Q; w[t].  Per block t:
-//   M_t = Linv_{t-1} Q (GEMM, Linv_{t-1} in LDS)   -> G = M_t' M_t (Gram, into LDS)
+//   M_t = Linv_{t-1} Q (MFMA, Linv_{t-1} in LDS, Q in registers) -> LDS over Linv_{t-1}
+//   G = M_t' M_t (MFMA from LDS, in registers)
 //   S = D_t - G, r = b_t + M_t' w_{t-1}             -> Linv_t = chol(S)^{-1} (wg_chol_inv)
 //   w_t = Linv_t r
 // backward: x_t = Linv_t' (w_t + z_t + M_{t+1} x_{t+1}).
@@ -587,72 +586,124 @@ __global__ __launch_bounds__(kSvNT) void k_sv_big(Dims d, const int* __restrict_
     __syncthreads();
   }
   const double* V0 = V0inv + (size_t)s * NN;
-  const int nt4 = (N + 3) / 4;
+  // MFMA operands (v_mfma_f64_16x16x4: A(lr, lq), B(lq, lr), D(lq + 4 r, lr)); N <= 128 is NB <= 8
+  // blocks of 16.  Wave J owns column block J of M_t = Linv_{t-1} Q: Q's column block is the same
+  // at every step, so it stays in registers for the whole forward pass (qb[4 K + kk] = Q(16 K +
+  // 4 kk + lq, 16 J + lr)).
+  const int wave = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int NB = (N + 15) >> 4;
+  double qb[32];
+#pragma unroll
+  for (int K = 0; K < 8; ++K)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int r = 16 * K + 4 * kk + lq, col = 16 * wave + lr;
+      qb[4 * K + kk] = (r < N && col < N) ? Q[r * N + col] : 0.0;
+    }
   // ---- forward: t = 0 .. T.  Entering step t >= 1 the LDS matrix holds Linv_{t-1}.
   for (int t = 0; t <= T; ++t) {
     double* Mcur = Mt + (size_t)t * NN;
     if (t > 0) {
-      if (!(skip & 1)) {
-        // M_t = Linv_{t-1} Q, 4 x 4 tiles (Linv lower: k <= row)
-        for (int tile = tid; tile < nt4 * nt4; tile += NT) {
-          const int i0 = 4 * (tile / nt4), j0 = 4 * (tile % nt4);
-          double acc[16];
+      // M_t = Linv_{t-1} Q: block (I, J) = sum_{K <= I} Linv(I, K) Q(K, J) (Linv lower), each
+      // block straight to global Mt[t]; the LDS copy replaces Linv_{t-1} after the barrier
+      if (wave < NB && !(skip & 1)) {
+        const int col = 16 * wave + lr;
+#pragma unroll 1
+        for (int I = 0; I < NB; ++I) {
+          dbl4 mb = dbl4{0.0, 0.0, 0.0, 0.0};
+          const int r = 16 * I + lr;
 #pragma unroll
-          for (int e = 0; e < 16; ++e) acc[e] = 0.0;
-          const int kend = min(i0 + 4, N);
-          for (int k = 0; k < kend; ++k) {
-            double a[4], b[4];
+          for (int K = 0; K < 8; ++K)
+            if (K <= I) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int i = min(i0 + r, N - 1);
-              a[r] = (k <= i0 + r) ? S[i * kNL + k] : 0.0;
-              b[r] = Q[k * N + min(j0 + r, N - 1)];
+              for (int kk = 0; kk < 4; ++kk) {
+                const int cix = 16 * K + 4 * kk + lq;
+                const double a = (r < N && cix <= r) ? S[r * kNL + cix] : 0.0;
+                mb = __builtin_amdgcn_mfma_f64_16x16x4f64(a, qb[4 * K + kk], mb, 0, 0, 0);
+              }
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-              for (int cc = 0; cc < 4; ++cc) acc[r * 4 + cc] = fma(a[r], b[cc], acc[r * 4 + cc]);
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const int row = 16 * I + lq + 4 * r4;
+            if (row < N && col < N) Mcur[row * N + col] = mb[r4];
           }
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc)
-              if (i0 + r < N && j0 + cc < N) Mcur[(i0 + r) * N + j0 + cc] = acc[r * 4 + cc];
         }
       }
+      __syncthreads();  // every read of Linv_{t-1} (kept in global Lt[t-1]) is done
+      for (int e = tid; e < N * N; e += NT) {
+        const int a = e / N, b = e - a * N;
+        S[a * kNL + b] = Mcur[e];
+      }
       __syncthreads();
-      // G = M_t' M_t into the LDS matrix (Linv_{t-1} is kept in global Lt[t-1])
-      if (!(skip & 2)) wg_gram<NT>(S, Mcur, 1, N, N, N, nullptr, 0);
-    }
-    // S = D_t - G, D_0 = V0inv + Q, D_t = 2Q + diag(ir_t) (t < T), D_T = Q + diag(ir_T)
-    for (int e = tid; e < N * N; e += NT) {
-      const int a = e / N, b = e - a * N;
-      if (b > a) continue;
-      double v;
-      if (t == 0) {
-        v = V0[a + b * N] + Q[e];
-      } else {
-        v = (t == T ? 1.0 : 2.0) * Q[e];
-        if (a == b) v += irv[(size_t)a * TP + t - 1];
-        v -= S[a * kNL + b];
+      // G = M_t' M_t, lower blocks (A, B), B <= A, round robin over the waves; the rhs
+      // b_t = obs_t ir_t + M_t' w_{t-1} (8 lanes per entry) from the same LDS copy of M_t
+      dbl4 g[5];
+      const int npair = NB * (NB + 1) / 2;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        g[j] = dbl4{0.0, 0.0, 0.0, 0.0};
+        const int pr = wave + 8 * j;
+        if (pr < npair && !(skip & 2)) {
+          int A = 0, Bb = pr;
+          while (Bb > A) {
+            Bb -= A + 1;
+            ++A;
+          }
+          const int ca = 16 * A + lr, cb = 16 * Bb + lr;
+          for (int I = 0; I < NB; ++I)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+              const int k = 16 * I + 4 * kk + lq;
+              const double a = (k < N && ca < N) ? S[k * kNL + ca] : 0.0;
+              const double b = (k < N && cb < N) ? S[k * kNL + cb] : 0.0;
+              g[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, g[j], 0, 0, 0);
+            }
+        }
       }
-      S[a * kNL + b] = v;
-    }
-    // rhs: b_0 = V0inv h0mean; b_t = obs_t ir_t + M_t' w_{t-1} (8 lanes per entry)
-    if (t == 0) {
-      for (int a = tid; a < N; a += NT) vec[a] = V0invm[(size_t)s * N + a];
+      {
+        const double* wp = wv + (size_t)(t - 1) * N;
+        for (int a0 = 0; a0 < N; a0 += NT / 8) {
+          const int a = a0 + gj;
+          double v = 0.0;
+          if (a < N)
+            for (int i = gq; i < N; i += 8) v = fma(S[i * kNL + a], wp[i], v);
+          v += dpp_d<0xB1>(v);
+          v += dpp_d<0x4E>(v);
+          v += dpp_d<0x141>(v);
+          if (a < N && gq == 0) vec[a] = v + obs[(size_t)a * TP + t - 1] * irv[(size_t)a * TP + t - 1];
+        }
+      }
+      __syncthreads();  // every read of M_t in LDS is done
+      // S = D_t - G, D_t = 2Q + diag(ir_t) (t < T), D_T = Q + diag(ir_T)
+      const double qf = (t == T) ? 1.0 : 2.0;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int pr = wave + 8 * j;
+        if (pr < npair) {
+          int A = 0, Bb = pr;
+          while (Bb > A) {
+            Bb -= A + 1;
+            ++A;
+          }
+          const int b = 16 * Bb + lr;
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const int a = 16 * A + lq + 4 * r4;
+            if (a < N && b <= a) {
+              double v = qf * Q[a * N + b] - g[j][r4];
+              if (a == b) v += irv[(size_t)a * TP + t - 1];
+              S[a * kNL + b] = v;
+            }
+          }
+        }
+      }
     } else {
-      const double* wp = wv + (size_t)(t - 1) * N;
-      for (int a0 = 0; a0 < N; a0 += NT / 8) {
-        const int a = a0 + gj;
-        double v = 0.0;
-        if (a < N)
-          for (int i = gq; i < N; i += 8) v = fma(Mcur[i * N + a], wp[i], v);
-        v += dpp_d<0xB1>(v);
-        v += dpp_d<0x4E>(v);
-        v += dpp_d<0x141>(v);
-        if (a < N && gq == 0) vec[a] = v + obs[(size_t)a * TP + t - 1] * irv[(size_t)a * TP + t - 1];
+      // S = D_0 = V0inv + Q; b_0 = V0inv h0mean
+      for (int e = tid; e < N * N; e += NT) {
+        const int a = e / N, b = e - a * N;
+        if (b <= a) S[a * kNL + b] = V0[a + b * N] + Q[e];
       }
+      for (int a = tid; a < N; a += NT) vec[a] = V0invm[(size_t)s * N + a];
     }
     __syncthreads();
     if (!(skip & 4)) wg_chol_inv<NT>(S, N, Tb, &bad);

@@ -112,10 +112,12 @@ __global__ __launch_bounds__(256) void k_post_stats(int S, int n, const double* 
 
 // forecast paths: chain c's record of kept draw m, forecast draw job, horizon h, variable i
 // at src[c * cap Nd H N + ((m Nd + job) H + h) N + i]; series s = r + nr h over the selected
-// rows (rows[r], nr of them); draw d = (cc, m, job), job fastest
+// rows (rows[r], nr of them); draw d = (cc, m, job), job fastest.  Variables with flo[i] != 0
+// are floored first, y(y < fl) = fl (mcmcVARshadowrate.m:642-645, 676-681: NaN stays NaN)
 __global__ void k_gather_fcst(const double* __restrict__ src, int chain0, int C, int M, int Nd, int H,
                               int N, int cap, const int* __restrict__ rows, int nr,
-                              const uint8_t* __restrict__ cum, double* dst) {
+                              const uint8_t* __restrict__ cum, const uint8_t* __restrict__ flo, double fl,
+                              double* dst) {
   const int n = C * M * Nd;
   const int S = nr * H;
   const size_t total = (size_t)n * nr;
@@ -126,9 +128,11 @@ __global__ void k_gather_fcst(const double* __restrict__ src, int chain0, int C,
     const int i = rows[r];
     const double* base = src + ((size_t)(chain0 + cc) * cap * Nd + (size_t)m * Nd + job) * H * N + i;
     const bool c = cum && cum[i];
+    const bool f = flo && flo[i];
     double run = 0.0;
     for (int h = 0; h < H; ++h) {
-      const double val = base[(size_t)h * N];
+      double val = base[(size_t)h * N];
+      if (f && val < fl) val = fl;
       run = c ? run + val : val;
       dst[(size_t)(r + nr * h) * n + d] = run;
     }
@@ -203,11 +207,12 @@ hipError_t post_summaries(hipStream_t st, int S, int n, const double* draws, dou
 }
 
 hipError_t post_gather_fcst(hipStream_t st, const double* src, int chain0, int C, int M, int Nd, int H, int N,
-                            int cap, const int* rows, int nr, const uint8_t* cum, double* dst) {
+                            int cap, const int* rows, int nr, const uint8_t* cum, const uint8_t* flo, double fl,
+                            double* dst) {
   const size_t total = (size_t)C * M * Nd * nr;
   const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(k_gather_fcst, dim3(blocks), dim3(256), 0, st, src, chain0, C, M, Nd, H, N, cap, rows,
-                     nr, cum, dst);
+                     nr, cum, flo, fl, dst);
   return hipGetLastError();
 }
 

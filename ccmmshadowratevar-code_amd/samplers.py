@@ -584,15 +584,18 @@ def matlab_prctile(x, pct, axis=0):
 def _bh_units(data0, ydates0, Tjumpoffs, p, np_, ndxSHADOWRATE, ndxOTHERYIELDS,
               minnesotaPriorMean, ELBbound, elbT0, doRATSprior, fcstNhorizons, model="blockhybrid"):
     """Host setup of every vintage (mcmcVARshadowrateBlockHybrid.m:30-295; model="hybrid":
-    mcmcVARhybridGibbs.m:33-339) and its yrealized (goVARshadowrateBlockHybrid.m:267-283)."""
+    mcmcVARhybridGibbs.m:33-339; model="shadowrate": mcmcVARshadowrate.m, every equation on the
+    shadow-rate design) and its yrealized (goVARshadowrateBlockHybrid.m:267-283)."""
     out = []
+    N = np.asarray(data0).shape[1]
     for thisT in Tjumpoffs:
         if model == "hybrid":
             bm = build_hybrid(int(thisT), p, np_, data0, ydates0, ndxSHADOWRATE, minnesotaPriorMean,
                               ELBbound, elbT0, doRATSprior)
         else:
             bm = build_bh(int(thisT), p, np_, data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS,
-                          minnesotaPriorMean, ELBbound, elbT0, doRATSprior)
+                          minnesotaPriorMean, ELBbound, elbT0, doRATSprior,
+                          **({"actualrateBlock": np.zeros(N, bool)} if model == "shadowrate" else {}))
         yr = realized_values(data0, int(thisT), fcstNhorizons, ndxSHADOWRATE, ELBbound)
         out.append((int(thisT), bm, yr))
     return out
@@ -609,18 +612,23 @@ def _bh_chain_set(ctx, units, C, *, seed, ids, store_capacity, gibbsburn, ELBbou
     elbTmax = max(max(u[1].elbT for u in units), 1)
     B = C * len(units)
     hybrid = model == "hybrid"
+    shadow = model == "shadowrate"
     ch = _abi.Chains(ctx, N=N, p=p, T=Tmax, B=B, ndata=len(units), crn=False,
                      store_capacity=store_capacity, seed=int(seed),
-                     model=_abi.MODEL_HYBRID if hybrid else _abi.MODEL_BLOCKHYBRID,
+                     model=_abi.MODEL_HYBRID if hybrid else (_abi.MODEL_SHADOWRATE if shadow else _abi.MODEL_BLOCKHYBRID),
                      Ns=len(bm0.ndxS), elbTmax=elbTmax, elb_gibbsburn=gibbsburn, elb=ELBbound)
     for s, (_, bm, _) in enumerate(units):
         m = bm.var
         ch.set_data(s, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
-    ch.set_elb_model(bm0.ndxS, None if hybrid else bm0.actual_block)
+    ch.set_elb_model(bm0.ndxS, None if (hybrid or shadow) else bm0.actual_block)
     yields = np.zeros(N, bool)
     yields[np.asarray(ndxYIELDS, int)] = True
     if fcstNhorizons:
         ch.set_fcst(fcstNhorizons, Nd, yields, keep_paths=keep_paths)
+        if shadow:                                   # mcmcVARshadowrate.m:539-546: ndxOTHERYIELDS only
+            other = yields.copy()
+            other[np.asarray(bm0.ndxS, int)] = False
+            ch.set_fcst_censor(other)
     slots = np.repeat(np.arange(len(units)), C).astype(np.int32)
     ch.set_slots(slots)
     K = bm0.var.K
@@ -690,6 +698,18 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
     vintage (K = N p + 1 + Ns p, PS proposals at every sweep, :458), modellabel ELBhybrid; the
     max-root block is commented out in that driver (:383-430), so maxlambda is refused.
 
+    model="shadowrate" runs goVARshadowrate.m (goVARshadowrate_batch): mcmcVARshadowrate per
+    vintage (every equation on the shadow-rate design, elb.Nproposals = 100).  Its forecast
+    outputs follow that driver: fcstYhat is the Rao-Blackwellised mean with the yields replaced by
+    the mean of their ELB-floored draws (mcmcVARshadowrate.m:639-645, 683-684), fcstYhatRB the
+    Rao-Blackwellised mean, fcstShadowYhat its yield rows, fcstYcensorhat the mean of the censored
+    paths (other yields floored inside the simulation, shadow rates after, :539-546, 676-681),
+    missingrateVintagesMid / Tails the median and prctile [5 25 75 95] of the kept missingrate_all
+    (goVARshadowrate.m:345-348, 523-529); postprocess=True adds the ydraws / ycumdraws /
+    ycensordraws summaries of goVARshadowrate.m:356-495 (fcstYcensor{median,crps,quantiles}), all
+    on the device (ccmm_chains_summaries_floor).  The forecast paths of every vintage stay in HBM
+    until the summaries are taken (Python engine only).
+
     engine="native" runs the rank's vintage loop (chain set, burn-in, kept sweeps, forecast
     records, device summaries, retries) inside the library, ccmm_run_batch (include/ccmm.h): the
     same Philox streams and the same per-vintage results (keep_draws / maxlambda not available
@@ -720,6 +740,13 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
     size = dist.get_world_size() if dist is not None else 1
     device = _rank_device(dist, device)
     hybrid = model == "hybrid"
+    is_sr = model == "shadowrate"
+    if model not in ("blockhybrid", "hybrid", "shadowrate"):
+        raise ValueError(f"unknown model {model!r}")
+    if is_sr and engine == "native":
+        raise ValueError("model='shadowrate' runs on the Python engine (ccmm_chains_summaries_floor)")
+    smask = np.zeros(N, bool)
+    smask[ndxSHADOWRATE] = True
     if hybrid and maxlambda:
         raise ValueError("goVARhybrid.m computes no max VAR roots (:383-430 commented out)")
     K = N * p + 1 + (ndxSHADOWRATE.size * p if hybrid else 0)
@@ -745,16 +772,22 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
         us = [units[i] for i in vidx]
         ids = np.array([(mine[i] * C + c) + attempt * 1_000_003 for i in vidx for c in range(C)],
                        dtype=np.uint32)
-        # postprocess: every kept draw and forecast path stays on the device until the
-        # per-vintage summaries (ccmm_chains_summaries) have been taken
+        # postprocess (and the shadow-rate VAR, whose yhat needs the floored draws): every kept
+        # draw and forecast path stays on the device until the per-vintage summaries
+        # (ccmm_chains_summaries) have been taken
+        dev = postprocess or is_sr
         ch, slots, yields = _bh_chain_set(ctx, us, C, seed=rndStream, ids=ids,
-                                          store_capacity=MCMCdraws if postprocess else chunk,
+                                          store_capacity=MCMCdraws if dev else chunk,
                                           gibbsburn=gibbsburn, ELBbound=ELBbound,
                                           ndxYIELDS=ndxYIELDS, fcstNhorizons=H, Nd=Nd,
-                                          keep_paths=postprocess, model=model)
-        if elb_ps and Nproposals and ch.elbTmax:
-            # block hybrid: m >= MCMCburnin * .5 (:435); hybrid: every sweep (mcmcVARhybridGibbs.m:458)
+                                          keep_paths=dev, model=model)
+        use_ps = bool(elb_ps and Nproposals and ch.elbTmax)
+        if use_ps:
+            # block hybrid, shadow rate: m >= MCMCburnin * .5 (:435, mcmcVARshadowrate.m:403);
+            # hybrid: every sweep (mcmcVARhybridGibbs.m:458)
             ch.set_elb_ps(Nproposals, 1 if hybrid else max(1, -(-burn // 2)))
+            if is_sr:
+                ch.keep_missingrate(True)                  # mcmcVARshadowrate.m:435, 498
         B = ch.B
         done = 0
         while done < burn:
@@ -766,6 +799,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
         scores = np.empty((Nd, MCMCdraws, 4, B))
         fYsum = np.zeros((N, H, B))
         fYcsum = np.zeros((N, H, B))
+        yhsum = np.zeros((N, H, B))
         Psum = np.zeros((K, N, B))
         P2sum = np.zeros((K, N, B))
         elbTmax = ch.elbTmax
@@ -776,7 +810,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
         while done < MCMCdraws:
             n = min(chunk, MCMCdraws - done)
             ch.sweep(n, store=True)
-            if not postprocess:
+            if not dev:
                 fc = ch.get_fcst()
                 dr = ch.get_draws(which={"PAI_all", "shadowrate_all"})
                 scores[:, done:done + n] = fc["scores"]
@@ -792,13 +826,28 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
             done += n
             if progress:
                 print(f"[rank {rank}] kept {done}/{MCMCdraws} ({time.perf_counter() - t1:.1f} s)", flush=True)
-        if postprocess:
+        miss = None
+        if dev:
             # goVARshadowrateBlockHybrid.m:349-480 on the device, per vintage (data slot)
             for k, i in enumerate(vidx):
                 thisT, bm, yr = units[i]
                 ycr = np.array(yr, float)
                 if cumcode is not None:
                     ycr[cumcode] = np.cumsum(ycr[cumcode], axis=1)              # :353
+                if is_sr:
+                    # goVARshadowrate.m:356-495: ydraws = uncensored paths, yields floored; the
+                    # censored paths with the shadow rates floored; shadowratedraws unfloored
+                    q = dict(ycr=ycr, pa=ch.summaries(2, k, pct=pct if postprocess else ()))
+                    q["yd"] = ch.summaries(0, k, realized=yr if postprocess else None,
+                                           pct=pct if postprocess else (), floor_rows=yields, floor=ELBbound)
+                    q["yz"] = ch.summaries(1, k, realized=yr if postprocess else None,
+                                           pct=pct if postprocess else (), floor_rows=smask, floor=ELBbound)
+                    if postprocess:
+                        q["yc"] = ch.summaries(0, k, cumcode=cumcode, realized=ycr, pct=pct, floor_rows=yields,
+                                               floor=ELBbound)
+                        q["sh"] = ch.summaries(0, k, rows=yields, pct=pct)
+                    post[i] = q
+                    continue
                 yd = ch.summaries(1, k, realized=yr, pct=pct)                   # ydraws
                 yc = ch.summaries(1, k, cumcode=cumcode, realized=ycr, pct=pct)  # ycumdraws
                 sh = ch.summaries(0, k, rows=yields, pct=pct)                   # shadowratedraws
@@ -811,6 +860,9 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
             scores[:] = fc["scores"]
             fYsum[:] = fc["fYsum"]
             fYcsum[:] = fc["fYcsum"]
+            yhsum[:] = fc["yhatsum"]
+            if is_sr and use_ps:
+                miss = ch.get_missingrate()                                     # M x Ns x elbTmax x B
             dr = ch.get_draws(which={"shadowrate_all"} | ({"PAI_all"} if PAIdraws is not None else set()))
             if shadow is not None:
                 shadow[:] = dr["shadowrate_all"]
@@ -818,7 +870,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                 PAIdraws[:] = dr["PAI_all"]
         status = ch.get_status()
         nacc = None
-        if elb_ps and Nproposals and ch.elbTmax:
+        if use_ps:
             psd = ch.get_ps()
             nacc = psd["countAccept"] + psd["countAcceptBurnin"]
         ch.close()
@@ -838,7 +890,45 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                      logscoreI=_logmeanexp(scores[:, :, 3, cs].ravel()),
                      fcstYhat=fYcsum[:, :, cs].sum(axis=2) / (nk * Nd),
                      fcstShadowYhat=fYsum[ndxYIELDS][:, :, cs].sum(axis=2) / (nk * Nd))
-            if i in post:
+            if is_sr:
+                q = post[i]
+                RB = yhsum[:, :, cs].sum(axis=2) / nk                          # mcmcVARshadowrate.m:639
+                yh = RB.copy()
+                yh[ndxYIELDS] = q["yd"]["mean"].reshape(N, H, order="F")[ndxYIELDS]   # :683-684
+                r.update(fcstYhat=yh, fcstYhatRB=RB, fcstShadowYhat=RB[ndxYIELDS],
+                         fcstYcensorhat=q["yz"]["mean"].reshape(N, H, order="F"),
+                         PAImean=q["pa"]["mean"].reshape(K, N, order="F"),
+                         PAIstdev=q["pa"]["stdev"].reshape(K, N, order="F"))
+                if postprocess:
+                    nq = pct.size
+                    yc = yh.copy()
+                    if cumcode is not None:
+                        yc[cumcode] = np.cumsum(yc[cumcode], axis=1)
+                    r.update(PAImedian=q["pa"]["median"].reshape(K, N, order="F"),
+                             PAIquantiles=q["pa"]["quantiles"].reshape(K, N, nq, order="F"),
+                             fcstYmedian=q["yd"]["median"].reshape(N, H, order="F"),
+                             fcstYcrps=q["yd"]["crps"].reshape(N, H, order="F"),
+                             fcstYquantiles=q["yd"]["quantiles"].reshape(N, H, nq, order="F"),
+                             fcstYcumrealized=q["ycr"], fcstYcumhat=yc,
+                             fcstYcummedian=q["yc"]["median"].reshape(N, H, order="F"),
+                             fcstYcumcrps=q["yc"]["crps"].reshape(N, H, order="F"),
+                             fcstYcumquantiles=q["yc"]["quantiles"].reshape(N, H, nq, order="F"),
+                             fcstYcensormedian=q["yz"]["median"].reshape(N, H, order="F"),
+                             fcstYcensorcrps=q["yz"]["crps"].reshape(N, H, order="F"),
+                             fcstYcensorquantiles=q["yz"]["quantiles"].reshape(N, H, nq, order="F"),
+                             fcstShadowYmedian=q["sh"]["median"].reshape(Ny, H, order="F"),
+                             fcstShadowYquantiles=q["sh"]["quantiles"].reshape(Ny, H, nq, order="F"),
+                             fcstYmvlogscoreDraws=scores[:, :, 1, cs].ravel(order="F"),
+                             fcstYmvlogscoreXdraws=scores[:, :, 2, cs].ravel(order="F"),
+                             fcstYmvlogscoreIdraws=scores[:, :, 3, cs].ravel(order="F"))
+                if miss is not None and bm.elbT > 0:
+                    # missingrate_all permuted to (Nobs, Ns, draws): MATLAB median (NaN if any draw
+                    # is NaN) and prctile (NaN draws removed), goVARshadowrate.m:345-348
+                    mr = miss[:, :, :bm.elbT, cs].transpose(2, 1, 0, 3).reshape(bm.elbT, Ns, -1)
+                    r["missingrateMid"] = np.median(mr, axis=2)
+                    r["missingrateTails"] = np.moveaxis(
+                        np.nanpercentile(mr, [5, 25, 75, 95], axis=2, method="hazen"), 0, 2)
+            elif i in post:
                 q = post[i]
                 nq = pct.size
                 r["PAImean"] = q["pa"]["mean"].reshape(K, N, order="F")
@@ -929,6 +1019,10 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                countELBaccept=np.full(V, -1),
                shadowrateVintagesMid=np.full((Tdata, Ns, V), np.nan),
                shadowrateVintagesTails=np.full((Tdata, Ns, 4, V), np.nan))
+    if is_sr:
+        out.update(fcstYhatRB=np.full((N, H, V), np.nan), fcstYcensorhat=np.full((N, H, V), np.nan),
+                   missingrateVintagesMid=np.full((Tdata, Ns, V), np.nan),
+                   missingrateVintagesTails=np.full((Tdata, Ns, 4, V), np.nan))
     if keep_draws:
         out["PAI_all"] = {}
     nq = pct.size
@@ -942,6 +1036,10 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                         ("fcstYmvlogscoreXdraws", (fcstNdraws * C,)),
                         ("fcstYmvlogscoreIdraws", (fcstNdraws * C,))):
             out[nm] = np.full(shp + (V,), np.nan)
+        if is_sr:
+            for nm, shp in (("fcstYcensormedian", (N, H)), ("fcstYcensorcrps", (N, H)),
+                            ("fcstYcensorquantiles", (N, H, nq))):
+                out[nm] = np.full(shp + (V,), np.nan)
     if maxlambda:
         out["drawsMaxVARroot"] = np.full((MCMCdraws * C, V), np.nan)
     jumpoff = p + elbT0                                                  # :497
@@ -963,15 +1061,23 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
             thisT = r["thisT"]
             out["shadowrateVintagesMid"][jumpoff:thisT, :, v] = r["shadowrateMid"]
             out["shadowrateVintagesTails"][jumpoff:thisT, :, :, v] = r["shadowrateTails"]
+        if "missingrateMid" in r:
+            out["missingrateVintagesMid"][jumpoff:r["thisT"], :, v] = r["missingrateMid"]       # :523-529
+            out["missingrateVintagesTails"][jumpoff:r["thisT"], :, :, v] = r["missingrateTails"]
         if keep_draws and "PAI_all" in r:
             out["PAI_all"][v] = r["PAI_all"]
         for nm in ("fcstYmedian", "fcstYcrps", "fcstYquantiles", "fcstYcumrealized", "fcstYcumhat",
                    "fcstYcummedian", "fcstYcumcrps", "fcstYcumquantiles", "fcstShadowYmedian",
                    "fcstShadowYquantiles", "PAImedian", "PAIquantiles", "fcstYmvlogscoreDraws",
-                   "fcstYmvlogscoreXdraws", "fcstYmvlogscoreIdraws", "drawsMaxVARroot"):
+                   "fcstYmvlogscoreXdraws", "fcstYmvlogscoreIdraws", "drawsMaxVARroot", "fcstYhatRB",
+                   "fcstYcensorhat", "fcstYcensormedian", "fcstYcensorcrps", "fcstYcensorquantiles"):
             if nm in r and nm in out:
                 out[nm][..., v] = r[nm]
     out["fcstYhaterror"] = out["fcstYrealized"] - out["fcstYhat"]                      # :453
+    if is_sr:
+        out["fcstYcensorhaterror"] = out["fcstYrealized"] - out["fcstYcensorhat"]      # goVARshadowrate.m:487
+        if postprocess:
+            out["fcstYcensormederror"] = out["fcstYrealized"] - out["fcstYcensormedian"]  # :488
     if postprocess:
         out["fcstYmederror"] = out["fcstYrealized"] - out["fcstYmedian"]              # :454
         out["fcstYcumhaterror"] = out["fcstYcumrealized"] - out["fcstYcumhat"]        # :463
@@ -1043,6 +1149,16 @@ def _native_batch(ctx, units, mine, *, C, N, p, K, Ns, H, Nd, MCMCdraws, burn, g
             r["shadowrateTails"] = np.moveaxis(matlab_prctile(sr, [5, 25, 75, 95], axis=2), 0, 2)
         res[mine[i]] = r
     return res, [retries] if retries else []
+
+
+def goVARshadowrate_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS, minnesotaPriorMean, *,
+                          Nproposals=100, **kw):
+    """goVARshadowrate.m (the quasi-real-time OOS run of the shadow-rate VAR, mcmcVARshadowrate per
+    vintage, parfor at :265, elb.Nproposals = 100 at mcmcVARshadowrate.m:169, modellabel
+    ELBsampling) as one device-resident chain set per rank; arguments and outputs of
+    goVARshadowrateBlockHybrid_batch plus fcstYhatRB, fcstYcensor*, missingrateVintages*."""
+    return goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS, minnesotaPriorMean,
+                                            model="shadowrate", Nproposals=Nproposals, **kw)
 
 
 def goVARhybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS, minnesotaPriorMean, **kw):

@@ -389,6 +389,15 @@ int ccmm_draw_summaries(ccmm_ctx* ctx, int S, int n, const double* draws, const 
 int ccmm_chains_summaries(ccmm_chains* ch, int source, int slot, const uint8_t* rows, const uint8_t* cumcode,
                           const double* realized, int nq, const double* pct, double* mean, double* median,
                           double* quantiles, double* stdev, double* crps);
+/* As ccmm_chains_summaries, with the forecast paths of the variables selected by floor_rows (N
+ * bytes) floored at `floor` first, y(y < floor) = floor, before any cumsum: the shadow-rate
+ * VAR's draws (mcmcVARshadowrate.m:642-645 fcstYdraws, yields floored on the uncensored paths;
+ * :676-681 fcstYcensorDraws, shadow rates floored on the censored paths) summarised by
+ * goVARshadowrate.m:356-478.  Sources 0 and 1 only. */
+int ccmm_chains_summaries_floor(ccmm_chains* ch, int source, int slot, const uint8_t* rows, const uint8_t* cumcode,
+                                const uint8_t* floor_rows, double floor, const double* realized, int nq,
+                                const double* pct, double* mean, double* median, double* quantiles, double* stdev,
+                                double* crps);
 
 /* ------------------------------------------------------------ batch run (the vintage loop)
  * ccmm_run_batch replaces the parfor over vintages of goVARshadowrateBlockHybrid.m:258-517
