@@ -1403,13 +1403,15 @@ struct ccmm_chains {
         (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns + N * Ns + N * p * Ns) * sizeof(double);
     const int a_lds = (lds_cond + (size_t)N * N * sizeof(double) <= 64 * 1024) ? 1 : 0;
     if (a_lds) lds_cond += (size_t)N * N * sizeof(double);
+    // one wave per censored month; four when the month's staging fills a CU's LDS (N > 64)
+    const int nth_cond = (N > 64) ? 256 : 64;
     launch(KID_ELBCOND, [&] {
       switch (Ns) {
 #define CASE_NSC(NS)                                                                                 \
   case NS:                                                                                           \
     HIPCHECK(hipFuncSetAttribute((const void*)k_elb_cond<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                  (int)lds_cond));                                                    \
-    hipLaunchKernelGGL(k_elb_cond<NS>, dim3(e.elbTmax, d.B), dim3(64), lds_cond, ctx->stream, d, e, cs, a_lds); \
+    hipLaunchKernelGGL(k_elb_cond<NS>, dim3(e.elbTmax, d.B), dim3(nth_cond), lds_cond, ctx->stream, d, e, cs, a_lds); \
     break;
         CASE_NSC(1)
         CASE_NSC(2)

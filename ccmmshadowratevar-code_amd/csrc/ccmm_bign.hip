@@ -400,19 +400,26 @@ __device__ void wg_chol_inv(double* S, int n, double* Tb, int* bad) {
   for (int p0 = 0; p0 < n; p0 += kCB) {
     const int pw = min(kCB, n - p0);
     if (wave == 0) {
-      double row[kCB], dv[kCB];
+      double row[kCB], dv[kCB], ipk[kCB];
 #pragma unroll
       for (int m = 0; m < kCB; ++m) row[m] = (lane < pw && m <= lane) ? S[(p0 + lane) * kNL + p0 + m] : 0.0;
 #pragma unroll
       for (int kk = 0; kk < kCB; ++kk) {
+        ipk[kk] = 1.0;
         if (kk < pw) {
           double dkk = readlane_d(row[kk], kk);
           if (!(dkk > 0.0)) {
             *bad = 1;
             dkk = 1.0;
           }
-          const double piv = sqrt(dkk), ip = 1.0 / piv;
-          if (lane == kk) row[kk] = piv;
+          // 1 / sqrt(d): hardware estimate + two Newton steps, no IEEE sqrt / division on the
+          // serial pivot chain; L_kk = d / sqrt(d), and 1 / L_kk is kept for the inverse below
+          double ip = __builtin_amdgcn_rsq(dkk);
+          const double hd = 0.5 * dkk;
+          ip = ip * fma(-hd * ip, ip, 1.5);
+          ip = ip * fma(-hd * ip, ip, 1.5);
+          ipk[kk] = ip;
+          if (lane == kk) row[kk] = dkk * ip;
           if (lane > kk) row[kk] *= ip;
           const double lik = row[kk];
 #pragma unroll
@@ -428,9 +435,8 @@ __device__ void wg_chol_inv(double* S, int n, double* Tb, int* bad) {
 #pragma unroll
       for (int k = 0; k < kCB; ++k) {
         if (k < pw) {
-          const double lkk = readlane_d(row[k], k);
           if (lane == k) {
-            const double il = 1.0 / lkk;
+            const double il = ipk[k];
 #pragma unroll
             for (int c = 0; c <= k; ++c) dv[c] *= il;
           }

@@ -205,8 +205,9 @@ __device__ inline void elb_small_inverse(const double* M, double* Minv, int n) {
 }
 
 template <int NS>  // = e.Ns: compile-time, so the per-shadow-rate arrays below stay in registers
-__global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs, int a_lds) {
+__global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState cs, int a_lds) {
   extern __shared__ double sm[];
+  __shared__ double red[4 * kElbNsMax];  // per-wave partial sums (blockDim.x = 64 or 256)
   const int c = blockIdx.y;
   const int s = cs.slot[c];
   const int ci = blockIdx.x;
@@ -215,7 +216,8 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
   constexpr int Ns = NS;
   const int T = e.elbT[s], T0 = e.elbT0[s];
   const int t = e.cens[(size_t)s * e.elbTmax + ci];
-  const int lane = threadIdx.x;
+  // one wave for N <= 64; four waves for larger N (the N x p x Ns staging alone fills one CU's LDS)
+  const int tid = threadIdx.x, nth = blockDim.x, lane = tid & 63, wv = tid >> 6, nwv = nth >> 6;
   const int ncol = 2 * p * Ns;
   const double* Phi = e.Phi + (size_t)c * N * Np;
   const double* Yt = e.Yt + (size_t)c * e.elbTmax * N;
@@ -233,18 +235,18 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
   for (int a = 0; a < kElbNsMax; ++a) S[a] = a < Ns ? e.ndxS[a] : 0;
   // every Φ read below is a shadow-rate column: stage those N p Ns values once per wave;
   // A too when it fits (a_lds: N <= 64), so the dependent sums below read LDS, not L1/L2
-  for (int q = lane; q < N * p * Ns; q += 64) {
+  for (int q = tid; q < N * p * Ns; q += nth) {
     const int b = q % Ns, jl = q / Ns, l = jl % p, jj = jl / p;
     PS[q] = Phi[(size_t)jj * Np + l * N + e.ndxS[b]];
   }
   double* Al = PS + N * p * Ns;
   if (a_lds)
-    for (int q = lane; q < N * N; q += 64) Al[q] = Ag[q];
+    for (int q = tid; q < N * N; q += nth) Al[q] = Ag[q];
   __syncthreads();
   const double* A = a_lds ? Al : Ag;
   // ---- Q_0 = Λ_t[S, :], Q_k = B_k' Λ_{t+k};  Λ = A' diag(1/SVol^2) A
   for (int k = 0; k <= kmax; ++k) {
-    for (int i = lane; i < N; i += 64) {
+    for (int i = tid; i < N; i += nth) {
       double w[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
       const double sv = cs.sqrtht[((size_t)c * N + i) * d.TP + T0 + t + k];
       const double iv = 1.0 / (sv * sv);
@@ -261,30 +263,30 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
     }
     __syncthreads();
     // Q_k[a][j] = Σ_{i >= j} W[i][a] A(i,j)
-    for (int a = 0; a < Ns; ++a)
-      for (int j = lane; j < N; j += 64) {
-        double v = 0.0;
-        for (int i = j; i < N; ++i) v = fma(Wl[i * Ns + a], A[i + j * N], v);
-        Q[((size_t)k * Ns + a) * N + j] = v;
-      }
+    for (int q = tid; q < Ns * N; q += nth) {
+      const int a = q / N, j = q - a * N;
+      double v = 0.0;
+      for (int i = j; i < N; ++i) v = fma(Wl[i * Ns + a], A[i + j * N], v);
+      Q[((size_t)k * Ns + a) * N + j] = v;
+    }
     __syncthreads();
   }
   __syncthreads();
   // ---- P = Λ_t,SS + Σ_k Q_k B_k
-  if (lane < Ns * Ns) {
-    const int a = lane / Ns, b = lane % Ns;
+  if (tid < Ns * Ns) {
+    const int a = tid / Ns, b = tid % Ns;
     double v = Q[(size_t)a * N + S[b]];
     for (int k = 1; k <= kmax; ++k) {
       const double* Qk = Q + ((size_t)k * Ns + a) * N;
       for (int j = 0; j < N; ++j) v = fma(Qk[j], PS[(j * p + k - 1) * Ns + b], v);
     }
-    Pm[lane] = v;
+    Pm[tid] = v;
   }
   // ---- base g0 = -Q_0 ε'_t + Σ_k Q_k ε'_{t+k}, ε' = ε with S_t = 0:
   //      ε'_t = ε_t - E_S Yb_S,t,  ε'_{t+k} = ε_{t+k} + Φ_k[:,S] Yb_S,t
   {
     double g0[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
-    for (int j = lane; j < N; j += 64) {
+    for (int j = tid; j < N; j += nth) {
       bool isS = false;
       for (int a = 0; a < Ns; ++a) isS |= (S[a] == j);
       const double et = Et[(size_t)t * N + j];
@@ -299,41 +301,44 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
     }
     for (int a = 0; a < Ns; ++a) {
       const double tot = wave_sum_dpp(g0[a]);
-      if (lane == 0) gS[a] = tot;
+      if (lane == 0) red[wv * kElbNsMax + a] = tot;  // summed over the waves after the barrier below
     }
   }
   // ---- unit responses, one neighbour column per lane
   //   past  (s', t-kp): Q_0 Φ_kp[:,s'] - Σ_{k + kp <= p} Q_k Φ_{k+kp}[:,s']
   //   future(s', t+kp): Q_kp[:,s']     - Σ_{k = kp+1..kmax} Q_k Φ_{k-kp}[:,s']
-  for (int col = lane; col < ncol; col += 64) {
+  //   (one (column, a) pair per thread)
+  for (int w = tid; w < ncol * Ns; w += nth) {
+    const int col = w / Ns, a = w - col * Ns;
     const int kk = col / Ns, sp = col % Ns;
     const int q = S[sp];
-    double g[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
+    double v = 0.0;
     if (kk < p) {
       const int kp = kk + 1;
-      if (t - kp >= 0)
-        for (int a = 0; a < Ns; ++a) {
-          double v = 0.0;
-          for (int j = 0; j < N; ++j) v = fma(Q[(size_t)a * N + j], PS[(j * p + kp - 1) * Ns + sp], v);
-          for (int k = 1; k <= kmax && k + kp <= p; ++k) {
-            const double* Qk = Q + ((size_t)k * Ns + a) * N;
-            for (int j = 0; j < N; ++j) v = fma(-Qk[j], PS[(j * p + k + kp - 1) * Ns + sp], v);
-          }
-          g[a] = v;
+      if (t - kp >= 0) {
+        for (int j = 0; j < N; ++j) v = fma(Q[(size_t)a * N + j], PS[(j * p + kp - 1) * Ns + sp], v);
+        for (int k = 1; k <= kmax && k + kp <= p; ++k) {
+          const double* Qk = Q + ((size_t)k * Ns + a) * N;
+          for (int j = 0; j < N; ++j) v = fma(-Qk[j], PS[(j * p + k + kp - 1) * Ns + sp], v);
         }
+      }
     } else {
       const int kp = kk - p + 1;
-      if (kp <= kmax)
-        for (int a = 0; a < Ns; ++a) {
-          double v = Q[((size_t)kp * Ns + a) * N + q];
-          for (int k = kp + 1; k <= kmax; ++k) {
-            const double* Qk = Q + ((size_t)k * Ns + a) * N;
-            for (int j = 0; j < N; ++j) v = fma(-Qk[j], PS[(j * p + k - kp - 1) * Ns + sp], v);
-          }
-          g[a] = v;
+      if (kp <= kmax) {
+        v = Q[((size_t)kp * Ns + a) * N + q];
+        for (int k = kp + 1; k <= kmax; ++k) {
+          const double* Qk = Q + ((size_t)k * Ns + a) * N;
+          for (int j = 0; j < N; ++j) v = fma(-Qk[j], PS[(j * p + k - kp - 1) * Ns + sp], v);
         }
+      }
     }
-    for (int a = 0; a < Ns; ++a) gS[(size_t)(1 + col) * Ns + a] = g[a];
+    gS[(size_t)(1 + col) * Ns + a] = v;
+  }
+  __syncthreads();
+  if (tid < Ns) {
+    double tot = red[tid];
+    for (int x = 1; x < nwv; ++x) tot += red[x * kElbNsMax + tid];
+    gS[tid] = tot;
   }
   __syncthreads();
   // ---- Ω = P^-1, a_t = Ω g0, betas (gibbsdrawShadowrates.m:130-145)
@@ -342,7 +347,7 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
   double* so = beta + Ns * (Ns - 1);
   double* Orec = so + Ns;
   double* G = Orec + Ns * Ns;
-  if (lane == 0) {
+  if (tid == 0) {
     double Pl[kElbNsMax * kElbNsMax], Oi[kElbNsMax * kElbNsMax];
     for (int q = 0; q < Ns * Ns; ++q) Pl[q] = Pm[q];
     elb_small_inverse(Pl, Oi, Ns);
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
   __syncthreads();
   // G = Ω g(unit); zero for uncensored or out-of-window neighbours
   const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * Ns;
-  for (int col = lane; col < ncol; col += 64) {
+  for (int col = tid; col < ncol; col += nth) {
     const int kk = col / Ns, sp = col % Ns;
     const int tn = (kk < p) ? t - (kk + 1) : t + (kk - p + 1);
     const bool live = tn >= 0 && tn < T && sN[(size_t)tn * Ns + sp];
@@ -398,10 +403,10 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
     //   b_PS = -(Λ_t ε_t)_S + Σ_k B_k' Λ_{t+k} ε_{t+k}  (ε of the PS model, censored cells at 0),
     // and the past neighbours' unit responses
     double* ext = rec + elb_cond_ps_off(Ns, p);
-    if (lane < Ns * Ns) ext[lane] = Pm[lane];
+    if (tid < Ns * Ns) ext[tid] = Pm[tid];
     const double* EP = e.EtPS + (size_t)c * e.elbTmax * N;
     double bp[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
-    for (int j = lane; j < N; j += 64) {
+    for (int j = tid; j < N; j += nth) {
       const double u0 = -EP[(size_t)t * N + j];
       for (int a = 0; a < Ns; ++a) bp[a] = fma(Q[(size_t)a * N + j], u0, bp[a]);
       for (int k = 1; k <= kmax; ++k) {
@@ -409,11 +414,18 @@ __global__ __launch_bounds__(64) void k_elb_cond(Dims d, ElbDev e, ChainState cs
         for (int a = 0; a < Ns; ++a) bp[a] = fma(Q[((size_t)k * Ns + a) * N + j], r, bp[a]);
       }
     }
+    __syncthreads();  // red is free again (read above before the last barrier)
     for (int a = 0; a < Ns; ++a) {
       const double tot = wave_sum_dpp(bp[a]);
-      if (lane == 0) ext[Ns * Ns + a] = tot;
+      if (lane == 0) red[wv * kElbNsMax + a] = tot;
     }
-    for (int q = lane; q < p * Ns * Ns; q += 64) ext[Ns * Ns + Ns + q] = gS[Ns + q];
+    for (int q = tid; q < p * Ns * Ns; q += nth) ext[Ns * Ns + Ns + q] = gS[Ns + q];
+    __syncthreads();
+    if (tid < Ns) {
+      double tot = red[tid];
+      for (int x = 1; x < nwv; ++x) tot += red[x * kElbNsMax + tid];
+      ext[Ns * Ns + tid] = tot;
+    }
   }
 }
 
