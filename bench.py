@@ -65,7 +65,10 @@ def parse():
     ap.add_argument("--s120-steps", type=int, default=2,
                     help="timed sweeps of the S120 stress line (configs[4], N=120); 0 = skip")
     ap.add_argument("--s120-warmup", type=int, default=1)
-    ap.add_argument("--s120-chains", default="64", help="chains per GPU of the S120 lines")
+    ap.add_argument("--s120-chains", default="96",
+                    help="chains per GPU of the S120 lines (96: ~200 GB of the 288 GB HBM for the 120 "
+                         "factored 1472 x 1472 systems per chain; 64 / 96 / 112 chains measured 91.4 / 99.2 / "
+                         "102.6 sweeps/s, profiles/r03i_s120_chains.json)")
     ap.add_argument("--s120-groups", type=int, default=2,
                     help="chain groups (HIP streams driven from host threads) of the S120 lines")
     ap.add_argument("--s120-only", action="store_true", help="run only the S120 lines (probe)")
