@@ -133,3 +133,21 @@ def test_govar_batch_floors_yrealized_and_picks_rank_device(pkg, monkeypatch):
     assert pkg.samplers._rank_device(object(), None) == 3
     assert pkg.samplers._rank_device(object(), 1) == 1
     assert pkg.samplers._rank_device(None, None) == 0
+
+
+def test_vintage_batch_argument_checks(pkg, fred):
+    """The batch drivers refuse what they do not build before touching a device: an unknown
+    model, the shadow-rate VAR on the native engine (its floored summaries run through the
+    Python driver), max VAR roots for the hybrid model (goVARhybrid.m:383-430 commented out)."""
+    S = pkg.samplers
+    ndxS, ndxO, _ = pkg.model.setShadowYields(fred["ncode"], 0.25)
+    mpm = pkg.model.setMinnesotaMean(fred["ncode"])
+    args = (fred["data"], fred["ydates"], ndxS, ndxO, mpm)
+    with pytest.raises(ValueError, match="unknown model"):
+        S.goVARshadowrateBlockHybrid_batch(*args, model="linear", Tjumpoffs=[700])
+    with pytest.raises(ValueError, match="Python engine"):
+        S.goVARshadowrate_batch(*args, engine="native", Tjumpoffs=[700])
+    with pytest.raises(ValueError, match="max VAR roots"):
+        S.goVARhybrid_batch(*args, maxlambda=True, Tjumpoffs=[700])
+    with pytest.raises(ValueError, match="multiple of MCMCdraws"):
+        S.goVARshadowrate_batch(*args, MCMCdraws=10, fcstNdraws=15, Tjumpoffs=[700])

@@ -2,7 +2,8 @@
 """Developer tool: per-kernel device time of the block-hybrid sweep (real data,
 ELB = 0.25, 2022-08 jump-off, B chains), for A/B and ablation runs driven by
 CCMM_* environment variables (CCMM_ELB_MODE, CCMM_LAG_MODE, ...).  Does not
-check results (ablation builds produce invalid draws)."""
+check results (ablation builds produce invalid draws).
+Usage: kernel_times_bh.py [B] [warmup] [steps] [nproposals (0: Gibbs every sweep)]"""
 import json
 import sys
 import time
@@ -13,7 +14,7 @@ sys.path.insert(0, str(ROOT))
 import __graft_entry__ as ge  # noqa: E402
 
 
-def main(B=256, warm=1, steps=3):
+def main(B=256, warm=1, steps=3, nproposals=0):
     pkg = ge.load_package()
     d = pkg.model.importdata_csv(ROOT / "tests/golden/data/fredblockMD20-2022-09.csv")
     p = 12
@@ -28,6 +29,8 @@ def main(B=256, warm=1, steps=3):
     ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
     ch.set_elb_model(bm.ndxS, bm.actual_block)
     ch.set_elb_slot(0, bm.elbT0, bm.sNaN)
+    if nproposals:                       # PS proposals with the Gibbs fallback at every sweep
+        ch.set_elb_ps(nproposals, 1)
     st = pkg.model.initial_state(m, B)
     ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
     try:
