@@ -129,3 +129,58 @@ def test_bh_vintages_crn(pkg, ctx, oracle, fred):
              "X": rel_err(X[:T, :, c], st["X"], 0.1), "Y": rel_err(Y[:T, :, c], st["Y"], 0.1)}
         print("chain", c, "T", T, "elbT", b.elbT, e)
         assert max(e.values()) < 1e-6, e
+
+
+def test_bh_vintage_range_crn(pkg, ctx, oracle, fred):
+    """Every eighth vintage of the configs[3] OOS set (goVARshadowrateBlockHybrid.m:127, jump-offs
+    after 2008-12) plus the last, one chain each on one chain set: ELB windows from two censored
+    months (the first vintages) to 165, vintages after the 2015 lift-off with uncensored months
+    inside the window; one CRN sweep per chain against its vintage's oracle sweep."""
+    from oracle import ccmm_oracle_bh as bh
+    ndxS, ndxO, _ = oracle.set_shadow_yields(fred["ncode"], 0.25)
+    mpm = oracle.set_minnesota_mean(fred["ncode"])
+    e0 = oracle.elb_t0(fred["data"], ndxS, 0.25, 12)
+    Tj = list(np.flatnonzero(fred["ydates"] > pkg.samplers.datenum(2008, 12, 1)) + 1)
+    assert len(Tj) == 164
+    thisTs = Tj[::8] + ([Tj[-1]] if (len(Tj) - 1) % 8 else [])
+    bss = [bh.bh_setup(int(t), 12, 12, fred["data"], fred["ydates"], ndxS, ndxO, mpm, 0.25, e0) for t in thisTs]
+    elbTs = [b.elbT for b in bss]
+    assert min(elbTs) <= 10 and max(elbTs) == 165
+    Tmax = max(b.lin.T for b in bss)
+    elbTmax = max(elbTs)
+    B = len(bss)
+    lin0 = bss[-1].lin
+    ch = pkg.Chains(ctx, N=lin0.N, p=12, T=Tmax, B=B, ndata=B, crn=True, model=pkg.MODEL_BLOCKHYBRID,
+                    Ns=len(ndxS), elbTmax=elbTmax, elb_gibbsburn=100, elb=0.25)
+    for s, b in enumerate(bss):
+        L = b.lin
+        ch.set_data(s, L.Y, L.X, L.iVdiag, L.iVb, L.sPHI, L.Vol_0mean, L.Vol_0vcvsqrt)
+    ch.set_slots(list(range(B)))
+    ch.set_elb_model(bss[0].ndxS, bss[0].actualrateBlock)
+    for s, b in enumerate(bss):
+        ch.set_elb_slot(s, b.elbT0, b.sNaN)
+    sts = []
+    for c, b in enumerate(bss):
+        st = random_state(oracle, b.lin, seed=500 + c)
+        st["X"], st["Y"] = b.lin.X.copy(), b.lin.Y.copy()
+        sts.append(st)
+    ch.set_state(*_stack_state(sts, Tmax))
+    rng = np.random.default_rng(51)
+    crns = [bh.bh_draw_crn(rng, b) for b in bss]
+    sizes_max = oracle.crn_sizes(lin0.N, lin0.K, Tmax, lin0.dPHI) + [("uELB", (len(ndxS), elbTmax, 101))]
+    flat = np.stack([_pad_flat(sizes_max, crns[c])[:, None] for c in range(B)], -1)
+    ch.sweep(1, crn=flat)
+    got = ch.get_state()
+    S = ch.get_shadowrate()
+    status = ch.get_status()
+    ch.close()
+    worst = 0.0
+    for c, b in enumerate(bss):
+        T = b.lin.T
+        st = bh.bh_sweep(sts[c], b, crns[c], elb_impl="stable")
+        e = {"PAI": rel_err(got["PAI"][..., c], st["PAI"], 1.0),
+             "sqrtht": rel_err(got["sqrtht"][:T, :, c], st["sqrtht"]),
+             "shadowrate": rel_err(S[:, :b.elbT, c], st["shadowrate"], 0.1)}
+        worst = max(worst, max(e.values()))
+        assert max(e.values()) < 1e-6, (thisTs[c], b.elbT, e)
+    print(f"{B} vintages (elbT {min(elbTs)}..{max(elbTs)}), worst rel err {worst:.2e}, status {set(status.tolist())}")
