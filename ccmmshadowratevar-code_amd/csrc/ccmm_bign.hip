@@ -726,8 +726,8 @@ __global__ __launch_bounds__(kSvNT) void k_sv_big(Dims d, const int* __restrict_
       if (a < N && gq == 0) wv[(size_t)t * N + a] = v;
     }
     if (!(skip & 32))
-      for (int e = tid; e < N * N; e += NT) {
-        const int a = e / N, b = e - a * N;
+      for (int e = tid; e < N * N; e += NT) {  // transposed: column b of Linv_t contiguous
+        const int b = e / N, a = e - b * N;
         Lcur[e] = (b <= a) ? S[a * kNL + b] : 0.0;
       }
     __syncthreads();
@@ -736,28 +736,67 @@ __global__ __launch_bounds__(kSvNT) void k_sv_big(Dims d, const int* __restrict_
   double* hout = cs.h + (size_t)c * N * TP;
   double* eta = cs.eta + (size_t)c * N * TP;
   double* sqh = cs.sqrtht + (size_t)c * N * TP;
+  // Both products read rows of 8 lanes (M_{t+1} row a, Linv_t' row a = Linv_t column a, stored
+  // transposed), and the next step's rows are loaded into registers while this step is computed,
+  // so no global round trip sits between two steps of the recursion.
+  constexpr int kRB = 16;  // row elements per lane (N <= 128: j = gq + 8 k)
+  double pm[2][kRB], pl[2][kRB];
+  auto load_m = [&](int tt) {  // M_{tt+1} rows a = gj, gj + 64 (zero at tt = T)
+    const double* Mn = Mt + (size_t)(tt + 1) * NN;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < kRB; ++k) {
+        const int a = 64 * h + gj, j = gq + 8 * k;
+        pm[h][k] = (tt < T && a < N && j < N) ? Mn[a * N + j] : 0.0;
+      }
+  };
+  auto load_l = [&](int tt) {  // Linv_tt(i, a), i >= a: row a of the transposed store
+    const double* Li = Lt + (size_t)tt * NN;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < kRB; ++k) {
+        const int a = 64 * h + gj, i = gq + 8 * k;
+        pl[h][k] = (a < N && i < N && i >= a) ? Li[a * N + i] : 0.0;
+      }
+  };
+  if (!(skip & 16)) {
+    load_m(T);
+    load_l(T);
+  }
+  // x_{T+1} := 0: the t = T product multiplies it by zero rows, and 0 * (stale LDS) may be NaN
+  for (int a = tid; a < 128; a += NT) vec2[a] = 0.0;
+  __syncthreads();
   for (int t = (skip & 16) ? -1 : T; t >= 0; --t) {
     // v = w_t + z_t + M_{t+1} x_{t+1}  (x_{t+1} in vec2)
-    const double* Mn = Mt + (size_t)(t + 1) * NN;
-    for (int a0 = 0; a0 < N; a0 += NT / 8) {
-      const int a = a0 + gj;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int a = 64 * h + gj;
       double v = 0.0;
-      if (a < N && t < T)
-        for (int j = gq; j < N; j += 8) v = fma(Mn[a * N + j], vec2[j], v);
+#pragma unroll
+      for (int k = 0; k < kRB; ++k) {
+        const int j = gq + 8 * k;
+        if (j < N) v = fma(pm[h][k], vec2[j], v);
+      }
       v += dpp_d<0xB1>(v);
       v += dpp_d<0x4E>(v);
       v += dpp_d<0x141>(v);
       if (a < N && gq == 0)
         vec[a] = v + wv[(size_t)t * N + a] + rng.normal(CCMM_RNG_SVZ, (uint32_t)(a + N * t));
     }
+    if (t > 0) load_m(t - 1);
     __syncthreads();
     // x_t(a) = sum_{i >= a} Linv_t(i, a) v(i)
-    const double* Li = Lt + (size_t)t * NN;
-    for (int a0 = 0; a0 < N; a0 += NT / 8) {
-      const int a = a0 + gj;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int a = 64 * h + gj;
       double x = 0.0;
-      if (a < N)
-        for (int i = a + gq; i < N; i += 8) x = fma(Li[i * N + a], vec[i], x);
+#pragma unroll
+      for (int k = 0; k < kRB; ++k) {
+        const int i = gq + 8 * k;
+        if (i < N) x = fma(pl[h][k], vec[i], x);
+      }
       x += dpp_d<0xB1>(x);
       x += dpp_d<0x4E>(x);
       x += dpp_d<0x141>(x);
@@ -770,6 +809,7 @@ __global__ __launch_bounds__(kSvNT) void k_sv_big(Dims d, const int* __restrict_
         vec2[a] = x;  // every other read of vec2 precedes the barrier above
       }
     }
+    if (t > 0) load_l(t - 1);
     __syncthreads();
   }
   if (bad && tid == 0) atomicOr(&cs.status[c], 8);
