@@ -397,16 +397,15 @@ constexpr int kCB = 16;
 template <int NT>
 __device__ void wg_chol_inv(double* S, int n, double* Tb, int* bad) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int p0 = 0; p0 < n; p0 += kCB) {
-    const int pw = min(kCB, n - p0);
-    if (wave == 0) {
+  // wave 0: factor the diagonal block at q0 (qw rows) and store its inverse Dv over it
+  auto diag = [&](int q0, int qw) {
       double row[kCB], dv[kCB], ipk[kCB];
 #pragma unroll
-      for (int m = 0; m < kCB; ++m) row[m] = (lane < pw && m <= lane) ? S[(p0 + lane) * kNL + p0 + m] : 0.0;
+      for (int m = 0; m < kCB; ++m) row[m] = (lane < qw && m <= lane) ? S[(q0 + lane) * kNL + q0 + m] : 0.0;
 #pragma unroll
       for (int kk = 0; kk < kCB; ++kk) {
         ipk[kk] = 1.0;
-        if (kk < pw) {
+        if (kk < qw) {
           double dkk = readlane_d(row[kk], kk);
           if (!(dkk > 0.0)) {
             *bad = 1;
@@ -434,7 +433,7 @@ __device__ void wg_chol_inv(double* S, int n, double* Tb, int* bad) {
       for (int c = 0; c < kCB; ++c) dv[c] = (lane == c) ? 1.0 : 0.0;
 #pragma unroll
       for (int k = 0; k < kCB; ++k) {
-        if (k < pw) {
+        if (k < qw) {
           if (lane == k) {
             const double il = ipk[k];
 #pragma unroll
@@ -448,11 +447,14 @@ __device__ void wg_chol_inv(double* S, int n, double* Tb, int* bad) {
           }
         }
       }
-      if (lane < pw)
+      if (lane < qw)
 #pragma unroll
         for (int m = 0; m < kCB; ++m)
-          if (m <= lane) S[(p0 + lane) * kNL + p0 + m] = dv[m];
-    }
+          if (m <= lane) S[(q0 + lane) * kNL + q0 + m] = dv[m];
+  };
+  if (wave == 0) diag(0, min(kCB, n));
+  for (int p0 = 0; p0 < n; p0 += kCB) {
+    const int pw = min(kCB, n - p0);
     __syncthreads();
     // 16 x 16 blocks on v_mfma_f64_16x16x4 (A(lr, lq), B(lq, lr), D(lq + 4 r, lr)), one block task
     // per wave round robin; Dv(r, q) = S(p0 + r, p0 + q), q <= r
@@ -493,7 +495,11 @@ __device__ void wg_chol_inv(double* S, int n, double* Tb, int* bad) {
     __syncthreads();
     // (c) S(I, I2) -= L(I, pb) L(I2, pb)', pb < I2 <= I;  (d) Linv(pb, J) = -Dv T(J), J < pb
     const int mb = NB - 1 - pb, nc = mb * (mb + 1) / 2;
-    for (int task = wave; task < nc + pb; task += NT / 64) {
+    // wave 0 takes task 0 only (when there is a next diagonal block to factor); the rest go
+    // round robin over waves 1..7
+    const bool la = pb + 1 < NB;
+    const int t0 = la ? (wave == 0 ? 0 : wave) : wave, tstep = la ? (wave == 0 ? (1 << 30) : NT / 64 - 1) : NT / 64;
+    for (int task = t0; task < nc + pb; task += tstep) {
       dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
       if (task < nc) {
         int x0 = 0, y0 = task;
@@ -515,6 +521,12 @@ __device__ void wg_chol_inv(double* S, int n, double* Tb, int* bad) {
           const int row = 16 * I + lq + 4 * r4;
           if (row < n && rb < n) S[row * kNL + rb] -= acc[r4];
         }
+        if (task == 0) {
+          // look-ahead: task 0 is the trailing update of the next diagonal block (wave 0's
+          // first task), so wave 0 factors and inverts it now, beside the other waves' tasks
+          wave_lds_sync();
+          diag(p0 + kCB, min(kCB, n - p0 - kCB));
+        }
       } else {
         const int J = task - nc;
 #pragma unroll
@@ -531,8 +543,8 @@ __device__ void wg_chol_inv(double* S, int n, double* Tb, int* bad) {
         }
       }
     }
-    __syncthreads();
   }
+  __syncthreads();
 }
 
 // ================================================================ SV (time-ordered sampler)
