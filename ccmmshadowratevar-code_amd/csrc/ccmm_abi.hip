@@ -1403,8 +1403,9 @@ struct ccmm_chains {
         (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns + N * Ns + N * p * Ns) * sizeof(double);
     const int a_lds = (lds_cond + (size_t)N * N * sizeof(double) <= 64 * 1024) ? 1 : 0;
     if (a_lds) lds_cond += (size_t)N * N * sizeof(double);
-    // one wave per censored month; four when the month's staging fills a CU's LDS (N > 64)
-    const int nth_cond = (N > 64) ? 256 : 64;
+    // two waves per censored month (BH N = 20: k_elb_cond 1.30 -> 1.13 ms at B = 256); four when the
+    // month's staging fills a CU's LDS (N > 64)
+    const int nth_cond = (N > 64) ? 256 : 128;
     launch(KID_ELBCOND, [&] {
       switch (Ns) {
 #define CASE_NSC(NS)                                                                                 \

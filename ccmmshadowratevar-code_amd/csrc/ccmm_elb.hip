@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState c
   constexpr int Ns = NS;
   const int T = e.elbT[s], T0 = e.elbT0[s];
   const int t = e.cens[(size_t)s * e.elbTmax + ci];
-  // one wave for N <= 64; four waves for larger N (the N x p x Ns staging alone fills one CU's LDS)
+  // two waves for N <= 64; four for larger N (the N x p x Ns staging alone then fills one CU's LDS)
   const int tid = threadIdx.x, nth = blockDim.x, lane = tid & 63, wv = tid >> 6, nwv = nth >> 6;
   const int ncol = 2 * p * Ns;
   const double* Phi = e.Phi + (size_t)c * N * Np;
