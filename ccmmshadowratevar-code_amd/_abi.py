@@ -64,7 +64,7 @@ class BatchConfig(C.Structure):
 BATCH_OUT_FIELDS = ("logscore", "fcstYhat", "fcstShadowYhat", "PAImean", "PAIstdev", "shadowrate_all",
                     "countELBaccept", "attempts", "fcstYmedian", "fcstYcrps", "fcstYquantiles", "fcstYcummedian",
                     "fcstYcumcrps", "fcstYcumquantiles", "fcstShadowYmedian", "fcstShadowYquantiles", "PAImedian",
-                    "PAIquantiles", "scoreDraws")
+                    "PAIquantiles", "scoreDraws", "shadowratePSRF")
 
 
 class BatchOut(C.Structure):
@@ -147,6 +147,8 @@ _SIGS = {
                             C.c_int, _dp, _dp, _dp, _dp, _ip]),
     "ccmm_run_batch": (C.c_int, [C.c_void_p, C.POINTER(BatchConfig), C.c_int, C.POINTER(Vintage),
                                  C.POINTER(BatchOut)]),
+    "ccmm_psrf": (C.c_int, [C.c_int, C.c_int, C.c_int, _dp, _dp]),
+    "ccmm_shadowrate_psrf": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _u8p, _dp]),
     "ccmm_selftest_mfma_f64": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
     "ccmm_selftest_mfma_f64_acc": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp]),
 }
@@ -197,6 +199,34 @@ def _ptr(a, ct=_dp):
     if a is None:
         return None
     return a.ctypes.data_as(ct)
+
+
+def psrf(X):
+    """ccmm_psrf: psrf(X) of DiagnosticsShadowrate.m:34-128; X n x D (one chain, split into thirds)
+    or n x D x M.  Returns R (D,).  Host computation inside libccmm (no GPU needed)."""
+    X = _f(X)
+    if X.ndim == 1:
+        X = X[:, None]
+    n, D = X.shape[:2]
+    M = X.shape[2] if X.ndim == 3 else 1
+    R = np.zeros(D)
+    _check(load_library().ccmm_psrf(n, D, M, _ptr(X), _ptr(R)), "ccmm_psrf")
+    return R
+
+
+def shadowrate_psrf(draws, mask, elbT=None):
+    """ccmm_shadowrate_psrf: shadowratePSRF(:, vintage) of goVARshadowrateBlockHybrid.m:322-325.
+    draws M x Ns x ldT [x C] kept shadow rates, mask Ns x elbT (ELBdummy(startELB:thisT, :)').
+    Returns Ns values."""
+    d = _f(draws)
+    M, Ns, ldT = d.shape[:3]
+    Cc = d.shape[3] if d.ndim == 4 else 1
+    mk = np.asfortranarray(np.asarray(mask, bool).reshape(Ns, -1), dtype=np.uint8)
+    eT = mk.shape[1] if elbT is None else int(elbT)
+    out = np.zeros(Ns)
+    _check(load_library().ccmm_shadowrate_psrf(M, Ns, eT, ldT, Cc, _ptr(d), _ptr(mk, _u8p), _ptr(out)),
+           "ccmm_shadowrate_psrf")
+    return out
 
 
 class Context:
@@ -483,6 +513,7 @@ class Context:
                       PAIstdev=(K, N, V), countELBaccept=(V,), attempts=(V,))
         if shadow:
             shapes["shadowrate_all"] = (MCMCdraws, Ns_, elbTall, C_, V)
+            shapes["shadowratePSRF"] = (Ns_, V)
         if postprocess:
             shapes.update(fcstYmedian=(N, H, V), fcstYcrps=(N, H, V), fcstYquantiles=(N, H, nq, V),
                           fcstYcummedian=(N, H, V), fcstYcumcrps=(N, H, V), fcstYcumquantiles=(N, H, nq, V),

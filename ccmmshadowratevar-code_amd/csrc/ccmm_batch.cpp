@@ -70,8 +70,7 @@ struct Runner {
     C = cf.nchains;
     H = cf.H;
     Nd = cf.MCMCdraws > 0 ? cf.fcstNdraws / cf.MCMCdraws : 0;
-    Ny = 0;
-    for (int i = 0; i < N; ++i) Ny += cf.ndxYields[i] != 0;
+    Ny = 0;  // counted in validate(), once ndxYields is known to be non-NULL
     elbTall = 0;
     for (int v = 0; v < V; ++v)
       if (shadow) elbTall = std::max(elbTall, vin[v].T - vin[v].elbT0);
@@ -89,6 +88,7 @@ struct Runner {
     arg(cf.fcstNdraws >= cf.MCMCdraws && cf.fcstNdraws % cf.MCMCdraws == 0,
         "fcstNdraws must be multiple of MCMCdraws");  // goVARshadowrateBlockHybrid.m:123-126
     arg(H >= 1 && cf.ndxYields, "H >= 1 and ndxYields required");
+    for (int i = 0; i < N; ++i) Ny += cf.ndxYields[i] != 0;
     arg(!shadow || (Ns >= 1 && cf.ndxS), "shadow-rate models need Ns >= 1 and ndxS");
     arg(!hybrid || !cf.actual_block, "actual_block must be NULL for the hybrid model");
     arg(cf.model != CCMM_MODEL_BLOCKHYBRID || cf.actual_block, "block hybrid needs actual_block");
@@ -126,6 +126,7 @@ struct Runner {
     nanfill(o->PAImedian, KN, v);
     nanfill(o->PAIquantiles, KN * nq, v);
     nanfill(o->scoreDraws, size_t(cf.fcstNdraws) * C * 4, v);
+    nanfill(o->shadowratePSRF, size_t(Ns), v);
   }
 
   // One chain set over the vintages `vs` (indices into vin) on attempt `attempt`; writes the
@@ -213,7 +214,7 @@ struct Runner {
     std::vector<double> fYsum(NH * B, 0.0), fYcsum(NH * B, 0.0), Psum, P2sum;
     std::vector<double> shadowd;  // M x Ns x elbTmax x B
     const int eT = cc.elbTmax;
-    if (shadow && o->shadowrate_all) shadowd.assign(size_t(M) * Ns * eT * B, kNaN);
+    if (shadow && (o->shadowrate_all || o->shadowratePSRF)) shadowd.assign(size_t(M) * Ns * eT * B, kNaN);
     if (!cf.postprocess) {
       Psum.assign(KN * B, 0.0);
       P2sum.assign(KN * B, 0.0);
@@ -355,6 +356,12 @@ struct Runner {
                 dst[((size_t(c) * elbTall + t) * Ns + j) * M + m] =
                     t < eT ? shadowd[((b * eT + t) * Ns + j) * M + m] : kNaN;
               }
+      }
+      if (o->shadowratePSRF && Ns > 0) {
+        // goVARshadowrateBlockHybrid.m:322-325: per shadow rate, psrf over its censored months
+        const ccmm_vintage& u = vin[v];
+        check(ccmm_shadowrate_psrf(M, Ns, u.T - u.elbT0, eT, C, shadowd.data() + size_t(s) * C * M * Ns * eT,
+                                   u.sNaN, o->shadowratePSRF + size_t(v) * Ns));
       }
       if (o->attempts) o->attempts[v] = attempt + 1;
     }

@@ -596,7 +596,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
         mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
         ++y;
       }
-      uint8_t fl;
+      uint8_t fl = 0;
       cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a], fl);
       if (e.flags && lane == 0)  // drawTruncNormal.m branch taken (oracle.draw_trunc_normal flags)
         e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
@@ -746,7 +746,7 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
           mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
           ++y;
         }
-        uint8_t fl;
+        uint8_t fl = 0;
         cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a], fl);
         if (e.flags && lane == 0)
           e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;

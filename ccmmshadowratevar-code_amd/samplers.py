@@ -12,6 +12,8 @@ Every numerical step goes through ``libccmm.so``; there is no CPU fallback.
 """
 from __future__ import annotations
 
+import warnings
+
 import numpy as np
 
 from . import _abi
@@ -576,9 +578,15 @@ def save_qrt_mat(filename, res, *, data, ydates, p, ncode, tcode, cumcode, ndxSH
 
 
 def matlab_prctile(x, pct, axis=0):
-    """MATLAB prctile (Statistics Toolbox): sorted values sit at percentiles
-    100 (i - 0.5) / n, linear interpolation between, clamped outside = numpy 'hazen'."""
-    return np.percentile(np.asarray(x, float), pct, axis=axis, method="hazen")
+    """MATLAB prctile (Statistics Toolbox): NaN values removed, the n sorted values sit at
+    percentiles 100 (i - 0.5) / n, linear interpolation between, clamped outside = numpy 'hazen'
+    (NaN where every value is NaN)."""
+    x = np.asarray(x, float)
+    if not np.isnan(x).any():
+        return np.percentile(x, pct, axis=axis, method="hazen")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)                # all-NaN slices: NaN
+        return np.nanpercentile(x, pct, axis=axis, method="hazen")
 
 
 def _bh_units(data0, ydates0, Tjumpoffs, p, np_, ndxSHADOWRATE, ndxOTHERYIELDS,
@@ -710,6 +718,11 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
     on the device (ccmm_chains_summaries_floor).  The forecast paths of every vintage stay in HBM
     until the summaries are taken (Python engine only).
 
+    keep_draws=True also returns the kept draws per vintage: PAI_all[v] (M x K x N x C) and
+    shadowrate_all[v] (M x Ns x elbT x C).  shadowratePSRF (Ns x V) is DiagnosticsShadowrate of each
+    vintage's kept shadow rates over the months at the ELB (:322-325, ccmm_shadowrate_psrf; one chain:
+    the reference's first-third / last-third split, C chains: psrf over the chains).
+
     engine="native" runs the rank's vintage loop (chain set, burn-in, kept sweeps, forecast
     records, device summaries, retries) inside the library, ccmm_run_batch (include/ccmm.h): the
     same Philox streams and the same per-vintage results (keep_draws / maxlambda not available
@@ -747,6 +760,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
         raise ValueError("model='shadowrate' runs on the Python engine (ccmm_chains_summaries_floor)")
     smask = np.zeros(N, bool)
     smask[ndxSHADOWRATE] = True
+    elbdummy = data0[:, ndxSHADOWRATE] <= ELBbound                      # ELBdummy, :131
     if hybrid and maxlambda:
         raise ValueError("goVARhybrid.m computes no max VAR roots (:383-430 commented out)")
     K = N * p + 1 + (ndxSHADOWRATE.size * p if hybrid else 0)
@@ -926,8 +940,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                     # is NaN) and prctile (NaN draws removed), goVARshadowrate.m:345-348
                     mr = miss[:, :, :bm.elbT, cs].transpose(2, 1, 0, 3).reshape(bm.elbT, Ns, -1)
                     r["missingrateMid"] = np.median(mr, axis=2)
-                    r["missingrateTails"] = np.moveaxis(
-                        np.nanpercentile(mr, [5, 25, 75, 95], axis=2, method="hazen"), 0, 2)
+                    r["missingrateTails"] = np.moveaxis(matlab_prctile(mr, [5, 25, 75, 95], axis=2), 0, 2)
             elif i in post:
                 q = post[i]
                 nq = pct.size
@@ -955,6 +968,12 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                 r["PAImean"] = Psum[:, :, cs].sum(axis=2) / nk
                 var = P2sum[:, :, cs].sum(axis=2) / nk - r["PAImean"] ** 2
                 r["PAIstdev"] = np.sqrt(np.maximum(var, 0.0))               # std(.,1,1): 1/n
+            if shadow is not None and keep_draws:
+                r["shadowrate_all"] = shadow[:, :, :bm.elbT, cs].copy()     # M x Ns x elbT x C
+            if shadow is not None:
+                # goVARshadowrateBlockHybrid.m:322-325: DiagnosticsShadowrate per shadow rate over
+                # its months at the ELB, ELBdummy(startELB:thisT, s)
+                r["shadowratePSRF"] = _abi.shadowrate_psrf(shadow[..., cs], elbdummy[startELB - 1:thisT].T)
             if shadow is not None and bm.elbT > 0:
                 # shadowrate_all permuted to (Nobs, Ns, draws) (:329-334)
                 sr = shadow[:, :, :bm.elbT, cs].transpose(2, 1, 0, 3).reshape(bm.elbT, Ns, -1)
@@ -1017,6 +1036,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                fcstShadowYhat=np.full((Ny, H, V), np.nan), fcstYrealized=np.full((N, H, V), np.nan),
                PAImean=np.full((K, N, V), np.nan), PAIstdev=np.full((K, N, V), np.nan),
                countELBaccept=np.full(V, -1),
+               shadowratePSRF=np.full((Ns, V), np.nan),                      # :213
                shadowrateVintagesMid=np.full((Tdata, Ns, V), np.nan),
                shadowrateVintagesTails=np.full((Tdata, Ns, 4, V), np.nan))
     if is_sr:
@@ -1025,6 +1045,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                    missingrateVintagesTails=np.full((Tdata, Ns, 4, V), np.nan))
     if keep_draws:
         out["PAI_all"] = {}
+        out["shadowrate_all"] = {}
     nq = pct.size
     if postprocess:
         for nm, shp in (("fcstYmedian", (N, H)), ("fcstYcrps", (N, H)), ("fcstYquantiles", (N, H, nq)),
@@ -1057,6 +1078,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
         out["PAIstdev"][..., v] = r["PAIstdev"]
         if r.get("countELBaccept") is not None:
             out["countELBaccept"][v] = r["countELBaccept"]
+        if "shadowratePSRF" in r:
+            out["shadowratePSRF"][:, v] = r["shadowratePSRF"]
         if "shadowrateMid" in r:
             thisT = r["thisT"]
             out["shadowrateVintagesMid"][jumpoff:thisT, :, v] = r["shadowrateMid"]
@@ -1066,6 +1089,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
             out["missingrateVintagesTails"][jumpoff:r["thisT"], :, :, v] = r["missingrateTails"]
         if keep_draws and "PAI_all" in r:
             out["PAI_all"][v] = r["PAI_all"]
+        if keep_draws and "shadowrate_all" in r:
+            out["shadowrate_all"][v] = r["shadowrate_all"]
         for nm in ("fcstYmedian", "fcstYcrps", "fcstYquantiles", "fcstYcumrealized", "fcstYcumhat",
                    "fcstYcummedian", "fcstYcumcrps", "fcstYcumquantiles", "fcstShadowYmedian",
                    "fcstShadowYquantiles", "PAImedian", "PAIquantiles", "fcstYmvlogscoreDraws",
@@ -1117,8 +1142,12 @@ def _native_batch(ctx, units, mine, *, C, N, p, K, Ns, H, Nd, MCMCdraws, burn, g
     Ny = int(np.count_nonzero(yields))
     for i, (thisT, bm, yr) in enumerate(units):
         a = int(out["attempts"][i])
-        if a > 1:
-            retries.append(mine[i])
+        # one list per retry attempt, as the Python engine reports them: vintage i was retried on
+        # attempts 1 .. a - 1 (a - 1 > max_retries: it failed every time)
+        for k in range(1, min(a, max_retries + 2)):
+            while len(retries) < k:
+                retries.append([])
+            retries[k - 1].append(mine[i])
         if a > max_retries + 1:
             res[mine[i]] = None
             continue
@@ -1142,13 +1171,14 @@ def _native_batch(ctx, units, mine, *, C, N, p, K, Ns, H, Nd, MCMCdraws, burn, g
                      fcstShadowYquantiles=out["fcstShadowYquantiles"][..., i].reshape(Ny, H, nq),
                      fcstYmvlogscoreDraws=out["scoreDraws"][:, 1, i], fcstYmvlogscoreXdraws=out["scoreDraws"][:, 2, i],
                      fcstYmvlogscoreIdraws=out["scoreDraws"][:, 3, i])
+        r["shadowratePSRF"] = out["shadowratePSRF"][:, i].copy()          # :322-325
         if bm.elbT > 0:
             sh = out["shadowrate_all"][:, :, :bm.elbT, :, i]                 # M x Ns x elbT x C
             sr = sh.transpose(2, 1, 0, 3).reshape(bm.elbT, Ns, -1)
             r["shadowrateMid"] = np.median(sr, axis=2)
             r["shadowrateTails"] = np.moveaxis(matlab_prctile(sr, [5, 25, 75, 95], axis=2), 0, 2)
         res[mine[i]] = r
-    return res, [retries] if retries else []
+    return res, retries
 
 
 def goVARshadowrate_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIELDS, minnesotaPriorMean, *,

@@ -480,6 +480,8 @@ typedef struct {                /* V = number of vintages; any pointer may be NU
   double* PAImedian;            /* K x N x V */
   double* PAIquantiles;         /* K x N x nq x V */
   double* scoreDraws;           /* (fcstNdraws * nchains) x 4 x V, order (Nd, kept draw, chain) */
+  double* shadowratePSRF;       /* Ns x V (shadow-rate models): ccmm_shadowrate_psrf of the vintage's kept
+                                   shadow rates (goVARshadowrateBlockHybrid.m:322-325) */
 } ccmm_batch_out;
 
 int ccmm_run_batch(ccmm_ctx* ctx, const ccmm_batch_config* cfg, int V, const ccmm_vintage* vintages,
@@ -516,6 +518,25 @@ int ccmm_girf_hybrid(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const 
                      const double* z, const double* svz, uint64_t seed, double* yhat);
 
 /* ------------------------------------------------------------ diagnostics */
+
+/* psrf(X) of DiagnosticsShadowrate.m:34-128 (== Diagnostics.m:28; Brooks & Gelman 1998, square-root
+ * form): X n x D x M, M sequences of n draws of D variables; M == 1 splits the one chain into its
+ * first and last floor(n/3) draws (:82-91).  R out: D.  Host computation.  CCMM_ERR_ARG "Too few
+ * samples" as :103-105 when a sequence would be empty. */
+int ccmm_psrf(int n, int D, int M, const double* X, double* R);
+
+/* shadowratePSRF(:, vintage) of goVARshadowrateBlockHybrid.m:322-325 (goVARhybrid.m:322-323,
+ * goVARshadowrate.m:332-333): for each shadow rate s, DiagnosticsShadowrate(shadowrate_all(:, s,
+ * ELBdummy(startELB:thisT, s))) = the mean of psrf over the rate's censored months (NaN when there
+ * are none).  draws M x Ns x ldT x C (the kept shadow rates of C chains; the first elbT months are
+ * the vintage's window), mask Ns x elbT (ELBdummy(startELB:thisT, :)', = elb.sNaN).  C == 1: the
+ * reference's one-chain split; C > 1: psrf over the C chains as sequences.  out: Ns (NaN where psrf
+ * would stop with 'Too few samples': M < 3 at C == 1, M < 2 at C > 1).  The
+ * reference's DiagnosticsShadowrate also evaluates ineff() (momentg), which errors below 100 draws
+ * (Diagnostics.m momentg 'needs a larger number of ndraws'); its result is not an output and the
+ * check is not reproduced. */
+int ccmm_shadowrate_psrf(int M, int Ns, int elbT, int ldT, int C, const double* draws, const uint8_t* mask,
+                         double* out);
 
 /* Predictive density of one kept draw per chain, batched over B chains.
  * Replaces the doPredictiveDensity block mcmcVAR.m:298-381 (same simulation in

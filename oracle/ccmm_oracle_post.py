@@ -34,6 +34,27 @@ def prctile(x, pct, axis=0):
     return np.percentile(np.asarray(x, float), pct, axis=axis, method="hazen")
 
 
+def prctile_nan(x, pct):
+    """MATLAB prctile of one vector with NaN values removed first (prctile ignores NaN; all NaN:
+    NaN), written out: the i-th of the n sorted values at percentile 100 (i - 0.5) / n."""
+    xs = np.sort(np.asarray(x, float)[~np.isnan(np.asarray(x, float))])
+    n = xs.size
+    out = []
+    for pc in np.atleast_1d(pct):
+        if n == 0:
+            out.append(np.nan)
+            continue
+        r = n * pc / 100.0 + 0.5                     # 1-based position
+        if r <= 1:
+            out.append(xs[0])
+        elif r >= n:
+            out.append(xs[-1])
+        else:
+            k = int(np.floor(r))
+            out.append(xs[k - 1] + (r - k) * (xs[k] - xs[k - 1]))
+    return np.array(out)
+
+
 def median(x, axis=0):
     return np.median(np.asarray(x, float), axis=axis)
 

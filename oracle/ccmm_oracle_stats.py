@@ -45,3 +45,47 @@ def momentg(draws):
         out[f"nse{k}"] = np.where(vn > 0, np.sqrt(np.maximum(vn, 0.0)), -1.0)
         out[f"rne{k}"] = varg / (nuse * vn)
     return out
+
+
+def psrf(X):
+    """Potential scale reduction factor as DiagnosticsShadowrate.m:34-134 computes it
+    (Brooks & Gelman 1998, square-root form; the same function as Diagnostics.m:28).
+
+    X: n x D (one chain: split into its first and last thirds, :82-91) or n x D x M
+    (M sequences).  Statement order of :106-128: W = sum_i sum_t (x - mean_i)^2 / ((n-1) M),
+    Bpn = sum_i (mean_i - m)^2 / (M - 1), S = (n-1)/n W + Bpn,
+    R = sqrt((M+1)/M S / W - (n-1)/M/n).  Returns R (D,)."""
+    X = np.asarray(X, dtype=float)
+    if X.ndim == 1:
+        X = X[:, None]
+    if X.ndim == 2:
+        n = X.shape[0] // 3                                  # floor(size(X,1)/3), :85
+        X = np.stack([X[:n], X[X.shape[0] - n:]], axis=2)    # first and last thirds, :87-88
+    n, D, M = X.shape
+    if n < 1:
+        raise ValueError("Too few samples")                  # :103-105
+    W = np.zeros(D)
+    for i in range(M):                                       # :108-113
+        x = X[:, :, i] - X[:, :, i].mean(axis=0)
+        W = W + (x * x).sum(axis=0)
+    W = W / ((n - 1) * M)
+    means = X.mean(axis=0)                                   # D x M
+    m = means.mean(axis=1)                                   # :117
+    Bpn = np.zeros(D)
+    for i in range(M):                                       # :118-122
+        x = means[:, i] - m
+        Bpn = Bpn + x * x
+    Bpn = Bpn / (M - 1)
+    S = (n - 1) / n * W + Bpn                                # :125-128
+    with np.errstate(divide="ignore", invalid="ignore"):
+        R = (M + 1) / M * S / W - (n - 1) / M / n
+        return np.sqrt(R)
+
+
+def diagnostics_shadowrate(draws):
+    """DiagnosticsShadowrate.m:1-22: mean over the shadow-rate cells of psrf(draws), draws
+    n x nObs (n x nObs x M for M chains); NaN when there are no cells (mean of an empty row)."""
+    draws = np.asarray(draws, dtype=float)
+    if draws.shape[1] == 0:
+        return float("nan")
+    return float(np.mean(psrf(draws)))

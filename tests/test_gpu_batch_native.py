@@ -10,7 +10,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 KEYS = ("fcstYmvlogscore", "fcstYmvlogscoreX", "fcstYmvlogscoreI", "fcstYhat", "fcstShadowYhat", "PAImean",
-        "PAIstdev", "countELBaccept", "shadowrateVintagesMid", "shadowrateVintagesTails")
+        "PAIstdev", "countELBaccept", "shadowrateVintagesMid", "shadowrateVintagesTails", "shadowratePSRF")
 POST = ("fcstYmedian", "fcstYcrps", "fcstYquantiles", "fcstYcummedian", "fcstYcumcrps", "fcstYcumquantiles",
         "fcstShadowYmedian", "fcstShadowYquantiles", "PAImedian", "PAIquantiles", "fcstYmvlogscoreDraws",
         "fcstYmvlogscoreXdraws", "fcstYmvlogscoreIdraws", "fcstYcumhat", "fcstYcumrealized")
@@ -51,3 +51,49 @@ def test_native_batch_argument_errors(pkg, ctx):
                       ndxYields=np.zeros(4, bool), nchains=1, MCMCdraws=4, burnin=0, gibbsburn=1, Nproposals=0,
                       fcstNdraws=6, H=2, elb=0.25, seed=1, chunk=2, max_retries=0, postprocess=False, pct=(),
                       cumcode=None, vintages=[])
+    with pytest.raises(RuntimeError, match="ndxYields required"):       # NULL ndxYields: an error, not a crash
+        ctx.run_batch(model=pkg.MODEL_BLOCKHYBRID, N=4, p=2, Ns=1, ndxS=[0], actual_block=np.ones(4, bool),
+                      ndxYields=None, nchains=1, MCMCdraws=4, burnin=0, gibbsburn=1, Nproposals=0,
+                      fcstNdraws=4, H=2, elb=0.25, seed=1, chunk=2, max_retries=0, postprocess=False, pct=(),
+                      cumcode=None, vintages=[])
+
+
+@pytest.mark.parametrize("model,C", [("blockhybrid", 1), ("blockhybrid", 3), ("hybrid", 1)])
+def test_shadowrate_psrf_matches_oracle(pkg, fred, model, C):
+    """shadowratePSRF (goVARshadowrateBlockHybrid.m:322-325 / goVARhybrid.m:322-323): per vintage and
+    shadow rate, DiagnosticsShadowrate = mean of psrf (DiagnosticsShadowrate.m:34-128) over the kept
+    draws of the months at the ELB, ELBdummy(startELB:thisT, s).  Checked against the oracle's psrf
+    on the kept draws the run returns (1e-12), on both engines."""
+    from oracle.ccmm_oracle_stats import diagnostics_shadowrate
+    S = pkg.samplers
+    d = fred
+    ELB = 0.25
+    ndxS, ndxO, _ = pkg.model.setShadowYields(d["ncode"], ELB)
+    mpm = pkg.model.setMinnesotaMean(d["ncode"])
+    nT = len(d["ydates"])
+    Tj = [nT - 160, nT - 100, nT - 30, nT]
+    kw = dict(Tjumpoffs=Tj, MCMCdraws=30, fcstNdraws=30, burnin=6, gibbsburn=5, nchains=C, chunk=10,
+              Nproposals=64, model=model, fcstNhorizons=6)
+    ref = S.goVARshadowrateBlockHybrid_batch(d["data"], d["ydates"], ndxS, ndxO, mpm, keep_draws=True, **kw)
+    nat = S.goVARshadowrateBlockHybrid_batch(d["data"], d["ydates"], ndxS, ndxO, mpm, engine="native", **kw)
+    e0 = pkg.model.elbT0_of(d["data"], ndxS, ELB, 12)
+    startELB = e0 + 1 + 12
+    dummy = d["data"][:, ndxS] <= ELB                                  # ELBdummy (:131)
+    assert ref["shadowratePSRF"].shape == (len(ndxS), len(Tj))
+    worst = 0.0
+    for v, thisT in enumerate(Tj):
+        sr = ref["shadowrate_all"][v]                                  # M x Ns x elbT x C
+        mask = dummy[startELB - 1:thisT]                               # elbT x Ns
+        assert sr.shape[2] == mask.shape[0]
+        for s in range(len(ndxS)):
+            cells = sr[:, s][:, mask[:, s], :]                         # M x nObs x C
+            want = diagnostics_shadowrate(cells[:, :, 0] if C == 1 else cells)
+            for got in (ref["shadowratePSRF"][s, v], nat["shadowratePSRF"][s, v]):
+                if np.isnan(want):
+                    assert np.isnan(got), (v, s)
+                    continue
+                err = abs(got - want) / max(1.0, abs(want))
+                worst = max(worst, err)
+                assert err < 1e-12, (v, s, got, want)
+    print(f"  {model} C={C}: shadowratePSRF {ref['shadowratePSRF'].round(3).tolist()} max rel {worst:.2e}")
+    assert np.all(np.isfinite(ref["shadowratePSRF"][:, 1:]))

@@ -151,3 +151,29 @@ def test_vintage_batch_argument_checks(pkg, fred):
         S.goVARhybrid_batch(*args, maxlambda=True, Tjumpoffs=[700])
     with pytest.raises(ValueError, match="multiple of MCMCdraws"):
         S.goVARshadowrate_batch(*args, MCMCdraws=10, fcstNdraws=15, Tjumpoffs=[700])
+
+
+def test_psrf_entry_points_match_oracle(pkg):
+    """ccmm_psrf / ccmm_shadowrate_psrf (host computations inside libccmm) against the oracle's psrf
+    restatement (DiagnosticsShadowrate.m:34-128): one chain (thirds), C chains, the ELB mask."""
+    from oracle.ccmm_oracle_stats import psrf, diagnostics_shadowrate
+    A = pkg._abi
+    rng = np.random.default_rng(11)
+    X = np.cumsum(rng.standard_normal((301, 6)), axis=0)
+    assert np.max(np.abs(A.psrf(X) - psrf(X))) < 1e-12
+    X3 = rng.standard_normal((40, 3, 5))
+    assert np.max(np.abs(A.psrf(X3) - psrf(X3))) < 1e-12
+    M, Ns, ldT, elbT = 120, 3, 9, 7
+    for C in (1, 3):
+        d = rng.standard_normal((M, Ns, ldT, C)) * rng.random((1, Ns, ldT, 1)) + rng.random((1, 1, ldT, C))
+        mask = rng.random((Ns, elbT)) < 0.5
+        mask[2] = False                                # rate with no month at the ELB: NaN
+        got = A.shadowrate_psrf(d, mask)
+        for s in range(Ns):
+            cells = d[:, s, :elbT, :][:, mask[s], :]
+            want = diagnostics_shadowrate(cells[:, :, 0] if C == 1 else cells)
+            if np.isnan(want):
+                assert np.isnan(got[s])
+            else:
+                assert abs(got[s] - want) < 1e-12 * max(1.0, abs(want)), (C, s, got[s], want)
+    assert np.all(np.isnan(A.shadowrate_psrf(np.ones((2, 2, 3)), np.ones((2, 3), bool))))   # too few draws

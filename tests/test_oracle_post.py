@@ -79,3 +79,47 @@ def test_save_qrt_mat_roundtrip(pkg, tmp_path):
     assert np.allclose(m["fcstYhat"], res["fcstYhat"])
     assert m["ndxSHADOWRATE"].ravel().tolist() == [3]      # 1-based
     assert m["fcstYmvlogscore"].shape == (1, V)
+
+
+def test_matlab_prctile_removes_nan(pkg, post):
+    """samplers.matlab_prctile (shadowrate* and missingrate* tails, goVARshadowrate.m:345-348) drops
+    NaN draws as MATLAB prctile does: equal to the written-out definition on the remaining values."""
+    S = pkg.samplers
+    rng = np.random.default_rng(8)
+    x = rng.standard_normal((5, 3, 41))
+    x[0, 0, :7] = np.nan
+    x[1, 2, ::3] = np.nan
+    x[2, 1, :] = np.nan                                # all NaN: NaN
+    got = np.moveaxis(S.matlab_prctile(x, [5, 25, 75, 95], axis=2), 0, 2)
+    for i in range(5):
+        for j in range(3):
+            want = post.prctile_nan(x[i, j], [5, 25, 75, 95])
+            assert np.array_equal(np.isnan(got[i, j]), np.isnan(want))
+            m = ~np.isnan(want)
+            assert np.allclose(got[i, j][m], want[m], rtol=0, atol=1e-14)
+    y = rng.standard_normal((4, 30))                   # no NaN: the plain hazen path
+    assert np.allclose(S.matlab_prctile(y, [2.5, 50], axis=1).T,
+                       [post.prctile_nan(r, [2.5, 50]) for r in y], rtol=0, atol=1e-14)
+
+
+def test_save_qrt_mat_varlist_has_psrf(pkg, tmp_path):
+    """The saved file holds every name of goVARshadowrateBlockHybrid.m:645-659's varlist that the batch
+    result carries, shadowratePSRF (Nshadowrates x Njumpoffs, :213) among the 'shadowrate*' names."""
+    from scipy.io import loadmat
+    S = pkg.samplers
+    N, H, V, Ns, T = 4, 3, 2, 2, 30
+    rng = np.random.default_rng(9)
+    res = dict(Tjumpoffs=np.array([25, 26]), fcstYhat=rng.standard_normal((N, H, V)),
+               shadowratePSRF=1.0 + rng.random((Ns, V)), shadowrateVintagesMid=rng.standard_normal((T, Ns, V)))
+    names = S.save_qrt_mat(tmp_path / "q.mat", res, data=rng.standard_normal((T, N)), ydates=np.arange(T), p=2,
+                           ncode=["A", "FEDFUNDS", "GS1", "GS10"], tcode=[5, 1, 1, 1],
+                           cumcode=[True, False, False, False], ndxSHADOWRATE=[1, 2], ndxOTHERYIELDS=[3],
+                           ELBbound=0.25, actualrateBlock=[True, False, False, False], datalabel="toy",
+                           modellabel="ELBblockhybrid", MCMCdraws=10, fcstNhorizons=H)
+    m = loadmat(tmp_path / "q.mat")
+    assert "shadowratePSRF" in names and m["shadowratePSRF"].shape == (Ns, V)
+    assert np.allclose(m["shadowratePSRF"], res["shadowratePSRF"])
+    fixed = {"data", "ydates", "p", "Tjumpoffs", "N", "ncode", "tcode", "cumcode", "fcstNhorizons",
+             "ndxSHADOWRATE", "ndxYIELDS", "ndxOTHERYIELDS", "ELBbound", "ELBdummy", "actualrateBlock",
+             "datalabel", "modellabel", "doQuarterly", "setQuantiles", "MCMCdraws"}
+    assert fixed <= set(names)

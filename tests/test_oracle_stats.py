@@ -90,3 +90,25 @@ def test_momentg_iid_and_ar1():
     # long-run sd of an AR(1) mean is sd / (1 - rho) per sqrt(n): the tapered estimates grow
     # toward it, the iid one does not
     assert w["nse3"][0] > 2.5 * w["nse"][0]
+
+
+def test_psrf_known_answer():
+    """psrf (DiagnosticsShadowrate.m:34-128) by hand: one chain 1..9 -> thirds [1 2 3], [7 8 9]:
+    W = 1, Bpn = 18, S = 2/3 + 18, R = sqrt(3/2 S - 1/3) = sqrt(83/3)."""
+    from oracle.ccmm_oracle_stats import psrf, diagnostics_shadowrate
+    assert abs(psrf(np.arange(1.0, 10.0))[0] - np.sqrt(83.0 / 3.0)) < 1e-14
+    # floor(10/3) = 3: [1 2 3] and the last three [8 9 10], Bpn = 2 * 3.5^2
+    assert abs(psrf(np.arange(1.0, 11.0))[0] - np.sqrt(1.5 * (2.0 / 3.0 + 24.5) - 1.0 / 3.0)) < 1e-14
+    # M sequences: R^2 = (M+1)/M S/W - (n-1)/(M n), S = (n-1)/n W + B/n
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((50, 2, 4)) + np.array([0.0, 0.3, -0.2, 0.5])[None, None, :]
+    n, M = 50, 4
+    for d in range(2):
+        x = X[:, d, :]
+        W = x.var(axis=0, ddof=1).mean()
+        B = n * x.mean(axis=0).var(ddof=1)
+        S = (n - 1) / n * W + B / n
+        assert abs(psrf(X)[d] - np.sqrt((M + 1) / M * S / W - (n - 1) / (M * n))) < 1e-13
+    # iid draws: R -> 1; no cells: NaN (mean of an empty row)
+    assert abs(diagnostics_shadowrate(rng.standard_normal((30000, 3))) - 1.0) < 0.01
+    assert np.isnan(diagnostics_shadowrate(np.zeros((300, 0))))
