@@ -207,12 +207,17 @@ def bh_sweep(st, bs: BHSetup, crn, return_flags=False, elb_impl="qr", use_ps=Fal
     draw in out["shadowrate_qr"].
 
     cta_form: "kron" = CTAsys.m as written; "syrk" = O.cta_sys_syrk (the same posterior in
-    the weighted-SYRK form; S120-sized systems)."""
+    the weighted-SYRK form; S120-sized systems); "mirror" = the device's operation order
+    (oracle/cta_mirror.cta with the per-equation designs)."""
     lin = bs.lin
     N, K, T = lin.N, lin.K, lin.T
     Y, X = st["Y"], st["X"]
     Xs = [bs.Xactual if bs.actualrateBlock[j] else X for j in range(N)]
-    if cta_form == "kron":
+    if cta_form == "mirror":
+        from . import cta_mirror
+        PAI = cta_mirror.cta(Y, Xs, N, K, st["A"], st["sqrtht"], lin.iVdiag, lin.iVb, st["PAI"], crn["zPAI"])
+        status = 0
+    elif cta_form == "kron":
         XX = np.empty((T, K, N))
         XX[:, :, bs.actualrateBlock] = bs.Xactual[:, :, None]
         XX[:, :, ~bs.actualrateBlock] = X[:, :, None]

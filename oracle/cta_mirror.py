@@ -97,16 +97,25 @@ def solve(fac, rhs, z):
 
 def cta(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z, factor_form="device"):
     """CTA.m:57-98 (CTA: one design) with the device's arithmetic throughout (factor_form="lapack":
-    LAPACK Cholesky and solves of the mirrored Gram and right-hand side)."""
+    LAPACK Cholesky and solves of the mirrored Gram and right-hand side).  X may also be a list of
+    N per-equation designs: CTAsys.m:57-108 (the block hybrid's actual-rate and shadow-rate slabs,
+    mcmcVARshadowrateBlockHybrid.m:341), each equation's Gram, right-hand side and residual on its
+    own design, in the same device order."""
     T = Y.shape[0]
-    Y, X, A, sh = _F(Y), _F(X), _F(A), _F(sqrtht)
+    Y, A, sh = _F(Y), _F(A), _F(sqrtht)
+    Xs = [_F(x) for x in X] if isinstance(X, (list, tuple)) else [_F(X)] * N
     PAI = _F(PAI).copy(order="F")
     E = np.zeros((T, N), order="F")
     L_ = lib()
-    L_.ccmm_mirror_resid(T, K, N, _p(Y), _p(X), _p(PAI), _p(E))
+    for j in range(N):                   # one residual column per equation, on its own design
+        Ej = np.zeros(T)
+        L_.ccmm_mirror_resid(T, K, 1, _p(np.ascontiguousarray(Y[:, j])), _p(Xs[j]),
+                             _p(np.ascontiguousarray(PAI[:, j])), _p(Ej))
+        E[:, j] = Ej
     v = np.zeros(T)
     rhs = np.zeros(K)
     for j in range(N):
+        X = Xs[j]
         sw = weights(A, sh, j)
         G = gram(X, sw)
         L_.ccmm_mirror_v(T, N, j, _p(A), _p(sh), _p(Y), _p(E), _p(v))

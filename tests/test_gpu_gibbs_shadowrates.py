@@ -71,3 +71,39 @@ def test_gibbs_shadowrates_dimension_mismatch(ctx, oracle, fred):
     with pytest.raises(RuntimeError, match="rc=-1"):
         ctx.gibbs_shadowrates(st["Y"][bs.elbT0:, :].T, bs.X0, Yhat, bs.ndxSmask, bs.sNaN[:2], lin.p,
                               C, Psi, SVol, 0.25, burnin=2)
+
+
+@pytest.mark.parametrize("burn", [0, 100])
+def test_gibbs_shadowrates_c3_drawn_state(ctx, oracle, fred, burn):
+    """The same drop-in on states the sampler visits: PAI, invA and sqrtht after one block-hybrid
+    sweep from a smooth-volatility state (the posterior draw of PAI shrinks the companion inside the
+    unit circle), so the conditionals are well conditioned and the GPU agrees with the oracle's
+    stable form to the north star's 1e-9 over 1 and 101 passes; branch flags bit-exact."""
+    from oracle import elb_fast as F
+    from helpers import random_state
+    bh, bs = _c3(oracle, fred)
+    lin = bs.lin
+    B = 2
+    ins, rho = [], []
+    for c in range(B):
+        rng = np.random.default_rng(90 + c)
+        st = random_state(oracle, lin, seed=90 + c)
+        st["X"], st["Y"] = lin.X.copy(), lin.Y.copy()
+        st = bh.bh_sweep(st, bs, bh.bh_draw_crn(rng, bs), elb_impl="stable")
+        C, Psi, SVol, Yhat = bh.elb_state_space(bs, st["PAI"], st["invA"], st["sqrtht"])
+        rho.append(float(np.max(np.abs(np.linalg.eigvals(C)))))
+        Y = st["Y"][bs.elbT0:, :].T.copy()
+        u = rng.random((len(bs.ndxS), bs.elbT, burn + 1))
+        ins.append((Y, bs.X0, Yhat, C, Psi, SVol, u))
+    stk = [np.stack([x[k] for x in ins], -1) for k in range(7)]
+    got, fl = ctx.gibbs_shadowrates(stk[0], stk[1], stk[2], bs.ndxSmask, bs.sNaN, lin.p, stk[3],
+                                    stk[4], stk[5], 0.25, burnin=burn, u=stk[6], flags=True)
+    for c in range(B):
+        Y, X0, Yhat, C, Psi, SVol, u = ins[c]
+        stab, sfl = F.gibbsdraw_shadowrates_stable(Y, X0, Yhat, bs.ndxSmask, bs.sNaN, lin.p, C, Psi, SVol, 0.25,
+                                                   1, burn, u, return_flags=True)
+        e_st = rel_err(got[:, :, 0, c], stab[:, :, 0], 0.1)
+        print("chain", c, "companion spectral radius", rho[c], "vs stable", e_st)
+        assert rho[c] < 1.0
+        assert e_st < 1e-9
+        np.testing.assert_array_equal(fl[..., c], sfl)

@@ -27,7 +27,7 @@ def test_bh_sweep_crn_ns5(pkg, ctx, oracle, bh):
     bs = toy_bh_setup(bh, N=7, p=2, ndxS=(1, 2, 3, 4, 5), ndxO=(6,), seed=11)
     assert len(bs.ndxS) == 5
     out = bh_run(pkg, ctx, oracle, bh, bs, B=2, nsweeps=2, seed=70)
-    bh_check(oracle, bs, *out, tol_pai=1e-7, tol_s=1e-7)
+    bh_check(oracle, bs, *out, tol_pai=1e-9, tol_s=1e-9)
 
 
 def test_ps_ns5_band_width_above_64(pkg, ctx, oracle, bh):
@@ -43,4 +43,4 @@ def test_ps_ns5_band_width_above_64(pkg, ctx, oracle, bh):
                      np.ones(N), 0.25, int(np.argmax(hit)) - p)
     assert len(bs.ndxS) == 5 and bs.sNaN[:, :40].all()   # band width 5 (p + 1) = 65
     got, S, ps, want = ps_run(pkg, ctx, oracle, bh, bs, B=2, nsweeps=2, NP=64, seed=13)
-    ps_check(oracle, bs, got, S, ps, want, 1e-7)
+    ps_check(oracle, bs, got, S, ps, want, 1e-9)

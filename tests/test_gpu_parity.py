@@ -155,14 +155,14 @@ def test_truncnorm_batch(ctx, oracle):
     assert np.all(got[100:] <= 0.25 + 1e-12)
 
 
-@pytest.mark.parametrize("B,nsweeps,tol", [(4, 1, 5e-8), (4, 3, 1e-6)])
-def test_linear_sweep_crn(pkg, ctx, oracle, fred, B, nsweeps, tol):
-    """Full linear BVAR-SV sweeps (CTA -> A -> SV -> PHI) on real data, CRN per chain.
-    One sweep from a common state: 5e-8 (in units of max(|x|, posterior sd)); the
-    blocks alone are at 1e-9 (toy) .. 5e-9 (real data) and the A/PHI draws inherit
-    the CTA difference through RESID and the SV shocks.
-    Three chained sweeps: rounding differences of ~1e-9 compound through the
-    chain (each block conditions on the previous draws), bar 1e-6."""
+@pytest.mark.parametrize("B,nsweeps,tol,form", [(4, 1, 5e-8, "kron"), (4, 3, 1e-6, "kron"), (4, 1, 1e-9, "mirror"),
+                                                (4, 3, 1e-9, "mirror")])
+def test_linear_sweep_crn(pkg, ctx, oracle, fred, B, nsweeps, tol, form):
+    """Full linear BVAR-SV sweeps (CTA -> A -> SV -> PHI) on real data, CRN per chain, in units of
+    max(|x|, posterior sd).  form="kron": the oracle's CTA as written (CTA.m); the summation
+    orders differ, so one sweep sits at 5e-8 and three chained sweeps compound to 1e-6.
+    form="mirror": the oracle's CTA in the device's operation order (oracle/cta_mirror.py): 1e-9
+    for one sweep and for three chained sweeps."""
     mpm = oracle.set_minnesota_mean(fred["ncode"])
     su = oracle.var_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], mpm, True)
     m = pkg.model.build_var(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], mpm, True)
@@ -185,14 +185,15 @@ def test_linear_sweep_crn(pkg, ctx, oracle, fred, B, nsweeps, tol):
         st = sts[c]
         for m_ in range(nsweeps):
             prev[c] = st["sqrtht"]
-            st = oracle.linear_sweep(st, su, crns[c][m_])
+            st = oracle.linear_sweep(st, su, crns[c][m_], cta_form=form)
         _, _, sd = oracle.cta(su.Y, su.X, su.N, su.K, st["A"], st["sqrtht"], su.iVdiag, su.iVb,
                               st["PAI"], np.zeros((su.K, su.N)), return_sd=True)
         e = {"PAI": rel_err(got["PAI"][..., c], st["PAI"], sd),
              "A": rel_err(got["A"][..., c], st["A"], oracle.a_step_sd(st["RESID"], prev_sqrtht(c))),
              "sqrtht": rel_err(got["sqrtht"][..., c], st["sqrtht"]),
              "sqrtPHI": rel_err(got["sqrtPHI"][..., c], st["sqrtPHI"], 1e-3)}
-        print("chain", c, nsweeps, e)
+        print("chain", c, nsweeps, form, e, "| PAI entries differing",
+              int(np.count_nonzero(got["PAI"][..., c] != st["PAI"])))
         assert max(e.values()) < tol, e
         np.testing.assert_array_equal(kai[..., c], st["kai"])  # KSC indicators: bit-exact
 
