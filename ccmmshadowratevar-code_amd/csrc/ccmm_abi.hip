@@ -553,6 +553,8 @@ struct ccmm_chains {
   }
   int lag_mode = std::getenv("CCMM_LAG_MODE") ? std::atoi(std::getenv("CCMM_LAG_MODE")) : 0;
   int sv_mode = std::getenv("CCMM_SV_MODE") ? std::atoi(std::getenv("CCMM_SV_MODE")) : 0;
+  // k_elb_gibbs_lanes (lane per (chain, pass)): -1 from B >= kElbLanesMinB, 0 never, 1 always
+  int elb_lanes = std::getenv("CCMM_ELB_LANES") ? std::atoi(std::getenv("CCMM_ELB_LANES")) : -1;
   // passes of the ELB step in flight (k_elb_gibbs_wf): 1 (sequential k_elb_gibbs), 4 or 8
   int elb_waves = [] {
     const char* v = std::getenv("CCMM_ELB_WAVES");
@@ -1435,6 +1437,25 @@ struct ccmm_chains {
     int W = elb_waves;
     while (W > 1 && gibbs_lds(W) > 160 * 1024) W = (W == 8) ? 4 : 1;  // long ELB windows
     const size_t lds_gibbs = gibbs_lds(W);
+    // large batches: one lane per (chain, pass) in flight, 8 passes x 8 chains per wave
+    // (k_elb_gibbs_lanes, bit-identical draws); CCMM_ELB_LANES=0 never, 1 always
+    const size_t lds_lanes = (size_t)8 * e.elbTmax * Ns * sizeof(double) + (size_t)8 * 2 * e.elbTmax * sizeof(int);
+    const bool lanes = elb_lanes == 1 || (elb_lanes < 0 && d.B >= kElbLanesMinB);
+    if (lanes && lds_lanes <= 160 * 1024) {
+      launch(KID_ELBGIBBS, [&] {
+        switch (Ns) {
+#define CASE_NSL(NS)                                                                                            case NS:                                                                                                        HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs_lanes<NS, 8>,                                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_lanes));                   hipLaunchKernelGGL((k_elb_gibbs_lanes<NS, 8>), dim3((d.B + 7) / 8), dim3(64), lds_lanes, ctx->stream, d,                        e, cs, ra);                                                                                break;
+          CASE_NSL(1)
+          CASE_NSL(2)
+          CASE_NSL(3)
+          CASE_NSL(4)
+          CASE_NSL(5)
+#undef CASE_NSL
+          default:
+            throw ArgError("Ns must be in [1, 5]");
+        }
+      });
+    } else
     launch(KID_ELBGIBBS, [&] {
 #define GIBBS_K(NS, WW)                                                                                     \
   do {                                                                                                      \

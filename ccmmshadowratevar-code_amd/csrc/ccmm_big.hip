@@ -252,12 +252,10 @@ __global__ __launch_bounds__(256, 2) void k_chol_big(Dims d, const int* __restri
               bad = 1;
               dkk = 1.0;
             }
-            // 1 / sqrt(d): hardware estimate + two Newton steps (no IEEE sqrt / division on
-            // the serial pivot chain); L_kk = d / sqrt(d)
-            double rp = __builtin_amdgcn_rsq(dkk);
-            const double hd = 0.5 * dkk;
-            rp = rp * fma(-hd * rp, rp, 1.5);
-            rp = rp * fma(-hd * rp, rp, 1.5);
+            // 1 / sqrt(d) by the deterministic iteration rsqrt_det (no IEEE sqrt / division on the
+            // serial pivot chain, and reproducible off the device: oracle/cta_big_mirror.c);
+            // L_kk = d / sqrt(d)
+            const double rp = rsqrt_det(dkk);
             if (lane == kk) {
               row[kk] = dkk * rp;
               rdg = rp;

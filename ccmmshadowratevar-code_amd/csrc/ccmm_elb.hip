@@ -763,6 +763,149 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
   for (int q = tid; q < T * NS; q += 64 * W) Sc[q] = Sl[q];
 }
 
+// ---------------------------------------------------------------- Gibbs passes, lane per (chain, pass)
+// For large batches (B >= kElbLanesMinB): the wavefront of k_elb_gibbs_wf with one LANE per pass in
+// flight instead of one wave, W passes of each of 64 / W chains per wave.  The wave kernels evaluate
+// every draw on all 64 lanes (uniform control flow over the month's 2 p Ns neighbour columns); here
+// each lane walks its own (chain, pass) through the months, so the truncated-normal draws run once and
+// the kernel is no longer issue-bound at large B.  The draws are bit-identical to k_elb_gibbs /
+// k_elb_gibbs_wf: the neighbour sum of each month is the same 64-leaf pairwise tree as wave_sum_dpp
+// (xor 1, xor 2, half-row mirror, row mirror, then (r0 + r1) + (r2 + r3) = the balanced binary tree of
+// the lane values in lane order), leaf l = fma(g_l, v_l, g_{l+64} v_{l+64}), and the wavefront rule is
+// the one above (a lane may draw month i of pass n once pass n - 1 has drawn every month up to
+// reach(i); the predecessor's progress is read with one cross-lane shuffle per step, and within a step
+// the (chain, pass) lanes touch disjoint cells of their chain's Sl).  Records are read straight from
+// the per-chain record array (one 2 p Ns^2 + head record per (lane, step)).
+constexpr int kElbLanesMinB = 512;
+template <int NS, int W>
+__global__ __launch_bounds__(64) void k_elb_gibbs_lanes(Dims d, ElbDev e, ChainState cs, RngArgs ra) {
+  constexpr int CPW = 64 / W;
+  extern __shared__ double sm[];
+  const int lane = threadIdx.x;
+  const int cw = lane / W, w = lane % W;
+  const int c = blockIdx.x * CPW + cw;
+  const bool live = c < d.B;
+  const int p = e.p;
+  const int pg = e.elbTmax * NS;
+  double* Sl = sm + (size_t)cw * pg;                                  // this chain's T x NS (t-major)
+  int* Tm = (int*)(sm + (size_t)CPW * pg) + (size_t)cw * 2 * e.elbTmax;  // t | (mask << 16)
+  int* reach = Tm + e.elbTmax;
+  const int s = live ? cs.slot[c] : 0;
+  const int T = live ? e.elbT[s] : 0;
+  int nc = live ? e.ncens[s] : 0;
+  if (live && e.psFlag && e.psFlag[c] > 0) nc = 0;  // a PS proposal was accepted (:453-454)
+  const int P = e.passes;
+  const int done_all = P * nc;
+  double* Sc = e.Scur + (size_t)(live ? c : 0) * pg;
+  const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * NS;
+  const int* cl = e.cens + (size_t)s * e.elbTmax;
+  if (nc > 0) {
+    for (int q = w; q < T * NS; q += W) Sl[q] = Sc[q];
+    for (int q = w; q < nc; q += W) {
+      const int t = cl[q];
+      int m = 0;
+      for (int a = 0; a < NS; ++a) m |= sN[t * NS + a] ? (1 << a) : 0;
+      Tm[q] = t | (m << 16);
+      int j = q;
+      while (j + 1 < nc && cl[j + 1] <= t + p) ++j;
+      reach[q] = j;
+    }
+  }
+  __syncthreads();
+  const Rng rng = ra.make(live ? c : 0);
+  const int ncol = 2 * p * NS;
+  const int head = elb_cond_head(NS);
+  const double* recs = e.cond + (size_t)(live ? c : 0) * e.elbTmax * e.condStride;
+  const int pred = cw * W + (w + W - 1) % W;
+  int n = w, i = 0;
+  int prog = (n < P && nc > 0) ? n * nc : done_all;
+  // exit condition every wave reaches: the wavefront needs at most P nc + W (nc + 1) steps
+  const int max_steps = P * e.elbTmax + W * (e.elbTmax + 1) + 8;
+  for (int step = 0; step < max_steps; ++step) {
+    const int pp = __shfl(prog, pred);
+    if (__ballot(prog < done_all) == 0) break;
+    bool can = nc > 0 && n < P;
+    if (can && n > 0) can = pp >= (n - 1) * nc + reach[i] + 1;
+    if (can) {
+      const int tm = Tm[i];
+      const int t = tm & 0xffff, msk = tm >> 16;
+      const double* r = recs + (size_t)i * e.condStride;
+      double hd[NS + NS * (NS - 1) + NS];
+#pragma unroll
+      for (int q = 0; q < NS + NS * (NS - 1) + NS; ++q) hd[q] = r[q];
+      // Spost = a_t + the 64-leaf tree of the neighbour products (wave_sum_dpp's order)
+      double acc[NS][6];
+#pragma unroll
+      for (int l = 0; l < 64; ++l) {
+        const int c0 = l, c1 = l + 64;
+        const bool h0 = c0 < ncol, h1 = c1 < ncol;
+        double x[NS];
+        if (h0 || h1) {
+          const int kk0 = c0 / NS, sp0 = c0 % NS, kk1 = c1 / NS, sp1 = c1 % NS;
+          const int tn0 = t + ((kk0 < p) ? -(kk0 + 1) : (kk0 - p + 1));
+          const int tn1 = t + ((kk1 < p) ? -(kk1 + 1) : (kk1 - p + 1));
+          const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
+          const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
+#pragma unroll
+          for (int a = 0; a < NS; ++a) {
+            const double g0 = h0 ? r[head + c0 * NS + a] : 0.0;
+            const double g1 = h1 ? r[head + c1 * NS + a] : 0.0;
+            x[a] = fma(g0, v0, g1 * v1);
+          }
+        } else {
+#pragma unroll
+          for (int a = 0; a < NS; ++a) x[a] = fma(0.0, 0.0, 0.0 * 0.0);
+        }
+#pragma unroll
+        for (int a = 0; a < NS; ++a) {
+          double v = x[a];
+          int lev = 0;
+#pragma unroll
+          for (; lev < 6 && ((l >> lev) & 1); ++lev) v = acc[a][lev] + v;
+          if (lev < 6) acc[a][lev] = v;
+          else acc[a][0] = v;  // l = 63: the root
+        }
+      }
+      double sp[NS];
+#pragma unroll
+      for (int a = 0; a < NS; ++a) sp[a] = hd[a] + acc[a][0];
+      // conditional draws in index order (gibbsdrawShadowrates.m:206-218)
+      const double* beta = hd + NS;
+      const double* so = beta + NS * (NS - 1);
+      double cur[NS];
+#pragma unroll
+      for (int a = 0; a < NS; ++a) cur[a] = Sl[t * NS + a];
+#pragma unroll
+      for (int a = 0; a < NS; ++a) {
+        if (!((msk >> a) & 1)) continue;
+        double mu = sp[a];
+        int y = 0;
+#pragma unroll
+        for (int b = 0; b < NS; ++b) {
+          if (b == a) continue;
+          mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
+          ++y;
+        }
+        const double u = (e.mode & 2) ? 0.5 : rng.uniform(CCMM_RNG_ELB, (uint32_t)(t * NS + a + T * NS * n));
+        uint8_t fl = 0;
+        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u, fl);
+        if (e.flags) e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
+      }
+#pragma unroll
+      for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
+      if (++i == nc) {
+        i = 0;
+        n += W;
+      }
+    }
+    prog = (nc > 0 && n < P) ? n * nc + i : done_all;
+  }
+  if (prog < done_all && live) atomicOr(&cs.status[c], 8);  // step cap reached (never expected)
+  __syncthreads();
+  if (nc > 0)
+    for (int q = w; q < T * NS; q += W) Sc[q] = Sl[q];
+}
+
 // ---------------------------------------------------------------- rebuild X, Y (per chain)
 // shadowYdata(p+elbT0+1:end, ndxS) = shadowrate'; X(t, 1+(l-1)N+s) = Y(t-l, s) (:501-509)
 __global__ void k_elb_rebuild(Dims d, ElbDev e, XSel xs, ChainState cs, int xslab0, double* dpool,

@@ -210,6 +210,22 @@ __device__ __forceinline__ double xsum32(double v) {
   return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
 }
 
+// 1 / sqrt(d) as a deterministic function of d's bits (restated bit for bit by oracle/cta_lag_mirror.c and
+// oracle/cta_big_mirror.c): the integer seed 0x5fe6eb50c7b537a9 - (bits >> 1) (relative error <= 3.5 %)
+// and two fourth-order steps r <- r + r e (1/2 + e (3/8 + 5/16 e)), e = 1 - d r^2 (error <= 1.4e-16
+// over the double range).  The hardware v_rsq_f64 estimate cannot be reproduced off the device.
+__device__ __forceinline__ double rsqrt_det(double d) {
+  const long long bits = __double_as_longlong(d);
+  double r = __longlong_as_double(0x5fe6eb50c7b537a9LL - (bits >> 1));
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const double e = __builtin_fma(-(d * r), r, 1.0);
+    const double q = __builtin_fma(__builtin_fma(0.3125, e, 0.375), e, 0.5);
+    r = __builtin_fma(r * e, q, r);
+  }
+  return r;
+}
+
 __device__ __forceinline__ double wave_sum_dpp(double v) {
   v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]

@@ -57,24 +57,12 @@ __device__ __forceinline__ int gl_opaque(int v) {
   return v;
 }
 
-// 1 / sqrt(d) as a deterministic function of d's bits, so that the factor can be reproduced bit for
-// bit by a restatement (oracle/cta_lag_mirror.c): the integer seed 0x5fe6eb50c7b537a9 - (bits >> 1)
-// (relative error <= 3.5 %) and two fourth-order steps r <- r + r e (1/2 + e (3/8 + 5/16 e)),
-// e = 1 - d r^2 (error <= 1.4e-16 over the double range; five dependent operations per step, against
-// three per Newton step of which four would be needed).  The hardware v_rsq_f64 estimate is not
-// reproducible off the device, and the IEEE sqrt + division pair puts ~25 dependent instructions on
-// the serial pivot path.
-__device__ __forceinline__ double gl_rsqrt_det(double d) {
-  const long long bits = __double_as_longlong(d);
-  double r = __longlong_as_double(0x5fe6eb50c7b537a9LL - (bits >> 1));
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const double e = fma(-(d * r), r, 1.0);
-    const double q = fma(fma(0.3125, e, 0.375), e, 0.5);
-    r = fma(r * e, q, r);
-  }
-  return r;
-}
+// 1 / sqrt(d) as a deterministic function of d's bits (rsqrt_det, ccmm_internal.h), so that the
+// factor can be reproduced bit for bit by a restatement (oracle/cta_lag_mirror.c): five dependent
+// operations per fourth-order step, against three per Newton step of which four would be needed.
+// The hardware v_rsq_f64 estimate is not reproducible off the device, and the IEEE sqrt + division
+// pair puts ~25 dependent instructions on the serial pivot path.
+__device__ __forceinline__ double gl_rsqrt_det(double d) { return rsqrt_det(d); }
 
 // Per-wave factor + inverse of the SPD 16 x 16 tile Dg (row-major, ld kGlLd, lower
 // triangle read): Ws := L^-1 (lower, row-major, ld kGlLd).  Lane i < 16 holds row i.

@@ -163,15 +163,20 @@ def hybrid_init_state(hs: HybridSetup):
     return O.init_state(hs.lin)  # :351-359 (PAI = X0\Y0 with the hybrid X0)
 
 
-def hybrid_sweep(st, hs: HybridSetup, crn, elb_impl="stable", use_ps=False):
+def hybrid_sweep(st, hs: HybridSetup, crn, elb_impl="stable", use_ps=False, cta_form="kron"):
     """One sweep of mcmcVARhybridGibbs.m:362-539 with the Gibbs ELB draw, or with use_ps the
     reference's PS proposals first (:458-483, crn["zPS"]) and the Gibbs draw as fallback.
     elb_impl as in ccmm_oracle_bh.bh_sweep ("qr", "stable" or "both")."""
     lin = hs.lin
     N, K = lin.N, lin.K
     Y, X = st["Y"], st["X"]
-    PAI, status = O.cta(Y, X, N, K, st["A"], st["sqrtht"], lin.iVdiag, lin.iVb, st["PAI"],
-                        crn["zPAI"])
+    if cta_form == "mirror":   # the device's large-system path in its operation order
+        from . import cta_mirror
+        PAI, status = cta_mirror.cta_big(Y, X, N, K, st["A"], st["sqrtht"], lin.iVdiag, lin.iVb, st["PAI"],
+                                         crn["zPAI"])
+    else:
+        PAI, status = O.cta(Y, X, N, K, st["A"], st["sqrtht"], lin.iVdiag, lin.iVb, st["PAI"],
+                            crn["zPAI"])
     RESID = Y - X @ PAI
     A, invA = O.a_step(RESID, st["sqrtht"], crn["zA"])
     logy2 = np.log((RESID @ A.T) ** 2 + lin.logy2offset)

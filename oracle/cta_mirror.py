@@ -29,7 +29,8 @@ def lib():
     global _LIB
     if _LIB is None:
         so = _HERE / "libccmm_mirror.so"
-        if not so.exists() or so.stat().st_mtime < (_HERE / "cta_lag_mirror.c").stat().st_mtime:
+        srcs = [_HERE / "cta_lag_mirror.c", _HERE / "cta_big_mirror.c"]
+        if not so.exists() or so.stat().st_mtime < max(f.stat().st_mtime for f in srcs):
             subprocess.run(["make", "-C", str(_HERE)], check=True, capture_output=True)
         _LIB = C.CDLL(str(so))
         for name, args in (("ccmm_mirror_weights", [C.c_int, C.c_int, C.c_int, _dp, _dp, _dp]),
@@ -44,6 +45,8 @@ def lib():
             f.restype = None
         _LIB.ccmm_mirror_factor.argtypes = [C.c_int, _dp, _dp, _dp, _dp, _dp]
         _LIB.ccmm_mirror_factor.restype = C.c_int
+        _LIB.ccmm_bmirror_cta.argtypes = [C.c_int, C.c_int, C.c_int] + [_dp] * 9
+        _LIB.ccmm_bmirror_cta.restype = C.c_int
     return _LIB
 
 
@@ -135,3 +138,15 @@ def cta(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z, factor_form="device"):
         L_.ccmm_mirror_resid_update(T, K, _p(X), _p(np.ascontiguousarray(Y[:, j])), _p(xj), _p(Ej))
         E[:, j] = Ej
     return np.array(PAI)
+
+
+def cta_big(Y, X, N, K, A, sqrtht, iVdiag, iVb, PAI, z):
+    """CTA.m:57-98 through the device's large-system path (ccmm_big.hip: k_gram_big, k_chol_big,
+    k_cta_solve_big; oracle/cta_big_mirror.c) in its operation order: the hybrid model's
+    K = 1 + (N + Ns) p design (mcmcVARhybridGibbs.m:74-84) and every system off the lag path.
+    Returns (PAI, bad) with bad = 1 for a non-positive pivot."""
+    T = Y.shape[0]
+    out = np.zeros((K, N), order="F")
+    bad = lib().ccmm_bmirror_cta(T, N, K, _p(_F(Y)), _p(_F(X)), _p(_F(A)), _p(_F(sqrtht)), _p(_F(iVdiag)),
+                                 _p(_F(iVb)), _p(_F(PAI)), _p(_F(z)), _p(out))
+    return np.array(out), int(bad)

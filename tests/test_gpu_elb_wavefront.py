@@ -16,8 +16,9 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 
-def _run(pkg, fred, waves, thisT, B=8, sweeps=3):
+def _run(pkg, fred, waves, thisT, B=8, sweeps=3, lanes=0):
     os.environ["CCMM_ELB_WAVES"] = str(waves)
+    os.environ["CCMM_ELB_LANES"] = str(lanes)
     try:
         mpm = pkg.model.setMinnesotaMean(fred["ncode"])
         ndxS, ndxO, _ = pkg.model.setShadowYields(fred["ncode"], 0.25)
@@ -43,6 +44,7 @@ def _run(pkg, fred, waves, thisT, B=8, sweeps=3):
         return out, bm.elbT
     finally:
         os.environ.pop("CCMM_ELB_WAVES", None)
+        os.environ.pop("CCMM_ELB_LANES", None)
 
 
 @pytest.mark.parametrize("jump", ["last", "2012-06"])
@@ -57,3 +59,19 @@ def test_wavefront_equals_sequential(pkg, fred, jump):
         for k in ref:
             np.testing.assert_array_equal(got[k], ref[k], err_msg=f"waves={w} {k}")
     print(f"{jump}: elbT {elbT}, {int(np.count_nonzero(ref['flags']))} flagged draws, identical for 4 and 8 waves")
+
+
+@pytest.mark.parametrize("jump,B", [("last", 19), ("2012-06", 8)])
+def test_lanes_equal_sequential(pkg, fred, jump, B):
+    """k_elb_gibbs_lanes (one lane per (chain, pass) in flight, 8 passes x 8 chains per wave; the kernel
+    for B >= 512, forced here with CCMM_ELB_LANES=1) against the sequential one-wave kernel: shadow
+    rates, every drawTruncNormal branch flag and the chain state bit for bit; B = 19 leaves a partly
+    filled last wave."""
+    yd = np.asarray(fred["ydates"], float)
+    jun2012 = date(2012, 6, 1).toordinal() + 366
+    thisT = len(yd) if jump == "last" else int(np.nonzero(yd == jun2012)[0][0]) + 1
+    ref, elbT = _run(pkg, fred, 1, thisT, B=B)
+    got, _ = _run(pkg, fred, 8, thisT, B=B, lanes=1)
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=f"lanes {k}")
+    print(f"{jump}: elbT {elbT}, B {B}: lane kernel identical ({int(np.count_nonzero(ref['flags']))} flagged draws)")

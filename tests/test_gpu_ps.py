@@ -249,14 +249,15 @@ def test_ps_hybrid_toy(pkg, ctx, oracle, bh):
         st = sts[c]
         acc = []
         for m in range(nsw):
-            st = hy.hybrid_sweep(st, hs, crns[c][m], use_ps=True)
+            st = hy.hybrid_sweep(st, hs, crns[c][m], use_ps=True, cta_form="mirror")
             acc.append(st["ps_accept"])
             em = rel_err(miss[m, :, :hs.elbT, c], st["missingrate"], 0.1)
-            assert em < 1e-7, (c, m, em)
+            assert em < 1e-9, (c, m, em)
         n_acc += sum(1 for a in acc if a)
         assert list(ps["stackAccept"][:, c]) == acc, (c, ps["stackAccept"][:, c], acc)
         e = {"PAI": rel_err(got["PAI"][..., c], st["PAI"], 1e-2),
              "shadowrate": rel_err(S[:, :, c], st["shadowrate"], 0.1)}
-        print("hybrid chain", c, "ndxAccept", acc, e)
-        assert max(e.values()) < 1e-7, e
+        print("hybrid chain", c, "ndxAccept", acc, e, "| PAI entries differing",
+              int(np.count_nonzero(got["PAI"][..., c] != st["PAI"])))
+        assert max(e.values()) < 1e-9, e
     assert n_acc > 0
