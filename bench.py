@@ -860,14 +860,41 @@ def _physical_cores():
     return len(phys) or None
 
 
+def _cpp_line(budget_s, workers):
+    """The compiled restatement (oracle/cpu_sweep.cpp): the linear sweep of mcmcVAR.m:211-274 as
+    written (kron-materialised CTA, explicit inverse; OpenBLAS, one thread per process), `workers`
+    processes at once, one chain each (parfor), real data T = 750, the reference initialisation."""
+    import sys as _s
+    import tempfile
+    _s.path.insert(0, str(ROOT))
+    from oracle import ccmm_oracle as O
+    from oracle import cpu_baseline as CB
+    fred = O.load_fred_csv(ROOT / "tests/golden/data/fredblockMD20-2022-09.csv")
+    mpm = O.set_minnesota_mean(fred["ncode"])
+    su = O.var_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], mpm, True)
+    with tempfile.TemporaryDirectory() as td:
+        sp = Path(td) / "state.bin"
+        CB.write_state(sp, su, O.init_state(su))
+        procs = [CB.bench_process(sp, budget_s, 1000 + w) for w in range(workers)]
+        res = [CB.bench_result(p_, budget_s * 20 + 300) for p_ in procs]
+    value = sum(n / el for n, el in res)
+    nsw = sum(n for n, _ in res)
+    return {"value": round(value, 4), "unit": "sweeps/s", "cores": workers, "kind": "port",
+            "scope": f"per-GPU share of the host: {workers} of its cores",
+            "per_core": round(value / workers, 4),
+            "sample": f"{nsw} sweeps: {workers} single-thread processes (parfor-style, one chain each) x "
+                      f"~{budget_s:.0f} s of oracle/cpu_sweep.cpp, the linear sweep as written (CTA.m kron "
+                      f"form, explicit inverse) in C++ on OpenBLAS {CB.blas_path().rsplit('/', 1)[-1]}"}
+
+
 def cpu_baseline(budget_s, workers=0):
     """The reference algorithm restated on the host (oracle/; MATLAB cannot run here),
     parfor-style: `workers` single-thread processes, one chain each, real data T = 750.
-    Three lines: the linear sampler as written (kron-materialised X_j,
-    explicit inverse: CTA.m:69-78), the linear sampler in the algorithmic weighted-SYRK
-    form, and the block-hybrid sampler as written (QR smoothing weights,
-    gibbsdrawShadowrates.m:74-127, 101 Gibbs passes).  The first is the reported
-    ``cpu_baseline``; the others ride along."""
+    The reported ``cpu_baseline`` is the compiled C++ restatement of the linear sampler as written
+    (oracle/cpu_sweep.cpp: kron-materialised X_j, explicit inverse, CTA.m:69-78; OpenBLAS).  The
+    numpy lines ride along: the linear sampler as written, in the algorithmic
+    weighted-SYRK form, and the block-hybrid sampler as written (QR smoothing weights,
+    gibbsdrawShadowrates.m:74-127, 101 Gibbs passes, the pass loop in the Python interpreter)."""
     import os
     if workers <= 0:
         workers = min(16, os.cpu_count() or 1)   # the GPU box's CPU share for one GPU
@@ -890,8 +917,8 @@ def cpu_baseline(budget_s, workers=0):
         pass
     env = f"numpy/scipy, BLAS {blas} (1 thread per process), CPU {cpu}, {os.cpu_count()} " \
           f"logical CPUs visible"
-    lin = _cpu_line("linear-kron", budget_s, workers,
-                    "oracle/ccmm_oracle.py linear sweep as written (kron CTA, explicit inverse), " + env)
+    lin = _cpp_line(budget_s, workers)
+    lin["sample"] += f", CPU {cpu}"
     # all host cores: the box allots a GPU job 16 of its CPUs, so the
     # whole-host line is the measured single-thread rate x the physical core count
     # (parfor workers are independent single-thread chains; no shared state to contend on
@@ -901,9 +928,13 @@ def cpu_baseline(budget_s, workers=0):
         lin["all_host_cores"] = {
             "value": round(lin["per_core"] * ncore, 3), "unit": "sweeps/s", "cores": ncore,
             "kind": "port", "cpu": cpu, "blas": blas,
+            "projected": True,
             "method": f"projected: measured per-core rate of the {workers}-process line x {ncore} "
                       "physical cores (one single-thread parfor worker per core)"}
     lin["lines"] = {
+        "linear_numpy": _cpu_line("linear-kron", budget_s, workers,
+                                  "oracle/ccmm_oracle.py linear sweep as written (kron CTA, explicit inverse), "
+                                  + env),
         "linear_syrk": _cpu_line("linear-syrk", budget_s, workers,
                                  "linear sweep, algorithmic CTA (weighted SYRK + Cholesky + "
                                  "triangular solves), " + env),

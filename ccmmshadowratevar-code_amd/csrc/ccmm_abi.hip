@@ -553,8 +553,9 @@ struct ccmm_chains {
   }
   int lag_mode = std::getenv("CCMM_LAG_MODE") ? std::atoi(std::getenv("CCMM_LAG_MODE")) : 0;
   int sv_mode = std::getenv("CCMM_SV_MODE") ? std::atoi(std::getenv("CCMM_SV_MODE")) : 0;
-  // k_elb_gibbs_lanes (lane per (chain, pass)): -1 from B >= kElbLanesMinB, 0 never, 1 always
-  int elb_lanes = std::getenv("CCMM_ELB_LANES") ? std::atoi(std::getenv("CCMM_ELB_LANES")) : -1;
+  // k_elb_gibbs_oct (eight passes in flight in one wave) from B >= kElbOctMinB; CCMM_ELB_OCT=0 never,
+  // 2 always
+  int elb_oct = std::getenv("CCMM_ELB_OCT") ? std::atoi(std::getenv("CCMM_ELB_OCT")) : 1;
   // passes of the ELB step in flight (k_elb_gibbs_wf): 1 (sequential k_elb_gibbs), 4 or 8
   int elb_waves = [] {
     const char* v = std::getenv("CCMM_ELB_WAVES");
@@ -1437,20 +1438,26 @@ struct ccmm_chains {
     int W = elb_waves;
     while (W > 1 && gibbs_lds(W) > 160 * 1024) W = (W == 8) ? 4 : 1;  // long ELB windows
     const size_t lds_gibbs = gibbs_lds(W);
-    // large batches: one lane per (chain, pass) in flight, 8 passes x 8 chains per wave
-    // (k_elb_gibbs_lanes, bit-identical draws); CCMM_ELB_LANES=0 never, 1 always
-    const size_t lds_lanes = (size_t)8 * e.elbTmax * Ns * sizeof(double) + (size_t)8 * 2 * e.elbTmax * sizeof(int);
-    const bool lanes = elb_lanes == 1 || (elb_lanes < 0 && d.B >= kElbLanesMinB);
-    if (lanes && lds_lanes <= 160 * 1024) {
+    // eight passes in flight inside one wave (k_elb_gibbs_oct, bit-identical draws): the default;
+    // CCMM_ELB_OCT=0 selects the wave kernels
+    const size_t lds_oct = (size_t)e.elbTmax * Ns * sizeof(double) + (size_t)2 * e.elbTmax * sizeof(int);
+    // (the per-chain wave kernels keep shorter months at B < kElbOctMinB: one wave per chain cannot
+    // fill the chip there, and a month costs the octet kernel more latency)
+    if (elb_oct && lds_oct <= 160 * 1024 && (elb_oct == 2 || d.B >= kElbOctMinB)) {
       launch(KID_ELBGIBBS, [&] {
         switch (Ns) {
-#define CASE_NSL(NS)                                                                                            case NS:                                                                                                        HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs_lanes<NS, 8>,                                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_lanes));                   hipLaunchKernelGGL((k_elb_gibbs_lanes<NS, 8>), dim3((d.B + 7) / 8), dim3(64), lds_lanes, ctx->stream, d,                        e, cs, ra);                                                                                break;
-          CASE_NSL(1)
-          CASE_NSL(2)
-          CASE_NSL(3)
-          CASE_NSL(4)
-          CASE_NSL(5)
-#undef CASE_NSL
+#define CASE_NSO(NS)                                                                                           \
+  case NS:                                                                                                     \
+    HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs_oct<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                 (int)lds_oct));                                                               \
+    hipLaunchKernelGGL(k_elb_gibbs_oct<NS>, dim3(d.B), dim3(64), lds_oct, ctx->stream, d, e, cs, ra);           \
+    break;
+          CASE_NSO(1)
+          CASE_NSO(2)
+          CASE_NSO(3)
+          CASE_NSO(4)
+          CASE_NSO(5)
+#undef CASE_NSO
           default:
             throw ArgError("Ns must be in [1, 5]");
         }

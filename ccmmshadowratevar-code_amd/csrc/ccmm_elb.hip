@@ -763,112 +763,125 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
   for (int q = tid; q < T * NS; q += 64 * W) Sc[q] = Sl[q];
 }
 
-// ---------------------------------------------------------------- Gibbs passes, lane per (chain, pass)
-// For large batches (B >= kElbLanesMinB): the wavefront of k_elb_gibbs_wf with one LANE per pass in
-// flight instead of one wave, W passes of each of 64 / W chains per wave.  The wave kernels evaluate
-// every draw on all 64 lanes (uniform control flow over the month's 2 p Ns neighbour columns); here
-// each lane walks its own (chain, pass) through the months, so the truncated-normal draws run once and
-// the kernel is no longer issue-bound at large B.  The draws are bit-identical to k_elb_gibbs /
-// k_elb_gibbs_wf: the neighbour sum of each month is the same 64-leaf pairwise tree as wave_sum_dpp
-// (xor 1, xor 2, half-row mirror, row mirror, then (r0 + r1) + (r2 + r3) = the balanced binary tree of
-// the lane values in lane order), leaf l = fma(g_l, v_l, g_{l+64} v_{l+64}), and the wavefront rule is
-// the one above (a lane may draw month i of pass n once pass n - 1 has drawn every month up to
-// reach(i); the predecessor's progress is read with one cross-lane shuffle per step, and within a step
-// the (chain, pass) lanes touch disjoint cells of their chain's Sl).  Records are read straight from
-// the per-chain record array (one 2 p Ns^2 + head record per (lane, step)).
-constexpr int kElbLanesMinB = 512;
-template <int NS, int W>
-__global__ __launch_bounds__(64) void k_elb_gibbs_lanes(Dims d, ElbDev e, ChainState cs, RngArgs ra) {
-  constexpr int CPW = 64 / W;
+// ---------------------------------------------------------------- Gibbs passes, eight per wave
+// The wavefront of k_elb_gibbs_wf inside ONE wave: eight lanes per pass in flight ("octets": lane
+// 8 w + j, pass slot w = 0..7 runs passes w, w + 8, ...), so the passes synchronise by cross-lane
+// shuffles instead of workgroup barriers and each truncated-normal draw is evaluated on 8 lanes
+// instead of 64 (the wave kernels are issue-bound on that redundancy from B = 256 up).  Lane j of an
+// octet owns the eight tree leaves 8 j .. 8 j + 7 of the month's 2 p Ns neighbour columns (leaf
+// l = fma(g_l, v_l, g_{l+64} v_{l+64})): its group sum ((x0 + x1) + (x2 + x3)) + ((x4 + x5) + (x6 + x7))
+// and the xor-1 / xor-2 / xor-4 sums over the octet give exactly the pairwise tree of wave_sum_dpp
+// over 64 lanes, so the draws, flags and states are bit-identical to k_elb_gibbs / k_elb_gibbs_wf.
+// Wavefront rule as there: pass n may draw month i once pass n - 1 has drawn every month up to
+// reach(i) (the predecessor octet's progress, read by one shuffle per step; within a step the eight
+// passes touch disjoint cells of Sl).
+constexpr int kElbOctMinB = 384;
+template <int NS>
+__global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainState cs, RngArgs ra) {
+  constexpr int W = 8;
   extern __shared__ double sm[];
-  const int lane = threadIdx.x;
-  const int cw = lane / W, w = lane % W;
-  const int c = blockIdx.x * CPW + cw;
-  const bool live = c < d.B;
+  const int c = blockIdx.x;
+  const int s = cs.slot[c];
   const int p = e.p;
-  const int pg = e.elbTmax * NS;
-  double* Sl = sm + (size_t)cw * pg;                                  // this chain's T x NS (t-major)
-  int* Tm = (int*)(sm + (size_t)CPW * pg) + (size_t)cw * 2 * e.elbTmax;  // t | (mask << 16)
-  int* reach = Tm + e.elbTmax;
-  const int s = live ? cs.slot[c] : 0;
-  const int T = live ? e.elbT[s] : 0;
-  int nc = live ? e.ncens[s] : 0;
-  if (live && e.psFlag && e.psFlag[c] > 0) nc = 0;  // a PS proposal was accepted (:453-454)
-  const int P = e.passes;
-  const int done_all = P * nc;
-  double* Sc = e.Scur + (size_t)(live ? c : 0) * pg;
-  const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * NS;
-  const int* cl = e.cens + (size_t)s * e.elbTmax;
-  if (nc > 0) {
-    for (int q = w; q < T * NS; q += W) Sl[q] = Sc[q];
-    for (int q = w; q < nc; q += W) {
-      const int t = cl[q];
-      int m = 0;
-      for (int a = 0; a < NS; ++a) m |= sN[t * NS + a] ? (1 << a) : 0;
-      Tm[q] = t | (m << 16);
-      int j = q;
-      while (j + 1 < nc && cl[j + 1] <= t + p) ++j;
-      reach[q] = j;
-    }
-  }
-  __syncthreads();
-  const Rng rng = ra.make(live ? c : 0);
+  const int T = e.elbT[s], nc = e.ncens[s];
+  if (nc == 0) return;
+  if (e.psFlag && e.psFlag[c] > 0) return;  // a PS proposal was accepted (:453-454)
+  const int lane = threadIdx.x;
+  const int w = lane >> 3, j = lane & 7;
+  const Rng rng = ra.make(c);
   const int ncol = 2 * p * NS;
   const int head = elb_cond_head(NS);
-  const double* recs = e.cond + (size_t)(live ? c : 0) * e.elbTmax * e.condStride;
-  const int pred = cw * W + (w + W - 1) % W;
+  double* Sl = sm;                                 // T x NS (t-major)
+  int* Tm = (int*)(sm + (size_t)e.elbTmax * NS);   // t | (mask << 16)
+  int* reach = Tm + e.elbTmax;
+  double* Sc = e.Scur + (size_t)c * e.elbTmax * NS;
+  const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * NS;
+  const int* cl = e.cens + (size_t)s * e.elbTmax;
+  const double* recs = e.cond + (size_t)c * e.elbTmax * e.condStride;
+  const int P = e.passes;
+  const int done_all = P * nc;
+  for (int q = lane; q < T * NS; q += 64) Sl[q] = Sc[q];
+  for (int q = lane; q < nc; q += 64) {
+    const int t = cl[q];
+    int m = 0;
+    for (int a = 0; a < NS; ++a) m |= sN[t * NS + a] ? (1 << a) : 0;
+    Tm[q] = t | (m << 16);
+    int jj = q;
+    while (jj + 1 < nc && cl[jj + 1] <= t + p) ++jj;
+    reach[q] = jj;
+  }
+  __syncthreads();
+  // this lane's leaves: l = 8 j + m; column l (and l + 64) -> neighbour month offset and rate
+  int off0[8], sp0[8], off1[8], sp1[8];
+  bool h0[8], h1[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int c0 = 8 * j + m, c1 = c0 + 64;
+    h0[m] = c0 < ncol;
+    h1[m] = c1 < ncol;
+    const int kk0 = c0 / NS, kk1 = c1 / NS;
+    sp0[m] = c0 % NS;
+    sp1[m] = c1 % NS;
+    off0[m] = (kk0 < p) ? -(kk0 + 1) : (kk0 - p + 1);
+    off1[m] = (kk1 < p) ? -(kk1 + 1) : (kk1 - p + 1);
+  }
+  const int pred = 8 * ((w + W - 1) % W) + j;
   int n = w, i = 0;
-  int prog = (n < P && nc > 0) ? n * nc : done_all;
+  int prog = (n < P) ? n * nc : done_all;
+  // the uniforms of the slot's next month (rand(Ns, elbT) page n, gibbsdrawShadowrates.m:173) are
+  // drawn one step ahead, so the generator stays off the month-to-month dependence chain
+  auto draw_u = [&](int nn, int ii, double (&uu)[NS]) {
+    const int tt = Tm[ii] & 0xffff;
+#pragma unroll
+    for (int a = 0; a < NS; ++a)
+      uu[a] = (e.mode & 2) ? 0.5 : rng.uniform(CCMM_RNG_ELB, (uint32_t)(tt * NS + a + T * NS * nn));
+  };
+  double ucur[NS];
+  if (n < P) draw_u(n, 0, ucur);
   // exit condition every wave reaches: the wavefront needs at most P nc + W (nc + 1) steps
-  const int max_steps = P * e.elbTmax + W * (e.elbTmax + 1) + 8;
+  const int max_steps = P * nc + W * (nc + 1) + 8;
   for (int step = 0; step < max_steps; ++step) {
     const int pp = __shfl(prog, pred);
     if (__ballot(prog < done_all) == 0) break;
-    bool can = nc > 0 && n < P;
+    bool can = n < P;
     if (can && n > 0) can = pp >= (n - 1) * nc + reach[i] + 1;
     if (can) {
       const int tm = Tm[i];
       const int t = tm & 0xffff, msk = tm >> 16;
       const double* r = recs + (size_t)i * e.condStride;
+      int nn = n, ni = i + 1;
+      if (ni == nc) {
+        ni = 0;
+        nn = n + W;
+      }
+      double unext[NS];
+      if (nn < P) draw_u(nn, ni, unext);
       double hd[NS + NS * (NS - 1) + NS];
 #pragma unroll
       for (int q = 0; q < NS + NS * (NS - 1) + NS; ++q) hd[q] = r[q];
-      // Spost = a_t + the 64-leaf tree of the neighbour products (wave_sum_dpp's order)
-      double acc[NS][6];
+      double x[8][NS];
 #pragma unroll
-      for (int l = 0; l < 64; ++l) {
-        const int c0 = l, c1 = l + 64;
-        const bool h0 = c0 < ncol, h1 = c1 < ncol;
-        double x[NS];
-        if (h0 || h1) {
-          const int kk0 = c0 / NS, sp0 = c0 % NS, kk1 = c1 / NS, sp1 = c1 % NS;
-          const int tn0 = t + ((kk0 < p) ? -(kk0 + 1) : (kk0 - p + 1));
-          const int tn1 = t + ((kk1 < p) ? -(kk1 + 1) : (kk1 - p + 1));
-          const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
-          const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
-#pragma unroll
-          for (int a = 0; a < NS; ++a) {
-            const double g0 = h0 ? r[head + c0 * NS + a] : 0.0;
-            const double g1 = h1 ? r[head + c1 * NS + a] : 0.0;
-            x[a] = fma(g0, v0, g1 * v1);
-          }
-        } else {
-#pragma unroll
-          for (int a = 0; a < NS; ++a) x[a] = fma(0.0, 0.0, 0.0 * 0.0);
-        }
+      for (int m = 0; m < 8; ++m) {
+        const int c0 = 8 * j + m, c1 = c0 + 64;
+        const int tn0 = t + off0[m], tn1 = t + off1[m];
+        const double v0 = (h0[m] && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0[m]] : 0.0;
+        const double v1 = (h1[m] && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1[m]] : 0.0;
 #pragma unroll
         for (int a = 0; a < NS; ++a) {
-          double v = x[a];
-          int lev = 0;
-#pragma unroll
-          for (; lev < 6 && ((l >> lev) & 1); ++lev) v = acc[a][lev] + v;
-          if (lev < 6) acc[a][lev] = v;
-          else acc[a][0] = v;  // l = 63: the root
+          const double g0 = h0[m] ? r[head + c0 * NS + a] : 0.0;
+          const double g1 = h1[m] ? r[head + c1 * NS + a] : 0.0;
+          x[m][a] = fma(g0, v0, g1 * v1);
         }
       }
       double sp[NS];
 #pragma unroll
-      for (int a = 0; a < NS; ++a) sp[a] = hd[a] + acc[a][0];
+      for (int a = 0; a < NS; ++a) {
+        double v = ((x[0][a] + x[1][a]) + (x[2][a] + x[3][a])) + ((x[4][a] + x[5][a]) + (x[6][a] + x[7][a]));
+        v += dpp_d<0xB1>(v);   // xor 1
+        v += dpp_d<0x4E>(v);   // xor 2
+        v += dpp_d<0x141>(v);  // row_half_mirror: xor 4 within the octet
+        sp[a] = hd[a] + v;
+      }
       // conditional draws in index order (gibbsdrawShadowrates.m:206-218)
       const double* beta = hd + NS;
       const double* so = beta + NS * (NS - 1);
@@ -886,24 +899,24 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_lanes(Dims d, ElbDev e, ChainS
           mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
           ++y;
         }
-        const double u = (e.mode & 2) ? 0.5 : rng.uniform(CCMM_RNG_ELB, (uint32_t)(t * NS + a + T * NS * n));
         uint8_t fl = 0;
-        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u, fl);
-        if (e.flags) e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
+        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, ucur[a], fl);
+        if (e.flags && j == 0) e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
       }
+      if (j == 0) {
 #pragma unroll
-      for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
-      if (++i == nc) {
-        i = 0;
-        n += W;
+        for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
       }
+      n = nn;
+      i = ni;
+#pragma unroll
+      for (int a = 0; a < NS; ++a) ucur[a] = unext[a];
     }
-    prog = (nc > 0 && n < P) ? n * nc + i : done_all;
+    prog = (n < P) ? n * nc + i : done_all;
   }
-  if (prog < done_all && live) atomicOr(&cs.status[c], 8);  // step cap reached (never expected)
+  if (prog < done_all && lane == 0) atomicOr(&cs.status[c], 8);  // step cap reached (never expected)
   __syncthreads();
-  if (nc > 0)
-    for (int q = w; q < T * NS; q += W) Sc[q] = Sl[q];
+  for (int q = lane; q < T * NS; q += 64) Sc[q] = Sl[q];
 }
 
 // ---------------------------------------------------------------- rebuild X, Y (per chain)

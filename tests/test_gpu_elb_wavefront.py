@@ -1,6 +1,6 @@
-"""The wavefront schedule of the ELB Gibbs passes (k_elb_gibbs_wf: up to 8 passes of
-gibbsdrawShadowrates.m in flight, one wave each) reproduces the sequential kernel
-(k_elb_gibbs, CCMM_ELB_WAVES=1) bit for bit: shadow rates, every drawTruncNormal branch flag
+"""The wavefront schedules of the ELB Gibbs passes (k_elb_gibbs_wf: up to 8 passes of
+gibbsdrawShadowrates.m in flight, one wave each; k_elb_gibbs_oct: 8 passes in flight in one wave,
+eight lanes each) reproduce the sequential kernel (k_elb_gibbs, CCMM_ELB_WAVES=1) bit for bit: shadow rates, every drawTruncNormal branch flag
 and the whole chain state after several block-hybrid sweeps on the reference's data
 (fredblockMD20-2022-09, ELB 0.25, 2022-08 jump-off: 109 censored months), with Philox draws
 and with CRN-free reuse of the same seed.  Also a short censored window (2012-06 jump-off),
@@ -16,9 +16,9 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 
-def _run(pkg, fred, waves, thisT, B=8, sweeps=3, lanes=0):
+def _run(pkg, fred, waves, thisT, B=8, sweeps=3, oct_=0):
     os.environ["CCMM_ELB_WAVES"] = str(waves)
-    os.environ["CCMM_ELB_LANES"] = str(lanes)
+    os.environ["CCMM_ELB_OCT"] = str(oct_)
     try:
         mpm = pkg.model.setMinnesotaMean(fred["ncode"])
         ndxS, ndxO, _ = pkg.model.setShadowYields(fred["ncode"], 0.25)
@@ -44,7 +44,7 @@ def _run(pkg, fred, waves, thisT, B=8, sweeps=3, lanes=0):
         return out, bm.elbT
     finally:
         os.environ.pop("CCMM_ELB_WAVES", None)
-        os.environ.pop("CCMM_ELB_LANES", None)
+        os.environ.pop("CCMM_ELB_OCT", None)
 
 
 @pytest.mark.parametrize("jump", ["last", "2012-06"])
@@ -62,16 +62,16 @@ def test_wavefront_equals_sequential(pkg, fred, jump):
 
 
 @pytest.mark.parametrize("jump,B", [("last", 19), ("2012-06", 8)])
-def test_lanes_equal_sequential(pkg, fred, jump, B):
-    """k_elb_gibbs_lanes (one lane per (chain, pass) in flight, 8 passes x 8 chains per wave; the kernel
-    for B >= 512, forced here with CCMM_ELB_LANES=1) against the sequential one-wave kernel: shadow
-    rates, every drawTruncNormal branch flag and the chain state bit for bit; B = 19 leaves a partly
-    filled last wave."""
+def test_octets_equal_sequential(pkg, fred, jump, B):
+    """k_elb_gibbs_oct (the kernel from B >= 384, forced with CCMM_ELB_OCT=2: eight passes in flight
+    inside one wave, eight lanes per pass, octet sums in wave_sum_dpp's tree order) against the sequential one-wave kernel
+    (CCMM_ELB_OCT=0, CCMM_ELB_WAVES=1): shadow rates, every drawTruncNormal branch flag and the chain
+    state bit for bit."""
     yd = np.asarray(fred["ydates"], float)
     jun2012 = date(2012, 6, 1).toordinal() + 366
     thisT = len(yd) if jump == "last" else int(np.nonzero(yd == jun2012)[0][0]) + 1
     ref, elbT = _run(pkg, fred, 1, thisT, B=B)
-    got, _ = _run(pkg, fred, 8, thisT, B=B, lanes=1)
+    got, _ = _run(pkg, fred, 8, thisT, B=B, oct_=2)
     for k in ref:
-        np.testing.assert_array_equal(got[k], ref[k], err_msg=f"lanes {k}")
-    print(f"{jump}: elbT {elbT}, B {B}: lane kernel identical ({int(np.count_nonzero(ref['flags']))} flagged draws)")
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=f"octets {k}")
+    print(f"{jump}: elbT {elbT}, B {B}: octet kernel identical ({int(np.count_nonzero(ref['flags']))} flagged draws)")
