@@ -985,7 +985,8 @@ struct ccmm_chains {
 
   // large-N blocks (N > 32; ccmm_bign.hip)
   void run_astep_big(const RngArgs& ra) {
-    bigW.alloc((size_t)d.B * d.N * d.TP);
+    const size_t np = (size_t)bign_astep_npad(d);
+    bigW.alloc((size_t)d.B * (d.N - 1) * np * np);
     ChainState cs = view();
     launch(KID_ASTEPBIG, [&] {
       HIPCHECK(bign_launch_astep(ctx->stream, d, Tslot.p, cs, ra, cfg.logy2offset, bigW.p));

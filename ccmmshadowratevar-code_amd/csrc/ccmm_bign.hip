@@ -244,8 +244,109 @@ __device__ void wave_trsv_lower_t(const double* L, int ld, double* v, int n) {
 // One workgroup per (row ii = 1..N-1, chain).  Regressors RESID(:, 0:ii-1) / sqrtht(:, ii),
 // regressand RESID(:, ii) / sqrtht(:, ii): the (ii+1) x (ii+1) weighted Gram of RESID(:, 0:ii)
 // with weights 1 / sqrtht(:, ii)^2 holds ZZ (leading block) and Zz (last row).
+// The weighted Grams of the A-step on FP64 MFMA: for every chain and row ii = 1..N-1,
+// G_ii = RESID' diag(1 / sqrtht(:, ii)^2) RESID over the lower 64 x 64 tiles of NPAD x NPAD
+// (mcmcVAR.m:240-244: ZZ = the leading ii x ii block, Zz = row ii).  One workgroup = one tile of
+// FOUR rows ii sharing the chain's residuals: the RESID panels are staged once in LDS and each wave
+// applies its own row's weights (the structure of k_gram_big).  Tiles wholly beyond the group's
+// largest ii are skipped.  Per entry the sum over t is one fma chain in t order, (x_a w) x_b: the
+// order of the scalar wg_gram it replaces.
+constexpr int kAC = 32;    // t rows per staged chunk
+constexpr int kALd = 80;   // LDS row stride of the staged panels
+__global__ __launch_bounds__(256) void k_astep_gram(Dims d, const int* __restrict__ Tslot, ChainState cs,
+                                                   double* __restrict__ gbuf, int NPAD) {
+  __shared__ double Pa[kAC][kALd];
+  __shared__ double Pb[kAC][kALd];
+  __shared__ double Wl[4][kAC];
+  const int N = d.N, TP = d.TP;
+  const int ngr = (N - 1 + 3) / 4;
+  const int c = blockIdx.y / ngr, gr = blockIdx.y - c * ngr;
+  const int ii0 = 1 + 4 * gr;
+  int tile = blockIdx.x, ti = 0;
+  while (tile > ti) {
+    tile -= ti + 1;
+    ++ti;
+  }
+  const int tj = tile;
+  const int a0 = ti * 64, b0 = tj * 64;
+  if (a0 > min(ii0 + 3, N - 1)) return;  // no row of this tile is needed by the group's systems
+  const int T = Tslot[cs.slot[c]];
+  const double* E = cs.E + (size_t)c * N * TP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int myii = ii0 + wave;
+  const int lcol = tid & 63, lt0 = (tid >> 6) * 8;
+  dbl4 acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = dbl4{0.0, 0.0, 0.0, 0.0};
+  const int nchunks = (T + kAC - 1) / kAC;
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int t0 = ch * kAC;
+    {
+      const int ca = a0 + lcol, cb = b0 + lcol;
+      const double* xa = E + (size_t)min(ca, N - 1) * TP;
+      const double* xb = E + (size_t)min(cb, N - 1) * TP;
+      double va[8], vb[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int t = t0 + lt0 + q;
+        va[q] = (ca < N && t < T) ? xa[t] : 0.0;
+        vb[q] = (cb < N && t < T) ? xb[t] : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        Pa[lt0 + q][lcol] = va[q];
+        Pb[lt0 + q][lcol] = vb[q];
+      }
+      if (tid < 4 * kAC) {
+        const int e = tid >> 5, t = tid & 31;
+        const int ii = ii0 + e;
+        double wv = 0.0;
+        if (ii < N && t0 + t < T) {
+          const double h = cs.sqrtht[((size_t)c * N + ii) * TP + t0 + t];
+          wv = 1.0 / (h * h);
+        }
+        Wl[e][t] = wv;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kAC / 4; ++kk) {
+      const int kr = kk * 4 + (lane >> 4);
+      const double wv = Wl[wave][kr];
+      double fa[4], fb[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        fb[x] = Pb[kr][x * 16 + (lane & 15)];       // MFMA A operand: rows = b
+        fa[x] = Pa[kr][x * 16 + (lane & 15)] * wv;  // MFMA B operand: cols = a (weighted)
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[x], fa[y], acc[x][y], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  if (myii >= N) return;
+  // D[row = b][col = a]: lane holds rows (lane >> 4) + 4 r of block x, column lane & 15 of block y
+  double* G = gbuf + ((size_t)c * (N - 1) + (myii - 1)) * NPAD * NPAD;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = b0 + x * 16 + (lane >> 4) + 4 * r;
+        const int a = a0 + y * 16 + (lane & 15);
+        G[(size_t)b * NPAD + a] = acc[x][y][r];
+      }
+}
+
 __global__ __launch_bounds__(256) void k_astep_big(Dims d, const int* __restrict__ Tslot,
-                                                   ChainState cs, RngArgs ra, double* __restrict__ wbuf) {
+                                                   ChainState cs, RngArgs ra, const double* __restrict__ gbuf,
+                                                   int NPAD) {
   extern __shared__ double sm[];
   const int ii = blockIdx.x + 1, c = blockIdx.y;
   const int N = d.N, TP = d.TP;
@@ -254,15 +355,16 @@ __global__ __launch_bounds__(256) void k_astep_big(Dims d, const int* __restrict
   const Rng rng = ra.make(c);
   double* G = sm;                    // (ii+1) x (ii+1), ld kNL
   double* vec = sm + 128 * kNL;      // ii
-  double* wv = wbuf + ((size_t)c * N + ii) * TP;  // 1 / sqrtht(:, ii)^2
-  const double* E = cs.E + (size_t)c * N * TP;
-  const double* sh = cs.sqrtht + ((size_t)c * N + ii) * TP;
-  for (int t = tid; t < T; t += 256) {
-    const double h = sh[t];
-    wv[t] = 1.0 / (h * h);
+  // the weighted Gram of RESID(:, 0:ii) (k_astep_gram), lower triangle into LDS
+  {
+    const double* Gs = gbuf + ((size_t)c * (N - 1) + (ii - 1)) * NPAD * NPAD;
+    const int m = ii + 1;
+    for (int e = tid; e < m * m; e += 256) {
+      const int b = e / m, a = e - b * m;
+      if (a >= b) G[a * kNL + b] = Gs[(size_t)b * NPAD + a];
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  wg_gram<256>(G, E, TP, 1, ii + 1, T, wv, 1);
   const int n = ii;
   for (int a = tid; a < n; a += 256) vec[a] = G[n * kNL + a];  // Zz
   __syncthreads();
@@ -832,13 +934,19 @@ size_t bign_sv_scratch(const Dims& d) {
   return (size_t)d.N * d.N * (1 + 2 * (size_t)(d.TP + 1)) + (size_t)(d.TP + 1) * d.N;
 }
 
+int bign_astep_npad(const Dims& d) { return d.N <= 64 ? 64 : 128; }
+
 hipError_t bign_launch_astep(hipStream_t st, const Dims& d, const int* Tslot, ChainState cs, RngArgs ra,
-                             double logy2offset, double* wbuf) {
+                             double logy2offset, double* gbuf) {
+  const int NPAD = bign_astep_npad(d);
+  const int nt = NPAD / 64;
+  const int ngr = (d.N - 1 + 3) / 4;
+  hipLaunchKernelGGL(k_astep_gram, dim3(nt * (nt + 1) / 2, d.B * ngr), dim3(256), 0, st, d, Tslot, cs, gbuf, NPAD);
   const size_t lds = (size_t)(128 * kNL + 128) * sizeof(double);
   hipError_t e = hipFuncSetAttribute((const void*)k_astep_big, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_astep_big, dim3(d.N - 1, d.B), dim3(256), lds, st, d, Tslot, cs, ra, wbuf);
+  hipLaunchKernelGGL(k_astep_big, dim3(d.N - 1, d.B), dim3(256), lds, st, d, Tslot, cs, ra, gbuf, NPAD);
   const size_t lds2 = (size_t)d.N * d.N * sizeof(double);
   e = hipFuncSetAttribute((const void*)k_astep_fin, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
   if (e != hipSuccess) return e;

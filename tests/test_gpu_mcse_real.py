@@ -48,12 +48,14 @@ def _vech_diag_index(N):
     return np.array(out)
 
 
-def _run(pkg, ctx, oracle, fred, g, kind, B=128, burn=1000, keep=2000, chunk=50):
+def _run(pkg, ctx, oracle, fred, g, kind, B=128, burn=1000, keep=2000, chunk=50, perturb=None):
     mpm = oracle.set_minnesota_mean(fred["ncode"])
     thisT = len(fred["ydates"])
     rows, cols, tsel = g["sel_rows"], g["sel_cols"], list(g["tsel"])
     if kind == "linear":
         m = pkg.model.build_var(thisT, 12, 12, fred["data"], fred["ydates"], mpm, True)
+        if perturb is not None:
+            m = perturb(m)
         ch = pkg.Chains(ctx, N=m.N, p=12, T=m.T, B=B, crn=False, store_capacity=chunk, seed=31337)
     else:
         ndxS, ndxO, _ = pkg.model.setShadowYields(fred["ncode"], 0.25)
@@ -97,6 +99,34 @@ def _run(pkg, ctx, oracle, fred, g, kind, B=128, burn=1000, keep=2000, chunk=50)
     ch.close()
     assert not np.any(status & ~1), status
     return sums / keep, acc                                                # nq x B chain means
+
+
+def _zscores(g, means):
+    B = means.shape[1]
+    m_gpu = means.mean(axis=1)
+    nse_gpu = means.std(axis=1, ddof=1) / np.sqrt(B)
+    se_o = np.maximum(g["nse3"], g["se_between"]) if "se_between" in g else g["nse3"]
+    return (m_gpu - g["pmean"]) / np.sqrt(se_o ** 2 + nse_gpu ** 2), m_gpu, nse_gpu, se_o
+
+
+@pytest.mark.parametrize("name", ["minnesota_precision_x1.5", "phi_prior_scale_x2"])
+def test_mcse_detects_a_perturbed_sampler(pkg, ctx, oracle, fred, name):
+    """Power of the posterior-level check: the same device run with ONE sampler detail changed
+    (the Minnesota prior precision iV scaled by 1.5, i.e. theta by 1/sqrt(1.5), mcmcVAR.m:129-150;
+    or the inverse-Wishart scale s_PHI doubled, mcmcVAR.m:165) must fail the 4.5-sigma bar that
+    the unperturbed sampler passes (test_real_data_posterior_means_within_mcse)."""
+    import dataclasses
+    g = _fixture("linear")
+
+    def perturb(m):
+        if name.startswith("minnesota"):
+            return dataclasses.replace(m, iVdiag=m.iVdiag * 1.5, iVb=m.iVb * 1.5)
+        return dataclasses.replace(m, sPHI=m.sPHI * 2.0)
+
+    means, _ = _run(pkg, ctx, oracle, fred, g, "linear", burn=int(g["burn"]), keep=int(g["keep"]), perturb=perturb)
+    z = _zscores(g, means)[0]
+    print(f"{name}: max |z| {np.abs(z).max():.1f}, {int(np.sum(np.abs(z) > 4.5))} of {z.size} quantities beyond 4.5")
+    assert np.abs(z).max() > 4.5
 
 
 @pytest.mark.parametrize("kind", ["linear", "bh"])
