@@ -1156,10 +1156,13 @@ struct ccmm_chains {
     if (staged <= 160 * 1024) {
       es_off = total + N * N;
       lds = staged;
-      if (lds > 64 * 1024)
-        HIPCHECK(hipFuncSetAttribute((const void*)k_astep,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     }
+    // k_astep_w (wave-parallel factorisations, the default) or the one-thread-per-regression
+    // k_astep (CCMM_ASTEP_V1=1, kept for A/B timing); same draws up to summation order inside
+    // the factorisation (identical update order, fma placement as written)
+    const bool v1 = std::getenv("CCMM_ASTEP_V1") && std::atoi(std::getenv("CCMM_ASTEP_V1")) != 0;
+    const void* fn = v1 ? (const void*)k_astep : (N <= 20 ? (const void*)k_astep_w<20> : (const void*)k_astep_w<32>);
+    if (lds > 64 * 1024) HIPCHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (!astepTab.p) {  // (ii, a, b) of every Gram entry, block ii = 1..N-1: packed lower ZZ, then Zz
       std::vector<int> tab;
       for (int ii = 1; ii < N; ++ii) {
@@ -1172,8 +1175,15 @@ struct ccmm_chains {
       HIPCHECK(hipMemcpy(astepTab.p, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice));
     }
     launch(KID_ASTEP, [&] {
-      hipLaunchKernelGGL(k_astep, dim3(d.B), dim3(256), lds, ctx->stream, d, Tslot.p, cs, ra,
-                         cfg.logy2offset, es_off, astepTab.p);
+      if (v1)
+        hipLaunchKernelGGL(k_astep, dim3(d.B), dim3(256), lds, ctx->stream, d, Tslot.p, cs, ra,
+                           cfg.logy2offset, es_off, astepTab.p);
+      else if (N <= 20)
+        hipLaunchKernelGGL(k_astep_w<20>, dim3(d.B), dim3(512), lds, ctx->stream, d, Tslot.p, cs, ra,
+                           cfg.logy2offset, es_off, astepTab.p);
+      else
+        hipLaunchKernelGGL(k_astep_w<32>, dim3(d.B), dim3(512), lds, ctx->stream, d, Tslot.p, cs, ra,
+                           cfg.logy2offset, es_off, astepTab.p);
     });
   }
 

@@ -588,6 +588,184 @@ __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ T
   }
 }
 
+// ============================================================== A-step, wave-parallel form
+// The same draws as k_astep (mcmcVAR.m:236-254, 259) with the per-regression work spread over
+// waves instead of one thread per regression: 8 waves share the Gram entries (one wave per
+// entry, lanes over t, E staged in LDS), then each wave factors whole regressions ii in
+// registers (lane r holds row r of ZZ_ii: readlane broadcasts of the pivot row, the same
+// left-to-right update order as k_astep's left-looking loop) and solves L tilde = Zz,
+// alpha = L' \ (tilde + z) by lane substitutions; wave 0 forms invA by lane-per-column
+// forward substitution.  Regressions are dealt to waves largest first in snake order.
+template <int NN>
+__global__ __launch_bounds__(512) void k_astep_w(Dims d, const int* __restrict__ Tslot, ChainState cs,
+                                                 RngArgs ra, double logy2offset, int es_off,
+                                                 const int* __restrict__ gtab) {
+  extern __shared__ double sm[];
+  constexpr int kWaves = 8;
+  const int c = blockIdx.x;
+  const int N = d.N, TP = d.TP;
+  const int T = Tslot[cs.slot[c]];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Rng rng = ra.make(c);
+  const double* E = cs.E + (size_t)c * N * TP;
+  const double* sh = cs.sqrtht + (size_t)c * N * TP;
+  double* Ac = cs.A + (size_t)c * N * N;
+  double* Ainv = cs.invA + (size_t)c * N * N;
+  __shared__ int boff[kMaxNSmall + 1];
+  if (tid == 0) {
+    int o = 0;
+    boff[0] = 0;
+    boff[1] = 0;
+    for (int ii = 1; ii < N; ++ii) {
+      boff[ii] = o;
+      o += ii * (ii + 1) / 2 + ii;
+    }
+    boff[N] = o;
+  }
+  if (es_off >= 0)
+    for (int q = tid; q < N * TP; q += blockDim.x) sm[es_off + q] = E[q];
+  __syncthreads();
+  const double* Ew = (es_off >= 0) ? sm + es_off : E;
+  const int total = boff[N];
+  double* Anew = sm + total;  // N x N
+  // ---- Gram entries (identical arithmetic to k_astep's wave-per-entry path)
+  constexpr int kAsTPL = 16;
+  {
+    double ih[kAsTPL];
+    int cur_ii = -1;
+    for (int g = wave; g < total; g += kWaves) {
+      const int v = gtab[g];
+      const int ii = v >> 16, a = (v >> 8) & 255, b = v & 255;
+      if (ii != cur_ii) {
+        cur_ii = ii;
+        const double* hh = sh + (size_t)ii * TP;
+#pragma unroll
+        for (int k = 0; k < kAsTPL; ++k) {
+          const int t = lane + 64 * k;
+          const double hv = (t < T) ? hh[t] : 1.0;
+          ih[k] = (t < T) ? 1.0 / (hv * hv) : 0.0;
+        }
+      }
+      const double* ea = Ew + (size_t)a * TP;
+      const double* eb = Ew + (size_t)b * TP;
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < kAsTPL; ++k) {
+        const int t = lane + 64 * k;
+        if (t < T) acc = fma(ea[t] * eb[t], ih[k], acc);
+      }
+      acc = wave_sum_dpp(acc);
+      if (lane == 0) sm[g] = acc;
+    }
+  }
+  for (int q = tid; q < N * N; q += blockDim.x) Anew[q] = ((q % N) == (q / N)) ? 1.0 : 0.0;
+  __syncthreads();
+  // ---- per-regression factor + solves, one wave per regression ii (rows on lanes)
+  int badf = 0;
+  for (int r8 = 0;; ++r8) {
+    // snake order over ii = N-1 .. 1: round r8 gives wave w the (w or 7-w)-th of that round
+    const int pos = r8 * kWaves + ((r8 & 1) ? (kWaves - 1 - wave) : wave);
+    const int ii = N - 1 - pos;
+    if (ii < 1) break;
+    double* Lp = sm + boff[ii];  // packed lower by columns, ii x ii, then Zz
+    const double* zz = Lp + ii * (ii + 1) / 2;
+    auto idx = [ii](int r, int col) { return col * ii - col * (col - 1) / 2 + (r - col); };
+    const int rl = lane < ii ? lane : 0;
+    double s[NN];
+#pragma unroll
+    for (int q = 0; q < NN; ++q) s[q] = (q <= rl && q < ii && lane < ii) ? Lp[idx(rl, q)] : 0.0;
+    double piv[NN];
+#pragma unroll
+    for (int q = 0; q < NN; ++q) {
+      if (q < ii) {
+        double dq = readlane_d(s[q], q);
+        if (!(dq > 0.0)) {
+          badf = 1;
+          dq = 1.0;
+        }
+        const double pq = sqrt(dq);
+        piv[q] = pq;
+        s[q] = (lane == q) ? pq : s[q] / pq;
+        // row r > q, entries q < k <= r: s[k] -= L(r, q) L(k, q)
+#pragma unroll
+        for (int k = q + 1; k < NN; ++k)
+          if (k < ii) s[k] = fma(-s[q], readlane_d(s[q], k), s[k]);
+      }
+    }
+    // tilde = L \ Zz (lane r holds entry r), + z, then alpha = L' \ (tilde + z)
+    double y = (lane < ii) ? zz[rl] : 0.0;
+#pragma unroll
+    for (int k = 0; k < NN; ++k) {
+      if (k < ii) {
+        const double yk = readlane_d(y, k) / piv[k];
+        y = (lane == k) ? yk : ((lane > k) ? fma(-s[k], yk, y) : y);
+      }
+    }
+    const int zoff = ii * (ii - 1) / 2;
+    if (lane < ii) y += rng.normal(CCMM_RNG_A, (uint32_t)(zoff + lane));
+    // back substitution in k_astep's order: x_r = (v_r - sum_{q > r, ascending} L(q, r) x_q) / L(r, r),
+    // evaluated uniformly (the factor goes back to the packed slots and is read by broadcast)
+    if (lane < ii) {
+#pragma unroll
+      for (int q = 0; q < NN; ++q)
+        if (q <= rl && q < ii) Lp[idx(rl, q)] = s[q];
+    }
+    wave_lds_sync();
+    double xs[NN];
+#pragma unroll
+    for (int r = NN - 1; r >= 0; --r) {
+      xs[r] = 0.0;
+      if (r < ii) {
+        double v = readlane_d(y, r);
+#pragma unroll
+        for (int q = r + 1; q < NN; ++q)
+          if (q < ii) v = fma(-Lp[idx(q, r)], xs[q], v);
+        xs[r] = v / piv[r];
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < NN; ++q)
+        if (q < ii) Anew[ii + q * N] = -xs[q];
+    }
+    wave_lds_sync();
+  }
+  if (badf && lane == 0) atomicOr(&cs.status[c], 4);
+  __syncthreads();
+  for (int q = tid; q < N * N; q += blockDim.x) Ac[q] = Anew[q];
+  // invA: lane col forms column col of A^-1 (unit lower forward substitution, A read by
+  // broadcast from LDS)
+  if (wave == 0) {
+    const int col = lane;
+    double x[NN];
+#pragma unroll
+    for (int r = 0; r < NN; ++r) {
+      double v = (r == col) ? 1.0 : 0.0;
+#pragma unroll
+      for (int q = 0; q < r; ++q)
+        if (q >= col) v = fma(-Anew[r + q * N], x[q], v);
+      x[r] = (r >= col) ? v : 0.0;
+    }
+    if (col < N) {
+#pragma unroll
+      for (int r = 0; r < NN; ++r)
+        if (r < N) Ainv[r + col * N] = x[r];
+    }
+  }
+  // logy2 = log((RESID * A').^2 + offset)
+  double* ly = cs.logy2 + (size_t)c * N * TP;
+  for (int t = tid; t < TP; t += blockDim.x) {
+    for (int i = 0; i < N; ++i) {
+      double sacc = 0.0;
+      if (t < T) {
+        for (int k = 0; k <= i; ++k) sacc = fma(Ew[(size_t)k * TP + t], Anew[i + k * N], sacc);
+      }
+      ly[(size_t)i * TP + t] = (t < T) ? log(sacc * sacc + logy2offset) : 0.0;
+    }
+  }
+}
+
 // ============================================================== SV: KSC mixture indicators
 __constant__ double cKSCprob[7] = {0.00730, 0.10556, 0.00002, 0.04395, 0.34001, 0.24566, 0.25750};
 __constant__ double cKSCmean[7] = {-10.12999 - 1.2704, -3.97281 - 1.2704, -8.56686 - 1.2704,

@@ -48,6 +48,16 @@ def unit_cost(T, K, N, n_cens=0, Nstate=None, Ny=None, passes=101):
     return float(f)
 
 
+def elb_wavefront_steps(n_cens, passes=101, p=12, waves=8):
+    """Serial steps of the ELB Gibbs passes of one chain (gibbsdrawShadowrates.m:181-245 as the
+    device runs them, k_elb_gibbs_wf): pass n may draw censored month i once pass n - 1 is p months
+    past it, so min(waves, n_cens / (p + 1)) passes are in flight (at least one)."""
+    if n_cens <= 0:
+        return 0.0
+    weff = min(float(waves), max(1.0, n_cens / (p + 1.0)))
+    return passes * n_cens / weff + (n_cens if weff > 1.0 else 0.0)
+
+
 def censored_months(data, ndxS, elb, startELB, thisT):
     """Censored months of one vintage: rows startELB..thisT (1-based, the vintage's ELB
     window, goVARshadowrateBlockHybrid.m:131-134) in which some shadow-rate series sits at
@@ -83,11 +93,12 @@ def shard_range(n, world_size, rank):
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def init(backend=None):
+def init(backend=None, min_world=2):
     """Initialise torch.distributed from the torchrun environment (RCCL on GPU,
-    gloo on CPU).  Returns (dist module or None, World)."""
+    gloo on CPU).  Returns (dist module or None, World); None below min_world ranks
+    (min_world=1 forms a one-rank group, which runs the collectives' code paths)."""
     w = world_from_env()
-    if w.size <= 1:
+    if w.size < min_world:
         return None, w
     import torch
     import torch.distributed as dist
