@@ -528,7 +528,7 @@ struct ccmm_chains {
     const size_t lds_max = 160 * 1024;
     if (!lag_supported_nt(lagNT) || N > 32 || 16 * lagNT + 1 > d.KP ||
         gl_lds_bytes(lagNT, drows, ldd, d.TP) > lds_max ||
-        sl_lds_bytes(lagNT, drows, ldd, d.TP, N) > lds_max)
+        sl_lds_bytes(lagNT, drows, ldd, d.TP, N <= 8 ? 8 : (N <= 20 ? 20 : 32)) > lds_max)
       return;
     lag_capable = true;
     Dpool.alloc((size_t)nX * drows * ldd);
@@ -1118,8 +1118,8 @@ struct ccmm_chains {
     });
     const LagSel ls = lagsel();
     const size_t lds_g = gl_lds_bytes(lagNT, drows, ldd, d.TP);
-    const size_t lds_s = sl_lds_bytes(lagNT, drows, ldd, d.TP, d.N);
     const int nmax = d.N <= 8 ? 8 : (d.N <= 20 ? 20 : 32);
+    const size_t lds_s = sl_lds_bytes(lagNT, drows, ldd, d.TP, nmax);
     std::unique_lock<std::mutex> lk;
     PhaseLock* L = nullptr;
     if (mfma_lock > 0) {  // same phase lock as run_cta_big
@@ -1405,13 +1405,20 @@ struct ccmm_chains {
     }
     const int N = d.N, p = cfg.p, Ns = cfg.Ns, Np = N * p;
     // Φ staged in LDS when it fits (N = 20, p = 12: 40 KB); N = 120 reads it from e.Phi
+    // and Yb - yhat, Yb too (2 elbTmax N doubles: 52 KB at elbT = 165) when they fit beside it
     size_t lds_prep = (size_t)(2 + Np + N * (Np + 1)) * sizeof(double);
-    const int phi_lds = lds_prep <= 160 * 1024 ? 1 : 0;
+    int phi_lds = lds_prep <= 160 * 1024 ? 1 : 0;
     if (!phi_lds) lds_prep = (size_t)(2 + Np) * sizeof(double);
+    const size_t lds_zy = lds_prep + (size_t)2 * cfg.elbTmax * N * sizeof(double);
+    if (phi_lds && lds_zy <= 160 * 1024) {
+      phi_lds |= 2;
+      lds_prep = lds_zy;
+    }
     launch(KID_ELBPREP, [&] {
       HIPCHECK(hipFuncSetAttribute((const void*)k_elb_prep, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds_prep));
-      hipLaunchKernelGGL(k_elb_prep, dim3(d.B), dim3(256), lds_prep, ctx->stream, d, e, xsel(), cs, phi_lds);
+      hipLaunchKernelGGL(k_elb_prep, dim3(d.B), dim3(kElbPrepThreads), lds_prep, ctx->stream, d, e, xsel(), cs,
+                         phi_lds);
     });
     size_t lds_cond =
         (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns + N * Ns + N * p * Ns) * sizeof(double);

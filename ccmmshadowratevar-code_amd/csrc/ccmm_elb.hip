@@ -81,8 +81,9 @@ __host__ __device__ inline int elb_cond_stride(int Ns, int p, int ps = 0) {
 // matrix is explosive, where the as-written form loses all digits to cancellation.
 //   Yt[τ] = Yb_τ   (the chain's Y with censored shadow-rate cells at 0)
 //   Et[τ] = ε_τ = Yb_τ - Σ_{l<=τ} Φ_l Yb_{τ-l} - e0_τ
-// phi_lds: stage Φ in LDS (N (Np + 1) doubles; N <= 32); else it is read back from e.Phi
-__global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, ChainState cs, int phi_lds) {
+// phi_lds bit 0: stage Φ in LDS (N (Np + 1) doubles; N <= 32); else it is read back from e.Phi
+constexpr int kElbPrepThreads = 512;
+__global__ __launch_bounds__(kElbPrepThreads) void k_elb_prep(Dims d, ElbDev e, XSel xs, ChainState cs, int phi_lds) {
   extern __shared__ double sm[];
   const int c = blockIdx.x;
   const int s = cs.slot[c];
@@ -93,27 +94,32 @@ __global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, Cha
   const int tid = threadIdx.x;
   const double* PAI = cs.PAI + (size_t)c * N * KP;  // PAI(k, i) at [i*KP + k]
   double* Phi = e.Phi + (size_t)c * N * Np;
-  double* Z = e.Y0 + (size_t)c * e.elbTmax * N;     // Yb - yhat
-  double* Yt = e.Yt + (size_t)c * e.elbTmax * N;
+  double* Zg = e.Y0 + (size_t)c * e.elbTmax * N;    // Yb - yhat
+  double* Ytg = e.Yt + (size_t)c * e.elbTmax * N;
   double* Et = e.Et + (size_t)c * e.elbTmax * N;
   double* X0 = sm;                   // K: elb.X0 = X(elbT0+1, :)'
-  double* sPhi = sm + (2 + Np);      // N x ldp (phi_lds)
+  double* sPhi = sm + (2 + Np);      // N x ldp (phi_lds & 1)
+  // phi_lds & 2: Yb - yhat and Yb also staged in LDS (T x N each), so that the lag sums of the residual
+  // pass below read LDS instead of global memory (same values, same operation order)
+  const bool zy_lds = (phi_lds & 2) != 0;
+  double* Z = zy_lds ? sPhi + (size_t)N * ldp : Zg;
+  double* Yt = zy_lds ? Z + (size_t)e.elbTmax * N : Ytg;
   // Φ = PAIshadow(2:1+Np, :)' with (ndxSHADOWRATELAGS, actualrateBlock) zeroed (:404-407)
-  for (int q = tid; q < N * Np; q += 256) {
+  for (int q = tid; q < N * Np; q += kElbPrepThreads) {
     const int i = q / Np, kp = q % Np;
     bool zero = false;
     if (e.actual[i])
       for (int si = 0; si < Ns; ++si) zero |= (kp % N) == e.ndxS[si];
     const double v = zero ? 0.0 : PAI[(size_t)i * KP + 1 + kp];
     Phi[q] = v;
-    if (phi_lds) sPhi[i * ldp + kp] = v;
+    if (phi_lds & 1) sPhi[i * ldp + kp] = v;
   }
   const double* Xa = e.Xactual + (size_t)s * KP * TP;        // Xactual(t, k) at [k*TP + t]
   const double* Yc = xs.ypool + (size_t)xs.yidx[c] * N * TP;  // chain's Y(t, i) at [i*TP + t]
-  for (int k = tid; k < 1 + Np; k += 256) X0[k] = Xa[(size_t)k * TP + T0];
+  for (int k = tid; k < 1 + Np; k += kElbPrepThreads) X0[k] = Xa[(size_t)k * TP + T0];
   const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * Ns;
   // Yb and Z = Yb - Yhatactual;  Yhatactual(:,t) = (Xactual(elbT0+t, lagmask) * PAIactual)' (:400-403)
-  for (int q = tid; q < T * N; q += 256) {
+  for (int q = tid; q < T * N; q += kElbPrepThreads) {
     const int t = q / N, i = q % N;
     double yh = 0.0;
     if (e.yhat) {  // gibbsdrawShadowrates' YHAT0 argument (ccmm_gibbs_shadowrates)
@@ -134,15 +140,19 @@ __global__ __launch_bounds__(256) void k_elb_prep(Dims d, ElbDev e, XSel xs, Cha
       if (e.ndxS[si] == i && sN[t * Ns + si]) yb = 0.0;
     Yt[q] = yb;
     Z[q] = yb - yh;
+    if (zy_lds) {
+      Ytg[q] = yb;
+      Zg[q] = yb - yh;
+    }
   }
   // Gibbs start values: the chain's current shadow rates (gibbsdrawShadowrates.m:171)
   double* Sc = e.Scur + (size_t)c * e.elbTmax * Ns;
-  for (int q = tid; q < T * Ns; q += 256) Sc[q] = Yc[(size_t)e.ndxS[q % Ns] * TP + T0 + q / Ns];
+  for (int q = tid; q < T * Ns; q += kElbPrepThreads) Sc[q] = Yc[(size_t)e.ndxS[q % Ns] * TP + T0 + q / Ns];
   __syncthreads();
   // ε_τ = Z_τ - Σ_{l<=τ} Φ_l Z_{τ-l} - [τ = 0: w_{-1};  τ >= 1: c + Σ_{l>τ} Φ_l w_{τ-1-l}]
-  for (int q = tid; q < T * N; q += 256) {
+  for (int q = tid; q < T * N; q += kElbPrepThreads) {
     const int t = q / N, i = q % N;
-    const double* ph = phi_lds ? sPhi + i * ldp : Phi + (size_t)i * Np;
+    const double* ph = (phi_lds & 1) ? sPhi + i * ldp : Phi + (size_t)i * Np;
     double v = Z[q];
     for (int l = 1; l <= p && t - l >= 0; ++l) {
       const double* zl = Z + (size_t)(t - l) * N;

@@ -55,8 +55,8 @@ constexpr int kSlThreads = 512;
 
 // LDS of k_cta_solve_lag: D | v + X'v partials | rl | xl | A | red | colmap
 __host__ __device__ inline int sl_union(int NT, int TP) { return TP + 512; }
-inline size_t sl_lds_bytes(int NT, int rows, int ldd, int TP, int N) {
-  const size_t n = (size_t)rows * ldd + sl_union(NT, TP) + 256 + 256 + N * N + 16;
+inline size_t sl_lds_bytes(int NT, int rows, int ldd, int TP, int nmax) {
+  const size_t n = (size_t)rows * ldd + sl_union(NT, TP) + 256 + 256 + (size_t)nmax * nmax + 16;
   return n * sizeof(double) + 16 * NT * sizeof(int);
 }
 

@@ -36,6 +36,8 @@
 // data and the identity prior (iVdiag padding 1): exactly decoupled, x = 0 there.
 #include "ccmm_lag.h"
 
+#include <cstdlib>
+
 namespace ccmm {
 
 struct GlArgs {
@@ -405,12 +407,13 @@ __global__ __launch_bounds__(512, 1) void k_gram_chol_lag(Dims d, const int* __r
 // k_gram_chol_lag (wave W holds slots W + 8k; element (lq + 4r, lr) of slot (ti, tj) =
 // M'_{tj,ti}(lq + 4r, lr), U~_pp^-1 on the diagonal): one coalesced HBM read per system,
 // issued after the v_t loads so that it overlaps the X'v product.
-template <int NT, int NMAX>
-__global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int* __restrict__ Tslot,
+template <int NT, int NMAX, int SW>
+__global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __restrict__ Tslot,
                                                               const double* __restrict__ iVb, XSel xs, LagSel ls,
                                                               ChainState cs, RngArgs ra) {
   constexpr int NTILE = gl_ntile(NT);
-  constexpr int TPW = gl_tpw(NT);
+  constexpr int NTH = 64 * SW;                      // SW waves (8 or 16)
+  constexpr int TPW = (gl_ntile(NT) + SW - 1) / SW;  // factor tiles held per wave
   constexpr int KL = 16 * NT;
   extern __shared__ double sm[];
   const int N = d.N, TP = d.TP, K = d.K, KP = d.KP;
@@ -420,8 +423,8 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
   double* part = vl + TP;            // 2 x 256       phase 2
   double* rl = vl + sl_union(NT, TP);  // 256  rhs, then c = y + z  (K-space)
   double* xl = rl + 256;             // 256  y, then x            (K-space)
-  double* Al = xl + 256;             // N x N
-  double* red = Al + N * N;          // 16
+  double* Al = xl + 256;             // N x N, column stride NMAX
+  double* red = Al + NMAX * NMAX;    // 16
   int* cm = reinterpret_cast<int*>(red + 16);  // KL
   const int c = blockIdx.x;
   const int s = cs.slot[c];
@@ -432,13 +435,13 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
   const double* ih2 = cs.ih2 + (size_t)c * N * TP;
   const double* Y = xs.ypool + (size_t)xs.yidx[c] * N * TP;
   double* E = cs.E + (size_t)c * N * TP;
-  for (int q = tid; q < N * N; q += kSlThreads) Al[q] = cs.A[(size_t)c * N * N + q];
-  for (int q = tid; q < KL; q += kSlThreads) cm[q] = ls.colmap[q];
+  for (int q = tid; q < N * N; q += NTH) Al[(q % N) + (q / N) * NMAX] = cs.A[(size_t)c * N * N + q];
+  for (int q = tid; q < KL; q += NTH) cm[q] = ls.colmap[q];
   // this wave's slots: (ti, tj) per register tile
   int sti[TPW], stj[TPW];
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
-    const int gi = wave + kGlWaves * k;
+    const int gi = wave + SW * k;
     sti[k] = gi < NTILE ? gl_ti(NT, gi) : 0;
     stj[k] = gi < NTILE ? gl_tj(NT, gi) : 0;
   }
@@ -455,29 +458,33 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
     if (slab != cur) {
       __syncthreads();
       const double* src = ls.dpool + (size_t)slab * rows * ldd;
-      for (int q = tid; q < rows * ldd; q += kSlThreads) Dl[q] = src[q];
+      for (int q = tid; q < rows * ldd; q += NTH) Dl[q] = src[q];
       cur = slab;
     }
     // ---- (1) v_t (E(:,j) = Y(:,j) stands for PAI(:,j) = 0, CTA.m:63)
-    for (int t = tid; t < TP; t += kSlThreads) {
+    for (int t = tid; t < TP; t += NTH) {
       double acc = 0.0;
       if (t < T && !(ls.mode & 16)) {
-        double e[NMAX], w2[NMAX];
+        double e[NMAX];
+        // per-lane element offsets (k TP + t) advanced in a register, so that no per-k base address
+        // is hoisted into scalar registers (the kernel's scalar file would spill)
+        int o = t;
 #pragma unroll
         for (int k = 0; k < NMAX; ++k) {
-          if (k < N) {
-            e[k] = (k == j) ? Y[(size_t)k * TP + t] : E[(size_t)k * TP + t];
-            w2[k] = (k >= j) ? ih2[(size_t)k * TP + t] : 0.0;  // rows i >= j only
-          }
+          if (k < N) e[k] = (k == j) ? Y[o] : E[o];
+          o += TP;
         }
+        // A in LDS with the compile-time column stride NMAX (every A(i, k) read is an immediate offset
+        // from row i's address); the row loop stays rolled so that only one row of A is in flight
+        // (unrolled, the compiler hoisted all N(N+1)/2 entries into registers and spilled)
+#pragma unroll 1
+        for (int i = j; i < N; ++i) {
+          const double* Ai = Al + i;
+          double ea = 0.0;
 #pragma unroll
-        for (int i = 0; i < NMAX; ++i) {
-          if (i >= j && i < N) {
-            double ea = 0.0;
-#pragma unroll
-            for (int k = 0; k <= i; ++k) ea = fma(e[k], Al[i + k * N], ea);
-            acc = fma(Al[i + j * N] * ea, w2[i], acc);
-          }
+          for (int k = 0; k < NMAX; ++k)
+            if (k <= i) ea = fma(e[k], Ai[k * NMAX], ea);
+          acc = fma(Ai[j * NMAX] * ea, ih2[i * TP + t], acc);  // 1 / sqrtht(t, i)^2, rows i >= j
         }
       }
       vl[t] = acc;
@@ -488,7 +495,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
     dbl4 lt[TPW];
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {
-      const int gi = wave + kGlWaves * k;
+      const int gi = wave + SW * k;
       if (gi < NTILE) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) lt[k][r] = Lo[gi * 256 + 64 * r + lane];
@@ -502,7 +509,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       const int th = ((T + 1) >> 1);
       const int t0 = h ? th : 0, t1 = h ? T : th;
       double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-      if (ls.mode & 32) {
+      if ((ls.mode & 32) || tid >= 512) {  // threads 512.. (SW = 16) idle: the t-halves fix the order
       } else if (a < KL) {
         // four strided chains (t mod 4); the loads of eight months are issued before their
         // fused multiply-adds so that one LDS round trip serves eight products
@@ -535,7 +542,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       } else if (a == KL) {
         for (int t = t0; t < t1; ++t) p0 += vl[t];
       }
-      part[h * 256 + a] = (p0 + p1) + (p2 + p3);
+      if (tid < 512) part[h * 256 + a] = (p0 + p1) + (p2 + p3);
     }
     __syncthreads();
     const double* ivb = iVb + ((size_t)s * N + j) * KP;
@@ -563,7 +570,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
     for (int p = 0; p < (subst ? NT - 1 : 0); ++p) {
 #pragma unroll
       for (int k = 0; k < TPW; ++k) {
-        const int gi = wave + kGlWaves * k;
+        const int gi = wave + SW * k;
         if (gi < NTILE && stj[k] == p && sti[k] > p) {
           const double v = colsum(lt[k], rl + 1 + 16 * p + lq);
           if (lq == 0) rl[1 + 16 * sti[k] + lr] -= v;
@@ -574,7 +581,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
     if (subst) {
 #pragma unroll
       for (int k = 0; k < TPW; ++k) {
-        const int gi = wave + kGlWaves * k;
+        const int gi = wave + SW * k;
         if (gi < NTILE && sti[k] == stj[k]) {
           const double v = colsum(lt[k], rl + 1 + 16 * sti[k] + lq);
           if (lq == 0) xl[1 + 16 * sti[k] + lr] = v;
@@ -609,7 +616,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       if (subst) {
 #pragma unroll
         for (int k = 0; k < TPW; ++k) {
-          const int gi = wave + kGlWaves * k;
+          const int gi = wave + SW * k;
           if (gi < NTILE && sti[k] == stj[k]) {
             const double q = fold(lt[k], rl[1 + 16 * sti[k] + lr]);
             if ((lr & 3) == 0) xl[1 + 16 * sti[k] + lq + 4 * (lr >> 2)] = q;
@@ -620,7 +627,7 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
       for (int p = (subst ? NT - 1 : 0); p >= 1; --p) {
 #pragma unroll
         for (int k = 0; k < TPW; ++k) {
-          const int gi = wave + kGlWaves * k;
+          const int gi = wave + SW * k;
           if (gi < NTILE && sti[k] == p && stj[k] < p) {
             const double q = fold(lt[k], xl[1 + 16 * p + lr]);
             if ((lr & 3) == 0) xl[1 + 16 * stj[k] + lq + 4 * (lr >> 2)] -= q;
@@ -637,14 +644,14 @@ __global__ __launch_bounds__(kSlThreads) void k_cta_solve_lag(Dims d, const int*
     __syncthreads();
     if (tid == KL) {
       double sacc = 0.0;
-      for (int w = 0; w < kSlThreads / 64; ++w) sacc += red[w];
+      for (int w = 0; w < NTH / 64; ++w) sacc += red[w];
       xl[0] = (rl[0] - sacc) * Lv[0];
     }
     __syncthreads();
     // ---- (5) PAI(:,j) = x; E(:,j) = Y(:,j) - X x
     double* pai = cs.PAI + ((size_t)c * N + j) * KP;
-    for (int k = tid; k < KP; k += kSlThreads) pai[k] = (k < K) ? xl[k] : 0.0;
-    for (int t = tid; t < TP; t += kSlThreads) {
+    for (int k = tid; k < KP; k += NTH) pai[k] = (k < K) ? xl[k] : 0.0;
+    for (int t = tid; t < TP; t += NTH) {
       double o = 0.0;
       if (t < T && !(ls.mode & 128)) {
         const double* rowp = Dl + t * ldd;
@@ -707,15 +714,26 @@ hipError_t lag_launch_gram(int NT, hipStream_t st, size_t lds, Dims d, const int
   return hipGetLastError();
 }
 
+// SW = 8 waves (default) or 16 (CCMM_SOLVE_WAVES=16: half the factor tiles per wave and four waves
+// per SIMD, but 128 registers per lane, which the kernel overflows).  Same arithmetic either way
+// (per-thread v_t and residual rows, per-tile substitution products, the X'v t-halves on threads
+// 0..511).
+template <int NT, int NM, int SW>
+static hipError_t solve_sw(hipStream_t st, size_t lds, Dims d, const int* Tslot, const double* iVb, XSel xs,
+                           LagSel ls, ChainState cs, RngArgs ra) {
+  hipError_t e = hipFuncSetAttribute((const void*)k_cta_solve_lag<NT, NM, SW>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_cta_solve_lag<NT, NM, SW>), dim3(d.B), dim3(64 * SW), lds, st, d, Tslot, iVb, xs, ls, cs,
+                     ra);
+  return hipGetLastError();
+}
 template <int NT, int NM>
 static hipError_t solve_one(hipStream_t st, size_t lds, Dims d, const int* Tslot, const double* iVb, XSel xs,
                             LagSel ls, ChainState cs, RngArgs ra) {
-  hipError_t e = hipFuncSetAttribute((const void*)k_cta_solve_lag<NT, NM>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_cta_solve_lag<NT, NM>), dim3(d.B), dim3(kSlThreads), lds, st, d, Tslot, iVb, xs, ls, cs,
-                     ra);
-  return hipGetLastError();
+  const char* v = std::getenv("CCMM_SOLVE_WAVES");
+  if (v && std::atoi(v) == 16) return solve_sw<NT, NM, 16>(st, lds, d, Tslot, iVb, xs, ls, cs, ra);
+  return solve_sw<NT, NM, 8>(st, lds, d, Tslot, iVb, xs, ls, cs, ra);
 }
 
 hipError_t lag_launch_solve(int NT, int nmax, hipStream_t st, size_t lds, Dims d, const int* Tslot,

@@ -47,6 +47,7 @@ def test_oos_vintage_predictive_density_within_mcse(pkg, ctx, fred):
         n = min(chunk, keep - done)
         ch.sweep(n, store=True)
         fc = ch.get_fcst()
+        ch.get_draws()                                          # drains the draw store for the next chunk
         sc = fc["scores"][:, :, 1, :]                           # Nd x n x B: fcstLogscoreDraws
         dens += np.exp(sc).mean(axis=0).sum(axis=0)
         lsc += sc.mean(axis=0).sum(axis=0)
