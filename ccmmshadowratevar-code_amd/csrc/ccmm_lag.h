@@ -57,7 +57,7 @@ constexpr int kSlThreads = 512;
 __host__ __device__ inline int sl_union(int NT, int TP) { return TP + 512; }
 inline size_t sl_lds_bytes(int NT, int rows, int ldd, int TP, int nmax) {
   const size_t n = (size_t)rows * ldd + sl_union(NT, TP) + 256 + 256 + (size_t)nmax * nmax + 16;
-  return n * sizeof(double) + 16 * NT * sizeof(int);
+  return n * sizeof(double) + (16 * NT + 32) * sizeof(int);  // colmap, then the RO hand-off flags
 }
 
 bool lag_supported_nt(int nt);

@@ -407,13 +407,17 @@ __global__ __launch_bounds__(512, 1) void k_gram_chol_lag(Dims d, const int* __r
 // k_gram_chol_lag (wave W holds slots W + 8k; element (lq + 4r, lr) of slot (ti, tj) =
 // M'_{tj,ti}(lq + 4r, lr), U~_pp^-1 on the diagonal): one coalesced HBM read per system,
 // issued after the v_t loads so that it overlaps the X'v product.
-template <int NT, int NMAX, int SW>
+template <int NT, int NMAX, int SW, bool RO>
 __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __restrict__ Tslot,
                                                               const double* __restrict__ iVb, XSel xs, LagSel ls,
                                                               ChainState cs, RngArgs ra) {
   constexpr int NTILE = gl_ntile(NT);
   constexpr int NTH = 64 * SW;                      // SW waves (8 or 16)
-  constexpr int TPW = (gl_ntile(NT) + SW - 1) / SW;  // factor tiles held per wave
+  // factor tiles held per wave: slots wave + SW k (barrier-stepped substitutions), or with RO (row
+  // ownership) whole block rows, NT tiles per wave: wave 0 row NT - 1, wave w >= 1 rows w - 1 and
+  // NT - 1 - w (NT = 15: sizes w + (15 - w))
+  static_assert(!RO || (SW == 8 && (NT == 1 || NT == 15)), "row-owned substitutions: 8 waves, NT 1 or 15");
+  constexpr int TPW = RO ? NT : (gl_ntile(NT) + SW - 1) / SW;
   constexpr int KL = 16 * NT;
   extern __shared__ double sm[];
   const int N = d.N, TP = d.TP, K = d.K, KP = d.KP;
@@ -426,6 +430,8 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
   double* Al = xl + 256;             // N x N, column stride NMAX
   double* red = Al + NMAX * NMAX;    // 16
   int* cm = reinterpret_cast<int*>(red + 16);  // KL
+  int* zdone = cm + KL;                        // RO: forward, block z_p final
+  int* cnt = zdone + 16;                       // RO: backward, rows p > i pushed into block i
   const int c = blockIdx.x;
   const int s = cs.slot[c];
   const int T = Tslot[s];
@@ -439,12 +445,27 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
   for (int q = tid; q < KL; q += NTH) cm[q] = ls.colmap[q];
   // this wave's slots: (ti, tj) per register tile
   int sti[TPW], stj[TPW];
+  // RO rows: rHi (register tiles 0 .. nHi - 1) and rLo (tiles nHi .. nHi + nLo - 1)
+  const int rHi = NT - 1 - wave, rLo = wave - 1;
+  const bool hasHi = rHi >= 0, hasLo = wave >= 1 && rLo < rHi;
+  const int nHi = hasHi ? rHi + 1 : 0, nLo = hasLo ? rLo + 1 : 0;
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
-    const int gi = wave + SW * k;
-    sti[k] = gi < NTILE ? gl_ti(NT, gi) : 0;
-    stj[k] = gi < NTILE ? gl_tj(NT, gi) : 0;
+    if constexpr (RO) {
+      sti[k] = (k < nHi) ? rHi : rLo;
+      stj[k] = (k < nHi) ? k : k - nHi;
+    } else {
+      const int gi = wave + SW * k;
+      sti[k] = gi < NTILE ? gl_ti(NT, gi) : 0;
+      stj[k] = gi < NTILE ? gl_tj(NT, gi) : 0;
+    }
   }
+  // slot of register tile k, or -1
+  auto slot_of = [&](int k) -> int {
+    if constexpr (RO) return (k < nHi + nLo) ? gl_tile(NT, sti[k], stj[k]) : -1;
+    const int gi = wave + SW * k;
+    return gi < NTILE ? gi : -1;
+  };
   int cur = -1;
 
   for (int j = 0; j < N; ++j) {
@@ -471,20 +492,29 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
         int o = t;
 #pragma unroll
         for (int k = 0; k < NMAX; ++k) {
-          if (k < N) e[k] = (k == j) ? Y[o] : E[o];
+          if (k < N) e[k] = ((k == j) ? Y : E)[o];
           o += TP;
         }
         // A in LDS with the compile-time column stride NMAX (every A(i, k) read is an immediate offset
         // from row i's address); the row loop stays rolled so that only one row of A is in flight
         // (unrolled, the compiler hoisted all N(N+1)/2 entries into registers and spilled)
+        // 1 / sqrtht(t, i)^2 of rows i >= j, fetched four rows ahead through a register queue
+        const double* wt = ih2 + t;
+        double w0 = (j < N) ? wt[j * TP] : 0.0, w1 = (j + 1 < N) ? wt[(j + 1) * TP] : 0.0;
+        double w2 = (j + 2 < N) ? wt[(j + 2) * TP] : 0.0, w3 = (j + 3 < N) ? wt[(j + 3) * TP] : 0.0;
 #pragma unroll 1
         for (int i = j; i < N; ++i) {
+          const double wi = w0;
+          w0 = w1;
+          w1 = w2;
+          w2 = w3;
+          w3 = (i + 4 < N) ? wt[(i + 4) * TP] : 0.0;
           const double* Ai = Al + i;
           double ea = 0.0;
 #pragma unroll
           for (int k = 0; k < NMAX; ++k)
             if (k <= i) ea = fma(e[k], Ai[k * NMAX], ea);
-          acc = fma(Ai[j * NMAX] * ea, ih2[i * TP + t], acc);  // 1 / sqrtht(t, i)^2, rows i >= j
+          acc = fma(Ai[j * NMAX] * ea, wi, acc);
         }
       }
       vl[t] = acc;
@@ -495,8 +525,8 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
     dbl4 lt[TPW];
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {
-      const int gi = wave + SW * k;
-      if (gi < NTILE) {
+      const int gi = slot_of(k);
+      if (gi >= 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) lt[k][r] = Lo[gi * 256 + 64 * r + lane];
       } else {
@@ -557,6 +587,10 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
     //         take M_ip z_p off r~_i, one barrier), and y_p = L~_pp^-1 z_p for all p at once
     if (tid < KL) rl[1 + tid] = fma(-Lv[1 + tid], rl[0] * Lv[0], rl[1 + tid]);
     if (tid == KL) xl[0] = rl[0] * Lv[0];
+    if (RO && tid < 16) {
+      zdone[tid] = 0;
+      cnt[tid] = 0;
+    }
     __syncthreads();
     // slot (ti, tj) times block tj of u, summed over the slot's rows: (M u)_ti (or U^-T u)
     auto colsum = [&](const dbl4& t, const double* u) {
@@ -567,7 +601,51 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       return xsum32(xsum16(v));
     };
     const bool subst = !(ls.mode & 64);
-    for (int p = 0; p < (subst ? NT - 1 : 0); ++p) {
+    // RO hand-offs between waves: LDS flags with workgroup-scope release / acquire, polled with a
+    // bounded spin (a cap that is never expected to be reached ends the wait and flags the chain)
+    bool stuck = false;
+    auto wait_eq = [&](int* f, int v) {
+      for (int it = 0; it < (1 << 22); ++it) {
+        if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == v) return;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      stuck = true;
+    };
+    auto post = [&](int* f, int v) {
+      if (lane == 0) __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    if constexpr (RO) {
+      // rows of L_u: the owner of block row i subtracts M_iq z_q from r~_i in q order as each z_q
+      // is posted (the same sequence of subtractions as the stepped form), posts z_i, and forms
+      // y_i = L~_ii^-1 z_i with its diagonal tile
+      if (subst) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // rLo, then rHi
+          const bool has = h ? hasHi : hasLo;
+          const int row = h ? rHi : rLo, k0 = h ? 0 : nHi;
+          if (has) {
+            double racc = rl[1 + 16 * row + lr];
+#pragma unroll
+            for (int k = 0; k < TPW; ++k) {
+              if (k >= k0 && k <= k0 + row) {
+                const int q = k - k0;
+                if (q < row) {
+                  wait_eq(zdone + q, 1);
+                  racc -= colsum(lt[k], rl + 1 + 16 * q + lq);
+                } else {
+                  if (lq == 0) rl[1 + 16 * row + lr] = racc;
+                  wave_lds_sync();
+                  post(zdone + row, 1);
+                  const double v = colsum(lt[k], rl + 1 + 16 * row + lq);
+                  if (lq == 0) xl[1 + 16 * row + lr] = v;
+                }
+              }
+            }
+          }
+        }
+      }
+    }
+    for (int p = 0; p < ((subst && !RO) ? NT - 1 : 0); ++p) {
 #pragma unroll
       for (int k = 0; k < TPW; ++k) {
         const int gi = wave + SW * k;
@@ -578,7 +656,7 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       }
       __syncthreads();
     }
-    if (subst) {
+    if (subst && !RO) {
 #pragma unroll
       for (int k = 0; k < TPW; ++k) {
         const int gi = wave + SW * k;
@@ -616,15 +694,45 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       if (subst) {
 #pragma unroll
         for (int k = 0; k < TPW; ++k) {
-          const int gi = wave + SW * k;
-          if (gi < NTILE && sti[k] == stj[k]) {
+          const bool diag = RO ? (slot_of(k) >= 0 && sti[k] == stj[k])
+                               : (wave + SW * k < NTILE && sti[k] == stj[k]);
+          if (diag) {
             const double q = fold(lt[k], rl[1 + 16 * sti[k] + lr]);
             if ((lr & 3) == 0) xl[1 + 16 * sti[k] + lq + 4 * (lr >> 2)] = q;
           }
         }
       }
       __syncthreads();
-      for (int p = (subst ? NT - 1 : 0); p >= 1; --p) {
+      if constexpr (RO) {
+        // columns of L_u' by pushes: the owner of block row p waits until the rows below have pushed
+        // into block p (x_p final), then takes M_pi' x_p off w_i for i = p - 1 .. 0, each push in
+        // turn after row p + 1's push into block i (the stepped form's order, p descending)
+        if (subst) {
+#pragma unroll
+          for (int h = 1; h >= 0; --h) {  // rHi, then rLo
+            const bool has = h ? hasHi : hasLo;
+            const int row = h ? rHi : rLo, k0 = h ? 0 : nHi;
+            if (has) {
+              wait_eq(cnt + row, NT - 1 - row);
+              const double xp = xl[1 + 16 * row + lr];
+#pragma unroll
+              for (int k = TPW - 1; k >= 0; --k) {
+                if (k >= k0 && k < k0 + row) {
+                  const int i = k - k0;
+                  const double q = fold(lt[k], xp);
+                  wait_eq(cnt + i, NT - 1 - row);
+                  if ((lr & 3) == 0) xl[1 + 16 * i + lq + 4 * (lr >> 2)] -= q;
+                  wave_lds_sync();
+                  post(cnt + i, NT - row);
+                }
+              }
+            }
+          }
+        }
+        if (stuck && lane == 0) atomicOr(&cs.status[c], 32);
+        __syncthreads();  // every x~ block final before l' x~
+      }
+      for (int p = ((subst && !RO) ? NT - 1 : 0); p >= 1; --p) {
 #pragma unroll
         for (int k = 0; k < TPW; ++k) {
           const int gi = wave + SW * k;
@@ -718,22 +826,26 @@ hipError_t lag_launch_gram(int NT, hipStream_t st, size_t lds, Dims d, const int
 // per SIMD, but 128 registers per lane, which the kernel overflows).  Same arithmetic either way
 // (per-thread v_t and residual rows, per-tile substitution products, the X'v t-halves on threads
 // 0..511).
-template <int NT, int NM, int SW>
+template <int NT, int NM, int SW, bool RO>
 static hipError_t solve_sw(hipStream_t st, size_t lds, Dims d, const int* Tslot, const double* iVb, XSel xs,
                            LagSel ls, ChainState cs, RngArgs ra) {
-  hipError_t e = hipFuncSetAttribute((const void*)k_cta_solve_lag<NT, NM, SW>,
+  hipError_t e = hipFuncSetAttribute((const void*)k_cta_solve_lag<NT, NM, SW, RO>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_cta_solve_lag<NT, NM, SW>), dim3(d.B), dim3(64 * SW), lds, st, d, Tslot, iVb, xs, ls, cs,
-                     ra);
+  hipLaunchKernelGGL((k_cta_solve_lag<NT, NM, SW, RO>), dim3(d.B), dim3(64 * SW), lds, st, d, Tslot, iVb, xs, ls,
+                     cs, ra);
   return hipGetLastError();
 }
 template <int NT, int NM>
 static hipError_t solve_one(hipStream_t st, size_t lds, Dims d, const int* Tslot, const double* iVb, XSel xs,
                             LagSel ls, ChainState cs, RngArgs ra) {
+  // row-owned substitutions with LDS flag hand-offs (default) or the barrier-stepped form
+  // (CCMM_SOLVE_ASYNC=0); CCMM_SOLVE_WAVES=16: the stepped form on sixteen waves
   const char* v = std::getenv("CCMM_SOLVE_WAVES");
-  if (v && std::atoi(v) == 16) return solve_sw<NT, NM, 16>(st, lds, d, Tslot, iVb, xs, ls, cs, ra);
-  return solve_sw<NT, NM, 8>(st, lds, d, Tslot, iVb, xs, ls, cs, ra);
+  const char* a = std::getenv("CCMM_SOLVE_ASYNC");
+  if (v && std::atoi(v) == 16) return solve_sw<NT, NM, 16, false>(st, lds, d, Tslot, iVb, xs, ls, cs, ra);
+  if (a && std::atoi(a) == 0) return solve_sw<NT, NM, 8, false>(st, lds, d, Tslot, iVb, xs, ls, cs, ra);
+  return solve_sw<NT, NM, 8, true>(st, lds, d, Tslot, iVb, xs, ls, cs, ra);
 }
 
 hipError_t lag_launch_solve(int NT, int nmax, hipStream_t st, size_t lds, Dims d, const int* Tslot,

@@ -228,7 +228,8 @@ int ccmm_chains_record_elb_flags(ccmm_chains* ch, int enable);
 int ccmm_chains_get_elb_flags(ccmm_chains* ch, uint8_t* flags);
 /* Per-chain status word since set_state (B ints, OR of: 2 CTA Cholesky, 4 A-step
  * Cholesky, 8 SV sampler, 16 PHI Cholesky found a non-positive pivot; the block
- * then continued with a unit pivot, so the chain's draws are invalid).  A CTA Cholesky
+ * then continued with a unit pivot, so the chain's draws are invalid; 32: a device hand-off
+ * between waves reached its spin cap, never expected).  A CTA Cholesky
  * failure is repaired within the sweep by the host QR branch of CTA.m:80-92, which
  * replaces bit 2 by bit 1 ("QR fallback used", informational: the draws are valid).
  * Returns 1 if any chain carries a bit other than 1, 0 otherwise; the batch driver re-runs
