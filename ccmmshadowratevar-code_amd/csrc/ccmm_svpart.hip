@@ -310,7 +310,9 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
         double x[NN];
 #pragma unroll
         for (int k = 0; k < NN; ++k) {
-          const int ro = sv_after(k * CLD, x[k > 0 ? k - 1 : 0], k > 0);
+          // row k's factor entries are read once x[k - 2] is known, i.e. while row k - 1 is being
+          // solved (one row in flight ahead: the LDS latency leaves the serial chain)
+          const int ro = sv_after(k * CLD, x[k > 1 ? k - 2 : 0], k > 1);
           double v = sgn * rhs[k * NN + rcol];
 #pragma unroll
           for (int m = 0; m < k; ++m) v = fma(-myC[ro + m], x[m], v);
