@@ -42,7 +42,7 @@ extern "C" {
 #define CCMM_OK 0
 #define CCMM_WARN_QR_FALLBACK 1    /* CTA.m:80-92 "switching to QR routine" */
 #define CCMM_WARN_ELBT0 2          /* mcmcVARshadowrateBlockHybrid.m:203-205 */
-#define CCMM_WARN_MVNCDF 3         /* censored log score with >= 4 series at the ELB: MATLAB mvncdf is randomised QMC there, score NaN */
+#define CCMM_WARN_MVNCDF 3         /* censored log score with more than 12 series at the ELB: score NaN (4..12: deterministic lattice estimate inside MATLAB mvncdf's QMC tolerance 1e-4) */
 #define CCMM_ERR_DIM (-1)          /* gibbsdrawShadowrates.m:50-52 "dimension mismatch" */
 #define CCMM_ERR_ARG (-2)          /* invalid argument / unsupported size */
 #define CCMM_ERR_HIP (-3)          /* HIP runtime failure */
@@ -289,8 +289,9 @@ int ccmm_chains_fcst_stored(const ccmm_chains* ch);
  *            fcstYdraws with the yields floored at the ELB, :697-700)
  *   yhatsum  N x H x B  sum of the zero-shock mean paths (linear yhatdraws; zero for bh)
  *   paths, paths_censored  N x H x Nd x M x B (only with keep_paths)
- * Any pointer may be NULL.  Returns CCMM_WARN_MVNCDF when some censored score needed
- * mvncdf in >= 4 dimensions (that score is NaN). */
+ * Any pointer may be NULL.  Censored scores with 4..12 series at the ELB use a deterministic
+ * lattice estimate of mvncdf (MATLAB: randomised QMC, absolute tolerance 1e-4); returns
+ * CCMM_WARN_MVNCDF when some censored score needed mvncdf in more than 12 dimensions (NaN). */
 int ccmm_chains_get_fcst(ccmm_chains* ch, double* scores, double* fYsum, double* fYcsum,
                          double* yhatsum, double* paths, double* paths_censored);
 
@@ -552,7 +553,7 @@ int ccmm_shadowrate_psrf(int M, int Ns, int elbT, int ldT, int C, const double* 
  * Outputs: fcstY, fcstYcensor N x H x Nd x B (fcstYdraws / fcstYcensorDraws),
  *   yhat N x H x B (yhatdraws), scores 4 x Nd x B = (fcstLogscoreDraws,
  *   fcstLogscoreELBdraws, fcstLogscoreXdraws, fcstLogscoreIdraws).
- * Returns CCMM_WARN_MVNCDF when some censored score needed mvncdf in >= 3
+ * Returns CCMM_WARN_MVNCDF when some censored score needed mvncdf in more than 12
  * dimensions (that score is NaN; status[c] bit 1 marks the chain). */
 int ccmm_fcst(ccmm_ctx* ctx, int B, int N, int p, int H, int Nd, const double* PAI,
               const double* invA, const double* logSV0, const double* sqrtPHI,

@@ -12,7 +12,10 @@ PARITY UNPINNED (MATLAB reference, no fixtures).  MATLAB built-ins restated:
 independent adaptive quadrature (scipy.integrate.quad) of the conditional
 univariate / bivariate integrals — MATLAB's own trivariate
 tolerance is 1e-8 absolute.  With 4+ censored series MATLAB switches to a
-randomised quasi-Monte Carlo rule that cannot be matched; the score is NaN.
+randomised quasi-Monte Carlo rule (absolute tolerance 1e-4) that cannot be matched draw for
+draw; the declared convention is a deterministic rank-1 lattice rule inside that tolerance
+(``mvn_lattice_cdf``, the device's rule), itself checked against scipy's randomised Genz
+lattice at 1e-6 (tests/test_oracle_fcst.py).
 """
 from __future__ import annotations
 
@@ -39,8 +42,36 @@ def bvn_cdf(h, k, r):
     return val
 
 
+MVN_PTS = 64 * 1024
+MVN_ALPHA = np.sqrt(np.array([2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31], float))
+
+
+def mvn_lattice_cdf(x, L, npts=MVN_PTS):
+    """P(X <= x), X ~ N(0, L L') (L lower, d = 4..12): Genz's separation of variables on the
+    rank-1 lattice w_q = |2 frac((q + 1) sqrt(prime_i)) - 1|, q = 0..npts-1 (the device's rule,
+    csrc/ccmm_fcst.hip mvn_lattice_cdf; MATLAB mvncdf uses a randomised QMC rule at d >= 4)."""
+    from scipy.special import ndtri
+    x = np.asarray(x, float)
+    d = len(x)
+    e1 = ndtr(x[0] / L[0, 0])
+    if not e1 > 0.0:
+        return 0.0
+    q = np.arange(1, npts + 1, dtype=float)
+    e = np.full(npts, e1)
+    f = e.copy()
+    Y = np.zeros((d, npts))
+    for i in range(1, d):
+        w = q * MVN_ALPHA[i - 1]
+        w = np.abs(2.0 * (w - np.floor(w)) - 1.0)
+        Y[i - 1] = ndtri(np.clip(w * e, 1e-300, 1.0 - 1e-16))
+        e = ndtr((x[i] - L[i, :i] @ Y[:i]) / L[i, i])
+        f = f * e
+    return float(min(1.0, max(0.0, f.mean())))
+
+
 def mvncdf(b, mu, S):
-    """mvncdf(b', mu', S) for dimension 1..3 (MATLAB mvncdf semantics, upper limits)."""
+    """mvncdf(b', mu', S) (MATLAB mvncdf semantics, upper limits): dimension 1..3 by adaptive
+    quadrature, 4..12 by the declared lattice rule (mvn_lattice_cdf)."""
     d = len(b)
     x = (np.asarray(b, float) - np.asarray(mu, float))
     if d == 1:
@@ -64,6 +95,8 @@ def mvncdf(b, mu, S):
         val, _ = integrate.quad(inner, -40.0, x[0] / L[0, 0], epsabs=1e-300, epsrel=1e-11,
                                 limit=400, points=pts or None)
         return val
+    if d <= 12:
+        return mvn_lattice_cdf(x, np.linalg.cholesky(S))
     return float("nan")
 
 

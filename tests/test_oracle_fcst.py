@@ -33,6 +33,22 @@ def test_tvn_cdf_vs_scipy(F):
         assert abs(F.mvncdf(b, mu, S) - want) < 2e-5  # scipy is a randomized QMC rule (~1e-5)
 
 
+@pytest.mark.parametrize("d", [4, 5, 6, 8])
+def test_mvn_lattice_vs_scipy(F, d):
+    """The declared 4+-dimensional mvncdf rule (deterministic rank-1 lattice, the device's) against
+    scipy's randomised Genz lattice at tight tolerance: within 1e-6 absolute (MATLAB mvncdf's own
+    tolerance at d >= 4 is 1e-4)."""
+    rng = np.random.default_rng(3 + d)
+    A = rng.normal(size=(d, d))
+    S = A @ A.T / d + 0.3 * np.eye(d)
+    b = rng.normal(size=d) * 0.8 - 0.3
+    mu = rng.uniform(-0.2, 0.2, d)
+    want = stats.multivariate_normal.cdf(b, mean=mu, cov=S, abseps=1e-10, releps=1e-10, maxpts=2_000_000)
+    got = F.mvncdf(b, mu, S)
+    print(d, got, want)
+    assert abs(got - want) < 1e-6
+
+
 def test_censored_one_at_elb_is_conditional_normal(F):
     """One censored series: llf = log N(y_off) + log Phi((y_at - E[y_at|y_off]) / sd)."""
     rng = np.random.default_rng(1)
