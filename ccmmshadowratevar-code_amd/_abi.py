@@ -111,6 +111,10 @@ _SIGS = {
                                          C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), _dp, _dp, _dp,
                                          _dp, _dp, _dp, C.c_double, C.c_int, C.c_int, _dp, _dp,
                                          C.POINTER(C.c_uint8)]),
+    "ccmm_gibbs_shadowrates_b3": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                            C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), _dp, _dp, _dp, _dp,
+                                            C.c_int, _dp, C.c_double, C.c_int, C.c_int, _dp, _dp,
+                                            C.POINTER(C.c_uint8)]),
     "ccmm_chains_get_status": (C.c_int, [C.c_void_p, _ip]),
     "ccmm_chains_set_fcst": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, C.c_int]),
     "ccmm_chains_set_fcst_slot": (C.c_int, [C.c_void_p, C.c_int, _dp]),
@@ -355,6 +359,32 @@ class Context:
             _ptr(_f(Psi)), _ptr(_f(SVol)), float(elbBound), int(Ndraws), int(burnin),
             _ptr(_f(u)) if u is not None else None, _ptr(out), _ptr(fl, _u8p) if flags else None)
         _check(rc, "ccmm_gibbs_shadowrates")
+        return (out, fl) if flags else out
+
+    def gibbs_shadowrates_b3(self, Y, STATE0, ndxS, sNaN, p, A, Bm, SVol, elbBound, burnin=100, u=None,
+                             Ndraws=1, flags=False, month_varying=None):
+        """gibbsdrawShadowratesB3 (ccmm_gibbs_shadowrates_b3), batched over a trailing chain axis.
+
+        Y Ny x elbT [x B], STATE0 K [x B], ndxS bool Ny, sNaN bool Ns x elbT, A K x K [x B],
+        Bm K x Ny [x B] or, with month_varying (default: Bm.ndim == 4, or 3 with B == 1 and the
+        last axis elbT), K x Ny x elbT [x B]; SVol Ny x elbT [x B]; u Ns x elbT x passes [x B] or None."""
+        Y = _f(Y)
+        Ny, T = Y.shape[:2]
+        B = Y.shape[2] if Y.ndim == 3 else 1
+        Bm = np.asarray(Bm, float)
+        if month_varying is None:
+            month_varying = Bm.ndim == 4 or (Bm.ndim == 3 and B == 1 and Bm.shape[2] == T)
+        nd = np.ascontiguousarray(np.asarray(ndxS, dtype=bool), dtype=np.uint8)
+        sN = np.asfortranarray(np.asarray(sNaN, dtype=bool).astype(np.uint8))
+        Ns = int(sN.shape[0])
+        passes = burnin + Ndraws
+        out = np.zeros((Ns, T, Ndraws, B), order="F")
+        fl = np.zeros((Ns, T, passes, B), dtype=np.uint8, order="F") if flags else None
+        rc = self.lib.ccmm_gibbs_shadowrates_b3(
+            self.handle, B, Ny, T, Ns, int(p), _ptr(nd, _u8p), _ptr(sN, _u8p), _ptr(Y), _ptr(_f(STATE0)),
+            _ptr(_f(A)), _ptr(_f(Bm)), int(bool(month_varying)), _ptr(_f(SVol)), float(elbBound), int(Ndraws),
+            int(burnin), _ptr(_f(u)) if u is not None else None, _ptr(out), _ptr(fl, _u8p) if flags else None)
+        _check(rc, "ccmm_gibbs_shadowrates_b3")
         return (out, fl) if flags else out
 
     def phi_iw(self, eta, sPHI, dPHI, Zdraw=None):

@@ -616,6 +616,8 @@ struct ccmm_chains {
   }
 
   const double* elb_yhat = nullptr;  // ccmm_gibbs_shadowrates: explicit YHAT0
+  int elb_b3 = 0;                    // ccmm_gibbs_shadowrates_b3: no Y0 path, intercept in the state
+  const double* elb_Amon = nullptr;  // ccmm_gibbs_shadowrates_b3: per-month structural matrices
   uint8_t* elb_flags = nullptr;      // drawTruncNormal branch flags of the last ELB step (or nullptr)
   DBuf<uint8_t> dElbFlags;
   ElbDev elb_view() const {
@@ -648,6 +650,8 @@ struct ccmm_chains {
     e.ps = 0;
     e.EtPS = eEtPS.p;
     e.psFlag = nullptr;
+    e.b3 = elb_b3;
+    e.Amon = elb_Amon;
     return e;
   }
 
@@ -2289,11 +2293,13 @@ int ccmm_draw_trunc_normal_batch(ccmm_ctx* ctx, int n, const double* mu, const d
 }
 
 // ------------------------------------------------------------ sweep-level API
-int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p, const uint8_t* ndxS,
-                           const uint8_t* sNaN, const double* Y, const double* STATE0,
-                           const double* YHAT0, const double* C, const double* Psi, const double* SVol,
-                           double elbBound, int Ndraws, int burnin, const double* u, double* out,
-                           uint8_t* flags) {
+// gibbsdrawShadowrates (b3 = 0) and gibbsdrawShadowratesB3 (b3 = 1; Psi K x Ny x elbT per chain when
+// psi3d, else K x Ny) on one chain set holding each call as a data slot
+static int gibbs_shadowrates_impl(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p, const uint8_t* ndxS,
+                                  const uint8_t* sNaN, const double* Y, const double* STATE0,
+                                  const double* YHAT0, const double* C, const double* Psi, const double* SVol,
+                                  double elbBound, int Ndraws, int burnin, const double* u, double* out,
+                                  uint8_t* flags, int b3, int psi3d) {
   return guarded([&] {
     require(ctx && ndxS && sNaN && Y && STATE0 && C && Psi && SVol && out, "null argument");
     require(B >= 1 && Ny >= 1 && Ny <= 128 && p >= 1 && elbT >= 1 && burnin >= 0, "bad size");
@@ -2350,18 +2356,36 @@ int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p
     // state: PAI = C(2:Ny+1, :)' (elb.A rows, :404-407), A = Psi(2:Ny+1, :) \ I, sqrtht = SVol'
     std::vector<double> PAI((size_t)K * Ny * B), A((size_t)Ny * Ny * B, 0.0), sh((size_t)T * Ny * B),
         hh((size_t)T * Ny * B), sq((size_t)Ny * Ny * B, 0.0);
-    for (int c = 0; c < B; ++c) {
-      const double* Cc = C + (size_t)c * KK;
-      const double* Pc = Psi + (size_t)c * K * Ny;
-      for (int i = 0; i < Ny; ++i)
-        for (int k = 0; k < K; ++k) PAI[((size_t)c * Ny + i) * K + k] = Cc[(1 + i) + (size_t)k * K];
-      double* Ac = A.data() + (size_t)c * Ny * Ny;
-      for (int col = 0; col < Ny; ++col)  // forward substitution with the lower triangle of invA
+    // A = Psi(2:Ny+1, :) \ I by forward substitution with the lower triangle (B3 with a 3-D B: per month)
+    auto inv_lower = [&](const double* Pc, double* Ac) {
+      for (int col = 0; col < Ny; ++col)
         for (int r = col; r < Ny; ++r) {
           double v = (r == col) ? 1.0 : 0.0;
           for (int q = col; q < r; ++q) v -= Pc[(1 + r) + (size_t)q * K] * Ac[q + (size_t)col * Ny];
           Ac[r + (size_t)col * Ny] = v / Pc[(1 + r) + (size_t)r * K];
         }
+    };
+    const int nPsi = psi3d ? T : 1;
+    for (int c = 0; c < B; ++c)  // the structural form needs a lower-triangular impact matrix
+      for (int m = 0; m < nPsi; ++m) {
+        const double* Pc = Psi + ((size_t)c * nPsi + m) * K * Ny;
+        for (int col = 1; col < Ny; ++col)
+          for (int r = 0; r < col; ++r)
+            if (Pc[(1 + r) + (size_t)col * K] != 0.0) {
+              g_err = "B(2:Ny+1, :) must be lower triangular";
+              return CCMM_ERR_ARG;
+            }
+      }
+    std::vector<double> Am(psi3d ? (size_t)B * T * Ny * Ny : 0, 0.0);
+    for (int c = 0; c < B; ++c) {
+      const double* Cc = C + (size_t)c * KK;
+      const double* Pc = Psi + (size_t)c * nPsi * K * Ny;
+      for (int i = 0; i < Ny; ++i)
+        for (int k = 0; k < K; ++k) PAI[((size_t)c * Ny + i) * K + k] = Cc[(1 + i) + (size_t)k * K];
+      double* Ac = A.data() + (size_t)c * Ny * Ny;
+      inv_lower(Pc, Ac);
+      for (int m = 0; m < (psi3d ? T : 0); ++m)
+        inv_lower(Pc + (size_t)m * K * Ny, Am.data() + ((size_t)c * T + m) * Ny * Ny);
       for (int i = 0; i < Ny; ++i) {
         sq[(size_t)c * Ny * Ny + i + (size_t)i * Ny] = 1.0;
         for (int t = 0; t < T; ++t) {
@@ -2387,6 +2411,13 @@ int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p
       HIPCHECK(hipMemcpy(dyh.p, yh.data(), yh.size() * sizeof(double), hipMemcpyHostToDevice));
     }
     ch.elb_yhat = dyh.p;
+    ch.elb_b3 = b3;
+    DBuf<double> dAm;
+    if (psi3d) {
+      dAm.alloc(Am.size());
+      HIPCHECK(hipMemcpy(dAm.p, Am.data(), Am.size() * sizeof(double), hipMemcpyHostToDevice));
+      ch.elb_Amon = dAm.p;
+    }
     DBuf<uint8_t> dfl;
     if (flags) {
       dfl.alloc((size_t)B * passes * T * Ns);
@@ -2407,6 +2438,23 @@ int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p
     if (flags) HIPCHECK(hipMemcpy(flags, dfl.p, dfl.n, hipMemcpyDeviceToHost));
     return 0;
   });
+}
+
+int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p, const uint8_t* ndxS,
+                           const uint8_t* sNaN, const double* Y, const double* STATE0,
+                           const double* YHAT0, const double* C, const double* Psi, const double* SVol,
+                           double elbBound, int Ndraws, int burnin, const double* u, double* out,
+                           uint8_t* flags) {
+  return gibbs_shadowrates_impl(ctx, B, Ny, elbT, Ns, p, ndxS, sNaN, Y, STATE0, YHAT0, C, Psi, SVol, elbBound,
+                                Ndraws, burnin, u, out, flags, 0, 0);
+}
+
+int ccmm_gibbs_shadowrates_b3(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p, const uint8_t* ndxS,
+                              const uint8_t* sNaN, const double* Y, const double* STATE0, const double* A,
+                              const double* Bmat, int B3d, const double* SVol, double elbBound, int Ndraws,
+                              int burnin, const double* u, double* out, uint8_t* flags) {
+  return gibbs_shadowrates_impl(ctx, B, Ny, elbT, Ns, p, ndxS, sNaN, Y, STATE0, nullptr, A, Bmat, SVol,
+                                elbBound, Ndraws, burnin, u, out, flags, 1, B3d ? 1 : 0);
 }
 
 ccmm_chains* ccmm_chains_create(ccmm_ctx* ctx, const ccmm_chain_config* cfg) {

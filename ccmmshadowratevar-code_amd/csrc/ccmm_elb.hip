@@ -55,6 +55,11 @@ struct ElbDev {
   int ps;              // 1: k_elb_prep / k_elb_cond also build the PS precision records
   double* EtPS;        // [B][elbTmax][N] residuals of the PS model (Yhatactual as intercept)
   const int* psFlag;   // [B] PS outcome of this sweep: > 0 accepted (k_elb_gibbs skips the chain)
+  // gibbsdrawShadowratesB3 (ccmm_gibbs_shadowrates_b3): the VAR on Y itself with the intercept in the
+  // state (base residuals in the PS model's form, yhat = 0) and, when Amon is set, a structural matrix
+  // per window month, A_tau = B(2:Ny+1, :, tau)^-1 ([B][elbTmax][N][N], lower)
+  int b3;
+  const double* Amon;
 };
 
 // condition record per censored month (doubles):
@@ -169,7 +174,7 @@ __global__ __launch_bounds__(kElbPrepThreads) void k_elb_prep(Dims d, ElbDev e, 
       v -= w;
     }
     Et[q] = v;
-    if (e.ps) {
+    if (e.ps || e.b3) {
       // PS model (mcmcVARshadowrateBlockHybrid.m:423-426): ε_τ = Yb_τ - c - yhat_τ
       //   - Σ_{l<=τ} Φ_l Yb_{τ-l} - Σ_{l>τ} Φ_l w_{τ-l}   (w_{-1-i} = lag block i of elb.X0)
       double u = Z[q] - PAI[(size_t)i * KP] * X0[0];  // Z = Yb - yhat
@@ -182,7 +187,8 @@ __global__ __launch_bounds__(kElbPrepThreads) void k_elb_prep(Dims d, ElbDev e, 
           for (int r = 0; r < N; ++r) u = fma(-ph[(l - 1) * N + r], wl[r], u);
         }
       }
-      e.EtPS[(size_t)c * e.elbTmax * N + q] = u;
+      if (e.ps) e.EtPS[(size_t)c * e.elbTmax * N + q] = u;
+      if (e.b3) Et[q] = u;  // gibbsdrawShadowratesB3.m:178-185: Yhat = C A STATElag, no Y0 path
     }
   }
 }
@@ -250,12 +256,13 @@ __global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState c
     PS[q] = Phi[(size_t)jj * Np + l * N + e.ndxS[b]];
   }
   double* Al = PS + N * p * Ns;
-  if (a_lds)
+  if (a_lds && !e.Amon)
     for (int q = tid; q < N * N; q += nth) Al[q] = Ag[q];
   __syncthreads();
   const double* A = a_lds ? Al : Ag;
-  // ---- Q_0 = Λ_t[S, :], Q_k = B_k' Λ_{t+k};  Λ = A' diag(1/SVol^2) A
+  // ---- Q_0 = Λ_t[S, :], Q_k = B_k' Λ_{t+k};  Λ = A' diag(1/SVol^2) A (B3: A of month t + k)
   for (int k = 0; k <= kmax; ++k) {
+    if (e.Amon) A = e.Amon + ((size_t)c * e.elbTmax + t + k) * N * N;
     for (int i = tid; i < N; i += nth) {
       double w[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
       const double sv = cs.sqrtht[((size_t)c * N + i) * d.TP + T0 + t + k];

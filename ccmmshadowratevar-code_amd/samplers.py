@@ -409,6 +409,20 @@ def CTAsysAswitching(Y, X, N, K, T, A_, Aelb_, atELB, sqrtht, iV, iVb_prior, PAI
     return out[..., 0]
 
 
+def gibbsdrawShadowratesB3(Y, STATE0, ndxS, sNaN, p, A, B, SVol, elbBound, Ndraws=1, burnin=0, rndStream=None,
+                           *, device=0):
+    """gibbsdrawShadowratesB3.m:1 signature (12 arguments): Y Ny x T, STATE0 K, ndxS logical Ny, sNaN
+    Ns x T, A K x K, B K x Ny or K x Ny x T (month-varying, :49-51), SVol Ny x T; rndStream: the
+    uniforms rand(Ns, T, burnin + Ndraws) (:163) or None (Philox).  Returns Ns x T x Ndraws."""
+    B = np.asarray(B, float)
+    u = None if rndStream is None else np.asarray(rndStream, float)[..., None]
+    out = context(device).gibbs_shadowrates_b3(np.asarray(Y, float)[..., None], np.asarray(STATE0, float)[:, None],
+                                               ndxS, sNaN, p, np.asarray(A, float)[..., None], B[..., None],
+                                               np.asarray(SVol, float)[..., None], elbBound, burnin=burnin,
+                                               u=u, Ndraws=Ndraws, month_varying=B.ndim == 3)
+    return out[..., 0]
+
+
 def drawTruncNormal(mu, sqrtVCV, elb, u):
     """drawTruncNormal.m:1 with the numeric-uniform form of the stream argument."""
     v, _ = _abi.draw_trunc_normal(mu, sqrtVCV, elb, u)

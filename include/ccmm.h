@@ -163,6 +163,21 @@ int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p
                            double elbBound, int Ndraws, int burnin, const double* u, double* out,
                            uint8_t* flags);
 
+/* gibbsdrawShadowratesB3 (gibbsdrawShadowratesB3.m:1-231, the 12-argument signature
+ * (Y, STATE0, ndxS, sNaN, p, A, B, SVol, elbBound, Ndraws, burnin, rndStream)), batched over B calls:
+ * the same Gibbs passes with the VAR run on Y itself (intercept in the state, STATElag starting at
+ * STATE0, no deterministic Y0 path: :171-185) and an impact matrix that may vary by month.
+ *   A      K x K x B (the companion with intercept)
+ *   Bmat   K x Ny x elbT x B when B3d != 0 (B(:,:,t), :49-62), else K x Ny x B (repeated over t);
+ *          rows 2..Ny+1 must be lower triangular (every caller's B = invA); CCMM_ERR_ARG otherwise
+ * The other arguments as ccmm_gibbs_shadowrates (no YHAT0).  The reference's only caller
+ * (mcmcVARshadowrateBlockHybridAelb.m:451-452, 469-470) passes 13 arguments to this 12-parameter
+ * function and cannot run as shipped; this entry serves the function itself. */
+int ccmm_gibbs_shadowrates_b3(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p, const uint8_t* ndxS,
+                              const uint8_t* sNaN, const double* Y, const double* STATE0, const double* A,
+                              const double* Bmat, int B3d, const double* SVol, double elbBound, int Ndraws,
+                              int burnin, const double* u, double* out, uint8_t* flags);
+
 /* One draw from N(mu, sig^2) truncated to (-inf, elb] by inverse CDF
  * (drawTruncNormal.m:31-86) with a pre-drawn uniform u (the numeric-stream
  * form of drawTruncNormal.m:47-48).  flags (may be NULL): bit0 = |sig| > 1e-10

@@ -770,3 +770,111 @@ def gibbsdraw_shadowrates(Y, STATE0, YHAT0, ndxS, sNaN, p, C, Psi, SVol, elbBoun
     if return_flags:
         return draws, flags
     return draws
+
+
+# --------------------------------------------------------------------------
+# gibbsdrawShadowratesB3 (gibbsdrawShadowratesB3.m:1-231) as written
+# --------------------------------------------------------------------------
+def gibbsdraw_shadowrates_b3(Y, STATE0, ndxS, sNaN, p, A, B, SVol, elbBound, Ndraws, burnin, udraws,
+                             return_flags=False):
+    """The B3 variant of gibbsdrawShadowrates: the impact matrix B may vary by month (K x Ny x T, or
+    K x Ny repeated, :49-51), the VAR runs on Y itself with the intercept in the state (STATElag
+    starts at STATE0, :171; Yhat = C A STATElag, :178; no Y0 path).  Y Ny x T; STATE0 K; ndxS bool
+    Ny; sNaN bool Ns x T; A K x K; SVol Ny x T; udraws Ns x T x (burnin + Ndraws)."""
+    Y = np.array(Y, dtype=float, copy=True)
+    Ny, T = Y.shape
+    ndxS = np.asarray(ndxS, dtype=bool)
+    ndxX = ~ndxS
+    S = Y[ndxS, :].copy()
+    Ns = int(ndxS.sum())
+    draws = np.full((Ns, T, Ndraws), np.nan)
+    Nstate = Ny * p
+    Nx = Ny - Ns
+    B = np.asarray(B, float)
+    if B.ndim == 2:  # :49-51
+        B = np.repeat(B[:, :, None], T, axis=2)
+    Nw = B.shape[1]
+    if Nw != Ny:
+        raise ValueError("dimension mismatch")
+    Bsvol = np.einsum("ijt,jt->ijt", B[1:1 + Ny, :, :], SVol)  # bb(:,:,t) * diag(SVol(:,t)), :58-62
+    J = np.full((Ns, Nstate + Nx, T), np.nan)
+    sqrtOm = np.full((Ns, Ns, T), np.nan)
+    aa = A[1:, 1:]
+    Ap = np.empty((Nstate, Nstate, p + 1))
+    Ap[:, :, 0] = np.eye(Nstate)
+    for k in range(p):
+        Ap[:, :, k + 1] = aa @ Ap[:, :, k]
+    Ap = Ap[:, :Ny, :]
+    t = 0
+    for t in range(1, T - p + 1):  # :79-100
+        if sNaN[:, t - 1].any():
+            M = np.zeros((Nstate + Nw, Nw * (p + 1)))
+            for j in range(p + 1):
+                M[:Nstate, Nw * j:Nw * (j + 1)] = Ap[:, :, p - j] @ Bsvol[:, :, t - 1 + j]
+            M[Nstate:Nstate + Nx, :Nw] = Bsvol[ndxX, :, t - 1]
+            M[Nstate + Nx:, :Nw] = Bsvol[ndxS, :, t - 1]
+            R = np.linalg.qr(M.T, mode="r").T
+            n1 = Nstate + Nx
+            J[:, :, t - 1] = solve_triangular(R[:n1, :n1].T, R[n1:n1 + Ns, :n1].T, lower=False).T
+            sqrtOm[:, :, t - 1] = R[n1:n1 + Ns, n1:n1 + Ns]
+    if T - p < 1:
+        t = 0
+    while t < T:  # :106-132
+        t += 1
+        if sNaN[:, t - 1].any():
+            k = T - t
+            Nsig = Ny * k + Nx
+            M = np.zeros((Nsig + Ns, Nsig + Ns))
+            for j in range(k + 1):
+                M[:Nsig, Nw * j:Nw * (j + 1)] = Ap[:Nsig, :, k - j] @ Bsvol[:, :, t - 1 + j]
+            M[k * Ny:k * Ny + Nx, :Nw] = Bsvol[ndxX, :, t - 1]
+            M[Nsig:, :Nw] = Bsvol[ndxS, :, t - 1]
+            R = np.linalg.qr(M.T, mode="r").T
+            J[:, :, t - 1] = 0.0
+            J[:, Ny * (p - k):, t - 1] = solve_triangular(R[:Nsig, :Nsig].T, R[Nsig:Nsig + Ns, :Nsig].T,
+                                                          lower=False).T
+            sqrtOm[:, :, t - 1] = R[Nsig:Nsig + Ns, Nsig:Nsig + Ns]
+    if Ns > 1:  # :135-150
+        sqrtOm1 = np.full((Ns, T), np.nan)
+        beta1 = np.full((Ns, Ns - 1, T), np.nan)
+        for t in range(T):
+            if sNaN[:, t].any():
+                vcv = sqrtOm[:, :, t] @ sqrtOm[:, :, t].T
+                for s in range(Ns):
+                    o = np.arange(Ns) != s
+                    b = np.linalg.solve(vcv[np.ix_(o, o)].T, vcv[s, o])
+                    beta1[s, :, t] = b
+                    sqrtOm1[s, t] = math.sqrt(vcv[s, s] - b @ vcv[o, s])
+    CAA = A[1:1 + Ny, :]                                  # C * A, :153
+    AApp1 = np.linalg.matrix_power(A, p + 1)[1:, :]       # :154-155
+    total = burnin + Ndraws
+    flags = np.zeros((Ns, T, total), dtype=np.uint8)
+    for n in range(total):                                # :168-229
+        STATElag = np.array(STATE0, dtype=float, copy=True)
+        YY = np.hstack([Y, np.zeros((Ny, p))])
+        for t in range(T):
+            if sNaN[:, t].any():
+                Yhat = CAA @ STATElag
+                Xresid = Y[ndxX, t] - Yhat[ndxX]
+                Shat = Yhat[ndxS]
+                STATEtilde = YY[:, t + p:t:-1].ravel(order="F") - AApp1 @ STATElag
+                Spost = Shat + J[:, :, t] @ np.concatenate([STATEtilde, Xresid])
+                if Ns == 1:
+                    S[0, t], flags[0, t, n] = draw_trunc_normal(Spost[0], sqrtOm[0, 0, t], elbBound,
+                                                                udraws[0, t, n])
+                else:
+                    for s in np.nonzero(sNaN[:, t])[0]:
+                        o = np.arange(Ns) != s
+                        mu = Spost[s] + beta1[s, :, t] @ (S[o, t] - Spost[o])
+                        S[s, t], flags[s, t, n] = draw_trunc_normal(mu, sqrtOm1[s, t], elbBound,
+                                                                    udraws[s, t, n])
+                Y[ndxS, t] = S[:, t]
+            if t + 1 >= p:                                # :213-221
+                STATElag[1:] = Y[:, t - p + 1:t + 1][:, ::-1].ravel(order="F")
+            else:
+                STATElag = np.concatenate([[1.0], Y[:, t], STATElag[1:1 + Ny * (p - 1)]])
+        if n >= burnin:
+            draws[:, :, n - burnin] = S
+    if return_flags:
+        return draws, flags
+    return draws
