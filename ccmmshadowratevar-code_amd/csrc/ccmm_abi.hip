@@ -556,6 +556,9 @@ struct ccmm_chains {
   // k_elb_gibbs_oct (eight passes in flight in one wave) from B >= kElbOctMinB; CCMM_ELB_OCT=0 never,
   // 2 always
   int elb_oct = std::getenv("CCMM_ELB_OCT") ? std::atoi(std::getenv("CCMM_ELB_OCT")) : 1;
+  // k_elb_gibbs_wf with per-wave LDS progress flags instead of a barrier per step (CCMM_ELB_ASYNC=0:
+  // the lock-step form)
+  int elb_async = std::getenv("CCMM_ELB_ASYNC") ? std::atoi(std::getenv("CCMM_ELB_ASYNC")) : 1;
   // passes of the ELB step in flight (k_elb_gibbs_wf): 1 (sequential k_elb_gibbs), 4 or 8
   int elb_waves = [] {
     const char* v = std::getenv("CCMM_ELB_WAVES");
@@ -1486,12 +1489,19 @@ struct ccmm_chains {
       });
     } else
     launch(KID_ELBGIBBS, [&] {
-#define GIBBS_K(NS, WW)                                                                                     \
+#define GIBBS_KA(NS, WW, AS)                                                                                \
   do {                                                                                                      \
-    HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs_wf<NS, WW>,                                       \
+    HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs_wf<NS, WW, AS>,                                   \
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gibbs));              \
-    hipLaunchKernelGGL((k_elb_gibbs_wf<NS, WW>), dim3(d.B), dim3(64 * WW), lds_gibbs, ctx->stream, d, e, cs, \
-                       ra);                                                                                 \
+    hipLaunchKernelGGL((k_elb_gibbs_wf<NS, WW, AS>), dim3(d.B), dim3(64 * WW), lds_gibbs, ctx->stream, d, e, \
+                       cs, ra);                                                                             \
+  } while (0)
+#define GIBBS_K(NS, WW)            \
+  do {                             \
+    if (elb_async)                 \
+      GIBBS_KA(NS, WW, true);      \
+    else                           \
+      GIBBS_KA(NS, WW, false);     \
   } while (0)
 #define CASE_NS(NS)                                                                            \
   case NS:                                                                                     \
@@ -1516,6 +1526,7 @@ struct ccmm_chains {
       }
 #undef CASE_NS
 #undef GIBBS_K
+#undef GIBBS_KA
     });
     const int nrb = e.elbTmax * Ns * (p + 1);
     launch(KID_ELBREBUILD, [&] {

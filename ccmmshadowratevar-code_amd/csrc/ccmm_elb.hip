@@ -644,7 +644,12 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
 // wave reads only what its predecessor published before the last barrier.  Within a step
 // the active months of different passes are more than p calendar months apart, so their
 // reads and writes of Sl never overlap.
-template <int NS, int W>
+//
+// ASYNC: no per-step barrier.  Each wave runs its passes month by month, waits (acquire) until its
+// predecessor's published progress covers reach(i), draws, and publishes (release) its own; a wave
+// with less work in a month (fewer censored series) no longer waits for the slowest wave of the step.
+// The reads and writes are those of the lock-step form, so the draws stay bit-identical.
+template <int NS, int W, bool ASYNC>
 __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, ChainState cs, RngArgs ra) {
   extern __shared__ double sm[];
   const int c = blockIdx.x;
@@ -723,6 +728,68 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
   Rec rc, rn;
   load_rec(0, rc);
   int tm = Tm[0];
+  if constexpr (ASYNC) {
+    // one month of pass n (the same draw code as the lock-step body below)
+    const int pred = (wave + W - 1) % W;
+    bool stuck = false;
+    for (; n < P && !stuck; n += W) {
+      uniforms(n);
+      for (i = 0; i < nc; ++i) {
+        if (n > 0) {
+          const int need = (n - 1) * nc + reach[i] + 1;
+          int it = 0;
+          while (__hip_atomic_load(&prog[pred], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++it > (1 << 24)) {
+              stuck = true;
+              break;
+            }
+          }
+          if (stuck) break;
+        }
+        const int ni = (i + 1 < nc) ? i + 1 : 0;
+        load_rec(ni, rn);  // next month of this wave (month 0 of its next pass after the last)
+        const int tmn = Tm[ni];
+        const int t = tm & 0xffff, msk = tm >> 16;
+        double u[NS];
+        for (int a = 0; a < NS; ++a) u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
+        const int tn0 = t + off0, tn1 = t + off1;
+        const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
+        const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
+        double sp[NS];
+        for (int a = 0; a < NS; ++a) sp[a] = fma(h0 ? rc.g0[a] : 0.0, v0, (h1 ? rc.g1[a] : 0.0) * v1);
+        for (int a = 0; a < NS; ++a) sp[a] = rc.hd[a] + wave_sum_dpp(sp[a]);
+        const double* beta = rc.hd + NS;
+        const double* so = beta + NS * (NS - 1);
+        double cur[NS];
+        for (int a = 0; a < NS; ++a) cur[a] = Sl[t * NS + a];
+        for (int a = 0; a < NS; ++a) {
+          if (!((msk >> a) & 1)) continue;
+          double mu = sp[a];
+          int y = 0;
+          for (int b = 0; b < NS; ++b) {
+            if (b == a) continue;
+            mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
+            ++y;
+          }
+          uint8_t fl = 0;
+          cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a], fl);
+          if (e.flags && lane == 0)
+            e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
+        }
+        for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
+        rc = rn;
+        tm = tmn;
+        if (lane == 0)
+          __hip_atomic_store(&prog[wave], n * nc + i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    if (lane == 0) __hip_atomic_store(&prog[wave], done_all, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (stuck && lane == 0) atomicOr(&cs.status[c], 32);
+    __syncthreads();
+    for (int q = tid; q < T * NS; q += 64 * W) Sc[q] = Sl[q];
+    return;
+  }
   for (int step = 0;; ++step) {
     const int* prd = prog + ((step + 1) & 1) * W;  // published before the last barrier
     int* pwr = prog + (step & 1) * W;

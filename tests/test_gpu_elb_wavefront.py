@@ -1,5 +1,5 @@
 """The wavefront schedules of the ELB Gibbs passes (k_elb_gibbs_wf: up to 8 passes of
-gibbsdrawShadowrates.m in flight, one wave each; k_elb_gibbs_oct: 8 passes in flight in one wave,
+gibbsdrawShadowrates.m in flight, one wave each, in lock-step or with per-wave progress flags; k_elb_gibbs_oct: 8 passes in flight in one wave,
 eight lanes each) reproduce the sequential kernel (k_elb_gibbs, CCMM_ELB_WAVES=1) bit for bit: shadow rates, every drawTruncNormal branch flag
 and the whole chain state after several block-hybrid sweeps on the reference's data
 (fredblockMD20-2022-09, ELB 0.25, 2022-08 jump-off: 109 censored months), with Philox draws
@@ -16,9 +16,10 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 
-def _run(pkg, fred, waves, thisT, B=8, sweeps=3, oct_=0):
+def _run(pkg, fred, waves, thisT, B=8, sweeps=3, oct_=0, async_=1):
     os.environ["CCMM_ELB_WAVES"] = str(waves)
     os.environ["CCMM_ELB_OCT"] = str(oct_)
+    os.environ["CCMM_ELB_ASYNC"] = str(async_)
     try:
         mpm = pkg.model.setMinnesotaMean(fred["ncode"])
         ndxS, ndxO, _ = pkg.model.setShadowYields(fred["ncode"], 0.25)
@@ -45,6 +46,7 @@ def _run(pkg, fred, waves, thisT, B=8, sweeps=3, oct_=0):
     finally:
         os.environ.pop("CCMM_ELB_WAVES", None)
         os.environ.pop("CCMM_ELB_OCT", None)
+        os.environ.pop("CCMM_ELB_ASYNC", None)
 
 
 @pytest.mark.parametrize("jump", ["last", "2012-06"])
@@ -55,10 +57,12 @@ def test_wavefront_equals_sequential(pkg, fred, jump):
     ref, elbT = _run(pkg, fred, 1, thisT)
     assert not np.any(ref["status"] & ~1)
     for w in (4, 8):
-        got, _ = _run(pkg, fred, w, thisT)
-        for k in ref:
-            np.testing.assert_array_equal(got[k], ref[k], err_msg=f"waves={w} {k}")
-    print(f"{jump}: elbT {elbT}, {int(np.count_nonzero(ref['flags']))} flagged draws, identical for 4 and 8 waves")
+        for asy in (0, 1):  # lock-step barriers / per-wave progress flags
+            got, _ = _run(pkg, fred, w, thisT, async_=asy)
+            for k in ref:
+                np.testing.assert_array_equal(got[k], ref[k], err_msg=f"waves={w} async={asy} {k}")
+    print(f"{jump}: elbT {elbT}, {int(np.count_nonzero(ref['flags']))} flagged draws, identical for 4 and 8 waves, "
+          "lock-step and asynchronous")
 
 
 @pytest.mark.parametrize("jump,B", [("last", 19), ("2012-06", 8)])
