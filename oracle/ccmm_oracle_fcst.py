@@ -134,10 +134,12 @@ def logscore_gaussian_censored(mu, sqrtOmega, y, elb, censorable=None):
         llf1 = 0.0
         y21 = muAt
     L22 = L[Noff:, Noff:]
+    # MATLAB's log: log(0) = -Inf (a probability that underflows)
+    mlog = lambda v: math.log(v) if v > 0.0 else -math.inf
     if Nat == 1:
-        llf2 = math.log(ndtr((yAt[0] - y21[0]) / L22[0, 0]))
+        llf2 = mlog(ndtr((yAt[0] - y21[0]) / L22[0, 0]))
     else:
-        llf2 = math.log(mvncdf(yAt, y21, L22 @ L22.T))
+        llf2 = mlog(mvncdf(yAt, y21, L22 @ L22.T))
     return llf1 + llf2
 
 
