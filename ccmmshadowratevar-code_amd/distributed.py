@@ -35,16 +35,25 @@ def world_from_env() -> World:
                  int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def unit_cost(T, K, N, n_cens=0, Nstate=None, Ny=None, passes=101):
-    """Relative per-chain sweep cost of one vintage:
-    F_CTA = N [T K (K+1) + K^3/3] plus the ELB setup n_cens (4/3)(Nstate+Ny)^3
-    and the ELB pass traffic (as flop-equivalents at the fp64/HBM ridge)."""
-    f = N * (T * K * (K + 1) + K ** 3 / 3.0)
+# Measured per-vintage cost of the OOS run (tools/calibrate_lpt.py on one MI355X, one chain per vintage
+# alone, 500 Gibbs + 500 PS + 1000 kept sweeps; profiles/r04s_lpt_calibration.json): seconds of a full
+# run = a T + e n_cens at N = 20, K = 241 (NNLS fit over 15 vintages, max relative residual 0.14; the
+# wavefront-step term of the fit came out zero: the ELB passes scale with the censored months).
+LPT_COEF = {"a_per_T": 0.017482263240311456, "e_per_cens_month": 0.06402049319623504}
+
+
+def unit_cost(T, K, N, n_cens=0, Nstate=None, Ny=None, passes=101, coef=None):
+    """Per-chain cost of one vintage for the LPT assignment, calibrated on the device:
+    the measured per-T term (CTA, SV, A-step: per-chain latency kernels, scaled by the CTA work
+    N K^2 relative to the calibration system) plus the measured per-censored-month term of the
+    ELB step (scaled by the passes and the state size relative to the calibration)."""
+    c = LPT_COEF if coef is None else coef
+    scale_t = (N * K * K) / (20.0 * 241.0 * 241.0)
+    f = c["a_per_T"] * T * scale_t
     if n_cens:
         Nstate = N * 12 if Nstate is None else Nstate
         Ny = N if Ny is None else Ny
-        f += n_cens * (4.0 / 3.0) * (Nstate + Ny) ** 3
-        f += passes * n_cens * (Nstate + Ny) * 8 * 10.0
+        f += c["e_per_cens_month"] * n_cens * (passes / 101.0) * ((Nstate + Ny) / 260.0)
     return float(f)
 
 
