@@ -264,10 +264,13 @@ def main():
                 "SQ_INSTS_VALU_MFMA_MOPS_F64": int(pk.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0)),
                 "GRBM_GUI_ACTIVE": int(pk.get("GRBM_GUI_ACTIVE", 0)),
                 "source": pmc_src}
-        # streamed (HBM-roofline) kernels: algorithmic bytes per launch / launch time
-        # (B_SV = 33*T*N bytes per chain-sweep for the SV block)
+        # streamed (HBM-roofline) kernels: algorithmic bytes per launch / launch time, each kernel's own
+        # inputs and outputs per chain-sweep: k_sv_mix reads logy2 and writes the mixture observation,
+        # inverse variance (doubles) and indicator (int8) = 25 T N bytes; k_sv_part reads those two
+        # doubles and writes h, sqrtht and the shocks = 40 T N bytes (SURVEY §8d's B_SV = 33 T N counts
+        # the SV block's external I/O only)
         hb = {}
-        for kn, nbytes in (("k_sv_part", B * 33 * T * N), ("k_sv_mix", B * 33 * T * N)):
+        for kn, nbytes in (("k_sv_part", B * 40 * T * N), ("k_sv_mix", B * 25 * T * N)):
             if ktimes.get(kn, (0, 0))[1]:
                 ms = ktimes[kn][0] / ktimes[kn][1]
                 gbs = nbytes / (ms * 1e-3) / 1e9

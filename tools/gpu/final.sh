@@ -4,7 +4,7 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${TAG:-r04}
-timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -s -rf \
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -s -rf \
   > gpurun_out/gpu_tests_$TAG.log 2>&1 &&
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke_$TAG.log 2>&1 &&
 rm -rf gpurun_out/prof_main_$TAG &&
