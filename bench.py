@@ -65,11 +65,11 @@ def parse():
     ap.add_argument("--s120-steps", type=int, default=2,
                     help="timed sweeps of the S120 stress line (configs[4], N=120); 0 = skip")
     ap.add_argument("--s120-warmup", type=int, default=1)
-    ap.add_argument("--s120-chains", default="96",
-                    help="chains per GPU of the S120 lines (96: ~200 GB of the 288 GB HBM for the 120 "
-                         "factored 1472 x 1472 systems per chain; 64 / 96 / 112 chains measured 91.4 / 99.2 / "
-                         "102.6 sweeps/s, profiles/r03i_s120_chains.json)")
-    ap.add_argument("--s120-groups", type=int, default=2,
+    ap.add_argument("--s120-chains", default="112",
+                    help="chains per GPU of the S120 lines (112: ~245 GB of the 288 GB HBM for the 120 "
+                         "factored 1472 x 1472 systems per chain; (chains, groups) = (96, 1) / (96, 3) / (112, 2) / "
+                         "(112, 4) measured 98.7 / 101.8 / 103.9 / 105.1 sweeps/s, profiles/r04u_s120_configs.json)")
+    ap.add_argument("--s120-groups", type=int, default=4,
                     help="chain groups (HIP streams driven from host threads) of the S120 lines")
     ap.add_argument("--s120-only", action="store_true", help="run only the S120 lines (probe)")
     ap.add_argument("--girf-draws", type=int, default=256,
