@@ -28,6 +28,9 @@
 // 1 / C_ii (only reciprocals are used in the substitutions).
 #include "ccmm_svpart.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace ccmm {
 
 __host__ __device__ inline int sv_nseg(int T) {
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
                                                       const double* __restrict__ V0inv,
                                                       const double* __restrict__ V0invm, ChainState cs,
                                                       RngArgs ra, double* __restrict__ sepbuf,
-                                                      double* __restrict__ gbuf, int mode) {
+                                                      double* __restrict__ gbuf, int mode, int nwg) {
   constexpr int CLD = NN + 1, XLD = 2 * NN + 1, NN2 = NN * NN;
   constexpr bool G3 = 3 * NN <= 64;
   using R = SvRec<NN>;
@@ -154,6 +157,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   lds_f64* myD = myF + NN2;
   const int n = d.N, TP = d.TP;
   const int c = blockIdx.x, s = cs.slot[c], T = Tslot[s];
+  const int wg = blockIdx.y;  // segment group of the chain (nwg > 1: phases A and C split over WGs)
   const int ln = lane < NN ? lane : 0;
   const bool real = lane < n;
   const double* sq = cs.sqrtPHI + (size_t)c * n * n;  // column-major lower n x n
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
   // ---------------------------------------------------------------- phase A: segments
   // per-wave LDS: myF[k*NN + r] fill column r of M_{t,left} (right-hand side of lane NN+r),
   // myD[r*NN + m] the left separator's accumulated -sum X2'X2 (row r)
-  for (int q = wave; q < ((mode & 1) ? 0 : P); q += NW) {
+  for (int q = wave + NW * wg; q < ((mode & 1) ? 0 : P); q += NW * nwg) {
     const int first = (q == 0) ? 0 : sv_sep(q - 1, T, P) + 1;
     const int last = (q == P - 1) ? T : sv_sep(q, T, P) - 1;
     const bool hasL = q > 0, hasR = q < P - 1;
@@ -529,7 +533,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
     }
   }
   __syncthreads();
-  for (int q = wave; q < ((mode & 8) ? 0 : P); q += NW) {
+  for (int q = wave + NW * wg; q < ((mode & 8) ? 0 : P); q += NW * nwg) {
     const int first = (q == 0) ? 0 : sv_sep(q - 1, T, P) + 1;
     const int last = (q == P - 1) ? T : sv_sep(q, T, P) - 1;
     const bool hasL = q > 0, hasR = q < P - 1;
@@ -602,7 +606,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
     }
   }
   // padding beyond T
-  for (int e = tid; e < n * (TP - T); e += 64 * NW) {
+  for (int e = wg == 0 ? tid : n * (TP - T); e < n * (TP - T); e += 64 * NW) {
     const int r = e / (TP - T), t = T + e % (TP - T);
     hout[(size_t)r * TP + t] = 0.0;
     eta[(size_t)r * TP + t] = 0.0;
@@ -635,8 +639,21 @@ static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_sv_normals, dim3(((d.TP + 1) * d.N + 255) / 256, d.B), dim3(256), 0, st, d, Tslot, cs, ra,
                      gbuf, NN);
-  hipLaunchKernelGGL((k_sv_part<NN, NW, PACK>), dim3(d.B), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm, cs,
-                     ra, sep, gbuf, mode);
+  // small batches (B <= 128, e.g. the OOS chains of one vintage): the segments of phases A and C
+  // are spread over nwg = 2 workgroups per chain (16 segments = one per wave), as two launches:
+  // phase A, then phases B + C, in which every workgroup of the chain redoes the serial
+  // separator pass (identical values and stores) instead of a third launch; same draws
+  int nwg = d.B <= 128 ? 2 : 1;
+  if (const char* ev = std::getenv("CCMM_SV_NWG")) nwg = std::max(1, std::min(2, std::atoi(ev)));
+  if (nwg == 1) {
+    hipLaunchKernelGGL((k_sv_part<NN, NW, PACK>), dim3(d.B), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm, cs,
+                       ra, sep, gbuf, mode, 1);
+  } else {
+    hipLaunchKernelGGL((k_sv_part<NN, NW, PACK>), dim3(d.B, nwg), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm,
+                       cs, ra, sep, gbuf, mode | 2 | 4 | 8, nwg);
+    hipLaunchKernelGGL((k_sv_part<NN, NW, PACK>), dim3(d.B, nwg), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm,
+                       cs, ra, sep, gbuf, mode | 1, nwg);
+  }
   return hipGetLastError();
 }
 

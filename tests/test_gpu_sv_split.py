@@ -1,0 +1,43 @@
+"""The partitioned SV smoother split over two workgroups per chain (default for B <= 128:
+phase A over 2 x 8 waves, then phases B + C with the serial separator pass redone by each
+workgroup) against the one-workgroup launch (CCMM_SV_NWG=1): the same segments, separators
+and operation order, so h, eta, sqrtht and the whole chain state agree bit for bit after
+several real-data linear sweeps (fredblockMD20-2022-09, N = 20, p = 12; Philox draws).
+T = 750 has 16 segments (one per wave of the pair); the short sample (T = 72) has 9, so
+the second workgroup runs one segment besides its copy of the separator pass."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(pkg, fred, nwg, thisT, B=6, sweeps=3):
+    os.environ["CCMM_SV_NWG"] = str(nwg)
+    try:
+        mpm = pkg.model.setMinnesotaMean(fred["ncode"])
+        m = pkg.model.build_var(thisT, 12, 12, fred["data"], fred["ydates"], mpm, True)
+        ctx = pkg.Context(0)
+        ch = pkg.Chains(ctx, N=m.N, p=12, T=m.T, B=B, crn=False, seed=7)
+        ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+        st = pkg.model.initial_state(m, B)
+        ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+        ch.sweep(sweeps)
+        out = dict(ch.get_state())
+        out["status"] = ch.get_status()
+        ch.close()
+        return out
+    finally:
+        os.environ.pop("CCMM_SV_NWG", None)
+
+
+@pytest.mark.parametrize("short", [False, True])
+def test_sv_two_workgroups_bit_identical(pkg, fred, short):
+    thisT = 12 + 12 + 60 if short else len(fred["ydates"])
+    ref = _run(pkg, fred, 1, thisT)
+    got = _run(pkg, fred, 2, thisT)
+    assert not np.any(ref["status"])
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    print("SV nwg=2 == nwg=1 over", sorted(ref), "T =", thisT)
