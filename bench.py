@@ -68,8 +68,9 @@ def parse():
     ap.add_argument("--s120-chains", default="112",
                     help="chains per GPU of the S120 lines (112: ~245 GB of the 288 GB HBM for the 120 "
                          "factored 1472 x 1472 systems per chain; (chains, groups) = (96, 1) / (96, 3) / (112, 2) / "
-                         "(112, 4) measured 98.7 / 101.8 / 103.9 / 105.1 sweeps/s, profiles/r04u_s120_configs.json)")
-    ap.add_argument("--s120-groups", type=int, default=4,
+                         "(112, 4) measured 98.7 / 101.8 / 103.9 / 105.1 sweeps/s standalone, profiles/r04u_s120_configs.json; inside "
+                         "the full bench run (112, 4) fell to 89.4 while (112, 2) holds 104.3, profiles/r04z_*)")
+    ap.add_argument("--s120-groups", type=int, default=2,
                     help="chain groups (HIP streams driven from host threads) of the S120 lines")
     ap.add_argument("--s120-only", action="store_true", help="run only the S120 lines (probe)")
     ap.add_argument("--girf-draws", type=int, default=256,
