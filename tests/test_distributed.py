@@ -126,3 +126,20 @@ def test_gloo_world2_govar_batch():
         assert yh == [40.0, 45.0, 50.0, 55.0, 58.0]
     x = _fake_vintage(40, None, 1012023)[0]
     assert abs(ref["fcstYmvlogscore"][0] - np.log(np.mean(np.exp(x)))) < 1e-10
+
+
+def test_lpt_cost_model_matches_device_calibration(pkg):
+    """distributed.unit_cost against the device calibration it was fitted on
+    (profiles/r04s_lpt_calibration.json: full-run seconds of 15 OOS vintages measured one chain
+    alone, tools/calibrate_lpt.py): the coefficients are the fitted ones, the model reproduces
+    the fit, and every measured vintage lies within the fit's stated residual."""
+    import json
+    from conftest import ROOT
+    cal = json.loads((ROOT / "profiles" / "r04s_lpt_calibration.json").read_text())
+    dm = pkg.distributed
+    assert dm.LPT_COEF["a_per_T"] == cal["coef"]["a_per_T"]
+    assert dm.LPT_COEF["e_per_cens_month"] == cal["coef"]["e_per_cens_month"]
+    for row, fit in zip(cal["rows"], cal["fit_s"]):
+        got = dm.unit_cost(row["T"], 241, 20, n_cens=row["n_cens"])
+        assert abs(got - fit) <= 1e-9 * fit, (row, got, fit)
+        assert abs(got - row["full_run_s"]) <= (cal["max_rel_residual"] + 1e-9) * row["full_run_s"], row
