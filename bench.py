@@ -62,6 +62,10 @@ def parse():
     ap.add_argument("--oos-steps", type=int, default=3,
                     help="timed kept sweeps (with forecasts) of the OOS line (configs[3]); 0 = skip")
     ap.add_argument("--oos-chains", default="1,8,32", help="chains per vintage of the OOS lines")
+    ap.add_argument("--oos-full-draws", type=int, default=1000,
+                    help="MCMCdraws of the measured full configs[3] run (burn-in = kept = this, C = 1, all 164 "
+                         "vintages LPT-sharded over the ranks, end-of-run log-score all-gather) and of the "
+                         "longest vintage alone (the per-rank floor); 0 = skip (projection only)")
     ap.add_argument("--s120-steps", type=int, default=2,
                     help="timed sweeps of the S120 stress line (configs[4], N=120); 0 = skip")
     ap.add_argument("--s120-warmup", type=int, default=1)
@@ -471,9 +475,62 @@ def bench_oos(pkg, ctx, d, C, args, rank, barrier, dist, H=48, Nd=10, floor=Fals
             "note": "expected N-GPU wall time = max(longest vintage alone, this line's 1-GPU time / N): "
                     "LPT puts the longest vintage on some rank, whose sweep cannot run faster than "
                     "that unit's own latency"}
+    if floor and args.oos_full_draws > 0:
+        res.update(oos_full_run(pkg, ctx, d, args.oos_full_draws, rank, barrier, dist, Tj, H, Nd, proj, world))
     if kt:
         res["kernel_ms_per_sweep"] = {k: round(v[0] / v[1], 4) for k, v in kt.items() if v[1]}
     return res
+
+
+def oos_full_run(pkg, ctx, d, draws, rank, barrier, dist, Tj, H, Nd, proj, world):
+    """configs[3] measured end to end (goVARshadowrateBlockHybrid.m:126-517 with one chain per vintage, as
+    the reference runs it): every vintage's `draws` burn-in + `draws` kept sweeps with the predictive
+    density, vintages LPT-sharded over the ranks, each rank's vintage loop in the library
+    (ccmm_run_batch, engine="native"), then the end-of-run exchange of the per-vintage log scores and
+    summaries (all_gather_object over RCCL) inside the timed region; max over ranks.  Beside it the
+    longest vintage (thisT = Tj[-1]) alone, the same full length on rank 0: the latency floor of any
+    sharding."""
+    import time as _t
+    S = pkg.samplers
+    ndxS, ndxO, _ = pkg.model.setShadowYields(d["ncode"], 0.25)
+    mpm = pkg.model.setMinnesotaMean(d["ncode"])
+    kw = dict(MCMCdraws=draws, fcstNdraws=Nd * draws, fcstNhorizons=H, ELBbound=0.25, nchains=1,
+              engine="native", chunk=100)
+    _progress(f"oos full run: {len(Tj)} vintages x {draws} + {draws} sweeps on {world} rank(s)")
+    barrier()
+    t0 = _t.perf_counter()
+    r = S.goVARshadowrateBlockHybrid_batch(d["data"], d["ydates"], ndxS, ndxO, mpm, dist=dist,
+                                           device=ctx.device, **kw)
+    barrier()
+    el = _t.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{ctx.device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ls = np.asarray(r["fcstYmvlogscore"], float)
+    out = {"measured_full_run_s": round(el, 2),
+           "measured_full_run": {
+               "workload": f"{len(Tj)} vintages x 1 chain x ({draws} burn-in + {draws} kept) sweeps, fcstNdraws = "
+                           f"{Nd * draws}, {H} horizons, reference ELB schedule; ccmm_run_batch per rank + "
+                           "end-of-run all-gather of the per-vintage log scores (timed)",
+               "seconds": round(el, 2), "ranks": world,
+               "sweeps_per_s": round(len(Tj) * 2 * draws / el, 1),
+               "finite_logscores": int(np.isfinite(ls).sum()),
+               "mean_logscore": round(float(np.nanmean(ls)), 5),
+               "retries": r["stats"]["retries"]}}
+    if rank == 0:
+        _progress(f"oos floor: vintage thisT = {Tj[-1]} alone, {draws} + {draws} sweeps")
+        t0 = _t.perf_counter()
+        rf = S.goVARshadowrateBlockHybrid_batch(d["data"], d["ydates"], ndxS, ndxO, mpm, Tjumpoffs=[Tj[-1]],
+                                                device=ctx.device, **kw)
+        ctx.synchronize()
+        fl = _t.perf_counter() - t0
+        out["per_rank_floor_measured"] = {
+            "unit": f"vintage thisT = {Tj[-1]} alone, 1 chain, {draws} + {draws} sweeps (full length, measured)",
+            "seconds": round(fl, 2), "logscore": round(float(rf["fcstYmvlogscore"][0]), 5)}
+        out["expected_full_run_s_measured"] = {str(n): round(max(fl, el * world / n), 1) for n in (1, 2, 4, 8)}
+    return out
 
 
 def bench_girf(pkg, ctx, d, M, rank, barrier, dist, nsim=1000, H=120):

@@ -75,6 +75,8 @@ class BatchOut(C.Structure):
 _SIGS = {
     "ccmm_abi_version": (C.c_int, []),
     "ccmm_last_error": (C.c_char_p, []),
+    "ccmm_ablation_build": (C.c_int, []),
+    "ccmm_env_ignored": (C.c_int, [C.c_char_p, C.c_int]),
     "ccmm_device_count": (C.c_int, []),
     "ccmm_create": (C.c_void_p, [C.c_int]),
     "ccmm_destroy": (None, [C.c_void_p]),
@@ -186,6 +188,19 @@ def exported_symbols():
 
 def last_error() -> str:
     return load_library().ccmm_last_error().decode(errors="replace")
+
+
+def env_ignored() -> tuple[int, list[str]]:
+    """Timing-only ablation variables set in the environment that this build ignores
+    (ccmm_env_ignored; host only, no GPU needed)."""
+    buf = C.create_string_buffer(1024)
+    n = load_library().ccmm_env_ignored(buf, len(buf))
+    names = buf.value.decode()
+    return n, (names.split(",") if names else [])
+
+
+def ablation_build() -> bool:
+    return bool(load_library().ccmm_ablation_build())
 
 
 def _check(rc, what):

@@ -222,6 +222,23 @@ static PhaseLock& phase_lock(int device, int id) {
   return *p;
 }
 
+// the predictive-density kernels of one kept draw per chain (ccmm_fcst.hip): the paths (one
+// single-wave workgroup per (draw, chain); job Nd = the linear model's mean path) then the scores
+static void launch_fcst(hipStream_t st, FcstArgs& a, double* sv1) {
+  a.hc = fcst_chunk(a.N, a.Kx, a.p, a.H);
+  a.sv1 = sv1;
+  const size_t lp = fcst_paths_lds_doubles(a.N, a.Kx, a.p, a.hc) * sizeof(double);
+  const size_t ls = fcst_scores_lds_doubles(a.N) * sizeof(double);
+  if (lp > 160 * 1024) throw std::runtime_error("forecast state does not fit LDS");
+  const int njobs = a.bh ? a.Nd : a.Nd + 1;
+  HIPCHECK(hipFuncSetAttribute((const void*)k_fcst, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lp));
+  hipLaunchKernelGGL(k_fcst, dim3(njobs, a.B), dim3(64), lp, st, a);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipFuncSetAttribute((const void*)k_fcst_scores, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ls));
+  hipLaunchKernelGGL(k_fcst_scores, dim3(a.Nd, a.B), dim3(64), ls, st, a);
+  HIPCHECK(hipGetLastError());
+}
+
 struct ccmm_chains {
   ccmm_ctx* ctx = nullptr;
   ccmm_chain_config cfg{};
@@ -264,11 +281,11 @@ struct ccmm_chains {
   // predictive density of every stored sweep (mcmcVAR.m:298-381,
   // mcmcVARshadowrateBlockHybrid.m:550-669), kept on the device
   bool have_fcst = false;
-  int fH = 0, fNd = 0, fKeep = 0, fstored = 0, fldXj = 0, fnw = 1;
+  int fH = 0, fNd = 0, fKeep = 0, fstored = 0, fldXj = 0;
   DBuf<uint8_t> fYields, fRecFloor;
   bool have_rec_floor = false;
   std::vector<bool> have_fcst_slot;
-  DBuf<double> fYreal, fXj, fY, fYc, fYhat, fSc, fYsum, fYcsum, fYhatsum, fScStore, fPaths, fPathsC;
+  DBuf<double> fYreal, fXj, fY, fYc, fYhat, fSc, fYsum, fYcsum, fYhatsum, fScStore, fPaths, fPathsC, fSv1;
   DBuf<int> fStatus;
   // Philox stream ids (counter word 1) per chain; default the chain index
   bool have_ids = false;
@@ -280,7 +297,7 @@ struct ccmm_chains {
   bool use_fused = std::getenv("CCMM_OLD_CHOL") == nullptr;
   bool gc18 = std::getenv("CCMM_GC18") != nullptr;
   // timing-only ablation of k_gram_chol (results invalid): 1 = no SYRK, 2 = no Cholesky
-  int gc_mode = std::getenv("CCMM_GC_MODE") ? std::atoi(std::getenv("CCMM_GC_MODE")) : 0;
+  int gc_mode = env_ablation("CCMM_GC_MODE", 0);
   std::vector<bool> have_slot;
   // lag-structured design (ccmm_lag.hip): D slabs parallel to the X slabs
   bool lag_capable = false;
@@ -551,8 +568,9 @@ struct ccmm_chains {
       if (!slot_lag[s]) return false;
     return true;
   }
-  int lag_mode = std::getenv("CCMM_LAG_MODE") ? std::atoi(std::getenv("CCMM_LAG_MODE")) : 0;
-  int sv_mode = std::getenv("CCMM_SV_MODE") ? std::atoi(std::getenv("CCMM_SV_MODE")) : 0;
+  int lag_mode = env_ablation("CCMM_LAG_MODE", 0);
+  // bit 128 (full-row block factors, same draws) is a selector; the other bits are ablations
+  int sv_mode = env_ablation("CCMM_SV_MODE", 0, 128);
   // k_elb_gibbs_oct (eight passes in flight in one wave) from B >= kElbOctMinB; CCMM_ELB_OCT=0 never,
   // 2 always
   int elb_oct = std::getenv("CCMM_ELB_OCT") ? std::atoi(std::getenv("CCMM_ELB_OCT")) : 1;
@@ -566,7 +584,7 @@ struct ccmm_chains {
     return (w == 1 || w == 4) ? w : 8;
   }();
   // timing-only ablation of k_elb_gibbs (results invalid): 1 no truncnorm, 2 no uniforms
-  int elb_mode = std::getenv("CCMM_ELB_MODE") ? std::atoi(std::getenv("CCMM_ELB_MODE")) : 0;
+  int elb_mode = env_ablation("CCMM_ELB_MODE", 0);
   LagSel lagsel() const { return LagSel{Dpool.p, xidx.p, dColmap.p, ldd, drows, cfg.p, lag_mode}; }
   // D (rows x ldd) of a slot from its X (T x K) and Y (T x N): rows 0..p-1 from the
   // lags of X's first row, rows p.. = Y.  Exact check that X is that lag design.
@@ -1025,7 +1043,7 @@ struct ccmm_chains {
 
   // CTA for large systems (ccmm_big.hip): weights -> multi-equation MFMA Gram -> per-system
   // blocked Cholesky -> per-chain sequential solve
-  int big_mask = std::getenv("CCMM_BIG_MASK") ? std::atoi(std::getenv("CCMM_BIG_MASK")) : 7;
+  int big_mask = env_ablation("CCMM_BIG_MASK", 7);
   void run_cta_big(const RngArgs& ra, const ChainState& cs) {
     Ubuf.alloc((size_t)d.B * d.N * d.TP);
     Dinv.alloc((size_t)d.nmat * d.KP * 64);
@@ -1167,7 +1185,8 @@ struct ccmm_chains {
     // k_astep_w (wave-parallel factorisations, the default) or the one-thread-per-regression
     // k_astep (CCMM_ASTEP_V1=1, kept for A/B timing); same draws up to summation order inside
     // the factorisation (identical update order, fma placement as written)
-    const bool v1 = std::getenv("CCMM_ASTEP_V1") && std::atoi(std::getenv("CCMM_ASTEP_V1")) != 0;
+    // k_astep_w's Gram path holds 16 months per lane (T <= 1024): longer samples take k_astep's loop
+    const bool v1 = env_select("CCMM_ASTEP_V1", 0) != 0 || cfg.T > 1024;
     const void* fn = v1 ? (const void*)k_astep : (N <= 20 ? (const void*)k_astep_w<20> : (const void*)k_astep_w<32>);
     if (lds > 64 * 1024) HIPCHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (!astepTab.p) {  // (ii, a, b) of every Gram entry, block ii = 1..N-1: packed lower ZZ, then Zz
@@ -1362,18 +1381,41 @@ struct ccmm_chains {
   // every PS sweep in the draw store (ccmm_chains_keep_missingrate)
   bool keep_first = false;
   DBuf<double> psFirst, sMissing;
+  // CCMM_PS_CHOL_V1=1: the first-generation k_ps_chol (LDS window) for every band width (A/B; same factor)
+  int ps_chol_v1 = env_select("CCMM_PS_CHOL_V1", 0);
   int last_ps = 0;  // whether the last ELB step ran the PS branch (draw store bookkeeping)
 
   void run_ps(const RngArgs& ra, ElbDev& e, bool kept) {
     ChainState cs = view();
     if (keep_first) psFirst.alloc((size_t)d.B * cfg.Ns * std::max(cfg.elbTmax, 1));
     const PsDev ps = ps_view();
-    const size_t lds = (size_t)(psW * psW + 2 * psW) * sizeof(double) + (size_t)ps_nmax * sizeof(int);
-    require(lds <= 160 * 1024, "PS branch: cell list does not fit LDS");
-    launch(KID_PSCHOL, [&] {
-      HIPCHECK(hipFuncSetAttribute((const void*)k_ps_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(k_ps_chol, dim3(d.B), dim3(psW > 64 ? 128 : 64), lds, ctx->stream, d, e, ps, cs);
-    });
+    if (psW <= 64 && !ps_chol_v1) {  // register-window factorisation, one wave per chain (k_ps_chol_w)
+      const size_t lds = ps_chol_w_lds_bytes(psW, std::max(cfg.elbTmax, 1), ps_nmax);
+      require(lds <= 160 * 1024, "PS branch: cell list does not fit LDS");
+      launch(KID_PSCHOL, [&] {
+        switch (psW) {
+#define CASE_PSC(W)                                                                                              \
+  case W:                                                                                                        \
+    HIPCHECK(hipFuncSetAttribute((const void*)k_ps_chol_w<W>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    hipLaunchKernelGGL(k_ps_chol_w<W>, dim3(d.B), dim3(64), lds, ctx->stream, d, e, ps, cs);                  \
+    break;
+          CASE_PSC(16)
+          CASE_PSC(32)
+          CASE_PSC(48)
+          CASE_PSC(64)
+#undef CASE_PSC
+          default:
+            throw ArgError("PS band width");
+        }
+      });
+    } else {
+      const size_t lds = (size_t)(psW * psW + 2 * psW) * sizeof(double) + (size_t)ps_nmax * sizeof(int);
+      require(lds <= 160 * 1024, "PS branch: cell list does not fit LDS");
+      launch(KID_PSCHOL, [&] {
+        HIPCHECK(hipFuncSetAttribute((const void*)k_ps_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(k_ps_chol, dim3(d.B), dim3(128), lds, ctx->stream, d, e, ps, cs);
+      });
+    }
     if (ps.first) {  // proposal 1's uncensored cells are the window's data (the chain's current Y)
       HIPCHECK(hipMemcpyAsync(psFirst.p, e.Scur, (size_t)d.B * ps.per * sizeof(double), hipMemcpyDeviceToDevice,
                               ctx->stream));
@@ -1578,10 +1620,9 @@ struct ccmm_chains {
       fPaths.alloc(B * cap * Nd * HN);
       fPathsC.alloc(B * cap * Nd * HN);
     }
-    int nw = std::min(((fcst_bh || hybrid) ? Nd : Nd + 1), kFcstMaxWaves);
-    while (nw > 1 && fcst_lds_bytes(N, p, cfg.K, nw) > 160 * 1024) --nw;
-    require(fcst_lds_bytes(N, p, cfg.K, nw) <= 160 * 1024, "forecast state does not fit LDS");
-    fnw = nw;
+    require(fcst_paths_lds_doubles(N, cfg.K, p, fcst_chunk(N, cfg.K, p, H)) * sizeof(double) <= 160 * 1024,
+            "forecast state does not fit LDS");
+    fSv1.alloc(B * Nd * N);
     have_fcst = true;
     reset_fcst();
     layout_crn();
@@ -1704,15 +1745,13 @@ struct ccmm_chains {
     a.seed = cfg.seed; a.sweep = ra.sweep; a.ids = ra.ids;
     a.fY = fY.p; a.fYc = fYc.p; a.yhat = fYhat.p; a.scores = fSc.p; a.status = fStatus.p;
     a.gl = gl;
-    const size_t lds = fcst_lds_bytes(N, cfg.p, cfg.K, fnw);
+    a.mode = env_ablation("CCMM_FCST_MODE", 0);  // timing-only: 1 no scores, 2 no horizons
     const XSel xs = xsel();
     launch(KID_FCST, [&] {
       hipLaunchKernelGGL(k_fcst_jumpoff, dim3(B), dim3(256), 0, ctx->stream, N, cfg.p, N * cfg.p + 1, d.TP,
                          Tslot.p, slot.p, xs.ypool, xs.yidx, fldXj, fXj.p, hybrid ? cfg.Ns : 0,
                          hybrid ? dNdxS.p : nullptr, cfg.elb);
-      HIPCHECK(hipFuncSetAttribute((const void*)k_fcst, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds));
-      hipLaunchKernelGGL(k_fcst, dim3(B), dim3(64 * fnw), lds, ctx->stream, a);
+      launch_fcst(ctx->stream, a, fSv1.p);
       hipLaunchKernelGGL(k_fcst_accum, dim3(B), dim3(256), 0, ctx->stream, N, H, Nd,
                          cfg.store_capacity, fstored, fY.p, fYc.p, (fcst_bh || hybrid) ? nullptr : fYhat.p, fSc.p,
                          fYsum.p, fYcsum.p, fYhatsum.p, fScStore.p, fKeep ? fPaths.p : nullptr,
@@ -1871,10 +1910,76 @@ void set_last_error(const std::string& msg) { g_err = msg; }
 }  // namespace ccmm
 
 // ============================================================== C ABI
+// ---------------------------------------------------------------- environment switches
+namespace {
+// timing-only ablations (results invalid), with the selector bits a default build still honours
+struct AblationVar {
+  const char* name;
+  int keep_mask;
+};
+const AblationVar kAblationVars[] = {
+    {"CCMM_CHOL_SKIP", 0},  {"CCMM_SOLVE_SKIP", 0}, {"CCMM_SV_SKIP", 0},  {"CCMM_GC_MODE", 0},
+    {"CCMM_LAG_MODE", 0},   {"CCMM_BIG_MASK", 0},   {"CCMM_ELB_MODE", 0}, {"CCMM_SV_MODE", 128},
+    {"CCMM_FCST_MODE", 0},
+};
+// an ablation variable is "ignored" when it is set and a bit outside its keep_mask is non-zero
+bool ablation_ignored(const AblationVar& v) {
+#ifdef CCMM_ABLATION
+  (void)v;
+  return false;
+#else
+  const char* e = std::getenv(v.name);
+  return e && (std::atoi(e) & ~v.keep_mask) != 0;
+#endif
+}
+std::string ignored_list() {
+  std::string out;
+  for (const auto& v : kAblationVars)
+    if (ablation_ignored(v)) out += (out.empty() ? "" : ",") + std::string(v.name);
+  return out;
+}
+}  // namespace
+
+int ccmm::env_select(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
+int ccmm::env_ablation(const char* name, int off, int keep_mask) {
+  const char* e = std::getenv(name);
+  if (!e) return off;
+#ifdef CCMM_ABLATION
+  (void)keep_mask;
+  return std::atoi(e);
+#else
+  return (off & ~keep_mask) | (std::atoi(e) & keep_mask);
+#endif
+}
+
 extern "C" {
 
 int ccmm_abi_version(void) { return CCMM_ABI_VERSION; }
 const char* ccmm_last_error(void) { return g_err.c_str(); }
+
+int ccmm_ablation_build(void) {
+#ifdef CCMM_ABLATION
+  return 1;
+#else
+  return 0;
+#endif
+}
+
+int ccmm_env_ignored(char* buf, int len) {
+  const std::string l = ignored_list();
+  if (buf && len > 0) {
+    const size_t n = std::min((size_t)len - 1, l.size());
+    std::memcpy(buf, l.data(), n);
+    buf[n] = 0;
+  }
+  int count = 0;
+  for (const auto& v : kAblationVars) count += ablation_ignored(v) ? 1 : 0;
+  return count;
+}
 
 int ccmm_device_count(void) {
   int n = 0;
@@ -2383,7 +2488,9 @@ static int gibbs_shadowrates_impl(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns
         for (int col = 1; col < Ny; ++col)
           for (int r = 0; r < col; ++r)
             if (Pc[(1 + r) + (size_t)col * K] != 0.0) {
-              g_err = "B(2:Ny+1, :) must be lower triangular";
+              g_err = std::string(b3 ? "ccmm_gibbs_shadowrates_b3: B" : "ccmm_gibbs_shadowrates: Psi") +
+                      "(2:Ny+1, :) must be lower triangular (the device evaluates the structural form A = its "
+                      "inverse; every reference caller passes invA)";
               return CCMM_ERR_ARG;
             }
       }
@@ -2479,6 +2586,9 @@ ccmm_chains* ccmm_chains_create(ccmm_ctx* ctx, const ccmm_chain_config* cfg) {
     const int extra = cfg->model != CCMM_MODEL_LINEAR ? cfg->B : 0;
     ch->init(ctx, *cfg, cfg->ndata + extra, cfg->ndata + extra);
     HIPCHECK(hipStreamSynchronize(ctx->stream));
+    const std::string ign = ignored_list();
+    if (!ign.empty())  // a warning, not an error: the draws are valid, the switches had no effect
+      g_err = "default build: timing-only ablation switches ignored (" + ign + "); build libccmm_ablation.so to use them";
     return 0;
   });
   if (rc != 0) {
@@ -3205,16 +3315,14 @@ int ccmm_fcst(ccmm_ctx* ctx, int B, int N, int p, int H, int Nd, const double* P
     for (int i = 0; i < N; ++i) nwx += ndxYields[i] ? 0 : 1;
     require(nwx > 0 && nwx < N, "need at least one macro series and one yield");
     HIPCHECK(hipSetDevice(ctx->device));
-    int nw = std::min(Nd + 1, kFcstMaxWaves);
-    while (nw > 1 && fcst_lds_bytes(N, p, K, nw) > 160 * 1024) --nw;
-    const size_t lds = fcst_lds_bytes(N, p, K, nw);
-    require(lds <= 160 * 1024, "forecast state does not fit LDS");
+    require(fcst_paths_lds_doubles(N, K, p, fcst_chunk(N, K, p, H)) * sizeof(double) <= 160 * 1024,
+            "forecast state does not fit LDS");
     static const GLNodes gl = make_gl_nodes();
     auto up = [&](DBuf<double>& d, const double* h, size_t n) {
       d.alloc(n);
       HIPCHECK(hipMemcpyAsync(d.p, h, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     };
-    DBuf<double> dPAI, dinvA, dlog, dsq, dXj, dy, dsvz, dz, dfY, dfYc, dyhat, dsc;
+    DBuf<double> dPAI, dinvA, dlog, dsq, dXj, dy, dsvz, dz, dfY, dfYc, dyhat, dsc, dsv1;
     DBuf<uint8_t> dmask;
     DBuf<int> dst;
     up(dPAI, PAI, (size_t)B * K * N);
@@ -3247,10 +3355,8 @@ int ccmm_fcst(ccmm_ctx* ctx, int B, int N, int p, int H, int Nd, const double* P
     a.seed = seed; a.sweep = (uint32_t)sweep;
     a.fY = dfY.p; a.fYc = dfYc.p; a.yhat = dyhat.p; a.scores = dsc.p; a.status = dst.p;
     a.gl = gl;
-    HIPCHECK(hipFuncSetAttribute((const void*)k_fcst, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)lds));
-    hipLaunchKernelGGL(k_fcst, dim3(B), dim3(64 * nw), lds, ctx->stream, a);
-    HIPCHECK(hipGetLastError());
+    dsv1.alloc((size_t)B * Nd * N);
+    launch_fcst(ctx->stream, a, dsv1.p);
     HIPCHECK(hipStreamSynchronize(ctx->stream));
     HIPCHECK(hipMemcpy(fcstY, dfY.p, nout * sizeof(double), hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(fcstYcensor, dfYc.p, nout * sizeof(double), hipMemcpyDeviceToHost));

@@ -685,8 +685,8 @@ hipError_t big_launch_cta(hipStream_t st, const Dims& d, const int* Tslot, const
                           const double* iVdiag, const double* iVb, XSel xs, ChainState cs,
                           const int4* groups, int ngroups, double* rdiag, RngArgs ra, double* Ubuf,
                           double* Dinv, int phase_mask) {
-  static const int skip = std::getenv("CCMM_SOLVE_SKIP") ? std::atoi(std::getenv("CCMM_SOLVE_SKIP")) : 0;
-  static const int cskip = std::getenv("CCMM_CHOL_SKIP") ? std::atoi(std::getenv("CCMM_CHOL_SKIP")) : 0;
+  static const int skip = env_ablation("CCMM_SOLVE_SKIP", 0);
+  static const int cskip = env_ablation("CCMM_CHOL_SKIP", 0);
   const int nt = d.KP / kBT;
   if (phase_mask & 1)
     hipLaunchKernelGGL(k_gram_big, dim3(nt * (nt + 1) / 2, ngroups), dim3(256), 0, st, d, Tslot, xs, cs,

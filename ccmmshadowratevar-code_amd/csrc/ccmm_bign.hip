@@ -972,7 +972,7 @@ hipError_t bign_launch_sv(hipStream_t st, const Dims& d, const int* Tslot, const
   if (e != hipSuccess) return e;
   // CCMM_SV_SKIP: timing ablation of k_sv_big phases (1 M_t, 2 M_t'M_t, 4 Cholesky + inverse,
   // 8 forward product, 16 backward pass, 32 Linv_t store); results are wrong when set
-  static const int skip = std::getenv("CCMM_SV_SKIP") ? std::atoi(std::getenv("CCMM_SV_SKIP")) : 0;
+  static const int skip = env_ablation("CCMM_SV_SKIP", 0);
   hipLaunchKernelGGL(k_sv_big, dim3(d.B), dim3(kSvNT), lds, st, d, Tslot, V0inv, V0invm, cs, ra, scr,
                      bign_sv_scratch(d), skip);
   return hipGetLastError();

@@ -998,7 +998,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
     }
     prog = (n < P) ? n * nc + i : done_all;
   }
-  if (prog < done_all && lane == 0) atomicOr(&cs.status[c], 8);  // step cap reached (never expected)
+  if (prog < done_all && lane == 0) atomicOr(&cs.status[c], 32);  // hand-off step cap reached (ccmm.h bit 32; never expected)
   __syncthreads();
   for (int q = lane; q < T * NS; q += 64) Sc[q] = Sl[q];
 }

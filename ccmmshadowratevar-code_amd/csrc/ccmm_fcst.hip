@@ -4,24 +4,18 @@
 // and the one-step predictive log scores (logscoreGaussian.m,
 // logscoreGaussianCensored.m).
 //
-// One workgroup per chain, one wave per forecast draw nn (plus one wave for the
-// zero-shock mean path).  PAI (K x N) is staged once in LDS and shared by all
-// waves; each wave keeps its lag state as a ring of p blocks of N values in LDS
-// (the companion shift x(1+N+r) <- x(1+r) becomes a head-pointer move), lanes
-// i < N each own one equation's dot product.  Scores run on lane 0 of the wave
-// over an N x N LDS scratch (N <= 32): the work is ~N^3 flop per draw.
+// k_fcst: one single-wave workgroup per (forecast draw nn, chain), plus one for the linear
+// model's zero-shock mean path: PAI (Kx x N) staged in LDS, the lag state a ring of p blocks of N
+// values in LDS (the companion shift x(1+N+r) <- x(1+r) becomes a head-pointer move), the shock
+// side of the simulation formed ahead of the recursion in chunks of horizons.  k_fcst_scores: the
+// four one-step log scores of each draw, one single-wave workgroup per (draw, chain), over an
+// N x N LDS scratch (N <= 32): ~N^3 flop per draw.
 #pragma once
 #include "ccmm_internal.h"
 
 namespace ccmm {
 
 constexpr int kFcstMaxN = 32;
-constexpr int kFcstMaxWaves = 8;
-
-// LDS shared by the waves of a chain (doubles): PAI | muY | yield flags | invA | yrealized
-__host__ __device__ inline size_t fcst_shared_doubles(int N, int K) {
-  return (size_t)K * N + 3 * (size_t)N + (size_t)N * N;
-}
 
 struct GLNodes {  // Gauss-Legendre half rules (negative nodes) for n = 6, 12, 20 (Genz BVN)
   double x[3][10];
@@ -67,6 +61,9 @@ struct FcstArgs {
   double* scores;         // [B][Nd][4]
   int* status;            // [B]  bit 1: NaN score (more than kMvnMaxD censored series)
   GLNodes gl;
+  int mode;               // timing-only ablation (CCMM_FCST_MODE; results invalid): 1 no scores, 2 no horizons
+  int hc;                 // horizons per shock chunk of k_fcst (fcst_paths_lds_doubles)
+  double* sv1;            // [B][Nd][N] SV at horizon 1 of each draw (k_fcst -> k_fcst_scores)
 };
 
 __device__ inline double ncdf(double x) { return 0.5 * erfc(-x * 0.70710678118654752440); }
@@ -343,51 +340,48 @@ __device__ double score_censored(const double* invA, const double* sv, const dou
 // the same lags with every yield replaced by its actual rate max(y, ELB) (:623, the
 // actual-rate states fcstX0(ndxfcstActual)); the actual-rate equations read ring c (their
 // PAIactual on the yield lags, PAIshadow zero there: :567-574), the others ring l.
-__global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
-  extern __shared__ double sm[];
-  const int c = blockIdx.x;
-  const int N = a.N, K = a.K, p = a.p, H = a.H, Nd = a.Nd;
-  const int nw = blockDim.x >> 6;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // LDS: PAI Kx x N | per wave: ring_l[p*N] ring_c[p*N] w[N] sv[N] mu[N] dev[N] order[N]
-  // sel[N] + cens[N] M[32*32] (the score index lists live in LDS: as private arrays their
-  // data-dependent indexing put them in scratch memory on the serial score path)
-  // (after PAI: muY[N] and the yield flags, shared by all waves of the chain)
-  double* sPAI = sm;
-  // invA and yrealized staged too: the score algebra walks them in serial loops
-  double* smu = sm + (size_t)a.Kx * N;
-  int* syl = (int*)(smu + N);
-  double* sinvA = smu + 2 * N;
-  double* sy = sinvA + N * N;
-  const int per_wave = 2 * p * N + 6 * N + kFcstMaxN * kFcstMaxN;
-  double* base = sm + fcst_shared_doubles(N, a.Kx) + (size_t)wave * per_wave;
-  double* ringl = base;
-  double* ringc = ringl + p * N;
-  double* w = ringc + p * N;
-  double* sv1 = w + N;
-  const double* mu = smu;  // muY: one per chain (the per-wave slot sv1 + N is unused)
-  double* dev = sv1 + 2 * N;
-  int* order = (int*)(dev + N);
-  int* sel = (int*)(dev + 2 * N);              // N ints
-  uint8_t* cens = (uint8_t*)(sel + N);         // N bytes (same N-double slot)
-  double* M = dev + 3 * N;
+//
+// k_fcst: one single-wave workgroup per (forecast draw, chain) -- job Nd is the linear model's
+// zero-shock mean path.  The shock side of the simulation does not depend on the simulated
+// path, so it is formed for a chunk of hc horizons at once by all 64 lanes before the
+// recursion: the SV normals and their sqrtPHI products, the log-volatility random walk
+// (mcmcVAR.m:302-312), the structural shocks w = sv .* z and their impact nu = invA w.  The
+// recursion itself (one horizon after the other) then only carries the companion product
+// fcstA * state, its 2 N p lag products spread over G lane groups (lane = i + N g takes the lags
+// l = g mod G) whose partials lane i adds by shuffles.  The draw's SV at horizon 1 goes to
+// a.sv1 for k_fcst_scores.
+__host__ __device__ inline size_t fcst_paths_lds_doubles(int N, int Kx, int p, int hc) {
+  return (size_t)Kx * N + 2 * (size_t)N * N + 2 * (size_t)p * N + 3 * (size_t)hc * N;
+}
 
+__global__ __launch_bounds__(64) void k_fcst(FcstArgs a) {
+  extern __shared__ double sm[];
+  const int job = blockIdx.x, c = blockIdx.y;
+  const int N = a.N, K = a.K, p = a.p, H = a.H, Nd = a.Nd, Kx = a.Kx, hc = a.hc;
+  const int lane = threadIdx.x;
+  const int njobs = a.bh ? Nd : Nd + 1;
+  if (job >= njobs) return;
+  const bool mean_path = job == Nd;
+  double* sPAI = sm;                          // Kx x N (column i = equation i)
+  double* sSq = sPAI + (size_t)Kx * N;        // sqrtPHI, N x N column-major
+  double* sinvA = sSq + N * N;                // invA, N x N column-major
+  double* ringl = sinvA + N * N;              // p x N
+  double* ringc = ringl + p * N;              // p x N
+  double* Wb = ringc + p * N;                 // hc x N: zz, then w = sv .* zz
+  double* NUb = Wb + (size_t)hc * N;          // hc x N: sqrtPHI dev, then nu = invA w
+  double* DVb = NUb + (size_t)hc * N;         // hc x N: the SV normals dev
   const int sl = a.slot ? a.slot[c] : 0;
-  const int Kx = a.Kx;
   const bool hy = a.bh == 2;
   const double* PAIc = a.PAI + (size_t)c * a.ldPAI * N;
-  for (int e = threadIdx.x; e < Kx * N; e += blockDim.x) {
+  for (int e = lane; e < Kx * N; e += 64) {
     const int j = e / Kx, k = e - j * Kx;
     sPAI[e] = PAIc[(size_t)j * a.ldPAI + k];
   }
   const double* Xj = a.Xj + (size_t)c * a.ldXj;
-  const double* invAg = a.invA + (size_t)c * N * N;
-  const double* sqrtPHI = a.sqrtPHI + (size_t)c * N * N;
-  const double* yg = a.yreal + (size_t)sl * a.ldY;
-  for (int e = threadIdx.x; e < N * N; e += blockDim.x) sinvA[e] = invAg[e];
-  if (threadIdx.x < N) sy[threadIdx.x] = yg[threadIdx.x];
-  const double* invA = sinvA;
-  const double* y = sy;
+  for (int e = lane; e < N * N; e += 64) {
+    sinvA[e] = a.invA[(size_t)c * N * N + e];
+    sSq[e] = a.sqrtPHI[(size_t)c * N * N + e];
+  }
   int hs[kElbNsMax] = {-1, -1, -1, -1, -1};  // hybrid: indices of the shadow-rate variables
   if (hy)
     for (int q = 0; q < a.Ns && q < kElbNsMax; ++q) hs[q] = a.ndxS[q];
@@ -403,84 +397,99 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
   rng.chain = a.ids ? a.ids[c] : (uint32_t)c;
   rng.sweep = a.sweep;
   const int nsv = N * H * Nd;
-  if (threadIdx.x < N) syl[threadIdx.x] = a.ndxYields[threadIdx.x];
-  __syncthreads();
-  // muY = fcstA(ndxfcstY, :) * Xjumpoff (mcmcVAR.m:326-328; block hybrid :577-580: the
-  // actual-rate equations read the yields' actual-rate lags), the same for every draw of
-  // the chain: lane i of wave 0 once, instead of every wave serially per draw
-  if (threadIdx.x < N) {
-    const int i = threadIdx.x;
-    const bool act = a.bh == 1 && a.actual[i];
-    double s = 0.0;
-    for (int k = 0; k < K; ++k) {
-      const double xv = (act && k > 0 && syl[(k - 1) % N]) ? Xj[K + k - 1] : Xj[k];
-      s += sPAI[(size_t)i * Kx + k] * xv;
-    }
-    for (int k = K; k < Kx; ++k) s += sPAI[(size_t)i * Kx + k] * Xj[k];  // hybrid: actual-rate lags (:592-594)
-    smu[i] = s;
+  // ring blocks: slot (head - l) mod p holds lag l+1 (l = 0..p-1)
+  for (int e = lane; e < p * N; e += 64) {
+    const int l = e / N, j = e - l * N;  // lag l+1 goes to slot (-l) mod p
+    const int slot = (l == 0) ? 0 : p - l;
+    ringl[slot * N + j] = Xj[1 + e];
+    // block hybrid: yields carry their actual-rate lags (Xjumpoff(K+1:end), :93-96);
+    // hybrid: the shadow-rate variables carry theirs (Xjumpoff(Kshadow+1:end), :111-121)
+    double cv = Xj[1 + e];
+    if (a.bh == 1 && a.ndxYields[j]) cv = Xj[K + e];
+    if (hy)
+      for (int q = 0; q < a.Ns && q < kElbNsMax; ++q)
+        if (hs[q] == j) cv = Xj[K + l * a.Ns + q];
+    ringc[slot * N + j] = cv;
   }
+  double logsv = (lane < N) ? a.logSV[((size_t)c * N + lane) * a.ldSV + tsv] : 0.0;
+  const int G = N <= 21 ? 3 : (N <= 32 ? 2 : 1);  // lane groups of the lag sums (G N <= 64)
+  const int g = lane / N, gi = lane - g * N;
+  const double* pcol = sPAI + (size_t)(g < G ? gi : 0) * Kx;
+  int head = 0;
   __syncthreads();
-
-  const int njobs = a.bh ? Nd : Nd + 1;  // job Nd = zero-shock mean path (linear model)
-  const int rounds = (njobs + nw - 1) / nw;
-  for (int r = 0; r < rounds; ++r) {
-    const int job = r * nw + wave;
-    const bool active = job < njobs;
-    const bool mean_path = job == Nd;
-    // ring blocks: slot (head - l) mod p holds lag l+1 (l = 0..p-1)
-    if (active)
-      for (int e = lane; e < p * N; e += 64) {
-        const int l = e / N, j = e - l * N;  // lag l+1 goes to slot (-l) mod p
-        const int slot = (l == 0) ? 0 : p - l;
-        ringl[slot * N + j] = Xj[1 + e];
-        // block hybrid: yields carry their actual-rate lags (Xjumpoff(K+1:end), :93-96);
-        // hybrid: the shadow-rate variables carry theirs (Xjumpoff(Kshadow+1:end), :111-121)
-        double cv = Xj[1 + e];
-        if (a.bh == 1 && a.ndxYields[j]) cv = Xj[K + e];
-        if (hy)
-          for (int q = 0; q < a.Ns && q < kElbNsMax; ++q)
-            if (hs[q] == j) cv = Xj[K + l * a.Ns + q];
-        ringc[slot * N + j] = cv;
+  for (int h0 = 0; h0 < ((a.mode & 2) ? 0 : H); h0 += hc) {
+    const int nh = min(hc, H - h0);
+    if (!mean_path) {
+      // SV normals randn(N, H*Nd) column hh + job H (mcmcVAR.m:302) and the shock normals
+      // randn(N, H, Nd) (:306) of the chunk's horizons
+      for (int q = lane; q < nh * N; q += 64) {
+        const int hh = h0 + q / N, i = q - (q / N) * N;
+        const int col = hh + job * H;
+        DVb[q] = svz ? svz[(size_t)col * N + i] : rng.normal(CCMM_RNG_FCST, (uint32_t)(col * N + i));
+        const size_t zi = ((size_t)job * H + hh) * N + i;
+        Wb[q] = zc ? zc[zi] : rng.normal(CCMM_RNG_FCST, (uint32_t)(nsv + zi));
       }
-    double logsv = (lane < N) ? a.logSV[((size_t)c * N + lane) * a.ldSV + tsv] : 0.0;
-    int head = 0;
-    __syncthreads();
-    for (int hh = 0; hh < H; ++hh) {
-      // SV path (mcmcVAR.m:302-312) and structural shock w = sv .* z.  Lane j draws the
-      // SV normal j of this horizon once (into dev, free until the scores), then every
-      // lane forms its row of sqrtPHI * z in the same j order as before
-      const int col = hh + job * H;
-      if (active && !mean_path && lane < N)
-        dev[lane] = svz ? svz[(size_t)col * N + lane] : rng.normal(CCMM_RNG_FCST, (uint32_t)(col * N + lane));
       wave_lds_sync();
-      if (active && !mean_path && lane < N) {
+      for (int q = lane; q < nh * N; q += 64) {  // sqrtPHI * dev, j in order
+        const int hq = q / N, i = q - hq * N;
+        const double* dv = DVb + (size_t)hq * N;
         double shock = 0.0;
-        for (int j = 0; j < N; ++j) shock += sqrtPHI[lane + j * N] * dev[j];
-        logsv += shock;
-        const double sv = exp(logsv * 0.5);
-        const size_t zi = ((size_t)job * H + hh) * N + lane;
-        const double zz = zc ? zc[zi] : rng.normal(CCMM_RNG_FCST, (uint32_t)(nsv + zi));
-        w[lane] = sv * zz;
-        if (hh == 0) sv1[lane] = sv;
+        for (int j = 0; j < N; ++j) shock = fma(sSq[i + j * N], dv[j], shock);
+        NUb[q] = shock;
       }
-      __syncthreads();
-      double yl = 0.0, yc = 0.0;
-      if (active && lane < N) {
+      wave_lds_sync();
+      if (lane < N)  // the log-volatility random walk and w = sv .* z
+        for (int hq = 0; hq < nh; ++hq) {
+          logsv += NUb[hq * N + lane];
+          const double sv = exp(logsv * 0.5);
+          Wb[hq * N + lane] *= sv;
+          if (h0 + hq == 0) a.sv1[((size_t)c * Nd + job) * N + lane] = sv;
+        }
+      wave_lds_sync();
+      for (int q = lane; q < nh * N; q += 64) {  // nu = invA w (invA unit lower, j = 0..i)
+        const int hq = q / N, i = q - hq * N;
+        const double* wv = Wb + (size_t)hq * N;
         double nu = 0.0;
-        if (!mean_path)
-          for (int j = 0; j <= lane; ++j) nu += invA[lane + j * N] * w[j];  // invA unit lower
-        const double* col = sPAI + (size_t)lane * Kx;
-        double sl2 = Xj[0] * col[0], sc = sl2;  // constant state stays 1 (fcstA(1,1) = 1)
-        for (int l = 0; l < p; ++l) {
+        for (int j = 0; j <= i; ++j) nu = fma(sinvA[i + j * N], wv[j], nu);
+        NUb[q] = nu;
+      }
+      wave_lds_sync();
+    }
+    for (int hq = 0; hq < nh; ++hq) {
+      const int hh = h0 + hq;
+      // fcstA * state on the lane groups
+      double sl2 = 0.0, sc = 0.0;
+      if (g < G) {
+        if (g == 0) sl2 = sc = Xj[0] * pcol[0];  // constant state stays 1 (fcstA(1,1) = 1)
+        for (int l = g; l < p; l += G) {
           int slot = head - l;
           slot += (slot < 0) ? p : 0;
           const double* rl = ringl + slot * N;
           const double* rc = ringc + slot * N;
-          const double* pc = col + 1 + l * N;
-          for (int j = 0; j < N; ++j) { sl2 += pc[j] * rl[j]; sc += pc[j] * rc[j]; }
+          const double* pc = pcol + 1 + l * N;
+#pragma unroll 4
+          for (int j = 0; j < N; ++j) {
+            sl2 = fma(pc[j], rl[j], sl2);
+            sc = fma(pc[j], rc[j], sc);
+          }
           if (hy)  // fcstA(ndxfcstY, Kshadow+1:end) on the actual-rate ring (:626)
-            for (int q = 0; q < a.Ns && q < kElbNsMax; ++q) sl2 += col[K + l * a.Ns + q] * rc[hs[q]];
+            for (int q = 0; q < a.Ns && q < kElbNsMax; ++q) sl2 = fma(pcol[K + l * a.Ns + q], rc[hs[q]], sl2);
         }
+      }
+      // every group's partial is read before any lane adds (lane i + N is also the source of
+      // lane i's group-2 partial through lane i + 2N ... and must still hold its own)
+      double pl[2] = {0.0, 0.0}, pcs[2] = {0.0, 0.0};
+      for (int q = 1; q < G; ++q) {
+        pl[q - 1] = __shfl(sl2, lane + q * N, 64);
+        pcs[q - 1] = __shfl(sc, lane + q * N, 64);
+      }
+      for (int q = 1; q < G; ++q) {
+        sl2 += pl[q - 1];
+        sc += pcs[q - 1];
+      }
+      double yl = 0.0, yc = 0.0;
+      if (lane < N) {
+        const double nu = mean_path ? 0.0 : NUb[hq * N + lane];
         if (hy) {
           yl = sl2 + nu;
           yc = (isyield && yl < a.elb) ? a.elb : yl;  // yields floored (:707-711); ring: max(shadow, ELB) (:634)
@@ -490,8 +499,7 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
         } else {
           yl = sl2 + nu;
           yc = sc + nu;
-          // censored simulation (mcmcVAR.m:360-366)
-          if (isrec && yc < a.elb) yc = a.elb;
+          if (isrec && yc < a.elb) yc = a.elb;        // censored simulation (mcmcVAR.m:360-366)
         }
         if (mean_path) {
           a.yhat[((size_t)c * H + hh) * N + lane] = yl;
@@ -501,72 +509,132 @@ __global__ __launch_bounds__(64 * kFcstMaxWaves) void k_fcst(FcstArgs a) {
           a.fYc[o] = yc;
         }
       }
-      __syncthreads();
+      wave_lds_sync();  // every lane has read the oldest lag block before it is overwritten
       head = (head + 1 == p) ? 0 : head + 1;
-      if (active && lane < N) { ringl[head * N + lane] = yl; ringc[head * N + lane] = yc; }
-      __syncthreads();
+      if (lane < N) {
+        ringl[head * N + lane] = yl;
+        ringc[head * N + lane] = yc;
+      }
+      wave_lds_sync();
     }
-    // one-step predictive log scores (mcmcVAR.m:326-352; block hybrid :577-608): every lane
-    // of the wave runs the same scalar algebra (uniform control flow, identical LDS
-    // writes); the trivariate mvncdf quadrature spreads its nodes over the lanes
-    if (active && !mean_path) {
-      int nx = 0, ni = 0, natelb = 0;
-      for (int i = 0; i < N; ++i) {
-        if (a.ndxYields[i]) { ++ni; natelb += (y[i] <= a.elb); } else ++nx;
-      }
-      double sc[4];
-      bool unsupported = false;
-      // (1) full vector: sqrtOmegaY = invA diag(sv1) is lower triangular, logdet = sum logSV(:,1)
-      {
-        double ld = 0.0;
-        for (int i = 0; i < N; ++i) {
-          M[i + i * kFcstMaxN] = sv1[i];  // unit-diagonal invA times sv
-          for (int r2 = i + 1; r2 < N; ++r2) M[r2 + i * kFcstMaxN] = invA[r2 + i * N] * sv1[i];
-          ld += 2.0 * log(sv1[i]);
-          dev[i] = y[i] - mu[i];
-        }
-        sc[0] = score_gauss(M, N, dev, ld);
-      }
-      // (2) censored full vector (ndxYIELDS censorable); the block-hybrid fcstLogscoreDraws
-      if (natelb > 0) {
-        for (int i = 0; i < N; ++i) { order[i] = i; cens[i] = a.ndxYields[i]; }
-        for (int i = 0; i < N; ++i) sel[i] = i;
-        sc[1] = score_censored(invA, sv1, mu, y, sel, cens, N, N, a.elb, M, dev, order, a.gl,
-                               &unsupported, lane);
-      } else {
-        sc[1] = sc[0];
-      }
-      // (3) macro block
-      {
-        int q = 0;
-        for (int i = 0; i < N; ++i) if (!a.ndxYields[i]) sel[q++] = i;
-        if (gram_rows_chol(invA, sv1, sel, nx, N, M, lane)) {
-          for (int i = 0; i < nx; ++i) dev[i] = y[sel[i]] - mu[sel[i]];
-          sc[2] = score_gauss(M, nx, dev, logdet_chol(M, nx));
-        } else {
-          sc[2] = NAN;
-        }
-      }
-      // (4) yields block: every yield censorable
-      {
-        int q = 0;
-        for (int i = 0; i < N; ++i) if (a.ndxYields[i]) { sel[q] = i; cens[q] = 1; ++q; }
-        if (natelb > 0) {
-          sc[3] = score_censored(invA, sv1, mu, y, sel, cens, ni, N, a.elb, M, dev, order, a.gl,
-                                 &unsupported, lane);
-        } else if (gram_rows_chol(invA, sv1, sel, ni, N, M, lane)) {
-          for (int i = 0; i < ni; ++i) dev[i] = y[sel[i]] - mu[sel[i]];
-          sc[3] = score_gauss(M, ni, dev, logdet_chol(M, ni));
-        } else {
-          sc[3] = NAN;
-        }
-      }
-      if (lane == 0) {
-        for (int q = 0; q < 4; ++q) a.scores[((size_t)c * Nd + job) * 4 + q] = sc[q];
-        if (unsupported) atomicOr(&a.status[c], 2);
-      }
+  }
+}
+
+// One-step predictive log scores of draw `job` of chain c (mcmcVAR.m:326-352; block hybrid
+// :577-608), one single-wave workgroup per (draw, chain): every lane runs the same scalar algebra
+// (uniform control flow, identical LDS writes); the trivariate mvncdf quadrature and the lattice
+// rule spread their nodes over the lanes.  Reads the draw's SV at horizon 1 (a.sv1, k_fcst).
+__host__ __device__ inline size_t fcst_scores_lds_doubles(int N) {
+  return 2 * (size_t)N * N + 6 * (size_t)N + kFcstMaxN * kFcstMaxN;
+}
+
+__global__ __launch_bounds__(64) void k_fcst_scores(FcstArgs a) {
+  extern __shared__ double sm[];
+  const int job = blockIdx.x, c = blockIdx.y;
+  const int N = a.N, K = a.K, Kx = a.Kx, Nd = a.Nd;
+  const int lane = threadIdx.x;
+  if (job >= Nd || (a.mode & 1)) return;
+  double* invA = sm;                  // N x N
+  double* mu = invA + N * N;          // muY (N)
+  double* y = mu + N;                 // yrealized(:,1) (N)
+  double* sv1 = y + N;                // SV at horizon 1 (N)
+  double* dev = sv1 + N;              // N
+  int* order = (int*)(dev + N);       // N ints
+  int* sel = (int*)(dev + 2 * N);     // N ints
+  uint8_t* cens = (uint8_t*)(sel + N);  // N bytes (same N-double slot)
+  double* M = dev + 3 * N;            // kFcstMaxN^2
+  int* syl = (int*)(M + kFcstMaxN * kFcstMaxN);  // yield flags (N ints in N doubles)
+  const int sl = a.slot ? a.slot[c] : 0;
+  for (int e = lane; e < N * N; e += 64) invA[e] = a.invA[(size_t)c * N * N + e];
+  if (lane < N) {
+    y[lane] = a.yreal[(size_t)sl * a.ldY + lane];
+    sv1[lane] = a.sv1[((size_t)c * Nd + job) * N + lane];
+    syl[lane] = a.ndxYields[lane];
+  }
+  __syncthreads();
+  // muY = fcstA(ndxfcstY, :) * Xjumpoff (mcmcVAR.m:326-328; block hybrid :577-580: the actual-rate
+  // equations read the yields' actual-rate lags)
+  const double* Xj = a.Xj + (size_t)c * a.ldXj;
+  const double* PAIc = a.PAI + (size_t)c * a.ldPAI * N;
+  if (lane < N) {
+    const int i = lane;
+    const bool act = a.bh == 1 && a.actual[i];
+    const double* col = PAIc + (size_t)i * a.ldPAI;
+    double s = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const double xv = (act && k > 0 && syl[(k - 1) % N]) ? Xj[K + k - 1] : Xj[k];
+      s += col[k] * xv;
     }
-    __syncthreads();
+    for (int k = K; k < Kx; ++k) s += col[k] * Xj[k];  // hybrid: actual-rate lags (:592-594)
+    mu[i] = s;
+  }
+  __syncthreads();
+  int nx = 0, ni = 0, natelb = 0;
+  for (int i = 0; i < N; ++i) {
+    if (a.ndxYields[i]) {
+      ++ni;
+      natelb += (y[i] <= a.elb);
+    } else {
+      ++nx;
+    }
+  }
+  double sc[4];
+  bool unsupported = false;
+  // (1) full vector: sqrtOmegaY = invA diag(sv1) is lower triangular, logdet = sum logSV(:,1)
+  {
+    double ld = 0.0;
+    for (int i = 0; i < N; ++i) {
+      M[i + i * kFcstMaxN] = sv1[i];  // unit-diagonal invA times sv
+      for (int r2 = i + 1; r2 < N; ++r2) M[r2 + i * kFcstMaxN] = invA[r2 + i * N] * sv1[i];
+      ld += 2.0 * log(sv1[i]);
+      dev[i] = y[i] - mu[i];
+    }
+    sc[0] = score_gauss(M, N, dev, ld);
+  }
+  // (2) censored full vector (ndxYIELDS censorable); the block-hybrid fcstLogscoreDraws
+  if (natelb > 0) {
+    for (int i = 0; i < N; ++i) {
+      order[i] = i;
+      cens[i] = a.ndxYields[i];
+    }
+    for (int i = 0; i < N; ++i) sel[i] = i;
+    sc[1] = score_censored(invA, sv1, mu, y, sel, cens, N, N, a.elb, M, dev, order, a.gl, &unsupported, lane);
+  } else {
+    sc[1] = sc[0];
+  }
+  // (3) macro block
+  {
+    int q = 0;
+    for (int i = 0; i < N; ++i)
+      if (!a.ndxYields[i]) sel[q++] = i;
+    if (gram_rows_chol(invA, sv1, sel, nx, N, M, lane)) {
+      for (int i = 0; i < nx; ++i) dev[i] = y[sel[i]] - mu[sel[i]];
+      sc[2] = score_gauss(M, nx, dev, logdet_chol(M, nx));
+    } else {
+      sc[2] = NAN;
+    }
+  }
+  // (4) yields block: every yield censorable
+  {
+    int q = 0;
+    for (int i = 0; i < N; ++i)
+      if (a.ndxYields[i]) {
+        sel[q] = i;
+        cens[q] = 1;
+        ++q;
+      }
+    if (natelb > 0) {
+      sc[3] = score_censored(invA, sv1, mu, y, sel, cens, ni, N, a.elb, M, dev, order, a.gl, &unsupported, lane);
+    } else if (gram_rows_chol(invA, sv1, sel, ni, N, M, lane)) {
+      for (int i = 0; i < ni; ++i) dev[i] = y[sel[i]] - mu[sel[i]];
+      sc[3] = score_gauss(M, ni, dev, logdet_chol(M, ni));
+    } else {
+      sc[3] = NAN;
+    }
+  }
+  if (lane == 0) {
+    for (int q = 0; q < 4; ++q) a.scores[((size_t)c * Nd + job) * 4 + q] = sc[q];
+    if (unsupported) atomicOr(&a.status[c], 2);
   }
 }
 
@@ -637,9 +705,11 @@ __global__ void k_fcst_accum(int N, int H, int Nd, int cap, int m, const double*
     }
 }
 
-inline size_t fcst_lds_bytes(int N, int p, int K, int nw) {
-  const size_t per_wave = 2 * (size_t)p * N + 6 * (size_t)N + kFcstMaxN * kFcstMaxN;
-  return (fcst_shared_doubles(N, K) + (size_t)nw * per_wave) * sizeof(double);
+// horizons per shock chunk so that k_fcst's LDS fits one CU (at most H; at least 1)
+inline int fcst_chunk(int N, int Kx, int p, int H) {
+  int hc = H;
+  while (hc > 1 && fcst_paths_lds_doubles(N, Kx, p, hc) * sizeof(double) > 160 * 1024) hc = (hc + 1) / 2;
+  return hc;
 }
 
 }  // namespace ccmm

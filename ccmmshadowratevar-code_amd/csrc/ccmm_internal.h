@@ -234,6 +234,17 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
   return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
 }
 
+// ---------------------------------------------------------------- environment switches (host)
+// Selectors choose between kernels or schedules whose draws are the same (bit-identical, or one
+// algorithm in another summation order) and are read in every build (CCMM_ELB_OCT, CCMM_SV_NWG, ...).
+// Timing-only ablations skip or truncate work and leave the draws invalid (CCMM_CHOL_SKIP,
+// CCMM_GC_MODE, ...): only a build with -DCCMM_ABLATION (make ablation -> libccmm_ablation.so) reads
+// them.  A default build returns `off` (the bits of keep_mask excepted: selector bits that share a
+// variable with ablation bits) and reports the variables it ignored through ccmm_env_ignored() and, on
+// ccmm_chains_create, ccmm_last_error().
+int env_select(const char* name, int dflt);
+int env_ablation(const char* name, int off, int keep_mask = 0);
+
 // host CTA draw of one chain with the QR branch of CTA.m:80-92 (ccmm_host_cta.cpp)
 int host_cta_chain(int N, int K, int T, const double* Y, int ldy, const double* const* Xs, int ldx,
                    const double* A, const double* sqrtht, int ldh, const double* iVdiag,

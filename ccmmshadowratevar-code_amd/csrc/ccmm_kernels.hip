@@ -596,6 +596,7 @@ __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ T
 // left-to-right update order as k_astep's left-looking loop) and solves L tilde = Zz,
 // alpha = L' \ (tilde + z) by lane substitutions; wave 0 forms invA by lane-per-column
 // forward substitution.  Regressions are dealt to waves largest first in snake order.
+// Lanes hold t = lane + 64 k, k < 16, of the Gram sums: T <= 1024 (run_astep dispatches k_astep beyond).
 template <int NN>
 __global__ __launch_bounds__(512) void k_astep_w(Dims d, const int* __restrict__ Tslot, ChainState cs,
                                                  RngArgs ra, double logy2offset, int es_off,
@@ -744,8 +745,8 @@ __global__ __launch_bounds__(512) void k_astep_w(Dims d, const int* __restrict__
       double v = (r == col) ? 1.0 : 0.0;
 #pragma unroll
       for (int q = 0; q < r; ++q)
-        if (q >= col) v = fma(-Anew[r + q * N], x[q], v);
-      x[r] = (r >= col) ? v : 0.0;
+        if (q >= col && r < N) v = fma(-Anew[r + q * N], x[q], v);  // rows r >= N (NN > N) stay out of A
+      x[r] = (r >= col && r < N) ? v : 0.0;
     }
     if (col < N) {
 #pragma unroll

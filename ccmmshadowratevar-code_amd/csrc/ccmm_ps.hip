@@ -134,6 +134,142 @@ __global__ __launch_bounds__(128) void k_ps_chol(Dims d, ElbDev e, PsDev ps, Cha
   }
 }
 
+// ---------------------------------------------------------------- banded Cholesky, register window
+// Band widths W <= 64 (the reference's Ns = 3 with p = 12: 39, padded to 48; S120's Ns = 4: 64).
+// One wave per chain.  Lane q owns the window row i = q (mod W): its band entries sit in registers
+// indexed by the column's distance to the pivot column k (reg[cc] = A(i, k + cc)), so every index
+// is static.  A step broadcasts the pivot column L(k + r, k) through LDS once, every lane applies
+// its row's rank-1 update and shifts its row one column left, and the lane whose row k just
+// finished takes row k + W from an LDS chunk of assembled rows.  Entries right of a row's diagonal
+// (cc > i - k) hold values no step reads.  Per column: one LDS write and W - 1 broadcast reads, two
+// wave-scope syncs, against k_ps_chol's three workgroup barriers and a W x W read-modify-write of
+// the window in LDS (and its serial assembly of the cell list).  Same band storage, same updates
+// (fma(-L(i,k), L(j,k), A(i,j)) and bb -= L(i,k) yk) in the same order per entry.
+constexpr int kPsChunk = 64;  // assembled band rows per LDS chunk
+
+__host__ __device__ inline size_t ps_chol_w_lds_bytes(int W, int elbTmax, int nmax) {
+  return (size_t)(kPsChunk * W + kPsChunk + W) * sizeof(double) + (size_t)(elbTmax + nmax) * sizeof(int);
+}
+
+template <int W>
+__global__ __launch_bounds__(64) void k_ps_chol_w(Dims d, ElbDev e, PsDev ps, ChainState cs) {
+  static_assert(W >= 2 && W <= 64, "one wave: W <= 64");
+  extern __shared__ double sm[];
+  double* prow = sm;                  // kPsChunk x W: P(i, i - W + 1 + cc) of row i at [(i - base) W + cc]
+  double* pb = prow + kPsChunk * W;   // kPsChunk: b(i) of the chunk's rows
+  double* sL = pb + kPsChunk;         // W: pivot column L(k + r, k) at [r]
+  int* scens = (int*)(sL + W);        // elbTmax: month of censored month ci
+  int* info = scens + e.elbTmax;      // nmax: (censored-month index << 3) | variable
+  const int c = blockIdx.x;
+  const int s = cs.slot[c];
+  const int lane = threadIdx.x;
+  const int Ns = e.Ns, p = e.p;
+  const int nc = e.ncens[s];
+  for (int ci = lane; ci < nc; ci += 64) scens[ci] = e.cens[(size_t)s * e.elbTmax + ci];
+  __syncthreads();
+  // cell list, month-major (variables in index order): per-month counts and a wave prefix sum
+  int n = 0;
+  for (int b0 = 0; b0 < nc; b0 += 64) {
+    const int ci = b0 + lane;
+    unsigned m = 0;
+    if (ci < nc) {
+      const uint8_t* f = e.sNaN + ((size_t)s * e.elbTmax + scens[ci]) * Ns;
+      for (int a = 0; a < Ns; ++a) m |= f[a] ? (1u << a) : 0u;
+    }
+    const int cnt = __popc(m);
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    int off = n + incl - cnt;
+    for (int a = 0; a < Ns; ++a)
+      if ((m >> a) & 1u) info[off++] = (ci << 3) | a;
+    n += __shfl(incl, 63, 64);
+  }
+  __syncthreads();
+  for (int i = lane; i < n; i += 64) ps.cell[(size_t)c * ps.nmax + i] = scens[info[i] >> 3] * Ns + (info[i] & 7);
+  if (lane == 0) ps.n[c] = n;
+  if (n == 0) return;
+  const double* recs = e.cond + (size_t)c * e.elbTmax * e.condStride;
+  const int xo = elb_cond_ps_off(Ns, p);
+  auto pentry = [&](int i, int j) -> double {  // P(i, j), i >= j (as k_ps_chol)
+    const int ci = info[i] >> 3, ai = info[i] & 7, cj = info[j] >> 3, aj = info[j] & 7;
+    const int kp = scens[ci] - scens[cj];
+    const double* x = recs + (size_t)ci * e.condStride + xo;
+    if (kp == 0) return x[ai * Ns + aj];
+    if (kp > p) return 0.0;
+    return -x[Ns * Ns + Ns + ((kp - 1) * Ns + aj) * Ns + ai];
+  };
+  auto fill = [&](int base) {  // band rows base .. base + kPsChunk - 1 and their b
+    for (int q = lane; q < kPsChunk * W; q += 64) {
+      const int i = base + q / W, cc = q % W, j = i - W + 1 + cc;
+      prow[q] = (i < n && j >= 0) ? pentry(i, j) : 0.0;
+    }
+    const int i = base + lane;
+    pb[lane] = i < n ? recs[(size_t)(info[i] >> 3) * e.condStride + xo + Ns * Ns + (info[i] & 7)] : 0.0;
+  };
+  int base = 0;
+  fill(0);
+  __syncthreads();
+  double reg[W];
+  double bbv = 0.0;
+  // step 0: lane q < W holds row q (columns 0..q; 0 right of the diagonal and for rows >= n)
+#pragma unroll
+  for (int cc = 0; cc < W; ++cc)
+    reg[cc] = (lane < W && cc <= lane) ? prow[lane * W + cc - lane + W - 1] : 0.0;
+  if (lane < W) bbv = pb[lane];
+  int r = lane < W ? lane : W;  // the lane's row relative to the pivot row (W: idle lane)
+  double* Lg = ps.L + (size_t)c * ps.nmax * W;
+  double* yb = ps.ybar + (size_t)c * ps.nmax;
+  bool fail = false;
+  int sk = 0;  // the pivot row's lane, k mod W
+  for (int k = 0; k < n; ++k) {
+    const double dkk = readlane_d(reg[0], sk);
+    fail |= !(dkk > 0.0);
+    const double lkk = sqrt(fabs(dkk) > 0.0 ? fabs(dkk) : 1.0);
+    const double l = (r == 0) ? lkk : (r < W ? reg[0] / lkk : 0.0);
+    const double yk = readlane_d(bbv, sk) / lkk;
+    if (r < W) {
+      Lg[(size_t)k * W + r] = l;
+      sL[r] = l;
+    }
+    if (lane == sk) yb[k] = yk;
+    wave_lds_sync();
+#pragma unroll
+    for (int cc = 1; cc < W; ++cc) reg[cc] = fma(-l, sL[cc], reg[cc]);
+    bbv = fma(-l, yk, bbv);
+#pragma unroll
+    for (int cc = 0; cc < W - 1; ++cc) reg[cc] = reg[cc + 1];
+    reg[W - 1] = 0.0;
+    const int inew = k + W;  // enters on lane sk, whose row k is finished
+    if (inew - base >= kPsChunk && inew < n) {
+      base += kPsChunk;
+      wave_lds_sync();
+      fill(base);
+    }
+    wave_lds_sync();
+    if (lane == sk) {
+      if (inew < n) {
+#pragma unroll
+        for (int cc = 0; cc < W; ++cc) reg[cc] = prow[(inew - base) * W + cc];
+        bbv = pb[inew - base];
+      } else {
+#pragma unroll
+        for (int cc = 0; cc < W; ++cc) reg[cc] = 0.0;
+        bbv = 0.0;
+      }
+    }
+    r = (r == 0) ? W - 1 : (r < W ? r - 1 : W);
+    sk = (sk + 1 == W) ? 0 : sk + 1;
+  }
+  if (fail && lane == 0) {  // not positive definite: no proposals, the Gibbs draw serves the sweep
+    ps.n[c] = 0;
+    cs.status[c] |= 32;
+  }
+}
+
 // x = L'^-1 (ybar + z_k): one proposal by back substitution, the W - 1 values x_{i+1..i+W-1}
 // in registers (win[j - 1] = x_{i + j}, shifted down one slot per step so every index is
 // static).  out != nullptr writes x into the chain's shadow rates.  Returns whether every
@@ -155,7 +291,11 @@ __device__ inline bool ps_backsub(const double* __restrict__ Lc, const double* _
     for (int j = W - 2; j >= 1; --j) win[j] = win[j - 1];
     win[0] = v;
     ok = ok && (v < elb);
-    if (out) out[cell[i]] = v;
+    if (out) {
+      out[cell[i]] = v;
+    } else if (!ok) {
+      break;  // rejected (a cell at or above the ELB): the rest of this proposal is never read
+    }
   }
   return ok;
 }

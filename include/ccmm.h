@@ -72,6 +72,15 @@ typedef struct ccmm_chains ccmm_chains;
 /* ---------------------------------------------------------------- context */
 int ccmm_abi_version(void);
 const char* ccmm_last_error(void);
+/* Environment switches (host only, no GPU needed).  Timing-only ablation variables (CCMM_CHOL_SKIP,
+ * CCMM_SOLVE_SKIP, CCMM_SV_SKIP, CCMM_GC_MODE, CCMM_LAG_MODE, CCMM_BIG_MASK, CCMM_ELB_MODE, the
+ * ablation bits of CCMM_SV_MODE, CCMM_FCST_MODE) leave the draws invalid and are read only by a build
+ * with -DCCMM_ABLATION (`make ablation`: libccmm_ablation.so); ccmm_ablation_build() returns 1 there.
+ * A default build ignores them: ccmm_env_ignored() returns how many are set in the environment and
+ * ignored (their names comma-separated in buf, len bytes with the terminator; buf may be NULL), and
+ * ccmm_chains_create() leaves the same list in ccmm_last_error() as a warning. */
+int ccmm_ablation_build(void);
+int ccmm_env_ignored(char* buf, int len);
 int ccmm_device_count(void);
 /* Create a context bound to HIP device `device`.  Returns NULL on failure. */
 ccmm_ctx* ccmm_create(int device);
@@ -155,7 +164,10 @@ int ccmm_phi_iw(ccmm_ctx* ctx, int B, int T, int N, const double* eta, const dou
  *                                        branches, as ccmm_draw_trunc_normal) or NULL
  * Ndraws must be 1 (the reference's only use).  Evaluated in the stable residual form of the
  * device ELB step (ccmm_elb.hip): the same conditional moments as the QR formulation of
- * gibbsdrawShadowrates.m:74-145 in exact arithmetic.  CCMM_ERR_DIM: sum(ndxS) != Ns
+ * gibbsdrawShadowrates.m:74-145 in exact arithmetic.  That form needs the structural matrix
+ * A = Psi(2:Ny+1, :)^-1, so Psi(2:Ny+1, :) must be lower triangular (every reference caller passes
+ * invA, mcmcVARshadowrateBlockHybrid.m:418; the QR form of the reference also takes a general
+ * impact matrix): CCMM_ERR_ARG otherwise.  CCMM_ERR_DIM: sum(ndxS) != Ns
  * (gibbsdrawShadowrates.m:50-52). */
 int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p, const uint8_t* ndxS,
                            const uint8_t* sNaN, const double* Y, const double* STATE0,

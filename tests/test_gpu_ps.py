@@ -261,3 +261,34 @@ def test_ps_hybrid_toy(pkg, ctx, oracle, bh):
               int(np.count_nonzero(got["PAI"][..., c] != st["PAI"])))
         assert max(e.values()) < 1e-9, e
     assert n_acc > 0
+
+
+@pytest.mark.parametrize("window", ["real", "toy"])
+def test_ps_chol_register_window_matches_lds_kernel(pkg, ctx, oracle, bh, fred, monkeypatch, window):
+    """k_ps_chol_w (register window, one wave, W <= 64) against the first-generation k_ps_chol
+    (CCMM_PS_CHOL_V1=1): the same band factor and forward solve in the same per-entry order, so the
+    PS centre, the accepted proposals and the shadow rates of a Philox run are identical."""
+    bs = _real_bs(bh, oracle, fred) if window == "real" else _toy_bs(bh, (80, 120))
+    lin = bs.lin
+    B, nsw = 4, 3
+    outs = []
+    for v1 in ("1", "0"):
+        monkeypatch.setenv("CCMM_PS_CHOL_V1", v1)
+        ch = pkg.Chains(ctx, N=lin.N, p=lin.p, T=lin.T, B=B, crn=False, model=pkg.MODEL_BLOCKHYBRID,
+                        Ns=len(bs.ndxS), elbTmax=bs.elbT, elb_gibbsburn=bs.gibbsburn, elb=bs.ELB,
+                        store_capacity=nsw, seed=1234)
+        ch.set_data(0, lin.Y, lin.X, lin.iVdiag, lin.iVb, lin.sPHI, lin.Vol_0mean, lin.Vol_0vcvsqrt)
+        ch.set_elb_model(bs.ndxS, bs.actualrateBlock)
+        ch.set_elb_slot(0, bs.elbT0, bs.sNaN)
+        ch.set_elb_ps(1000, 1)
+        st = oracle.init_state(lin)
+        ch.set_state(*[np.repeat(st[k][..., None], B, -1) for k in ("PAI", "A", "sqrtht", "h", "sqrtPHI")])
+        ch.sweep(nsw, store=True)
+        outs.append((ch.get_ps_mean(), ch.get_ps()["stackAccept"], ch.get_shadowrate(), ch.get_status()))
+        ch.close()
+    (m1, a1, s1, st1), (m2, a2, s2, st2) = outs
+    print(window, "accepted", int(np.count_nonzero(a2)), "max |centre diff|", float(np.nanmax(np.abs(m1 - m2))))
+    assert np.all(st1 == 0) and np.all(st2 == 0)
+    assert np.array_equal(a1, a2)
+    np.testing.assert_array_equal(m1, m2)
+    np.testing.assert_array_equal(s1, s2)

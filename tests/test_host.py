@@ -177,3 +177,37 @@ def test_psrf_entry_points_match_oracle(pkg):
             else:
                 assert abs(got[s] - want) < 1e-12 * max(1.0, abs(want)), (C, s, got[s], want)
     assert np.all(np.isnan(A.shadowrate_psrf(np.ones((2, 2, 3)), np.ones((2, 3), bool))))   # too few draws
+
+
+ABLATION_VARS = ("CCMM_CHOL_SKIP", "CCMM_SOLVE_SKIP", "CCMM_SV_SKIP", "CCMM_GC_MODE", "CCMM_LAG_MODE",
+                 "CCMM_BIG_MASK", "CCMM_ELB_MODE", "CCMM_SV_MODE", "CCMM_FCST_MODE")
+
+
+def test_default_build_ignores_timing_ablations(pkg, monkeypatch):
+    """The timing-only ablation switches (results invalid) are read only by a -DCCMM_ABLATION build
+    (libccmm_ablation.so); the default library ignores them and names them (include/ccmm.h)."""
+    lib = pkg.load_library()
+    assert lib.ccmm_ablation_build() == 0
+    for v in ABLATION_VARS:
+        monkeypatch.delenv(v, raising=False)
+    assert pkg._abi.env_ignored() == (0, [])
+    for v in ABLATION_VARS:
+        monkeypatch.setenv(v, "1")
+    n, names = pkg._abi.env_ignored()
+    assert n == len(ABLATION_VARS) and sorted(names) == sorted(ABLATION_VARS)
+    # CCMM_SV_MODE bit 128 is a selector (full-row SV block factors, same draws): honoured, not reported
+    monkeypatch.setenv("CCMM_SV_MODE", "128")
+    n, names = pkg._abi.env_ignored()
+    assert "CCMM_SV_MODE" not in names and n == len(ABLATION_VARS) - 1
+
+
+def test_ablation_build_honours_switches(monkeypatch):
+    """libccmm_ablation.so (make ablation), when built, reports ablation mode and ignores nothing."""
+    import ctypes
+    p = ROOT / "ccmmshadowratevar-code_amd" / "csrc" / "libccmm_ablation.so"
+    if not p.exists():
+        pytest.skip("libccmm_ablation.so not built")
+    lib = ctypes.CDLL(str(p))
+    monkeypatch.setenv("CCMM_CHOL_SKIP", "1")
+    assert lib.ccmm_ablation_build() == 1
+    assert lib.ccmm_env_ignored(None, 0) == 0
