@@ -64,7 +64,7 @@ class BatchConfig(C.Structure):
 BATCH_OUT_FIELDS = ("logscore", "fcstYhat", "fcstShadowYhat", "PAImean", "PAIstdev", "shadowrate_all",
                     "countELBaccept", "attempts", "fcstYmedian", "fcstYcrps", "fcstYquantiles", "fcstYcummedian",
                     "fcstYcumcrps", "fcstYcumquantiles", "fcstShadowYmedian", "fcstShadowYquantiles", "PAImedian",
-                    "PAIquantiles", "scoreDraws", "shadowratePSRF")
+                    "PAIquantiles", "scoreDraws", "shadowratePSRF", "shadowratePSRFchains")
 
 
 class BatchOut(C.Structure):
@@ -155,6 +155,7 @@ _SIGS = {
                                  C.POINTER(BatchOut)]),
     "ccmm_psrf": (C.c_int, [C.c_int, C.c_int, C.c_int, _dp, _dp]),
     "ccmm_shadowrate_psrf": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _u8p, _dp]),
+    "ccmm_shadowrate_psrf_chains": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _u8p, _dp]),
     "ccmm_selftest_mfma_f64": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
     "ccmm_selftest_mfma_f64_acc": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp]),
 }
@@ -233,18 +234,20 @@ def psrf(X):
     return R
 
 
-def shadowrate_psrf(draws, mask, elbT=None):
-    """ccmm_shadowrate_psrf: shadowratePSRF(:, vintage) of goVARshadowrateBlockHybrid.m:322-325.
-    draws M x Ns x ldT [x C] kept shadow rates, mask Ns x elbT (ELBdummy(startELB:thisT, :)').
-    Returns Ns values."""
+def shadowrate_psrf(draws, mask, elbT=None, chains=False):
+    """ccmm_shadowrate_psrf: shadowratePSRF(:, vintage) of goVARshadowrateBlockHybrid.m:322-325 (the
+    reference's one-chain statistic, averaged over C chains); chains=True: ccmm_shadowrate_psrf_chains
+    (psrf across the C chains).  draws M x Ns x ldT [x C] kept shadow rates, mask Ns x elbT
+    (ELBdummy(startELB:thisT, :)').  Returns Ns values."""
     d = _f(draws)
     M, Ns, ldT = d.shape[:3]
     Cc = d.shape[3] if d.ndim == 4 else 1
     mk = np.asfortranarray(np.asarray(mask, bool).reshape(Ns, -1), dtype=np.uint8)
     eT = mk.shape[1] if elbT is None else int(elbT)
     out = np.zeros(Ns)
-    _check(load_library().ccmm_shadowrate_psrf(M, Ns, eT, ldT, Cc, _ptr(d), _ptr(mk, _u8p), _ptr(out)),
-           "ccmm_shadowrate_psrf")
+    lib = load_library()
+    fn = lib.ccmm_shadowrate_psrf_chains if chains else lib.ccmm_shadowrate_psrf
+    _check(fn(M, Ns, eT, ldT, Cc, _ptr(d), _ptr(mk, _u8p), _ptr(out)), "ccmm_shadowrate_psrf")
     return out
 
 
@@ -559,6 +562,7 @@ class Context:
         if shadow:
             shapes["shadowrate_all"] = (MCMCdraws, Ns_, elbTall, C_, V)
             shapes["shadowratePSRF"] = (Ns_, V)
+            shapes["shadowratePSRFchains"] = (Ns_, V)
         if postprocess:
             shapes.update(fcstYmedian=(N, H, V), fcstYcrps=(N, H, V), fcstYquantiles=(N, H, nq, V),
                           fcstYcummedian=(N, H, V), fcstYcumcrps=(N, H, V), fcstYcumquantiles=(N, H, nq, V),

@@ -1497,9 +1497,9 @@ struct ccmm_chains {
     if (ps) run_ps(ra, e, kept);
     // Gibbs passes: elb_waves passes in flight (k_elb_gibbs_wf, bit-identical draws), or the
     // one-wave sequential kernel (CCMM_ELB_WAVES=1)
-    auto gibbs_lds = [&](int w) {
-      return w == 1 ? (size_t)2 * e.elbTmax * Ns * sizeof(double) + (size_t)e.elbTmax * sizeof(int)
-                    : (size_t)(1 + w) * e.elbTmax * Ns * sizeof(double) + (size_t)2 * e.elbTmax * sizeof(int) +
+    auto gibbs_lds = [&](int w) {  // shadow rates | per pass: uniforms and their elb_ppnd16 | month tables
+      return w == 1 ? (size_t)3 * e.elbTmax * Ns * sizeof(double) + (size_t)e.elbTmax * sizeof(int)
+                    : (size_t)(1 + 2 * w) * e.elbTmax * Ns * sizeof(double) + (size_t)2 * e.elbTmax * sizeof(int) +
                           (size_t)2 * w * sizeof(int);
     };
     int W = elb_waves;

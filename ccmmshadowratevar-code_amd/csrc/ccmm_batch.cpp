@@ -127,6 +127,7 @@ struct Runner {
     nanfill(o->PAIquantiles, KN * nq, v);
     nanfill(o->scoreDraws, size_t(cf.fcstNdraws) * C * 4, v);
     nanfill(o->shadowratePSRF, size_t(Ns), v);
+    nanfill(o->shadowratePSRFchains, size_t(Ns), v);
   }
 
   // One chain set over the vintages `vs` (indices into vin) on attempt `attempt`; writes the
@@ -214,7 +215,7 @@ struct Runner {
     std::vector<double> fYsum(NH * B, 0.0), fYcsum(NH * B, 0.0), Psum, P2sum;
     std::vector<double> shadowd;  // M x Ns x elbTmax x B
     const int eT = cc.elbTmax;
-    if (shadow && (o->shadowrate_all || o->shadowratePSRF)) shadowd.assign(size_t(M) * Ns * eT * B, kNaN);
+    if (shadow && (o->shadowrate_all || o->shadowratePSRF || o->shadowratePSRFchains)) shadowd.assign(size_t(M) * Ns * eT * B, kNaN);
     if (!cf.postprocess) {
       Psum.assign(KN * B, 0.0);
       P2sum.assign(KN * B, 0.0);
@@ -362,6 +363,12 @@ struct Runner {
         const ccmm_vintage& u = vin[v];
         check(ccmm_shadowrate_psrf(M, Ns, u.T - u.elbT0, eT, C, shadowd.data() + size_t(s) * C * M * Ns * eT,
                                    u.sNaN, o->shadowratePSRF + size_t(v) * Ns));
+      }
+      if (o->shadowratePSRFchains && Ns > 0) {  // the across-chains form (no reference counterpart)
+        const ccmm_vintage& u = vin[v];
+        check(ccmm_shadowrate_psrf_chains(M, Ns, u.T - u.elbT0, eT, C,
+                                          shadowd.data() + size_t(s) * C * M * Ns * eT, u.sNaN,
+                                          o->shadowratePSRFchains + size_t(v) * Ns));
       }
       if (o->attempts) o->attempts[v] = attempt + 1;
     }

@@ -78,15 +78,19 @@ extern "C" int ccmm_psrf(int n, int D, int M, const double* X, double* R) {
   return CCMM_OK;
 }
 
-extern "C" int ccmm_shadowrate_psrf(int M, int Ns, int elbT, int ldT, int C, const double* draws,
-                                    const uint8_t* mask, double* out) {
+namespace {
+// mean over the rate's months at the ELB of psrf(.) per cell: chains = false averages the reference's
+// one-chain statistic (first / last thirds of each chain, DiagnosticsShadowrate.m:82-91) over the C
+// chains; chains = true treats the C chains as the sequences of one psrf (M >= 2 draws each)
+int shadow_psrf(int M, int Ns, int elbT, int ldT, int C, const double* draws, const uint8_t* mask, double* out,
+                bool chains, const char* who) {
   if (M < 1 || Ns < 1 || elbT < 0 || ldT < elbT || C < 1 || !out || (elbT > 0 && (!draws || !mask))) {
-    ccmm::set_last_error("ccmm_shadowrate_psrf: invalid arguments");
+    ccmm::set_last_error(std::string(who) + ": invalid arguments");
     return CCMM_ERR_ARG;
   }
   // psrf stops with 'Too few samples' (DiagnosticsShadowrate.m:103-105) when a sequence would be
   // empty; here the diagnostic is NaN instead, so a short run still returns its draws
-  const bool too_few = C == 1 ? M / 3 < 1 : M < 2;
+  const bool too_few = chains ? (C < 2 || M < 2) : M / 3 < 1;
   for (int s = 0; s < Ns; ++s) {
     if (too_few) {
       out[s] = kNaN;
@@ -100,17 +104,28 @@ extern "C" int ccmm_shadowrate_psrf(int M, int Ns, int elbT, int ldT, int C, con
       if (!mask[size_t(t) * Ns + s]) continue;
       // draws M x Ns x ldT x C: element (m, s, t, c)
       auto at = [&](int m, int c) { return draws[((size_t(c) * ldT + t) * Ns + s) * M + m]; };
-      double R;
-      if (C == 1) {
-        const int m3 = M / 3;
-        R = psrf_one(m3, 2, [&](int k, int i) { return at(i == 0 ? k : M - m3 + k, 0); });
+      if (chains) {
+        sum += psrf_one(M, C, [&](int k, int i) { return at(k, i); });
       } else {
-        R = psrf_one(M, C, [&](int k, int i) { return at(k, i); });
+        const int m3 = M / 3;
+        double rc = 0.0;
+        for (int c = 0; c < C; ++c) rc += psrf_one(m3, 2, [&](int k, int i) { return at(i == 0 ? k : M - m3 + k, c); });
+        sum += rc / C;
       }
-      sum += R;
       ++cells;
     }
     out[s] = cells ? sum / cells : kNaN;
   }
   return CCMM_OK;
+}
+}  // namespace
+
+extern "C" int ccmm_shadowrate_psrf(int M, int Ns, int elbT, int ldT, int C, const double* draws,
+                                    const uint8_t* mask, double* out) {
+  return shadow_psrf(M, Ns, elbT, ldT, C, draws, mask, out, false, "ccmm_shadowrate_psrf");
+}
+
+extern "C" int ccmm_shadowrate_psrf_chains(int M, int Ns, int elbT, int ldT, int C, const double* draws,
+                                           const uint8_t* mask, double* out) {
+  return shadow_psrf(M, Ns, elbT, ldT, C, draws, mask, out, true, "ccmm_shadowrate_psrf_chains");
 }

@@ -453,43 +453,77 @@ __global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState c
 // with wave-uniform branches (every lane draws the same cell); the library erfcinv inlined
 // into k_elb_gibbs's month loop needs ~480 registers (one wave per SIMD).
 __device__ __forceinline__ double elb_ppnd16(double p) {
+  // every multiply-add is an explicit fma and nothing else may contract, so the value does not
+  // depend on the context it is inlined into (the Gibbs kernels precompute it for the pass's
+  // uniforms, elb_trunc_normal_pz, and evaluate it on the draw path: both must agree bit for bit)
+#pragma clang fp contract(off)
   const double q = p - 0.5;
   if (fabs(q) <= 0.425) {
-    const double r = 0.180625 - q * q;
-    const double num = (((((((2509.0809287301226727 * r + 33430.575583588128105) * r + 67265.770927008700853) * r +
-                            45921.953931549871457) * r + 13731.693765509461125) * r + 1971.5909503065514427) * r +
-                          133.14166789178437745) * r + 3.387132872796366608);
-    const double den = (((((((5226.495278852545925 * r + 28729.085735721942674) * r + 39307.89580009271061) * r +
-                            21213.794301586595867) * r + 5394.1960214247511077) * r + 687.1870074920579083) * r +
-                          42.313330701600911252) * r + 1.0);
+    const double r = fma(-q, q, 0.180625);
+    double num = 2509.0809287301226727;
+    num = fma(num, r, 33430.575583588128105);
+    num = fma(num, r, 67265.770927008700853);
+    num = fma(num, r, 45921.953931549871457);
+    num = fma(num, r, 13731.693765509461125);
+    num = fma(num, r, 1971.5909503065514427);
+    num = fma(num, r, 133.14166789178437745);
+    num = fma(num, r, 3.387132872796366608);
+    double den = 5226.495278852545925;
+    den = fma(den, r, 28729.085735721942674);
+    den = fma(den, r, 39307.89580009271061);
+    den = fma(den, r, 21213.794301586595867);
+    den = fma(den, r, 5394.1960214247511077);
+    den = fma(den, r, 687.1870074920579083);
+    den = fma(den, r, 42.313330701600911252);
+    den = fma(den, r, 1.0);
     return q * num / den;
   }
   double r = (q < 0.0) ? p : 1.0 - p;
   r = sqrt(-log(r));
-  double z;
+  double num, den;
   if (r <= 5.0) {
     r -= 1.6;
-    const double num = (((((((7.7454501427834140764e-4 * r + 0.0227238449892691845833) * r + 0.24178072517745061177) * r +
-                            1.27045825245236838258) * r + 3.64784832476320460504) * r + 5.7694972214606914055) * r +
-                          4.6303378461565452959) * r + 1.42343711074968357734);
-    const double den = (((((((1.05075007164441684324e-9 * r + 5.475938084995344946e-4) * r + 0.0151986665636164571966) * r +
-                            0.14810397642748007459) * r + 0.68976733498510000455) * r + 1.6763848301838038494) * r +
-                          2.05319162663775882187) * r + 1.0);
-    z = num / den;
+    num = 7.7454501427834140764e-4;
+    num = fma(num, r, 0.0227238449892691845833);
+    num = fma(num, r, 0.24178072517745061177);
+    num = fma(num, r, 1.27045825245236838258);
+    num = fma(num, r, 3.64784832476320460504);
+    num = fma(num, r, 5.7694972214606914055);
+    num = fma(num, r, 4.6303378461565452959);
+    num = fma(num, r, 1.42343711074968357734);
+    den = 1.05075007164441684324e-9;
+    den = fma(den, r, 5.475938084995344946e-4);
+    den = fma(den, r, 0.0151986665636164571966);
+    den = fma(den, r, 0.14810397642748007459);
+    den = fma(den, r, 0.68976733498510000455);
+    den = fma(den, r, 1.6763848301838038494);
+    den = fma(den, r, 2.05319162663775882187);
+    den = fma(den, r, 1.0);
   } else {
     r -= 5.0;
-    const double num = (((((((2.01033439929228813265e-7 * r + 2.71155556874348757815e-5) * r + 0.0012426609473880784386) * r +
-                            0.026532189526576123093) * r + 0.29656057182850489123) * r + 1.7848265399172913358) * r +
-                          5.4637849111641143699) * r + 6.6579046435011037772);
-    const double den = (((((((2.04426310338993978564e-15 * r + 1.4215117583164458887e-7) * r + 1.8463183175100546818e-5) * r +
-                            7.868691311456132591e-4) * r + 0.0148753612908506148525) * r + 0.13692988092273580531) * r +
-                          0.59983220655588793769) * r + 1.0);
-    z = num / den;
+    num = 2.01033439929228813265e-7;
+    num = fma(num, r, 2.71155556874348757815e-5);
+    num = fma(num, r, 0.0012426609473880784386);
+    num = fma(num, r, 0.026532189526576123093);
+    num = fma(num, r, 0.29656057182850489123);
+    num = fma(num, r, 1.7848265399172913358);
+    num = fma(num, r, 5.4637849111641143699);
+    num = fma(num, r, 6.6579046435011037772);
+    den = 2.04426310338993978564e-15;
+    den = fma(den, r, 1.4215117583164458887e-7);
+    den = fma(den, r, 1.8463183175100546818e-5);
+    den = fma(den, r, 7.868691311456132591e-4);
+    den = fma(den, r, 0.0148753612908506148525);
+    den = fma(den, r, 0.13692988092273580531);
+    den = fma(den, r, 0.59983220655588793769);
+    den = fma(den, r, 1.0);
   }
+  const double z = num / den;
   return (q < 0.0) ? -z : z;
 }
 
 __device__ __forceinline__ double elb_trunc_normal(double mu, double sig, double elb, double u, uint8_t& fl) {
+#pragma clang fp contract(off)
   const double tol = 1e-10;
   const double eps = 2.220446049250313080847e-16;
   sig = fabs(sig);
@@ -499,9 +533,26 @@ __device__ __forceinline__ double elb_trunc_normal(double mu, double sig, double
     const double PHIbar = 0.5 * erfc(-0.70710678118654752440 * ub);
     fl = (PHIbar > eps) ? 3 : 1;
     const double z = (PHIbar > eps) ? elb_ppnd16(u * PHIbar) : ub;
-    return mu + sig * z;
+    return fma(sig, z, mu);
   }
   return mu;
+}
+
+// The same draw with zu = elb_ppnd16(u) computed beforehand (off the month-to-month path).  When
+// ub = (elb - mu) / sig >= 9, erfc(-ub / sqrt 2) = 2 - erfc(ub / sqrt 2) with erfc(6.36) ~ 1e-19, below
+// half an ulp of 2: PHIbar is exactly 1, u PHIbar = u, and the full evaluation returns mu + sig zu.  So
+// the draw is bit-identical without erfc and AS241 on the path (on the real window about half of the
+// draws: the conditional means sit far below the ELB, ub median 8.9).
+constexpr double kElbFastUb = 9.0;
+__device__ __forceinline__ double elb_trunc_normal_pz(double mu, double sig, double elb, double u, double zu,
+                                                      uint8_t& fl) {
+#pragma clang fp contract(off)
+  const double as = fabs(sig);
+  if (as > 1e-10 && (elb - mu) / as >= kElbFastUb) {
+    fl = 3;
+    return fma(as, zu, mu);
+  }
+  return elb_trunc_normal(mu, sig, elb, u, fl);
 }
 
 // ---------------------------------------------------------------- Gibbs passes (per chain)
@@ -527,7 +578,8 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
   const int head = elb_cond_head(NS);
   double* Sl = sm;                      // T x NS (t-major)
   double* Ul = sm + T * NS;             // this pass's uniforms, T x NS (t-major)
-  int* Tm = (int*)(sm + 2 * T * NS);    // censored months: t | (censored-series mask << 16)
+  double* Zl = sm + 2 * T * NS;         // their AS241 values elb_ppnd16(u) (elb_trunc_normal_pz)
+  int* Tm = (int*)(sm + 3 * T * NS);    // censored months: t | (censored-series mask << 16)
   double* Sc = e.Scur + (size_t)c * e.elbTmax * NS;
   const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * NS;
   const int* cl = e.cens + (size_t)s * e.elbTmax;
@@ -566,7 +618,11 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
   // page), so no generator sits on the serial month-to-month path
   auto uniforms = [&](int n) {
     if (rng.crn) {
-      for (int q = lane; q < T * NS; q += 64) Ul[q] = rng.uniform(CCMM_RNG_ELB, (uint32_t)(q + T * NS * n));
+      for (int q = lane; q < T * NS; q += 64) {
+        const double uu = rng.uniform(CCMM_RNG_ELB, (uint32_t)(q + T * NS * n));
+        Ul[q] = uu;
+        Zl[q] = elb_ppnd16(uu);
+      }
     } else {
       const uint32_t base = (uint32_t)(T * NS * n);  // even when T * NS is odd: handle by index
       for (int q = 2 * lane; q < T * NS + 1; q += 128) {
@@ -574,8 +630,15 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
         const uint32_t i0 = base + (uint32_t)q - ((base + (uint32_t)q) & 1u);
         const u32x4 r = rng.raw(CCMM_RNG_ELB, i0 >> 1);
         const int q0 = (int)(i0 - base), q1 = q0 + 1;
-        if (q0 >= 0 && q0 < T * NS) Ul[q0] = u01(r.x, r.y);
-        if (q1 >= 0 && q1 < T * NS) Ul[q1] = u01(r.z, r.w);
+        const double u0 = u01(r.x, r.y), u1 = u01(r.z, r.w);
+        if (q0 >= 0 && q0 < T * NS) {
+          Ul[q0] = u0;
+          Zl[q0] = elb_ppnd16(u0);
+        }
+        if (q1 >= 0 && q1 < T * NS) {
+          Ul[q1] = u1;
+          Zl[q1] = elb_ppnd16(u1);
+        }
       }
     }
     __syncthreads();
@@ -590,8 +653,11 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
     load_rec(cn, rn);  // past the last month: a harmless reload of month 0
     const int tmn = Tm[cn];
     const int t = tm & 0xffff, msk = tm >> 16;
-    double u[NS];
-    for (int a = 0; a < NS; ++a) u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
+    double u[NS], zu[NS];
+    for (int a = 0; a < NS; ++a) {
+      u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
+      zu[a] = (e.mode & 2) ? 0.0 : Zl[t * NS + a];
+    }
     // Spost = a_t + Σ G S(neighbours)
     const int tn0 = t + off0, tn1 = t + off1;
     const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
@@ -614,7 +680,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
         ++y;
       }
       uint8_t fl = 0;
-      cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a], fl);
+      cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
       if (e.flags && lane == 0)  // drawTruncNormal.m branch taken (oracle.draw_trunc_normal flags)
         e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
     }
@@ -666,7 +732,8 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
   const int pg = e.elbTmax * NS;
   double* Sl = sm;                              // T x NS (t-major), shared by all passes
   double* Ul = sm + (size_t)pg * (1 + wave);    // this wave's pass uniforms, T x NS
-  int* Tm = (int*)(sm + (size_t)pg * (1 + W));  // censored months: t | (mask << 16)
+  double* Zl = sm + (size_t)pg * (1 + W + wave);  // their elb_ppnd16(u) (elb_trunc_normal_pz)
+  int* Tm = (int*)(sm + (size_t)pg * (1 + 2 * W));  // censored months: t | (mask << 16)
   int* reach = Tm + e.elbTmax;                  // reach(i)
   int* prog = reach + e.elbTmax;                // [2][W] next draw of each wave, n nc + i
   double* Sc = e.Scur + (size_t)c * e.elbTmax * NS;
@@ -711,15 +778,26 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
   // pass n's uniforms rand(Ns, elbT) (gibbsdrawShadowrates.m:173, page n), drawn by this wave
   auto uniforms = [&](int n) {
     if (rng.crn) {
-      for (int q = lane; q < T * NS; q += 64) Ul[q] = rng.uniform(CCMM_RNG_ELB, (uint32_t)(q + T * NS * n));
+      for (int q = lane; q < T * NS; q += 64) {
+        const double uu = rng.uniform(CCMM_RNG_ELB, (uint32_t)(q + T * NS * n));
+        Ul[q] = uu;
+        Zl[q] = elb_ppnd16(uu);
+      }
     } else {
       const uint32_t base = (uint32_t)(T * NS * n);
       for (int q = 2 * lane; q < T * NS + 1; q += 128) {
         const uint32_t i0 = base + (uint32_t)q - ((base + (uint32_t)q) & 1u);
         const u32x4 r = rng.raw(CCMM_RNG_ELB, i0 >> 1);
         const int q0 = (int)(i0 - base), q1 = q0 + 1;
-        if (q0 >= 0 && q0 < T * NS) Ul[q0] = u01(r.x, r.y);
-        if (q1 >= 0 && q1 < T * NS) Ul[q1] = u01(r.z, r.w);
+        const double u0 = u01(r.x, r.y), u1 = u01(r.z, r.w);
+        if (q0 >= 0 && q0 < T * NS) {
+          Ul[q0] = u0;
+          Zl[q0] = elb_ppnd16(u0);
+        }
+        if (q1 >= 0 && q1 < T * NS) {
+          Ul[q1] = u1;
+          Zl[q1] = elb_ppnd16(u1);
+        }
       }
     }
     wave_lds_sync();
@@ -751,8 +829,11 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
         load_rec(ni, rn);  // next month of this wave (month 0 of its next pass after the last)
         const int tmn = Tm[ni];
         const int t = tm & 0xffff, msk = tm >> 16;
-        double u[NS];
-        for (int a = 0; a < NS; ++a) u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
+        double u[NS], zu[NS];
+        for (int a = 0; a < NS; ++a) {
+          u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
+          zu[a] = (e.mode & 2) ? 0.0 : Zl[t * NS + a];
+        }
         const int tn0 = t + off0, tn1 = t + off1;
         const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
         const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
@@ -773,7 +854,7 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
             ++y;
           }
           uint8_t fl = 0;
-          cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a], fl);
+          cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
           if (e.flags && lane == 0)
             e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
         }
@@ -809,8 +890,11 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
       load_rec(ni, rn);  // this wave's next month (a harmless reload past its last pass)
       const int tmn = Tm[ni];
       const int t = tm & 0xffff, msk = tm >> 16;
-      double u[NS];
-      for (int a = 0; a < NS; ++a) u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
+      double u[NS], zu[NS];
+      for (int a = 0; a < NS; ++a) {
+        u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
+        zu[a] = (e.mode & 2) ? 0.0 : Zl[t * NS + a];
+      }
       const int tn0 = t + off0, tn1 = t + off1;
       const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
       const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
@@ -831,7 +915,7 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
           ++y;
         }
         uint8_t fl = 0;
-        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, u[a], fl);
+        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
         if (e.flags && lane == 0)
           e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
       }
@@ -914,14 +998,16 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
   int prog = (n < P) ? n * nc : done_all;
   // the uniforms of the slot's next month (rand(Ns, elbT) page n, gibbsdrawShadowrates.m:173) are
   // drawn one step ahead, so the generator stays off the month-to-month dependence chain
-  auto draw_u = [&](int nn, int ii, double (&uu)[NS]) {
+  auto draw_u = [&](int nn, int ii, double (&uu)[NS], double (&zz)[NS]) {
     const int tt = Tm[ii] & 0xffff;
 #pragma unroll
-    for (int a = 0; a < NS; ++a)
+    for (int a = 0; a < NS; ++a) {
       uu[a] = (e.mode & 2) ? 0.5 : rng.uniform(CCMM_RNG_ELB, (uint32_t)(tt * NS + a + T * NS * nn));
+      zz[a] = (e.mode & 2) ? 0.0 : elb_ppnd16(uu[a]);
+    }
   };
-  double ucur[NS];
-  if (n < P) draw_u(n, 0, ucur);
+  double ucur[NS], zcur[NS];
+  if (n < P) draw_u(n, 0, ucur, zcur);
   // exit condition every wave reaches: the wavefront needs at most P nc + W (nc + 1) steps
   const int max_steps = P * nc + W * (nc + 1) + 8;
   for (int step = 0; step < max_steps; ++step) {
@@ -938,8 +1024,8 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
         ni = 0;
         nn = n + W;
       }
-      double unext[NS];
-      if (nn < P) draw_u(nn, ni, unext);
+      double unext[NS], znext[NS];
+      if (nn < P) draw_u(nn, ni, unext, znext);
       double hd[NS + NS * (NS - 1) + NS];
 #pragma unroll
       for (int q = 0; q < NS + NS * (NS - 1) + NS; ++q) hd[q] = r[q];
@@ -984,7 +1070,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
           ++y;
         }
         uint8_t fl = 0;
-        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, ucur[a], fl);
+        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, ucur[a], zcur[a], fl);
         if (e.flags && j == 0) e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
       }
       if (j == 0) {
@@ -994,7 +1080,10 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
       n = nn;
       i = ni;
 #pragma unroll
-      for (int a = 0; a < NS; ++a) ucur[a] = unext[a];
+      for (int a = 0; a < NS; ++a) {
+        ucur[a] = unext[a];
+        zcur[a] = znext[a];
+      }
     }
     prog = (n < P) ? n * nc + i : done_all;
   }

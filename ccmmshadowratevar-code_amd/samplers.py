@@ -585,7 +585,8 @@ def save_qrt_mat(filename, res, *, data, ydates, p, ncode, tcode, cumcode, ndxSH
              missingrateVintagesMid=np.full((Tdata, Ns, V), np.nan),
              missingrateVintagesTails=np.full((Tdata, Ns, 4, V), np.nan))
     for k, v in res.items():
-        if k.startswith(("fcst", "PAI", "shadowrate")) and isinstance(v, np.ndarray):
+        # the reference's wildcards; shadowratePSRFchains (psrf across chains) is not a reference output
+        if k.startswith(("fcst", "PAI", "shadowrate")) and k != "shadowratePSRFchains" and isinstance(v, np.ndarray):
             m[k] = v[None, :] if v.ndim == 1 else v
     savemat(filename, m, do_compression=True)
     return sorted(m)
@@ -734,8 +735,9 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
 
     keep_draws=True also returns the kept draws per vintage: PAI_all[v] (M x K x N x C) and
     shadowrate_all[v] (M x Ns x elbT x C).  shadowratePSRF (Ns x V) is DiagnosticsShadowrate of each
-    vintage's kept shadow rates over the months at the ELB (:322-325, ccmm_shadowrate_psrf; one chain:
-    the reference's first-third / last-third split, C chains: psrf over the chains).
+    vintage's kept shadow rates over the months at the ELB (:322-325, ccmm_shadowrate_psrf: the
+    reference's first-third / last-third split of each chain, averaged over the C chains);
+    shadowratePSRFchains the psrf across the C chains (NaN for one chain; not a reference output).
 
     engine="native" runs the rank's vintage loop (chain set, burn-in, kept sweeps, forecast
     records, device summaries, retries) inside the library, ccmm_run_batch (include/ccmm.h): the
@@ -988,6 +990,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                 # goVARshadowrateBlockHybrid.m:322-325: DiagnosticsShadowrate per shadow rate over
                 # its months at the ELB, ELBdummy(startELB:thisT, s)
                 r["shadowratePSRF"] = _abi.shadowrate_psrf(shadow[..., cs], elbdummy[startELB - 1:thisT].T)
+                r["shadowratePSRFchains"] = _abi.shadowrate_psrf(shadow[..., cs], elbdummy[startELB - 1:thisT].T,
+                                                                 chains=True)
             if shadow is not None and bm.elbT > 0:
                 # shadowrate_all permuted to (Nobs, Ns, draws) (:329-334)
                 sr = shadow[:, :, :bm.elbT, cs].transpose(2, 1, 0, 3).reshape(bm.elbT, Ns, -1)
@@ -1051,6 +1055,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
                PAImean=np.full((K, N, V), np.nan), PAIstdev=np.full((K, N, V), np.nan),
                countELBaccept=np.full(V, -1),
                shadowratePSRF=np.full((Ns, V), np.nan),                      # :213
+               shadowratePSRFchains=np.full((Ns, V), np.nan),                # psrf across chains (no ref.)
                shadowrateVintagesMid=np.full((Tdata, Ns, V), np.nan),
                shadowrateVintagesTails=np.full((Tdata, Ns, 4, V), np.nan))
     if is_sr:
@@ -1094,6 +1099,8 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
             out["countELBaccept"][v] = r["countELBaccept"]
         if "shadowratePSRF" in r:
             out["shadowratePSRF"][:, v] = r["shadowratePSRF"]
+        if "shadowratePSRFchains" in r:
+            out["shadowratePSRFchains"][:, v] = r["shadowratePSRFchains"]
         if "shadowrateMid" in r:
             thisT = r["thisT"]
             out["shadowrateVintagesMid"][jumpoff:thisT, :, v] = r["shadowrateMid"]
@@ -1186,6 +1193,7 @@ def _native_batch(ctx, units, mine, *, C, N, p, K, Ns, H, Nd, MCMCdraws, burn, g
                      fcstYmvlogscoreDraws=out["scoreDraws"][:, 1, i], fcstYmvlogscoreXdraws=out["scoreDraws"][:, 2, i],
                      fcstYmvlogscoreIdraws=out["scoreDraws"][:, 3, i])
         r["shadowratePSRF"] = out["shadowratePSRF"][:, i].copy()          # :322-325
+        r["shadowratePSRFchains"] = out["shadowratePSRFchains"][:, i].copy()
         if bm.elbT > 0:
             sh = out["shadowrate_all"][:, :, :bm.elbT, :, i]                 # M x Ns x elbT x C
             sr = sh.transpose(2, 1, 0, 3).reshape(bm.elbT, Ns, -1)

@@ -510,7 +510,10 @@ typedef struct {                /* V = number of vintages; any pointer may be NU
   double* PAIquantiles;         /* K x N x nq x V */
   double* scoreDraws;           /* (fcstNdraws * nchains) x 4 x V, order (Nd, kept draw, chain) */
   double* shadowratePSRF;       /* Ns x V (shadow-rate models): ccmm_shadowrate_psrf of the vintage's kept
-                                   shadow rates (goVARshadowrateBlockHybrid.m:322-325) */
+                                   shadow rates (goVARshadowrateBlockHybrid.m:322-325; the reference's
+                                   one-chain statistic, averaged over the vintage's chains) */
+  double* shadowratePSRFchains; /* Ns x V: ccmm_shadowrate_psrf_chains (psrf across the vintage's chains;
+                                   NaN for one chain) -- not in the reference's output */
 } ccmm_batch_out;
 
 int ccmm_run_batch(ccmm_ctx* ctx, const ccmm_batch_config* cfg, int V, const ccmm_vintage* vintages,
@@ -558,14 +561,20 @@ int ccmm_psrf(int n, int D, int M, const double* X, double* R);
  * goVARshadowrate.m:332-333): for each shadow rate s, DiagnosticsShadowrate(shadowrate_all(:, s,
  * ELBdummy(startELB:thisT, s))) = the mean of psrf over the rate's censored months (NaN when there
  * are none).  draws M x Ns x ldT x C (the kept shadow rates of C chains; the first elbT months are
- * the vintage's window), mask Ns x elbT (ELBdummy(startELB:thisT, :)', = elb.sNaN).  C == 1: the
- * reference's one-chain split; C > 1: psrf over the C chains as sequences.  out: Ns (NaN where psrf
- * would stop with 'Too few samples': M < 3 at C == 1, M < 2 at C > 1).  The
+ * the vintage's window), mask Ns x elbT (ELBdummy(startELB:thisT, :)', = elb.sNaN).  The reference's
+ * one-chain statistic (first / last thirds, :82-91) for every chain, averaged over the C chains, so the
+ * value keeps the reference's meaning for any C.  out: Ns (NaN where psrf would stop with 'Too few
+ * samples': M < 3).  The
  * reference's DiagnosticsShadowrate also evaluates ineff() (momentg), which errors below 100 draws
  * (Diagnostics.m momentg 'needs a larger number of ndraws'); its result is not an output and the
  * check is not reproduced. */
 int ccmm_shadowrate_psrf(int M, int Ns, int elbT, int ldT, int C, const double* draws, const uint8_t* mask,
                          double* out);
+/* The multi-chain form (no reference counterpart; parity unpinned beyond the psrf formula): per cell,
+ * psrf over the C chains as its M-draw sequences (Brooks-Gelman across chains), averaged over the rate's
+ * months at the ELB as ccmm_shadowrate_psrf.  out: Ns, NaN when C < 2 or M < 2. */
+int ccmm_shadowrate_psrf_chains(int M, int Ns, int elbT, int ldT, int C, const double* draws, const uint8_t* mask,
+                                double* out);
 
 /* Predictive density of one kept draw per chain, batched over B chains.
  * Replaces the doPredictiveDensity block mcmcVAR.m:298-381 (same simulation in

@@ -89,3 +89,10 @@ def diagnostics_shadowrate(draws):
     if draws.shape[1] == 0:
         return float("nan")
     return float(np.mean(psrf(draws)))
+
+
+def diagnostics_shadowrate_chain_mean(draws):
+    """DiagnosticsShadowrate (one-chain form: first / last thirds) of each of the C chains of draws
+    n x nObs x C, averaged over the chains: the reference's statistic for a multi-chain run."""
+    draws = np.asarray(draws, dtype=float)
+    return float(np.mean([diagnostics_shadowrate(draws[:, :, c]) for c in range(draws.shape[2])]))

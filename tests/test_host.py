@@ -156,7 +156,7 @@ def test_vintage_batch_argument_checks(pkg, fred):
 def test_psrf_entry_points_match_oracle(pkg):
     """ccmm_psrf / ccmm_shadowrate_psrf (host computations inside libccmm) against the oracle's psrf
     restatement (DiagnosticsShadowrate.m:34-128): one chain (thirds), C chains, the ELB mask."""
-    from oracle.ccmm_oracle_stats import psrf, diagnostics_shadowrate
+    from oracle.ccmm_oracle_stats import psrf, diagnostics_shadowrate, diagnostics_shadowrate_chain_mean
     A = pkg._abi
     rng = np.random.default_rng(11)
     X = np.cumsum(rng.standard_normal((301, 6)), axis=0)
@@ -169,13 +169,16 @@ def test_psrf_entry_points_match_oracle(pkg):
         mask = rng.random((Ns, elbT)) < 0.5
         mask[2] = False                                # rate with no month at the ELB: NaN
         got = A.shadowrate_psrf(d, mask)
+        gotc = A.shadowrate_psrf(d, mask, chains=True)
         for s in range(Ns):
             cells = d[:, s, :elbT, :][:, mask[s], :]
-            want = diagnostics_shadowrate(cells[:, :, 0] if C == 1 else cells)
-            if np.isnan(want):
-                assert np.isnan(got[s])
-            else:
-                assert abs(got[s] - want) < 1e-12 * max(1.0, abs(want)), (C, s, got[s], want)
+            want = diagnostics_shadowrate_chain_mean(cells)     # the reference's statistic per chain
+            wantc = diagnostics_shadowrate(cells) if C > 1 else np.nan   # psrf across the chains
+            for g, w in ((got[s], want), (gotc[s], wantc)):
+                if np.isnan(w):
+                    assert np.isnan(g)
+                else:
+                    assert abs(g - w) < 1e-12 * max(1.0, abs(w)), (C, s, g, w)
     assert np.all(np.isnan(A.shadowrate_psrf(np.ones((2, 2, 3)), np.ones((2, 3), bool))))   # too few draws
 
 
