@@ -1,9 +1,10 @@
 """Driver of the compiled CPU restatement (oracle/cpu_sweep.cpp) -- TEST / BASELINE INFRASTRUCTURE ONLY:
 bench.py's cpu_baseline leg and tests/test_cpu_baseline.py call it; the product never does.
 
-The linear sweep of mcmcVAR.m:211-274 as written (kron-materialised CTA, explicit inverse), one
-single-threaded process per chain (the parfor worker of goVAR*.m), BLAS / LAPACK from the OpenBLAS
-that numpy and scipy use (opened by the binary with dlopen)."""
+The linear sweep of mcmcVAR.m:211-274 as written (kron-materialised CTA, explicit inverse) and the
+block-hybrid sweep of mcmcVARshadowrateBlockHybrid.m:332-520 as written (kron CTAsys, the QR form of
+gibbsdrawShadowrates), one single-threaded process per chain (the parfor worker of goVAR*.m), BLAS /
+LAPACK from the OpenBLAS that numpy and scipy use (opened by the binary with dlopen)."""
 from __future__ import annotations
 
 import json
@@ -33,14 +34,23 @@ def ensure_built():
     return BIN
 
 
-def write_state(path, su, st):
-    """state.bin of cpu_sweep.cpp: the setup (oracle.var_setup) and a chain state."""
+def write_state(path, su, st, bs=None):
+    """state.bin of cpu_sweep.cpp: the setup (oracle.var_setup) and a chain state; with bs (an
+    oracle.ccmm_oracle_bh.BHSetup) the block-hybrid block, Y / X then being the chain's shadow-rate data
+    (st["Y"], st["X"])."""
     F = lambda a: np.asfortranarray(np.asarray(a, np.float64)).ravel(order="F")
+    Y, X = (st["Y"], st["X"]) if bs is not None else (su.Y, su.X)
     with open(path, "wb") as fh:
         np.array([su.N, su.K, su.T, su.dPHI], np.int32).tofile(fh)
-        for a in (su.Y, su.X, su.iVdiag, su.iVb, su.sPHI, su.Vol_0mean, su.Vol_0vcvsqrt,
+        for a in (Y, X, su.iVdiag, su.iVb, su.sPHI, su.Vol_0mean, su.Vol_0vcvsqrt,
                   np.array([su.logy2offset]), st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"]):
             F(a).tofile(fh)
+        if bs is not None:
+            np.array([0x31304842, su.p, len(bs.ndxS), bs.elbT0, bs.elbT, bs.gibbsburn, bs.Ydata.shape[0]],
+                     np.int32).tofile(fh)
+            for a in (np.array([bs.ELB]), bs.Xactual, bs.actualrateBlock.astype(float),
+                      np.asarray(bs.ndxS, float), bs.sNaN.astype(float), bs.Ydata):
+                F(a).tofile(fh)
 
 
 def _env():
@@ -51,22 +61,25 @@ def _env():
     return env
 
 
-def crn_sweep(su, st, crn, workdir):
-    """One sweep on the injected common random numbers (oracle.crn_sizes order); returns the new
-    PAI, A, sqrtht, h, sqrtPHI and the KSC indicators."""
+def crn_sweep(su, st, crn, workdir, bs=None):
+    """One sweep on the injected common random numbers (oracle.crn_sizes order; block hybrid: + uELB);
+    returns the new PAI, A, sqrtht, h, sqrtPHI, the KSC indicators and (bs) the shadow rates."""
     ensure_built()
     workdir = Path(workdir)
     sp, cp, op = workdir / "state.bin", workdir / "crn.bin", workdir / "out.bin"
-    write_state(sp, su, st)
+    write_state(sp, su, st, bs)
     with open(cp, "wb") as fh:
-        for k in ("zPAI", "zA", "uSV", "zSV", "zPHI"):
+        for k in ("zPAI", "zA", "uSV", "zSV", "zPHI") + (("uELB",) if bs is not None else ()):
             np.asfortranarray(crn[k], dtype=np.float64).ravel(order="F").tofile(fh)
     subprocess.run([str(BIN), "crn", str(sp), str(cp), str(op)], check=True, env=_env(), capture_output=True)
     v = np.fromfile(op, np.float64)
     N, K, T = su.N, su.K, su.T
     out, o = {}, 0
-    for k, shp in (("PAI", (K, N)), ("A", (N, N)), ("sqrtht", (T, N)), ("h", (T, N)), ("sqrtPHI", (N, N)),
-                   ("kai", (N, T))):
+    shapes = [("PAI", (K, N)), ("A", (N, N)), ("sqrtht", (T, N)), ("h", (T, N)), ("sqrtPHI", (N, N)),
+              ("kai", (N, T))]
+    if bs is not None:
+        shapes.append(("shadowrate", (len(bs.ndxS), bs.elbT)))
+    for k, shp in shapes:
         n = int(np.prod(shp))
         out[k] = v[o:o + n].reshape(shp, order="F")
         o += n
