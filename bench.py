@@ -635,14 +635,25 @@ def bench_block_hybrid(pkg, ctx, d, B, args, rank, barrier, dist):
         # minus the Ns x Ns Omega block: 228 doubles at Ns=3, p=12) once per pass and reads
         # and writes the chain's Ns x elbT shadow rates once (ccmm_elb.hip k_elb_gibbs)
         if kt.get("k_elb_gibbs", (0, 0))[1]:
+            # the ELB passes are bound by VALU issue and the dependent month-to-month chain, not by HBM
+            # (the month records stay in L2): report the VALU issue fraction from the newest committed
+            # PMC summary of this line (tools/gpu/pmc_issue.sh: SQ_INSTS_VALU x 4 cycles per wave64
+            # instruction over the chip's SIMD cycles; profiles/*pmc_issue*.json), beside the record bytes
             rec = Ns + Ns * (Ns - 1) + Ns + 2 * p * Ns * Ns
             nbytes = B * (101 * ncens * rec * 8 + 2 * 8 * Ns * bm.elbT)
             ms = kt["k_elb_gibbs"][0] / kt["k_elb_gibbs"][1]
             gbs = nbytes / (ms * 1e-3) / 1e9
-            res["elb_gibbs"] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                "bytes_per_launch": int(nbytes), "avg_launch_ms": round(ms, 4),
-                                "note": "one wave per chain, 101 sequential passes: latency-bound"}
+            res["elb_gibbs"] = {"bound": "valu-issue + dependent latency", "avg_launch_ms": round(ms, 4),
+                                "record_bytes_per_launch": int(nbytes), "record_GBs": round(gbs, 1),
+                                "note": "101 sequential passes per chain, up to 8 in flight as a wavefront"}
+            pmc, src = load_pmc("*pmc_issue*.json")
+            for kn in ("k_elb_gibbs_wf", "k_elb_gibbs_oct", "k_elb_gibbs"):
+                if pmc.get(kn, {}).get("valu_issue_frac") is not None:
+                    res["elb_gibbs"].update(valu_issue_frac=round(pmc[kn]["valu_issue_frac"], 4),
+                                            issue_kernel=kn, issue_source=src,
+                                            issue_note="PMC pass over the B = 256 block-hybrid sweep "
+                                                       "(tools/kernel_times_bh.py 256)")
+                    break
     ch.close()
     return res
 
@@ -826,16 +837,16 @@ def bench_s120(pkg, ctx, B, args, rank, barrier, dist, groups=None):
     return res
 
 
-def load_pmc():
-    """HBM bytes per launch from the newest committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, written by tools/pmc_summary.py from separate
-    FETCH_SIZE / WRITE_SIZE passes over this same bench command)."""
+def load_pmc(pattern="*_pmc.json"):
+    """Per-kernel counters from the newest committed rocprofv3 PMC summary (profiles/<pattern>, written
+    by tools/pmc_summary.py from separate passes: FETCH_SIZE / WRITE_SIZE over this same bench command
+    for HBM bytes; the issue counters for the ELB passes)."""
     import re
 
     def natural(pth):  # r01_v11 after r01_v9
         return [int(x) if x.isdigit() else x for x in re.split(r"(\d+)", pth.name)]
 
-    files = sorted((ROOT / "profiles").glob("*_pmc.json"), key=natural)
+    files = sorted((ROOT / "profiles").glob(pattern), key=natural)
     if not files:
         return {}, None
     try:

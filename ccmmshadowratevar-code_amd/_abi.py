@@ -147,6 +147,7 @@ _SIGS = {
     "ccmm_chains_get_missingrate": (C.c_int, [C.c_void_p, _dp]),
     "ccmm_chains_get_xy": (C.c_int, [C.c_void_p, _dp, _dp]),
     "ccmm_chains_profile": (C.c_int, [C.c_void_p, C.c_int]),
+    "ccmm_chains_pai_moments": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp]),
     "ccmm_chains_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _dp, _i64p, C.c_char_p, C.c_int]),
     "ccmm_fcst": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp,
                             _dp, _dp, _dp, _dp, _u8p, C.c_double, _dp, _dp, C.c_uint64,

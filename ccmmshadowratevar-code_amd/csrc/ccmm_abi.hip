@@ -255,6 +255,8 @@ struct ccmm_chains {
   DBuf<double> crn;
   // storage of kept draws
   DBuf<double> sPAI, sPHI_, sInvA, sSqrtht, sShadow;
+  DBuf<double> paiMom;  // running PAI sums | sums of squares (ccmm_chains_pai_moments)
+  int mom_done = 0;     // stored draws already added to paiMom
   // block-hybrid ELB model (mcmcVARshadowrateBlockHybrid.m): X/Y slabs 0..ndata-1 hold
   // the vintages' actual data, slabs ndata + c the chain's shadow-rate data
   bool bh = false;
@@ -326,6 +328,12 @@ struct ccmm_chains {
   hipEvent_t mfma_ev = nullptr;
 
   ~ccmm_chains() {
+    if (aux) {
+      (void)hipStreamSynchronize(aux);
+      (void)hipEventDestroy(evFork);
+      (void)hipEventDestroy(evJoin);
+      (void)hipStreamDestroy(aux);
+    }
     if (mfma_ev) {
       PhaseLock& L = phase_lock(ctx->device, mfma_lock);
       std::lock_guard<std::mutex> g(L.m);
@@ -351,19 +359,32 @@ struct ccmm_chains {
   }
 
   template <class L>
-  void launch(int kid, L&& fn) {
+  void launch(int kid, L&& fn, hipStream_t on = nullptr) {
     hipEvent_t a = nullptr, b = nullptr;
+    hipStream_t st = on ? on : ctx->stream;
     if (profiling) {
       a = get_event();
       b = get_event();
-      HIPCHECK(hipEventRecord(a, ctx->stream));
+      HIPCHECK(hipEventRecord(a, st));
     }
     fn();
     HIPCHECK(hipGetLastError());
     if (profiling) {
-      HIPCHECK(hipEventRecord(b, ctx->stream));
+      HIPCHECK(hipEventRecord(b, st));
       pending.push_back({kid, a, b});
     }
+  }
+
+  // auxiliary stream of the sweep: the inverse-Wishart block runs on it beside the ELB step, which
+  // reads none of its inputs or outputs (mcmcVARshadowrateBlockHybrid.m:386-392 vs :395-520); the
+  // main stream waits for it before the draw store, the forecasts and the next sweep's SV block
+  hipStream_t aux = nullptr;
+  hipEvent_t evFork = nullptr, evJoin = nullptr;
+  void ensure_aux() {
+    if (aux) return;
+    HIPCHECK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+    HIPCHECK(hipEventCreateWithFlags(&evFork, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
   }
 
   void collect_profile() {
@@ -1239,17 +1260,18 @@ struct ccmm_chains {
     });
   }
 
-  void run_phi(const RngArgs& ra) {
+  void run_phi(const RngArgs& ra, hipStream_t on = nullptr) {
     if (d.N > kMaxNSmall) {
       run_phi_big(ra);
       return;
     }
+    hipStream_t st = on ? on : ctx->stream;
     Zphi.alloc((size_t)d.B * d.N * (d.TP + cfg.dPHI));
     ChainState cs = view();
     launch(KID_PHIGEN, [&] {
       hipLaunchKernelGGL(k_phi_gen, dim3((d.N * (d.TP + cfg.dPHI) + 255) / 256, d.B), dim3(256), 0,
-                         ctx->stream, d, Tslot.p, cfg.dPHI, cs, ra);
-    });
+                         st, d, Tslot.p, cfg.dPHI, cs, ra);
+    }, st);
     size_t lds = (size_t)(4 * d.N * (d.N + 1)) * sizeof(double);
     const size_t staged = lds + (size_t)d.N * (d.TP + 1) * sizeof(double);
     const int stage_eta = staged <= 160 * 1024 ? 1 : 0;
@@ -1260,9 +1282,8 @@ struct ccmm_chains {
                                      (int)lds));
     }
     launch(KID_PHI, [&] {
-      hipLaunchKernelGGL(k_phi, dim3(d.B), dim3(256), lds, ctx->stream, d, Tslot.p, cfg.dPHI,
-                         sPHI.p, cs, stage_eta);
-    });
+      hipLaunchKernelGGL(k_phi, dim3(d.B), dim3(256), lds, st, d, Tslot.p, cfg.dPHI, sPHI.p, cs, stage_eta);
+    }, st);
   }
 
   void run_store() {
@@ -1767,6 +1788,8 @@ struct ccmm_chains {
   // of Kailath's array where it fails) from the same previous draw and normals; status
   // bit 2 is then replaced by bit 1 ("QR fallback used", informational).  CCMM_FORCE_QR=1
   // routes every chain through the host QR branch (tests); CCMM_NO_QR_FALLBACK=1 disables.
+  // CCMM_PHI_OVERLAP=0: the PHI block in stream order before the ELB step (A/B; same draws)
+  bool phi_overlap = env_select("CCMM_PHI_OVERLAP", 1) != 0;
   bool qr_fallback = std::getenv("CCMM_NO_QR_FALLBACK") == nullptr;
   bool force_qr = std::getenv("CCMM_FORCE_QR") != nullptr;
   DBuf<double> paiPrev, zHost;
@@ -1883,8 +1906,21 @@ struct ccmm_chains {
     cta_fallback(ra);
     run_astep(ra);
     run_sv(ra);
-    run_phi(ra);
-    if (bh) run_elb(ra, store);
+    // block hybrid, N <= 32: the PHI block on the auxiliary stream beside the ELB step (the ELB kernels
+    // read PAI, A, invA, sqrtht and the chain's data; PHI reads eta and writes sqrtPHI / PHI / Zphi)
+    const bool fork = bh && cfg.elbTmax > 0 && d.N <= kMaxNSmall && phi_overlap;
+    if (fork) {
+      ensure_aux();
+      HIPCHECK(hipEventRecord(evFork, ctx->stream));
+      HIPCHECK(hipStreamWaitEvent(aux, evFork, 0));
+      run_phi(ra, aux);
+      HIPCHECK(hipEventRecord(evJoin, aux));
+      run_elb(ra, store);
+      HIPCHECK(hipStreamWaitEvent(ctx->stream, evJoin, 0));
+    } else {
+      run_phi(ra);
+      if (bh) run_elb(ra, store);
+    }
     if (store) run_store();
     if (store && have_fcst) run_fcst(ra);
     ++sweep;
@@ -2834,6 +2870,37 @@ int ccmm_chains_get_draws(ccmm_chains* ch, double* PAI_all, double* PHI_all, dou
     fetch(ch->sSqrtht, T * N, sqrtht_all);
     if (ch->bh && ch->cfg.elbTmax > 0) fetch(ch->sShadow, (size_t)ch->cfg.Ns * ch->cfg.elbTmax, shadowrate_all);
     ch->stored = 0;
+    ch->mom_done = 0;
+    return 0;
+  });
+}
+
+int ccmm_chains_pai_moments(ccmm_chains* ch, int reset, double* sum, double* sumsq) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    HIPCHECK(hipSetDevice(ch->ctx->device));
+    const size_t B = ch->d.B, per = (size_t)ch->d.K * ch->d.N;
+    if (!ch->paiMom.p || reset) {
+      ch->paiMom.alloc(2 * B * per);
+      HIPCHECK(hipMemsetAsync(ch->paiMom.p, 0, 2 * B * per * sizeof(double), ch->ctx->stream));
+      ch->mom_done = 0;
+    }
+    if (ch->stored > ch->mom_done && ch->sPAI.p) {
+      hipLaunchKernelGGL(k_pai_moments, dim3((unsigned)((B * per + 255) / 256)), dim3(256), 0, ch->ctx->stream,
+                         ch->sPAI.p, ch->cfg.store_capacity, ch->mom_done, ch->stored, (int)per, (int)B,
+                         ch->paiMom.p, ch->paiMom.p + B * per);
+      HIPCHECK(hipGetLastError());
+      ch->mom_done = ch->stored;
+    }
+    if (sum || sumsq) {
+      std::vector<double> buf(2 * B * per);
+      HIPCHECK(hipMemcpyAsync(buf.data(), ch->paiMom.p, buf.size() * sizeof(double), hipMemcpyDeviceToHost,
+                              ch->ctx->stream));
+      HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
+      // device [c][e] (e = a + K j) -> K x N x B
+      if (sum) std::copy(buf.begin(), buf.begin() + B * per, sum);
+      if (sumsq) std::copy(buf.begin() + B * per, buf.end(), sumsq);
+    }
     return 0;
   });
 }

@@ -220,7 +220,7 @@ struct Runner {
       Psum.assign(KN * B, 0.0);
       P2sum.assign(KN * B, 0.0);
     }
-    std::vector<double> sc, fy, fyc, Pd, sd;
+    std::vector<double> sc, fy, fyc, sd;
     for (int done = 0; done < M;) {
       const int n = std::min(chunk, M - done);
       check(ccmm_chains_sweep(ch, n, nullptr, 1));
@@ -229,9 +229,11 @@ struct Runner {
         fy.assign(NH * B, 0.0);
         fyc.assign(NH * B, 0.0);
         fcst_rc(ccmm_chains_get_fcst(ch, sc.data(), fy.data(), fyc.data(), nullptr, nullptr, nullptr));
-        Pd.assign(size_t(n) * KN * B, 0.0);
         if (!shadowd.empty()) sd.assign(size_t(n) * Ns * eT * B, 0.0);
-        check(ccmm_chains_get_draws(ch, Pd.data(), nullptr, nullptr, nullptr, sd.empty() ? nullptr : sd.data()));
+        // PAI sums over the draws on the device (running, in draw order: the host loop's order and
+        // rounding), so the draws themselves never cross PCIe
+        check(ccmm_chains_pai_moments(ch, done == 0, nullptr, nullptr));
+        check(ccmm_chains_get_draws(ch, nullptr, nullptr, nullptr, nullptr, sd.empty() ? nullptr : sd.data()));
         for (size_t i = 0; i < NH * B; ++i) {
           fYsum[i] += fy[i];
           fYcsum[i] += fyc[i];
@@ -240,19 +242,13 @@ struct Runner {
         for (size_t kb = 0; kb < size_t(4) * B; ++kb)
           std::copy(sc.begin() + kb * Nd * n, sc.begin() + (kb + 1) * Nd * n,
                     scores.begin() + kb * Nd * M + size_t(done) * Nd);
-        // PAI_all n x K x N x B: sums over the draws
-        for (size_t e = 0; e < KN * B; ++e)
-          for (int m = 0; m < n; ++m) {
-            const double x = Pd[e * n + m];
-            Psum[e] += x;
-            P2sum[e] += x * x;
-          }
         if (!shadowd.empty())  // n x (Ns eT B) into M x (Ns eT B)
           for (size_t e = 0; e < size_t(Ns) * eT * B; ++e)
             for (int m = 0; m < n; ++m) shadowd[e * M + done + m] = sd[e * n + m];
       }
       done += n;
     }
+    if (!cf.postprocess) check(ccmm_chains_pai_moments(ch, 0, Psum.data(), P2sum.data()));
     std::vector<int> status(B, 0), ca(B, 0), cb(B, 0);
     check(ccmm_chains_get_status(ch, status.data()));
     if (ps) check(ccmm_chains_get_ps(ch, ca.data(), cb.data(), nullptr));

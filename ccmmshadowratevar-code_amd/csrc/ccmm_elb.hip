@@ -998,16 +998,17 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
   int prog = (n < P) ? n * nc : done_all;
   // the uniforms of the slot's next month (rand(Ns, elbT) page n, gibbsdrawShadowrates.m:173) are
   // drawn one step ahead, so the generator stays off the month-to-month dependence chain
-  auto draw_u = [&](int nn, int ii, double (&uu)[NS], double (&zz)[NS]) {
+  // (no precomputed AS241 here, unlike the wave kernels: the eight passes of a wave draw different
+  // months, so the fast path of elb_trunc_normal_pz would only help when all eight take it at once, and
+  // the per-step precompute costs more issue than it saves; the full evaluation gives the same bits)
+  auto draw_u = [&](int nn, int ii, double (&uu)[NS]) {
     const int tt = Tm[ii] & 0xffff;
 #pragma unroll
-    for (int a = 0; a < NS; ++a) {
+    for (int a = 0; a < NS; ++a)
       uu[a] = (e.mode & 2) ? 0.5 : rng.uniform(CCMM_RNG_ELB, (uint32_t)(tt * NS + a + T * NS * nn));
-      zz[a] = (e.mode & 2) ? 0.0 : elb_ppnd16(uu[a]);
-    }
   };
-  double ucur[NS], zcur[NS];
-  if (n < P) draw_u(n, 0, ucur, zcur);
+  double ucur[NS];
+  if (n < P) draw_u(n, 0, ucur);
   // exit condition every wave reaches: the wavefront needs at most P nc + W (nc + 1) steps
   const int max_steps = P * nc + W * (nc + 1) + 8;
   for (int step = 0; step < max_steps; ++step) {
@@ -1024,8 +1025,8 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
         ni = 0;
         nn = n + W;
       }
-      double unext[NS], znext[NS];
-      if (nn < P) draw_u(nn, ni, unext, znext);
+      double unext[NS];
+      if (nn < P) draw_u(nn, ni, unext);
       double hd[NS + NS * (NS - 1) + NS];
 #pragma unroll
       for (int q = 0; q < NS + NS * (NS - 1) + NS; ++q) hd[q] = r[q];
@@ -1070,7 +1071,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
           ++y;
         }
         uint8_t fl = 0;
-        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, ucur[a], zcur[a], fl);
+        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, ucur[a], fl);
         if (e.flags && j == 0) e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
       }
       if (j == 0) {
@@ -1080,10 +1081,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
       n = nn;
       i = ni;
 #pragma unroll
-      for (int a = 0; a < NS; ++a) {
-        ucur[a] = unext[a];
-        zcur[a] = znext[a];
-      }
+      for (int a = 0; a < NS; ++a) ucur[a] = unext[a];
     }
     prog = (n < P) ? n * nc + i : done_all;
   }

@@ -981,6 +981,23 @@ __global__ void k_store(Dims d, ChainState cs, Store st) {
   }
 }
 
+// running sums of the stored PAI draws m0 <= m < m1 per (chain, entry), in store order; no contraction
+// (x * x rounded, then added), the order and rounding of the host loop it replaces
+__global__ void k_pai_moments(const double* __restrict__ sPAI, int cap, int m0, int m1, int per, int B,
+                              double* __restrict__ sum, double* __restrict__ sumsq) {
+  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (size_t)B * per) return;
+  const size_t c = q / per, e = q - c * per;
+  double s = sum[q], s2 = sumsq[q];
+  for (int m = m0; m < m1; ++m) {
+    const double x = sPAI[(c * cap + m) * per + e];
+    s = __dadd_rn(s, x);
+    s2 = __dadd_rn(s2, __dmul_rn(x, x));
+  }
+  sum[q] = s;
+  sumsq[q] = s2;
+}
+
 // ============================================================== truncated normal
 // drawTruncNormal.m:53-86: inverse CDF, upper truncation at elb.
 __device__ __forceinline__ double trunc_normal_dev(double mu, double sig, double elb, double u,

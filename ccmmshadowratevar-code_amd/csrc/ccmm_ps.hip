@@ -281,9 +281,14 @@ __device__ inline bool ps_backsub(const double* __restrict__ Lc, const double* _
 #pragma unroll
   for (int j = 0; j < W - 1; ++j) win[j] = 0.0;
   bool ok = true;
+  // the normal of the next cell is drawn while this cell's dependent chain of W fused multiply-adds
+  // runs (the generator does not depend on the substitution): software-pipelined by one cell
+  double znext = rng.normal(CCMM_RNG_PS, (uint32_t)(n - 1 + n * k));
   for (int i = n - 1; i >= 0; --i) {
     const double* li = Lc + (size_t)i * W;
-    double v = yb[i] + rng.normal(CCMM_RNG_PS, (uint32_t)(i + n * k));
+    const double z = znext;
+    if (i > 0) znext = rng.normal(CCMM_RNG_PS, (uint32_t)(i - 1 + n * k));
+    double v = yb[i] + z;
 #pragma unroll
     for (int j = 1; j < W; ++j) v = fma(-li[j], win[j - 1], v);
     v /= li[0];

@@ -282,6 +282,12 @@ int ccmm_chains_stored(const ccmm_chains* ch);
  *   NaN beyond a vintage's elbT).  Any pointer may be NULL.  Resets the store. */
 int ccmm_chains_get_draws(ccmm_chains* ch, double* PAI_all, double* PHI_all, double* invA_all,
                           double* sqrtht_all, double* shadowrate_all);
+/* Running moments of the stored PAI draws on the device (the PAImean / PAIstdev accumulation of
+ * goVARshadowrateBlockHybrid.m:376-377 without copying every draw to the host): adds the draws stored
+ * so far (in store order, x then x * x, one rounding each) to per-chain running sums, reset first when
+ * reset != 0; copies the sums out (K x N x B each) when the pointers are non-NULL.  Does not reset the
+ * store (call before ccmm_chains_get_draws). */
+int ccmm_chains_pai_moments(ccmm_chains* ch, int reset, double* sum, double* sumsq);
 
 /* ---- predictive density inside the chain set (post-burn-in block of
  *      mcmcVAR.m:298-381 and mcmcVARshadowrateBlockHybrid.m:550-669) ----

@@ -60,6 +60,10 @@ def main(out, *dirs):
             r["mfma_f64_flop"] = 512.0 * r["SQ_INSTS_VALU_MFMA_MOPS_F64"]
         if "SQ_VALU_MFMA_BUSY_CYCLES" in r and r.get("GRBM_GUI_ACTIVE"):
             r["mfma_busy_frac"] = r["SQ_VALU_MFMA_BUSY_CYCLES"] / (r["GRBM_GUI_ACTIVE"] / 8.0 * 256 * 4)
+        if "SQ_INSTS_VALU" in r and r.get("GRBM_GUI_ACTIVE"):
+            # VALU issue: a wave64 VALU instruction holds its SIMD for 4 cycles (16 lanes per cycle; FP64
+            # FMA is full rate on gfx950), over every SIMD cycle of the chip while the kernel runs
+            r["valu_issue_frac"] = 4.0 * r["SQ_INSTS_VALU"] / (r["GRBM_GUI_ACTIVE"] / 8.0 * 256 * 4)
         res[k] = r
     Path(out).write_text(json.dumps(res, indent=1, sort_keys=True))
     for k in sorted(res):
