@@ -1484,11 +1484,18 @@ struct ccmm_chains {
       phi_lds |= 2;
       lds_prep = lds_zy;
     }
+    // small batches: the window's residual rows over several workgroups per chain (Yb / Z in LDS)
+    int prep_rows = 0, prep_wg = 1;
+    if ((phi_lds & 2) && d.B < 128) {
+      const int per = std::max(1, 256 / d.B);
+      prep_rows = std::max(16, (cfg.elbTmax + per - 1) / per);
+      prep_wg = (cfg.elbTmax + prep_rows - 1) / prep_rows;
+    }
     launch(KID_ELBPREP, [&] {
       HIPCHECK(hipFuncSetAttribute((const void*)k_elb_prep, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds_prep));
-      hipLaunchKernelGGL(k_elb_prep, dim3(d.B), dim3(kElbPrepThreads), lds_prep, ctx->stream, d, e, xsel(), cs,
-                         phi_lds);
+      hipLaunchKernelGGL(k_elb_prep, dim3(d.B, prep_wg), dim3(kElbPrepThreads), lds_prep, ctx->stream, d, e, xsel(),
+                         cs, phi_lds, prep_rows);
     });
     size_t lds_cond =
         (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns + N * Ns + N * p * Ns) * sizeof(double);

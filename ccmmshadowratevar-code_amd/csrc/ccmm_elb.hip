@@ -87,8 +87,12 @@ __host__ __device__ inline int elb_cond_stride(int Ns, int p, int ps = 0) {
 //   Yt[τ] = Yb_τ   (the chain's Y with censored shadow-rate cells at 0)
 //   Et[τ] = ε_τ = Yb_τ - Σ_{l<=τ} Φ_l Yb_{τ-l} - e0_τ
 // phi_lds bit 0: stage Φ in LDS (N (Np + 1) doubles; N <= 32); else it is read back from e.Phi
+// rows > 0 (small batches, phi_lds & 2): workgroup blockIdx.y forms the residual rows
+// [rows y, rows (y + 1)) of the window only, from the Yb / Z rows p months before them (the lag sums);
+// the same values and operation order per row as one workgroup per chain
 constexpr int kElbPrepThreads = 512;
-__global__ __launch_bounds__(kElbPrepThreads) void k_elb_prep(Dims d, ElbDev e, XSel xs, ChainState cs, int phi_lds) {
+__global__ __launch_bounds__(kElbPrepThreads) void k_elb_prep(Dims d, ElbDev e, XSel xs, ChainState cs, int phi_lds,
+                                                              int rows) {
   extern __shared__ double sm[];
   const int c = blockIdx.x;
   const int s = cs.slot[c];
@@ -96,6 +100,12 @@ __global__ __launch_bounds__(kElbPrepThreads) void k_elb_prep(Dims d, ElbDev e, 
   const int Np = N * p, ldp = Np + 1;
   const int T0 = e.elbT0[s], T = e.elbT[s];
   if (T <= 0) return;
+  // this workgroup's residual rows [ta, tb) and the Yb / Z rows they read [tz, tb)
+  const int ta = rows > 0 ? blockIdx.y * rows : 0;
+  if (ta >= T) return;
+  const int tb = rows > 0 ? min(T, ta + rows) : T;
+  const int tz = max(0, ta - p);
+  const bool lead = blockIdx.y == 0;  // writes the chain-wide outputs (Φ, the Gibbs start values)
   const int tid = threadIdx.x;
   const double* PAI = cs.PAI + (size_t)c * N * KP;  // PAI(k, i) at [i*KP + k]
   double* Phi = e.Phi + (size_t)c * N * Np;
@@ -116,7 +126,7 @@ __global__ __launch_bounds__(kElbPrepThreads) void k_elb_prep(Dims d, ElbDev e, 
     if (e.actual[i])
       for (int si = 0; si < Ns; ++si) zero |= (kp % N) == e.ndxS[si];
     const double v = zero ? 0.0 : PAI[(size_t)i * KP + 1 + kp];
-    Phi[q] = v;
+    if (lead) Phi[q] = v;
     if (phi_lds & 1) sPhi[i * ldp + kp] = v;
   }
   const double* Xa = e.Xactual + (size_t)s * KP * TP;        // Xactual(t, k) at [k*TP + t]
@@ -124,7 +134,7 @@ __global__ __launch_bounds__(kElbPrepThreads) void k_elb_prep(Dims d, ElbDev e, 
   for (int k = tid; k < 1 + Np; k += kElbPrepThreads) X0[k] = Xa[(size_t)k * TP + T0];
   const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * Ns;
   // Yb and Z = Yb - Yhatactual;  Yhatactual(:,t) = (Xactual(elbT0+t, lagmask) * PAIactual)' (:400-403)
-  for (int q = tid; q < T * N; q += kElbPrepThreads) {
+  for (int q = tz * N + tid; q < tb * N; q += kElbPrepThreads) {
     const int t = q / N, i = q % N;
     double yh = 0.0;
     if (e.yhat) {  // gibbsdrawShadowrates' YHAT0 argument (ccmm_gibbs_shadowrates)
@@ -145,17 +155,18 @@ __global__ __launch_bounds__(kElbPrepThreads) void k_elb_prep(Dims d, ElbDev e, 
       if (e.ndxS[si] == i && sN[t * Ns + si]) yb = 0.0;
     Yt[q] = yb;
     Z[q] = yb - yh;
-    if (zy_lds) {
+    if (zy_lds && t >= ta) {
       Ytg[q] = yb;
       Zg[q] = yb - yh;
     }
   }
   // Gibbs start values: the chain's current shadow rates (gibbsdrawShadowrates.m:171)
   double* Sc = e.Scur + (size_t)c * e.elbTmax * Ns;
-  for (int q = tid; q < T * Ns; q += kElbPrepThreads) Sc[q] = Yc[(size_t)e.ndxS[q % Ns] * TP + T0 + q / Ns];
+  if (lead)
+    for (int q = tid; q < T * Ns; q += kElbPrepThreads) Sc[q] = Yc[(size_t)e.ndxS[q % Ns] * TP + T0 + q / Ns];
   __syncthreads();
   // ε_τ = Z_τ - Σ_{l<=τ} Φ_l Z_{τ-l} - [τ = 0: w_{-1};  τ >= 1: c + Σ_{l>τ} Φ_l w_{τ-1-l}]
-  for (int q = tid; q < T * N; q += kElbPrepThreads) {
+  for (int q = ta * N + tid; q < tb * N; q += kElbPrepThreads) {
     const int t = q / N, i = q % N;
     const double* ph = (phi_lds & 1) ? sPhi + i * ldp : Phi + (size_t)i * Np;
     double v = Z[q];

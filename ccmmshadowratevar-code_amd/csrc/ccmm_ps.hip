@@ -10,13 +10,14 @@
 // precision and the unit responses of the past neighbours) and, for the PS model, the
 // linear term b (Yhatactual as an intercept, :423).  Then
 //
-//   k_ps_chol  per chain, one wave: banded Cholesky P = L L' with a W x W window in LDS
-//              that streams the assembled rows in and the finished columns out (band
-//              storage L(i + j, i), j < W), and the forward solve ybar = L^-1 b
+//   k_ps_chol_w per chain, one wave (W <= 64): banded Cholesky P = L L' with the window rows in
+//              registers (band storage L(i + j, i), j < W) and the forward solve ybar = L^-1 b;
+//              k_ps_chol (W x W window in LDS) for wider bands
 //   k_ps_prop  per (chain, 256 proposals): x_k = L'^-1 (ybar + z_k) by back substitution,
 //              one proposal per thread with its last W values in registers (a shift
-//              window, static indices), acceptance = all x < ELB,
-//              the smallest accepted index by an LDS then a global atomic min
+//              window, static indices), acceptance = all x < ELB (a
+//              proposal stops at its first cell above the ELB), the smallest accepted index
+//              by an LDS then a global atomic min
 //   k_ps_apply per chain: recompute the accepted proposal into the chain's shadow rates
 //              (k_elb_gibbs skips those chains), bookkeeping of :453-460
 #pragma once
@@ -272,8 +273,11 @@ __global__ __launch_bounds__(64) void k_ps_chol_w(Dims d, ElbDev e, PsDev ps, Ch
 
 // x = L'^-1 (ybar + z_k): one proposal by back substitution, the W - 1 values x_{i+1..i+W-1}
 // in registers (win[j - 1] = x_{i + j}, shifted down one slot per step so every index is
-// static).  out != nullptr writes x into the chain's shadow rates.  Returns whether every
-// cell lies below the ELB.
+// static).  The W - 1 products of a cell go to four interleaved accumulators (j mod 4), so the
+// cell's dependent chain is W / 4 fused multiply-adds, not W - 1.  Lc: the chain's band factor.
+// out != nullptr writes x into the chain's shadow
+// rates.  Returns whether every cell lies below the ELB (a rejected proposal stops at its first cell
+// at or above it unless out is set).
 template <int W>
 __device__ inline bool ps_backsub(const double* __restrict__ Lc, const double* __restrict__ yb, int n,
                                   const Rng& rng, int k, double elb, double* out, const int* cell) {
@@ -281,17 +285,17 @@ __device__ inline bool ps_backsub(const double* __restrict__ Lc, const double* _
 #pragma unroll
   for (int j = 0; j < W - 1; ++j) win[j] = 0.0;
   bool ok = true;
-  // the normal of the next cell is drawn while this cell's dependent chain of W fused multiply-adds
-  // runs (the generator does not depend on the substitution): software-pipelined by one cell
+  // the normal of the next cell is drawn while this cell's substitution runs (the generator does
+  // not depend on it): software-pipelined by one cell
   double znext = rng.normal(CCMM_RNG_PS, (uint32_t)(n - 1 + n * k));
   for (int i = n - 1; i >= 0; --i) {
     const double* li = Lc + (size_t)i * W;
     const double z = znext;
     if (i > 0) znext = rng.normal(CCMM_RNG_PS, (uint32_t)(i - 1 + n * k));
-    double v = yb[i] + z;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int j = 1; j < W; ++j) v = fma(-li[j], win[j - 1], v);
-    v /= li[0];
+    for (int j = 1; j < W; ++j) acc[j & 3] = fma(li[j], win[j - 1], acc[j & 3]);
+    const double v = ((yb[i] + z) - ((acc[1] + acc[2]) + (acc[3] + acc[0]))) / li[0];
 #pragma unroll
     for (int j = W - 2; j >= 1; --j) win[j] = win[j - 1];
     win[0] = v;
@@ -305,6 +309,9 @@ __device__ inline bool ps_backsub(const double* __restrict__ Lc, const double* _
   return ok;
 }
 
+// proposals k = blockIdx.x * 256 + threadIdx.x of chain blockIdx.y.  The band rows of L are read with
+// wave-uniform addresses (scalar loads through the constant cache); staging L in LDS instead measured
+// slower (0.34 -> 0.37 ms at B = 1: 48 vector LDS reads per cell against three scalar loads)
 template <int W>
 __global__ __launch_bounds__(256) void k_ps_prop(ElbDev e, PsDev ps, RngArgs ra) {
   const int c = blockIdx.y;
