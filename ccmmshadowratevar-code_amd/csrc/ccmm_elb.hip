@@ -463,6 +463,14 @@ __global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState c
 // drawTruncNormal.m:47-48, z = -sqrt(2) erfcinv(2 u PHIbar), is Phi^{-1}(u PHIbar).  Inline
 // with wave-uniform branches (every lane draws the same cell); the library erfcinv inlined
 // into k_elb_gibbs's month loop needs ~480 registers (one wave per SIMD).
+// A double constant materialised in SGPRs at its use: the month loops of the Gibbs kernels would
+// otherwise keep every AS241 coefficient live in VGPRs across the loop (two each), crowding the
+// draw's working registers into scratch.  (The asm is empty: the value is unchanged.)
+__device__ __forceinline__ double elb_k(double c) {
+  asm volatile("" : "+s"(c));
+  return c;
+}
+
 __device__ __forceinline__ double elb_ppnd16(double p) {
   // every multiply-add is an explicit fma and nothing else may contract, so the value does not
   // depend on the context it is inlined into (the Gibbs kernels precompute it for the pass's
@@ -471,21 +479,21 @@ __device__ __forceinline__ double elb_ppnd16(double p) {
   const double q = p - 0.5;
   if (fabs(q) <= 0.425) {
     const double r = fma(-q, q, 0.180625);
-    double num = 2509.0809287301226727;
-    num = fma(num, r, 33430.575583588128105);
-    num = fma(num, r, 67265.770927008700853);
-    num = fma(num, r, 45921.953931549871457);
-    num = fma(num, r, 13731.693765509461125);
-    num = fma(num, r, 1971.5909503065514427);
-    num = fma(num, r, 133.14166789178437745);
-    num = fma(num, r, 3.387132872796366608);
-    double den = 5226.495278852545925;
-    den = fma(den, r, 28729.085735721942674);
-    den = fma(den, r, 39307.89580009271061);
-    den = fma(den, r, 21213.794301586595867);
-    den = fma(den, r, 5394.1960214247511077);
-    den = fma(den, r, 687.1870074920579083);
-    den = fma(den, r, 42.313330701600911252);
+    double num = elb_k(2509.0809287301226727);
+    num = fma(num, r, elb_k(33430.575583588128105));
+    num = fma(num, r, elb_k(67265.770927008700853));
+    num = fma(num, r, elb_k(45921.953931549871457));
+    num = fma(num, r, elb_k(13731.693765509461125));
+    num = fma(num, r, elb_k(1971.5909503065514427));
+    num = fma(num, r, elb_k(133.14166789178437745));
+    num = fma(num, r, elb_k(3.387132872796366608));
+    double den = elb_k(5226.495278852545925);
+    den = fma(den, r, elb_k(28729.085735721942674));
+    den = fma(den, r, elb_k(39307.89580009271061));
+    den = fma(den, r, elb_k(21213.794301586595867));
+    den = fma(den, r, elb_k(5394.1960214247511077));
+    den = fma(den, r, elb_k(687.1870074920579083));
+    den = fma(den, r, elb_k(42.313330701600911252));
     den = fma(den, r, 1.0);
     return q * num / den;
   }
@@ -494,39 +502,39 @@ __device__ __forceinline__ double elb_ppnd16(double p) {
   double num, den;
   if (r <= 5.0) {
     r -= 1.6;
-    num = 7.7454501427834140764e-4;
-    num = fma(num, r, 0.0227238449892691845833);
-    num = fma(num, r, 0.24178072517745061177);
-    num = fma(num, r, 1.27045825245236838258);
-    num = fma(num, r, 3.64784832476320460504);
-    num = fma(num, r, 5.7694972214606914055);
-    num = fma(num, r, 4.6303378461565452959);
-    num = fma(num, r, 1.42343711074968357734);
-    den = 1.05075007164441684324e-9;
-    den = fma(den, r, 5.475938084995344946e-4);
-    den = fma(den, r, 0.0151986665636164571966);
-    den = fma(den, r, 0.14810397642748007459);
-    den = fma(den, r, 0.68976733498510000455);
-    den = fma(den, r, 1.6763848301838038494);
-    den = fma(den, r, 2.05319162663775882187);
+    num = elb_k(7.7454501427834140764e-4);
+    num = fma(num, r, elb_k(0.0227238449892691845833));
+    num = fma(num, r, elb_k(0.24178072517745061177));
+    num = fma(num, r, elb_k(1.27045825245236838258));
+    num = fma(num, r, elb_k(3.64784832476320460504));
+    num = fma(num, r, elb_k(5.7694972214606914055));
+    num = fma(num, r, elb_k(4.6303378461565452959));
+    num = fma(num, r, elb_k(1.42343711074968357734));
+    den = elb_k(1.05075007164441684324e-9);
+    den = fma(den, r, elb_k(5.475938084995344946e-4));
+    den = fma(den, r, elb_k(0.0151986665636164571966));
+    den = fma(den, r, elb_k(0.14810397642748007459));
+    den = fma(den, r, elb_k(0.68976733498510000455));
+    den = fma(den, r, elb_k(1.6763848301838038494));
+    den = fma(den, r, elb_k(2.05319162663775882187));
     den = fma(den, r, 1.0);
   } else {
     r -= 5.0;
-    num = 2.01033439929228813265e-7;
-    num = fma(num, r, 2.71155556874348757815e-5);
-    num = fma(num, r, 0.0012426609473880784386);
-    num = fma(num, r, 0.026532189526576123093);
-    num = fma(num, r, 0.29656057182850489123);
-    num = fma(num, r, 1.7848265399172913358);
-    num = fma(num, r, 5.4637849111641143699);
-    num = fma(num, r, 6.6579046435011037772);
-    den = 2.04426310338993978564e-15;
-    den = fma(den, r, 1.4215117583164458887e-7);
-    den = fma(den, r, 1.8463183175100546818e-5);
-    den = fma(den, r, 7.868691311456132591e-4);
-    den = fma(den, r, 0.0148753612908506148525);
-    den = fma(den, r, 0.13692988092273580531);
-    den = fma(den, r, 0.59983220655588793769);
+    num = elb_k(2.01033439929228813265e-7);
+    num = fma(num, r, elb_k(2.71155556874348757815e-5));
+    num = fma(num, r, elb_k(0.0012426609473880784386));
+    num = fma(num, r, elb_k(0.026532189526576123093));
+    num = fma(num, r, elb_k(0.29656057182850489123));
+    num = fma(num, r, elb_k(1.7848265399172913358));
+    num = fma(num, r, elb_k(5.4637849111641143699));
+    num = fma(num, r, elb_k(6.6579046435011037772));
+    den = elb_k(2.04426310338993978564e-15);
+    den = fma(den, r, elb_k(1.4215117583164458887e-7));
+    den = fma(den, r, elb_k(1.8463183175100546818e-5));
+    den = fma(den, r, elb_k(7.868691311456132591e-4));
+    den = fma(den, r, elb_k(0.0148753612908506148525));
+    den = fma(den, r, elb_k(0.13692988092273580531));
+    den = fma(den, r, elb_k(0.59983220655588793769));
     den = fma(den, r, 1.0);
   }
   const double z = num / den;
@@ -565,6 +573,17 @@ __device__ __forceinline__ double elb_trunc_normal_pz(double mu, double sig, dou
   }
   return elb_trunc_normal(mu, sig, elb, u, fl);
 }
+
+// timing-only ablation bits of ElbDev::mode (CCMM_ELB_MODE, read by the ablation build only; a
+// default build compiles them out): 1 no draws (fmin), 2 fixed uniforms, 64 cycle attribution,
+// 128 no record loads, 256 no predecessor wait, 512 no month sums
+#ifdef CCMM_ABLATION
+#define ELB_CLK(x) const unsigned long long x = (e.mode & 64) ? clock64() : 0ull
+#define ELB_ABL(bit) ((e.mode & (bit)) != 0)
+#else
+#define ELB_CLK(x) const unsigned long long x = 0ull
+#define ELB_ABL(bit) false
+#endif
 
 // ---------------------------------------------------------------- Gibbs passes (per chain)
 // One wave per chain.  Each lane owns neighbour columns lane and lane + 64 of every
@@ -666,8 +685,8 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
     const int t = tm & 0xffff, msk = tm >> 16;
     double u[NS], zu[NS];
     for (int a = 0; a < NS; ++a) {
-      u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
-      zu[a] = (e.mode & 2) ? 0.0 : Zl[t * NS + a];
+      u[a] = ELB_ABL(2) ? 0.5 : Ul[t * NS + a];
+      zu[a] = ELB_ABL(2) ? 0.0 : Zl[t * NS + a];
     }
     // Spost = a_t + Σ G S(neighbours)
     const int tn0 = t + off0, tn1 = t + off1;
@@ -675,7 +694,8 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
     const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
     double sp[NS];
     for (int a = 0; a < NS; ++a) sp[a] = fma(h0 ? rc.g0[a] : 0.0, v0, (h1 ? rc.g1[a] : 0.0) * v1);
-    for (int a = 0; a < NS; ++a) sp[a] = rc.hd[a] + wave_sum_dpp(sp[a]);
+    wave_sum_dpp_n(sp);
+    for (int a = 0; a < NS; ++a) sp[a] = rc.hd[a] + sp[a];
     // conditional draws in index order (gibbsdrawShadowrates.m:206-218)
     const double* beta = rc.hd + NS;
     const double* so = beta + NS * (NS - 1);
@@ -691,7 +711,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
         ++y;
       }
       uint8_t fl = 0;
-      cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
+      cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
       if (e.flags && lane == 0)  // drawTruncNormal.m branch taken (oracle.draw_trunc_normal flags)
         e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
     }
@@ -726,6 +746,20 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
 // predecessor's published progress covers reach(i), draws, and publishes (release) its own; a wave
 // with less work in a month (fewer censored series) no longer waits for the slowest wave of the step.
 // The reads and writes are those of the lock-step form, so the draws stay bit-identical.
+#ifdef CCMM_ABLATION
+// timing-only attribution of the ASYNC month body (ablation build, CCMM_ELB_PROF=1): per wave,
+// shader-clock cycles spent waiting for the predecessor, in the neighbour sums, in the draws and
+// in the store/publish tail, plus the month count (read by ccmm_elb_prof)
+__device__ unsigned long long g_elb_prof[8 * 6];
+extern "C" int ccmm_elb_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_elb_prof), sizeof(g_elb_prof)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[8 * 6] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_elb_prof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 template <int NS, int W, bool ASYNC>
 __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, ChainState cs, RngArgs ra) {
   extern __shared__ double sm[];
@@ -818,13 +852,24 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
   load_rec(0, rc);
   int tm = Tm[0];
   if constexpr (ASYNC) {
-    // one month of pass n (the same draw code as the lock-step body below)
+    // one month of pass n (the same draw code as the lock-step body below); the censored-month
+    // entries are fetched two months ahead, so no LDS round trip of them sits on the month's path
     const int pred = (wave + W - 1) % W;
     bool stuck = false;
+    unsigned long long acc_w = 0, acc_s = 0, acc_d = 0, acc_t = 0, months = 0;
+    int tmn = Tm[nc > 1 ? 1 : 0];
     for (; n < P && !stuck; n += W) {
       uniforms(n);
       for (i = 0; i < nc; ++i) {
-        if (n > 0) {
+        ELB_CLK(t0);
+        const int ni = (i + 1 < nc) ? i + 1 : 0;
+        const int nni = (ni + 1 < nc) ? ni + 1 : 0;
+        const int tmnn = Tm[nni];
+        if (!ELB_ABL(128))
+          load_rec(ni, rn);  // next month of this wave (month 0 of its next pass after the last)
+        else
+          rn = rc;  // (128: timing only, no record loads)
+        if (n > 0 && !ELB_ABL(256)) {  // (256: timing only, no predecessor wait)
           const int need = (n - 1) * nc + reach[i] + 1;
           int it = 0;
           while (__hip_atomic_load(&prog[pred], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
@@ -836,25 +881,26 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
           }
           if (stuck) break;
         }
-        const int ni = (i + 1 < nc) ? i + 1 : 0;
-        load_rec(ni, rn);  // next month of this wave (month 0 of its next pass after the last)
-        const int tmn = Tm[ni];
-        const int t = tm & 0xffff, msk = tm >> 16;
+        ELB_CLK(t1);
+        const int t = __builtin_amdgcn_readfirstlane(tm) & 0xffff, msk = __builtin_amdgcn_readfirstlane(tm) >> 16;
         double u[NS], zu[NS];
         for (int a = 0; a < NS; ++a) {
-          u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
-          zu[a] = (e.mode & 2) ? 0.0 : Zl[t * NS + a];
+          u[a] = ELB_ABL(2) ? 0.5 : Ul[t * NS + a];
+          zu[a] = ELB_ABL(2) ? 0.0 : Zl[t * NS + a];
         }
+        // the neighbour cells and the month's own cells, one LDS round trip
         const int tn0 = t + off0, tn1 = t + off1;
         const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
         const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
-        double sp[NS];
-        for (int a = 0; a < NS; ++a) sp[a] = fma(h0 ? rc.g0[a] : 0.0, v0, (h1 ? rc.g1[a] : 0.0) * v1);
-        for (int a = 0; a < NS; ++a) sp[a] = rc.hd[a] + wave_sum_dpp(sp[a]);
-        const double* beta = rc.hd + NS;
-        const double* so = beta + NS * (NS - 1);
         double cur[NS];
         for (int a = 0; a < NS; ++a) cur[a] = Sl[t * NS + a];
+        double sp[NS];
+        for (int a = 0; a < NS; ++a) sp[a] = fma(h0 ? rc.g0[a] : 0.0, v0, (h1 ? rc.g1[a] : 0.0) * v1);
+        if (!ELB_ABL(512)) wave_sum_dpp_n(sp);
+        for (int a = 0; a < NS; ++a) sp[a] = rc.hd[a] + sp[a];
+        const double* beta = rc.hd + NS;
+        const double* so = beta + NS * (NS - 1);
+        ELB_CLK(t2);
         for (int a = 0; a < NS; ++a) {
           if (!((msk >> a) & 1)) continue;
           double mu = sp[a];
@@ -865,17 +911,39 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
             ++y;
           }
           uint8_t fl = 0;
-          cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
+          cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
           if (e.flags && lane == 0)
             e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
         }
+        ELB_CLK(t3);
         for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
         rc = rn;
         tm = tmn;
+        tmn = tmnn;
         if (lane == 0)
           __hip_atomic_store(&prog[wave], n * nc + i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef CCMM_ABLATION
+        if (e.mode & 64) {
+          ELB_CLK(t4);
+          acc_w += t1 - t0;
+          acc_s += t2 - t1;
+          acc_d += t3 - t2;
+          acc_t += t4 - t3;
+          ++months;
+        }
+#endif
       }
     }
+#ifdef CCMM_ABLATION
+    if ((e.mode & 64) && lane == 0 && c == 0 && wave < 8) {
+      atomicAdd(&g_elb_prof[wave * 6 + 0], acc_w);
+      atomicAdd(&g_elb_prof[wave * 6 + 1], acc_s);
+      atomicAdd(&g_elb_prof[wave * 6 + 2], acc_d);
+      atomicAdd(&g_elb_prof[wave * 6 + 3], acc_t);
+      atomicAdd(&g_elb_prof[wave * 6 + 4], months);
+      atomicAdd(&g_elb_prof[wave * 6 + 5], 1ull);
+    }
+#endif
     if (lane == 0) __hip_atomic_store(&prog[wave], done_all, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (stuck && lane == 0) atomicOr(&cs.status[c], 32);
     __syncthreads();
@@ -903,15 +971,16 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
       const int t = tm & 0xffff, msk = tm >> 16;
       double u[NS], zu[NS];
       for (int a = 0; a < NS; ++a) {
-        u[a] = (e.mode & 2) ? 0.5 : Ul[t * NS + a];
-        zu[a] = (e.mode & 2) ? 0.0 : Zl[t * NS + a];
+        u[a] = ELB_ABL(2) ? 0.5 : Ul[t * NS + a];
+        zu[a] = ELB_ABL(2) ? 0.0 : Zl[t * NS + a];
       }
       const int tn0 = t + off0, tn1 = t + off1;
       const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
       const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
       double sp[NS];
       for (int a = 0; a < NS; ++a) sp[a] = fma(h0 ? rc.g0[a] : 0.0, v0, (h1 ? rc.g1[a] : 0.0) * v1);
-      for (int a = 0; a < NS; ++a) sp[a] = rc.hd[a] + wave_sum_dpp(sp[a]);
+      wave_sum_dpp_n(sp);
+    for (int a = 0; a < NS; ++a) sp[a] = rc.hd[a] + sp[a];
       const double* beta = rc.hd + NS;
       const double* so = beta + NS * (NS - 1);
       double cur[NS];
@@ -926,7 +995,7 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
           ++y;
         }
         uint8_t fl = 0;
-        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
+        cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
         if (e.flags && lane == 0)
           e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
       }
@@ -1016,7 +1085,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
     const int tt = Tm[ii] & 0xffff;
 #pragma unroll
     for (int a = 0; a < NS; ++a)
-      uu[a] = (e.mode & 2) ? 0.5 : rng.uniform(CCMM_RNG_ELB, (uint32_t)(tt * NS + a + T * NS * nn));
+      uu[a] = ELB_ABL(2) ? 0.5 : rng.uniform(CCMM_RNG_ELB, (uint32_t)(tt * NS + a + T * NS * nn));
   };
   double ucur[NS];
   if (n < P) draw_u(n, 0, ucur);
@@ -1082,7 +1151,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
           ++y;
         }
         uint8_t fl = 0;
-        cur[a] = (e.mode & 1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, ucur[a], fl);
+        cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, ucur[a], fl);
         if (e.flags && j == 0) e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
       }
       if (j == 0) {

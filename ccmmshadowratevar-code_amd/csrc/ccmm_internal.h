@@ -234,6 +234,42 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
   return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
 }
 
+// row-masked DPP move of a double: lanes of the rows outside ROWS read 0
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_rows_d(double v) {
+  union {
+    double d;
+    int i[2];
+  } u, r;
+  u.d = v;
+  r.i[0] = __builtin_amdgcn_update_dpp(0, u.i[0], CTRL, ROWS, 0xF, false);
+  r.i[1] = __builtin_amdgcn_update_dpp(0, u.i[1], CTRL, ROWS, 0xF, false);
+  return r.d;
+}
+
+// wave_sum_dpp of K independent values at once, stage by stage (the DPP hazards and add latencies of
+// one value fill with the others' work), bit-identical to K calls: the same pairwise tree inside each
+// row, and the cross-row combine (r0 + r1) + (r2 + r3) formed by row_bcast:15 into rows 1, 3 (r1 + r0,
+// r3 + r2) and row_bcast:31 into rows 2, 3 (lane 63: (r3 + r2) + (r1 + r0)) -- the same roundings, as
+// IEEE addition commutes -- and read from lane 63 (one readlane pair instead of four).
+template <int K>
+__device__ __forceinline__ void wave_sum_dpp_n(double (&v)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<0xB1>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<0x4E>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<0x141>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<0x140>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_rows_d<0x142, 0xA>(v[k]);  // row_bcast:15
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_rows_d<0x143, 0xC>(v[k]);  // row_bcast:31
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = readlane_d(v[k], 63);
+}
+
 // ---------------------------------------------------------------- environment switches (host)
 // Selectors choose between kernels or schedules whose draws are the same (bit-identical, or one
 // algorithm in another summation order) and are read in every build (CCMM_ELB_OCT, CCMM_SV_NWG, ...).
