@@ -255,6 +255,12 @@ struct ccmm_chains {
   DBuf<double> crn;
   // storage of kept draws
   DBuf<double> sPAI, sPHI_, sInvA, sSqrtht, sShadow;
+  DBuf<double> solveXch;  // k_cta_solve_lag split: X'v half partials (SolveXch)
+  DBuf<unsigned> solveFlag;
+  unsigned solve_epoch = 0;
+  // two workgroups per chain in k_cta_solve_lag at B <= kSolveSplitMaxB (bit-identical);
+  // CCMM_SOLVE_SPLIT=0 keeps one, 1 splits at any B
+  int solve_split = env_select("CCMM_SOLVE_SPLIT", -1);
   DBuf<double> paiMom;  // running PAI sums | sums of squares (ccmm_chains_pai_moments)
   int mom_done = 0;     // stored draws already added to paiMom
   // block-hybrid ELB model (mcmcVARshadowrateBlockHybrid.m): X/Y slabs 0..ndata-1 hold
@@ -1182,8 +1188,17 @@ struct ccmm_chains {
       L->last = mfma_ev;
       lk.unlock();
     }
+    SolveXch xc{nullptr, nullptr, 0};
+    if (solve_split > 0 || (solve_split < 0 && d.B <= kSolveSplitMaxB)) {
+      if (!solveFlag.p) {
+        solveXch.alloc((size_t)d.B * 2 * 2 * 256);
+        solveFlag.alloc((size_t)d.B * 2);
+        HIPCHECK(hipMemsetAsync(solveFlag.p, 0, (size_t)d.B * 2 * sizeof(unsigned), ctx->stream));
+      }
+      xc = SolveXch{solveXch.p, solveFlag.p, ++solve_epoch};
+    }
     launch(KID_SOLVELAG, [&] {
-      HIPCHECK(lag_launch_solve(lagNT, nmax, ctx->stream, lds_s, d, Tslot.p, iVb.p, xsel(), ls, cs, ra));
+      HIPCHECK(lag_launch_solve(lagNT, nmax, ctx->stream, lds_s, d, Tslot.p, iVb.p, xsel(), ls, cs, ra, xc));
     });
   }
 

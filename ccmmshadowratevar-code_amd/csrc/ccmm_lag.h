@@ -18,6 +18,15 @@ struct LagSel {
                         // b, c) and stop (ccmm_chains_get_cta_gram, parity tests)
 };
 
+// k_cta_solve_lag split over two workgroups per chain (small B): X'v half partials, [B][2 halves]
+// [2 equation parities][256], and one progress flag per workgroup; part == nullptr: one workgroup
+struct SolveXch {
+  double* part;
+  unsigned* flag;
+  unsigned epoch;  // launch counter: equation j of this launch posts epoch * 64 + j + 1
+};
+constexpr int kSolveSplitMaxB = 64;
+
 constexpr int kGlWaves = 8;
 constexpr int kGlLd = 17;     // LDS row stride of a 16 x 16 tile
 constexpr int kGlTile = 16 * kGlLd;
@@ -64,6 +73,6 @@ bool lag_supported_nt(int nt);
 hipError_t lag_launch_gram(int NT, hipStream_t st, size_t lds, Dims d, const int* Tslot, LagSel ls,
                            ChainState cs, const double* iVdiag);
 hipError_t lag_launch_solve(int NT, int nmax, hipStream_t st, size_t lds, Dims d, const int* Tslot,
-                            const double* iVb, XSel xs, LagSel ls, ChainState cs, RngArgs ra);
+                            const double* iVb, XSel xs, LagSel ls, ChainState cs, RngArgs ra, SolveXch xc);
 
 }  // namespace ccmm

@@ -407,10 +407,18 @@ __global__ __launch_bounds__(512, 1) void k_gram_chol_lag(Dims d, const int* __r
 // k_gram_chol_lag (wave W holds slots W + 8k; element (lq + 4r, lr) of slot (ti, tj) =
 // M'_{tj,ti}(lq + 4r, lr), U~_pp^-1 on the diagonal): one coalesced HBM read per system,
 // issued after the v_t loads so that it overlaps the X'v product.
+//
+// Split (gridDim.y == 2, small B): two workgroups per chain, on two CUs.  Workgroup h owns the months
+// of X'v half h, t in [0, th) or [th, T) with th = ceil(T / 2): it forms v_t and the residuals of
+// those months only (a month's v_t reads that month's residuals alone, so the halves never read each
+// other's months) and the X'v partial of its half; the halves swap partials through global memory
+// (one agent-scope flag per workgroup and equation, double-buffered by equation parity), and both
+// run the substitutions on the same right-hand side part_0 + part_1 + iVb, so x is the same in both.
+// Every sum is formed in the order of the one-workgroup kernel: the draws are bit-identical.
 template <int NT, int NMAX, int SW, bool RO>
 __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __restrict__ Tslot,
                                                               const double* __restrict__ iVb, XSel xs, LagSel ls,
-                                                              ChainState cs, RngArgs ra) {
+                                                              ChainState cs, RngArgs ra, SolveXch xc) {
   constexpr int NTILE = gl_ntile(NT);
   constexpr int NTH = 64 * SW;                      // SW waves (8 or 16)
   // factor tiles held per wave: slots wave + SW k (barrier-stepped substitutions), or with RO (row
@@ -438,6 +446,10 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
   const int tid = threadIdx.x, lane0 = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Rng rng = ra.make(c);
+  const bool split = gridDim.y > 1;
+  const int hh = split ? (int)blockIdx.y : 0;
+  const int th = (T + 1) >> 1;
+  const int tlo = (split && hh) ? th : 0, thi = (split && !hh) ? th : TP;  // this workgroup's months
   const double* ih2 = cs.ih2 + (size_t)c * N * TP;
   const double* Y = xs.ypool + (size_t)xs.yidx[c] * N * TP;
   double* E = cs.E + (size_t)c * N * TP;
@@ -483,7 +495,7 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       cur = slab;
     }
     // ---- (1) v_t (E(:,j) = Y(:,j) stands for PAI(:,j) = 0, CTA.m:63)
-    for (int t = tid; t < TP; t += NTH) {
+    for (int t = tlo + tid; t < thi; t += NTH) {
       double acc = 0.0;
       if (t < T && !(ls.mode & 16)) {
         double e[NMAX];
@@ -534,12 +546,12 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       }
     }
     // ---- (2) rhs = iVb_j + X' v, two t-halves per column
+    const int nxv = split ? 256 : 512;  // threads forming X'v partials (one half when split)
     {
-      const int h = tid >> 8, a = tid & 255;
-      const int th = ((T + 1) >> 1);
+      const int h = split ? hh : tid >> 8, a = tid & 255;
       const int t0 = h ? th : 0, t1 = h ? T : th;
       double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-      if ((ls.mode & 32) || tid >= 512) {  // threads 512.. (SW = 16) idle: the t-halves fix the order
+      if ((ls.mode & 32) || tid >= nxv) {  // threads 512.. (SW = 16) idle: the t-halves fix the order
       } else if (a < KL) {
         // four strided chains (t mod 4); the loads of eight months are issued before their
         // fused multiply-adds so that one LDS round trip serves eight products
@@ -572,9 +584,33 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       } else if (a == KL) {
         for (int t = t0; t < t1; ++t) p0 += vl[t];
       }
-      if (tid < 512) part[h * 256 + a] = (p0 + p1) + (p2 + p3);
+      if (tid < nxv) part[h * 256 + a] = (p0 + p1) + (p2 + p3);
     }
     __syncthreads();
+    if (split) {  // swap the halves' partials with the chain's other workgroup
+      const int par = j & 1;
+      double* mine = xc.part + (((size_t)c * 2 + hh) * 2 + par) * 256;
+      const double* other = xc.part + (((size_t)c * 2 + (1 - hh)) * 2 + par) * 256;
+      if (tid <= KL) mine[tid] = part[hh * 256 + tid];
+      __threadfence();
+      __syncthreads();
+      const unsigned seq = xc.epoch * 64u + (unsigned)j + 1u;
+      if (tid == 0) {
+        __hip_atomic_store(&xc.flag[c * 2 + hh], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        for (int it = 0;; ++it) {
+          if (__hip_atomic_load(&xc.flag[c * 2 + 1 - hh], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= seq) break;
+          if (it > (1 << 22)) {  // never expected: flag the chain and go on (no hang)
+            atomicOr(&cs.status[c], 32);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      __syncthreads();
+      if (tid <= KL)
+        part[(1 - hh) * 256 + tid] = __hip_atomic_load(other + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+    }
     const double* ivb = iVb + ((size_t)s * N + j) * KP;
     if (tid <= KL) {
       const int kx = (tid == KL) ? 0 : 1 + tid;
@@ -758,8 +794,9 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
     __syncthreads();
     // ---- (5) PAI(:,j) = x; E(:,j) = Y(:,j) - X x
     double* pai = cs.PAI + ((size_t)c * N + j) * KP;
-    for (int k = tid; k < KP; k += NTH) pai[k] = (k < K) ? xl[k] : 0.0;
-    for (int t = tid; t < TP; t += NTH) {
+    if (hh == 0)
+      for (int k = tid; k < KP; k += NTH) pai[k] = (k < K) ? xl[k] : 0.0;
+    for (int t = tlo + tid; t < thi; t += NTH) {
       double o = 0.0;
       if (t < T && !(ls.mode & 128)) {
         const double* rowp = Dl + t * ldd;
@@ -828,30 +865,30 @@ hipError_t lag_launch_gram(int NT, hipStream_t st, size_t lds, Dims d, const int
 // 0..511).
 template <int NT, int NM, int SW, bool RO>
 static hipError_t solve_sw(hipStream_t st, size_t lds, Dims d, const int* Tslot, const double* iVb, XSel xs,
-                           LagSel ls, ChainState cs, RngArgs ra) {
+                           LagSel ls, ChainState cs, RngArgs ra, SolveXch xc) {
   hipError_t e = hipFuncSetAttribute((const void*)k_cta_solve_lag<NT, NM, SW, RO>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_cta_solve_lag<NT, NM, SW, RO>), dim3(d.B), dim3(64 * SW), lds, st, d, Tslot, iVb, xs, ls,
-                     cs, ra);
+  hipLaunchKernelGGL((k_cta_solve_lag<NT, NM, SW, RO>), dim3(d.B, xc.part ? 2 : 1), dim3(64 * SW), lds, st, d,
+                     Tslot, iVb, xs, ls, cs, ra, xc);
   return hipGetLastError();
 }
 template <int NT, int NM>
 static hipError_t solve_one(hipStream_t st, size_t lds, Dims d, const int* Tslot, const double* iVb, XSel xs,
-                            LagSel ls, ChainState cs, RngArgs ra) {
+                            LagSel ls, ChainState cs, RngArgs ra, SolveXch xc) {
   // row-owned substitutions with LDS flag hand-offs (default) or the barrier-stepped form
   // (CCMM_SOLVE_ASYNC=0); CCMM_SOLVE_WAVES=16: the stepped form on sixteen waves
   const char* v = std::getenv("CCMM_SOLVE_WAVES");
   const char* a = std::getenv("CCMM_SOLVE_ASYNC");
-  if (v && std::atoi(v) == 16) return solve_sw<NT, NM, 16, false>(st, lds, d, Tslot, iVb, xs, ls, cs, ra);
-  if (a && std::atoi(a) == 0) return solve_sw<NT, NM, 8, false>(st, lds, d, Tslot, iVb, xs, ls, cs, ra);
-  return solve_sw<NT, NM, 8, true>(st, lds, d, Tslot, iVb, xs, ls, cs, ra);
+  if (v && std::atoi(v) == 16) return solve_sw<NT, NM, 16, false>(st, lds, d, Tslot, iVb, xs, ls, cs, ra, xc);
+  if (a && std::atoi(a) == 0) return solve_sw<NT, NM, 8, false>(st, lds, d, Tslot, iVb, xs, ls, cs, ra, xc);
+  return solve_sw<NT, NM, 8, true>(st, lds, d, Tslot, iVb, xs, ls, cs, ra, xc);
 }
 
 hipError_t lag_launch_solve(int NT, int nmax, hipStream_t st, size_t lds, Dims d, const int* Tslot,
-                            const double* iVb, XSel xs, LagSel ls, ChainState cs, RngArgs ra) {
+                            const double* iVb, XSel xs, LagSel ls, ChainState cs, RngArgs ra, SolveXch xc) {
 #define SL_CASE(NT_, NM_) \
-  if (NT == NT_ && nmax == NM_) return solve_one<NT_, NM_>(st, lds, d, Tslot, iVb, xs, ls, cs, ra);
+  if (NT == NT_ && nmax == NM_) return solve_one<NT_, NM_>(st, lds, d, Tslot, iVb, xs, ls, cs, ra, xc);
   SL_CASE(1, 8) SL_CASE(1, 20) SL_CASE(1, 32) SL_CASE(15, 8) SL_CASE(15, 20) SL_CASE(15, 32)
 #undef SL_CASE
   return hipErrorInvalidValue;

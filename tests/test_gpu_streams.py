@@ -1,13 +1,16 @@
-"""The block-hybrid sweep with the PHI block on the auxiliary stream beside the ELB step (the default)
-against the same sweep in plain stream order (CCMM_PHI_OVERLAP=0): the two blocks touch disjoint state,
-so every draw, the shadow rates, the forecasts and the status words are identical."""
+"""Schedules of the block-hybrid sweep that must not change a bit: the PHI block on the auxiliary
+stream beside the ELB step (the default) against plain stream order (CCMM_PHI_OVERLAP=0) -- the two
+blocks touch disjoint state -- and the lag-structured CTA solve on two workgroups per chain (the
+default at small B) against one (CCMM_SOLVE_SPLIT=0) -- every sum in the same order.  Every draw, the
+shadow rates, the forecasts and the status words are identical."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-def test_phi_overlap_bit_identical(pkg, ctx, fred, monkeypatch):
+@pytest.mark.parametrize("var,B", [("CCMM_PHI_OVERLAP", 8), ("CCMM_SOLVE_SPLIT", 8), ("CCMM_SOLVE_SPLIT", 1)])
+def test_schedule_bit_identical(pkg, ctx, fred, monkeypatch, var, B):
     d = fred
     p = 12
     mpm = pkg.model.setMinnesotaMean(d["ncode"])
@@ -18,10 +21,10 @@ def test_phi_overlap_bit_identical(pkg, ctx, fred, monkeypatch):
     yields = np.zeros(m.N, bool)
     yields[ndxY] = True
     yreal = pkg.samplers.realized_values(d["data"], len(d["ydates"]) - 1, 12, ndxS, 0.25)
-    B, nsw = 8, 4
+    nsw = 4
     outs = []
     for ov in ("0", "1"):
-        monkeypatch.setenv("CCMM_PHI_OVERLAP", ov)
+        monkeypatch.setenv(var, ov)
         ch = pkg.Chains(ctx, N=m.N, p=p, T=m.T, B=B, crn=False, store_capacity=nsw, seed=77,
                         model=pkg.MODEL_BLOCKHYBRID, Ns=len(bm.ndxS), elbTmax=bm.elbT, elb_gibbsburn=20, elb=0.25)
         ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
