@@ -631,7 +631,7 @@ __global__ void k_sv_normals(Dims d, const int* __restrict__ Tslot, ChainState c
 template <int NN, int NW, bool PACK>
 static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
                                 const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
-                                int mode) {
+                                int mode, int nwg) {
   constexpr int CLD = NN + 1, XLD = 2 * NN + 1;
   const size_t lds = (size_t)(2 * NN * NN + kSvMaxSeg * NN + NW * sv_wave_lds(NN)) * sizeof(double);
   hipError_t e = hipFuncSetAttribute((const void*)k_sv_part<NN, NW, PACK>,
@@ -640,11 +640,9 @@ static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const
   hipLaunchKernelGGL(k_sv_normals, dim3(((d.TP + 1) * d.N + 255) / 256, d.B), dim3(256), 0, st, d, Tslot, cs, ra,
                      gbuf, NN);
   // small batches (B <= 128, e.g. the OOS chains of one vintage): the segments of phases A and C
-  // are spread over nwg = 2 workgroups per chain (16 segments = one per wave), as two launches:
-  // phase A, then phases B + C, in which every workgroup of the chain redoes the serial
+  // are spread over nwg = 2 (or 4) workgroups per chain (16 segments = one per wave), as two
+  // launches: phase A, then phases B + C, in which every workgroup of the chain redoes the serial
   // separator pass (identical values and stores) instead of a third launch; same draws
-  int nwg = d.B <= 128 ? 2 : 1;
-  if (const char* ev = std::getenv("CCMM_SV_NWG")) nwg = std::max(1, std::min(2, std::atoi(ev)));
   if (nwg == 1) {
     hipLaunchKernelGGL((k_sv_part<NN, NW, PACK>), dim3(d.B), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm, cs,
                        ra, sep, gbuf, mode, 1);
@@ -663,22 +661,41 @@ static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const
 template <int NN, int NW>
 static hipError_t sv_launch_one(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
                                 const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
-                                int mode) {
-  if (mode & 128) return sv_launch_one_<NN, NW, false>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
-  return sv_launch_one_<NN, NW, true>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+                                int mode, int nwg) {
+  if (mode & 128) return sv_launch_one_<NN, NW, false>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
+  return sv_launch_one_<NN, NW, true>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
 }
 
+// Workgroups per chain: 1 from B = 129 (the chip is full), 2 of 8 waves down to B = 33, and at
+// B <= 32 (NN <= 20) 4 of 4 waves -- one wave per SIMD on 4 CUs, so that the serial block chains of
+// phases A and C no longer share a SIMD's issue (the OOS floor runs one chain).  CCMM_SV_NWG=1|2|4
+// overrides.  The segments, their order of operations and the draws are the same in every layout.
 hipError_t sv_launch_part(int N, hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
                           const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf, int mode) {
-  switch (sv_bucket(N)) {
-    case 4: return sv_launch_one<4, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
-    case 8: return sv_launch_one<8, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
-    case 12: return sv_launch_one<12, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
-    case 16: return sv_launch_one<16, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
-    case 20: return sv_launch_one<20, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
-    case 24: return sv_launch_one<24, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
-    case 28: return sv_launch_one<28, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
-    default: return sv_launch_one<32, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode);
+  const int nb = sv_bucket(N);
+  int nwg = d.B <= 32 && nb <= 20 ? 4 : (d.B <= 128 ? 2 : 1);
+  if (const char* ev = std::getenv("CCMM_SV_NWG")) {
+    const int v = std::atoi(ev);
+    nwg = v >= 4 && nb <= 20 ? 4 : std::max(1, std::min(2, v));
+  }
+  if (nwg == 4) {
+    switch (nb) {
+      case 4: return sv_launch_one<4, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, 4);
+      case 8: return sv_launch_one<8, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, 4);
+      case 12: return sv_launch_one<12, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, 4);
+      case 16: return sv_launch_one<16, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, 4);
+      default: return sv_launch_one<20, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, 4);
+    }
+  }
+  switch (nb) {
+    case 4: return sv_launch_one<4, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
+    case 8: return sv_launch_one<8, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
+    case 12: return sv_launch_one<12, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
+    case 16: return sv_launch_one<16, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
+    case 20: return sv_launch_one<20, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
+    case 24: return sv_launch_one<24, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
+    case 28: return sv_launch_one<28, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
+    default: return sv_launch_one<32, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
   }
 }
 

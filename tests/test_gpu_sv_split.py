@@ -1,10 +1,11 @@
-"""The partitioned SV smoother split over two workgroups per chain (default for B <= 128:
+"""The partitioned SV smoother split over two workgroups per chain (default for 32 < B <= 128:
 phase A over 2 x 8 waves, then phases B + C with the serial separator pass redone by each
-workgroup) against the one-workgroup launch (CCMM_SV_NWG=1): the same segments, separators
-and operation order, so h, eta, sqrtht and the whole chain state agree bit for bit after
-several real-data linear sweeps (fredblockMD20-2022-09, N = 20, p = 12; Philox draws).
-T = 750 has 16 segments (one per wave of the pair); the short sample (T = 72) has 9, so
-the second workgroup runs one segment besides its copy of the separator pass."""
+workgroup) and over four (default for B <= 32: 4 x 4 waves, one per SIMD) against the
+one-workgroup launch (CCMM_SV_NWG=1): the same segments, separators and operation order, so h,
+eta, sqrtht and the whole chain state agree bit for bit after several real-data linear sweeps
+(fredblockMD20-2022-09, N = 20, p = 12; Philox draws).  T = 750 has 16 segments (one per wave);
+the short sample (T = 72) has 9, so some workgroups run one segment or none besides their copy of
+the separator pass."""
 import os
 
 import numpy as np
@@ -33,11 +34,12 @@ def _run(pkg, fred, nwg, thisT, B=6, sweeps=3):
 
 
 @pytest.mark.parametrize("short", [False, True])
-def test_sv_two_workgroups_bit_identical(pkg, fred, short):
+@pytest.mark.parametrize("nwg", [2, 4])
+def test_sv_split_workgroups_bit_identical(pkg, fred, short, nwg):
     thisT = 12 + 12 + 60 if short else len(fred["ydates"])
     ref = _run(pkg, fred, 1, thisT)
-    got = _run(pkg, fred, 2, thisT)
+    got = _run(pkg, fred, nwg, thisT)
     assert not np.any(ref["status"])
     for k in ref:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
-    print("SV nwg=2 == nwg=1 over", sorted(ref), "T =", thisT)
+    print(f"SV nwg={nwg} == nwg=1 over", sorted(ref), "T =", thisT)
