@@ -1221,18 +1221,15 @@ struct ccmm_chains {
     // k_astep_w (wave-parallel factorisations, the default) or the one-thread-per-regression
     // k_astep (CCMM_ASTEP_V1=1, kept for A/B timing); same draws up to summation order inside
     // the factorisation (identical update order, fma placement as written)
-    // k_astep_w's Gram path holds 16 months per lane (T <= 1024): longer samples take k_astep's loop
-    const bool v1 = env_select("CCMM_ASTEP_V1", 0) != 0 || cfg.T > 1024;
+    const bool v1 = env_select("CCMM_ASTEP_V1", 0) != 0;
     const void* fn = v1 ? (const void*)k_astep : (N <= 20 ? (const void*)k_astep_w<20> : (const void*)k_astep_w<32>);
     if (lds > 64 * 1024) HIPCHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (!astepTab.p) {  // (ii, a, b) of every Gram entry, block ii = 1..N-1: packed lower ZZ, then Zz
-      std::vector<int> tab;
-      for (int ii = 1; ii < N; ++ii) {
-        for (int b = 0; b < ii; ++b)
-          for (int a = b; a < ii; ++a) tab.push_back(ii << 16 | a << 8 | b);
-        for (int a = 0; a < ii; ++a) tab.push_back(ii << 16 | a << 8 | ii);
-      }
-      tab.push_back(0);
+    if (!astepTab.p) {  // the 4 x 4 Gram tiles (ii, A, B) of astep_gram_tiles, largest ii first
+      std::vector<int> tab(1, 0);
+      for (int ii = N - 1; ii >= 1; --ii)
+        for (int A = 0; 4 * A <= ii; ++A)
+          for (int Bk = 0; Bk <= A && 4 * Bk < ii; ++Bk) tab.push_back(ii << 16 | A << 8 | Bk);
+      tab[0] = (int)tab.size() - 1;
       astepTab.alloc(tab.size());
       HIPCHECK(hipMemcpy(astepTab.p, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice));
     }

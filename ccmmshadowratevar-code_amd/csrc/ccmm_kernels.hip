@@ -432,8 +432,114 @@ __global__ __launch_bounds__(256) void k_cta_solve(Dims d, const int* __restrict
 // mcmcVAR.m:236-254 (flat prior: OMEGA_A_inv = 0, MU_A = 0, mcmcVAR.m:153-161),
 // invA = A \ I (mcmcVAR.m:254), logy2 = log((RESID*A').^2 + offset) (mcmcVAR.m:259).
 // LDS: per ii a packed lower ZZ (ii x ii) followed by Zz (ii).
-// gtab[g] = ii << 16 | a << 8 | b: the (regression, row, column) of Gram entry g (host-built,
-// replaces a per-entry decode loop)
+
+// The Gram entries of every regression ii = 1..N-1,
+//   ZZ_ii(a, b) = sum_t E(a,t) E(b,t) w_ii(t)  (b <= a < ii),   Zz_ii(b) = the same with a = ii,
+//   w_ii(t) = 1 / sqrtht(ii,t)^2,
+// as 4 x 4 register tiles: gtab = [ntiles, ii << 16 | A << 8 | B ...] (host-built, largest ii first),
+// rows 4A.., columns 4B..; each 16-lane row of a wave takes one tile, lane j the months t = j mod 16
+// (sequential fused multiply-adds fma(E_a E_b, w, acc)), then a DPP tree over the row's 16 lanes.
+// The weights are formed once per chain into the chain's logy2 rows (overwritten by logy2 at the end
+// of the A-step).  Per entry the arithmetic depends on the tile alone, so every launch shape gives the
+// same sums.  (Before: one wave per entry, 2 LDS reads per product and a 64-lane reduction per entry.)
+__device__ __forceinline__ void astep_gram_tiles(const double* Ew, const double* sh, double* W, double* sm,
+                                                 const int* boff, const int* __restrict__ gtab, int N, int TP,
+                                                 int T, int tid, int nthreads) {
+  for (int q = tid; q < (N - 1) * TP; q += nthreads) {
+    const int ii = 1 + q / TP, t = q - (ii - 1) * TP;
+    const double hv = (t < T) ? sh[(size_t)ii * TP + t] : 1.0;
+    W[q] = (t < T) ? 1.0 / (hv * hv) : 0.0;
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6, nwv = nthreads >> 6;
+  const int r = lane >> 4, j = lane & 15;
+  const int ntiles = gtab[0];
+  for (int g0 = 4 * wave; g0 < ntiles; g0 += 4 * nwv) {
+    const int gi = g0 + r;
+    const int v = gi < ntiles ? gtab[1 + gi] : gtab[1];  // idle rows redo tile 0 and store nothing
+    const int ii = v >> 16, A4 = 4 * ((v >> 8) & 255), B4 = 4 * (v & 255);
+    const double* ea[4];
+    const double* eb[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      ea[p] = Ew + (size_t)min(A4 + p, N - 1) * TP;
+      eb[p] = Ew + (size_t)min(B4 + p, N - 1) * TP;
+    }
+    const double* wr = W + (size_t)(ii - 1) * TP;
+    double acc[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.0;
+    // the weights (global, L2) run kAsPf months ahead of the products in a register ring, so no
+    // load latency sits between two batches of fused multiply-adds
+    constexpr int kAsPf = 8;
+    const int M = (T - j + 15) >> 4;  // months t = j + 16 m < T of this lane
+    double wq[kAsPf];
+#pragma unroll
+    for (int u = 0; u < kAsPf; ++u) wq[u] = (u < M) ? wr[j + 16 * u] : 0.0;
+    for (int m0 = 0; m0 < M; m0 += kAsPf) {
+      double wn[kAsPf];
+#pragma unroll
+      for (int u = 0; u < kAsPf; ++u) wn[u] = (m0 + kAsPf + u < M) ? wr[j + 16 * (m0 + kAsPf + u)] : 0.0;
+#pragma unroll
+      for (int u = 0; u < kAsPf; ++u) {
+        if (m0 + u < M) {
+          const int t = j + 16 * (m0 + u);
+          double xa[4], xb[4];
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            xa[p] = ea[p][t];
+            xb[p] = eb[p][t];
+          }
+#pragma unroll
+          for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[4 * p + q] = fma(xa[p] * xb[q], wq[u], acc[4 * p + q]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kAsPf; ++u) wq[u] = wn[u];
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] += dpp_d<0xB1>(acc[e]);   // xor 1
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] += dpp_d<0x4E>(acc[e]);   // xor 2
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] += dpp_d<0x141>(acc[e]);  // row_half_mirror
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] += dpp_d<0x140>(acc[e]);  // row_mirror: the row sum
+    // lane j of the row stores entry (A4 + j / 4, B4 + j % 4)
+    double mine = acc[0];
+#pragma unroll
+    for (int e = 1; e < 16; ++e) mine = (j == e) ? acc[e] : mine;
+    const int a = A4 + (j >> 2), b = B4 + (j & 3);
+    if (gi < ntiles && a <= ii && b < ii && b <= a) {
+      const int o = (a < ii) ? b * ii - b * (b - 1) / 2 + (a - b) : ii * (ii + 1) / 2 + b;
+      sm[boff[ii] + o] = mine;
+    }
+  }
+}
+
+// logy2 = log((RESID * A').^2 + offset) (mcmcVAR.m:259): one month per thread, its residuals read
+// once into registers (NN >= N), row i's sum over k <= i in ascending order
+template <int NN>
+__device__ __forceinline__ void astep_logy2(const double* Ew, const double* Anew, double* ly, int N, int TP,
+                                            int T, int tid, int nthreads, double logy2offset) {
+  for (int t = tid; t < TP; t += nthreads) {
+    double e[NN];
+#pragma unroll
+    for (int k = 0; k < NN; ++k) e[k] = (k < N && t < T) ? Ew[(size_t)k * TP + t] : 0.0;
+    for (int i = 0; i < N; ++i) {
+      double sacc = 0.0;
+      if (t < T) {
+#pragma unroll
+        for (int k = 0; k < NN; ++k)
+          if (k <= i) sacc = fma(e[k], Anew[i + k * N], sacc);
+      }
+      ly[(size_t)i * TP + t] = (t < T) ? log(sacc * sacc + logy2offset) : 0.0;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ Tslot, ChainState cs,
                                                RngArgs ra, double logy2offset, int es_off,
                                                const int* __restrict__ gtab) {
@@ -466,60 +572,7 @@ __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ T
   const double* Ew = (es_off >= 0) ? sm + es_off : E;
   const int total = boff[N];
   double* Anew = sm + total;  // N x N
-  // entry g of block ii: (a, b) of the ii x ii Gram ZZ = E(:,0:ii-1)' diag(1/h_ii^2) E(:,0:ii-1)
-  // (packed lower) or of Zz = E(:,0:ii-1)' diag(1/h_ii^2) E(:,ii)
-  auto entry = [&](int g, int& ii, int& a, int& b) {
-    const int v = gtab[g];
-    ii = v >> 16;
-    a = (v >> 8) & 255;
-    b = v & 255;
-  };
-  constexpr int kAsTPL = 16;  // t values per lane on the wave-per-entry path (T <= 1024)
-  if (T <= 64 * kAsTPL) {
-    // one wave per entry, lanes over t (coalesced rows of E), 1/h_ii^2 cached in registers
-    // while consecutive entries of this wave stay in the same block ii; DPP reduction
-    const int lane = tid & 63, wave = tid >> 6, nwv = blockDim.x >> 6;
-    double ih[kAsTPL];
-    int cur_ii = -1;
-    for (int g = wave; g < total; g += nwv) {
-      int ii, a, b;
-      entry(g, ii, a, b);
-      if (ii != cur_ii) {
-        cur_ii = ii;
-        const double* hh = sh + (size_t)ii * TP;
-#pragma unroll
-        for (int k = 0; k < kAsTPL; ++k) {
-          const int t = lane + 64 * k;
-          const double hv = (t < T) ? hh[t] : 1.0;
-          ih[k] = (t < T) ? 1.0 / (hv * hv) : 0.0;
-        }
-      }
-      const double* ea = Ew + (size_t)a * TP;
-      const double* eb = Ew + (size_t)b * TP;
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < kAsTPL; ++k) {
-        const int t = lane + 64 * k;
-        if (t < T) acc = fma(ea[t] * eb[t], ih[k], acc);
-      }
-      acc = wave_sum_dpp(acc);
-      if (lane == 0) sm[g] = acc;
-    }
-  } else {
-    for (int g = tid; g < total; g += blockDim.x) {
-      int ii, a, b;
-      entry(g, ii, a, b);
-      const double* ea = E + (size_t)a * TP;
-      const double* eb = E + (size_t)b * TP;
-      const double* hh = sh + (size_t)ii * TP;
-      double acc = 0.0;
-      for (int t = 0; t < T; ++t) {
-        const double hv = hh[t];
-        acc = fma(ea[t] / hv, eb[t] / hv, acc);
-      }
-      sm[g] = acc;
-    }
-  }
+  astep_gram_tiles(Ew, sh, cs.logy2 + (size_t)c * N * TP, sm, boff, gtab, N, TP, T, tid, blockDim.x);
   for (int q = tid; q < N * N; q += blockDim.x) Anew[q] = ((q % N) == (q / N)) ? 1.0 : 0.0;
   __syncthreads();
   // per-ii Cholesky + solves, one thread per ii
@@ -575,28 +628,37 @@ __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ T
     }
     for (int r = 0; r < N; ++r) Ainv[r + col * N] = Xs[r + col * N];
   }
-  // logy2 = log((RESID * A').^2 + offset)
-  double* ly = cs.logy2 + (size_t)c * N * TP;
-  for (int t = tid; t < TP; t += blockDim.x) {
-    for (int i = 0; i < N; ++i) {
-      double s = 0.0;
-      if (t < T) {
-        for (int k = 0; k <= i; ++k) s = fma(Ew[(size_t)k * TP + t], Anew[i + k * N], s);
-      }
-      ly[(size_t)i * TP + t] = (t < T) ? log(s * s + logy2offset) : 0.0;
-    }
-  }
+  astep_logy2<kMaxNSmall>(Ew, Anew, cs.logy2 + (size_t)c * N * TP, N, TP, T, tid, blockDim.x, logy2offset);
 }
 
 // ============================================================== A-step, wave-parallel form
 // The same draws as k_astep (mcmcVAR.m:236-254, 259) with the per-regression work spread over
-// waves instead of one thread per regression: 8 waves share the Gram entries (one wave per
-// entry, lanes over t, E staged in LDS), then each wave factors whole regressions ii in
+// waves instead of one thread per regression: 8 waves share the Gram tiles (astep_gram_tiles,
+// E staged in LDS), then each wave factors whole regressions ii in
 // registers (lane r holds row r of ZZ_ii: readlane broadcasts of the pivot row, the same
 // left-to-right update order as k_astep's left-looking loop) and solves L tilde = Zz,
 // alpha = L' \ (tilde + z) by lane substitutions; wave 0 forms invA by lane-per-column
 // forward substitution.  Regressions are dealt to waves largest first in snake order.
-// Lanes hold t = lane + 64 k, k < 16, of the Gram sums: T <= 1024 (run_astep dispatches k_astep beyond).
+#ifdef CCMM_ABLATION
+// timing-only phase attribution of k_astep_w (ablation build): shader-clock cycles of chain 0's
+// workgroup between its barriers (stage E | Gram | factor + solves | invA | logy2), read by
+// ccmm_astep_prof
+__device__ unsigned long long g_astep_prof[8];
+extern "C" int ccmm_astep_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_astep_prof), sizeof(g_astep_prof)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_astep_prof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#define AS_CLK(x) const unsigned long long x = clock64()
+#define AS_ACC(k, a, b) \
+  if (c == 0 && tid == 0) atomicAdd(&g_astep_prof[k], (b) - (a))
+#else
+#define AS_CLK(x)
+#define AS_ACC(k, a, b)
+#endif
 template <int NN>
 __global__ __launch_bounds__(512) void k_astep_w(Dims d, const int* __restrict__ Tslot, ChainState cs,
                                                  RngArgs ra, double logy2offset, int es_off,
@@ -614,6 +676,7 @@ __global__ __launch_bounds__(512) void k_astep_w(Dims d, const int* __restrict__
   double* Ac = cs.A + (size_t)c * N * N;
   double* Ainv = cs.invA + (size_t)c * N * N;
   __shared__ int boff[kMaxNSmall + 1];
+  AS_CLK(k0);
   if (tid == 0) {
     int o = 0;
     boff[0] = 0;
@@ -627,41 +690,15 @@ __global__ __launch_bounds__(512) void k_astep_w(Dims d, const int* __restrict__
   if (es_off >= 0)
     for (int q = tid; q < N * TP; q += blockDim.x) sm[es_off + q] = E[q];
   __syncthreads();
+  AS_CLK(k1);
   const double* Ew = (es_off >= 0) ? sm + es_off : E;
   const int total = boff[N];
   double* Anew = sm + total;  // N x N
-  // ---- Gram entries (identical arithmetic to k_astep's wave-per-entry path)
-  constexpr int kAsTPL = 16;
-  {
-    double ih[kAsTPL];
-    int cur_ii = -1;
-    for (int g = wave; g < total; g += kWaves) {
-      const int v = gtab[g];
-      const int ii = v >> 16, a = (v >> 8) & 255, b = v & 255;
-      if (ii != cur_ii) {
-        cur_ii = ii;
-        const double* hh = sh + (size_t)ii * TP;
-#pragma unroll
-        for (int k = 0; k < kAsTPL; ++k) {
-          const int t = lane + 64 * k;
-          const double hv = (t < T) ? hh[t] : 1.0;
-          ih[k] = (t < T) ? 1.0 / (hv * hv) : 0.0;
-        }
-      }
-      const double* ea = Ew + (size_t)a * TP;
-      const double* eb = Ew + (size_t)b * TP;
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < kAsTPL; ++k) {
-        const int t = lane + 64 * k;
-        if (t < T) acc = fma(ea[t] * eb[t], ih[k], acc);
-      }
-      acc = wave_sum_dpp(acc);
-      if (lane == 0) sm[g] = acc;
-    }
-  }
+  // ---- Gram entries (the same tiles as k_astep)
+  astep_gram_tiles(Ew, sh, cs.logy2 + (size_t)c * N * TP, sm, boff, gtab, N, TP, T, tid, 512);
   for (int q = tid; q < N * N; q += blockDim.x) Anew[q] = ((q % N) == (q / N)) ? 1.0 : 0.0;
   __syncthreads();
+  AS_CLK(k2);
   // ---- per-regression factor + solves, one wave per regression ii (rows on lanes)
   int badf = 0;
   for (int r8 = 0;; ++r8) {
@@ -734,6 +771,7 @@ __global__ __launch_bounds__(512) void k_astep_w(Dims d, const int* __restrict__
   }
   if (badf && lane == 0) atomicOr(&cs.status[c], 4);
   __syncthreads();
+  AS_CLK(k3);
   for (int q = tid; q < N * N; q += blockDim.x) Ac[q] = Anew[q];
   // invA: lane col forms column col of A^-1 (unit lower forward substitution, A read by
   // broadcast from LDS)
@@ -754,17 +792,18 @@ __global__ __launch_bounds__(512) void k_astep_w(Dims d, const int* __restrict__
         if (r < N) Ainv[r + col * N] = x[r];
     }
   }
-  // logy2 = log((RESID * A').^2 + offset)
-  double* ly = cs.logy2 + (size_t)c * N * TP;
-  for (int t = tid; t < TP; t += blockDim.x) {
-    for (int i = 0; i < N; ++i) {
-      double sacc = 0.0;
-      if (t < T) {
-        for (int k = 0; k <= i; ++k) sacc = fma(Ew[(size_t)k * TP + t], Anew[i + k * N], sacc);
-      }
-      ly[(size_t)i * TP + t] = (t < T) ? log(sacc * sacc + logy2offset) : 0.0;
-    }
-  }
+  AS_CLK(k4);
+  astep_logy2<NN>(Ew, Anew, cs.logy2 + (size_t)c * N * TP, N, TP, T, tid, blockDim.x, logy2offset);
+#ifdef CCMM_ABLATION
+  __syncthreads();
+  AS_CLK(k5);
+  AS_ACC(0, k0, k1);
+  AS_ACC(1, k1, k2);
+  AS_ACC(2, k2, k3);
+  AS_ACC(3, k3, k4);
+  AS_ACC(4, k4, k5);
+  if (c == 0 && tid == 0) atomicAdd(&g_astep_prof[5], 1ull);
+#endif
 }
 
 // ============================================================== SV: KSC mixture indicators

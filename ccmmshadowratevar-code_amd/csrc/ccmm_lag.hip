@@ -408,6 +408,27 @@ __global__ __launch_bounds__(512, 1) void k_gram_chol_lag(Dims d, const int* __r
 // M'_{tj,ti}(lq + 4r, lr), U~_pp^-1 on the diagonal): one coalesced HBM read per system,
 // issued after the v_t loads so that it overlaps the X'v product.
 //
+#ifdef CCMM_ABLATION
+// timing-only phase attribution of k_cta_solve_lag (ablation build): shader-clock cycles of chain
+// 0's first workgroup per phase -- v_t | X'v (+ the halves' swap) | forward | backward | residuals
+// -- summed over equations and launches (read by ccmm_solve_prof)
+__device__ unsigned long long g_solve_prof[8];
+extern "C" int ccmm_solve_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solve_prof), sizeof(g_solve_prof)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_solve_prof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#define SL_CLK(x) const unsigned long long x = clock64()
+#define SL_ACC(k, a, b) \
+  if (c == 0 && blockIdx.y == 0 && tid == 0) atomicAdd(&g_solve_prof[k], (b) - (a))
+#else
+#define SL_CLK(x)
+#define SL_ACC(k, a, b)
+#endif
+//
 // Split (gridDim.y == 2, small B): two workgroups per chain, on two CUs.  Workgroup h owns the months
 // of X'v half h, t in [0, th) or [th, T) with th = ceil(T / 2): it forms v_t and the residuals of
 // those months only (a month's v_t reads that month's residuals alone, so the halves never read each
@@ -494,6 +515,7 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       for (int q = tid; q < rows * ldd; q += NTH) Dl[q] = src[q];
       cur = slab;
     }
+    SL_CLK(q0);
     // ---- (1) v_t (E(:,j) = Y(:,j) stands for PAI(:,j) = 0, CTA.m:63)
     for (int t = tlo + tid; t < thi; t += NTH) {
       double acc = 0.0;
@@ -532,6 +554,7 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       vl[t] = acc;
     }
     __syncthreads();
+    SL_CLK(q1);
     // factor tiles of this system -> registers (consumed in phases 3-4); issued after the
     // barrier so that they cannot be hoisted into the v_t loop (register pressure)
     dbl4 lt[TPW];
@@ -587,6 +610,8 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       if (tid < nxv) part[h * 256 + a] = (p0 + p1) + (p2 + p3);
     }
     __syncthreads();
+    SL_CLK(q1b);
+    SL_ACC(6, q1, q1b);
     if (split) {  // swap the halves' partials with the chain's other workgroup
       const int par = j & 1;
       double* mine = xc.part + (((size_t)c * 2 + hh) * 2 + par) * 256;
@@ -611,6 +636,7 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
         part[(1 - hh) * 256 + tid] = __hip_atomic_load(other + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
     }
+    SL_CLK(q2);
     const double* ivb = iVb + ((size_t)s * N + j) * KP;
     if (tid <= KL) {
       const int kx = (tid == KL) ? 0 : 1 + tid;
@@ -703,6 +729,7 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       }
     }
     __syncthreads();
+    SL_CLK(q3);
     // ---- (4) c = y + z_j (randn(K,N) of CTA.m:58, column j); back substitution L' x = c:
     //         w_p = L~_pp^-T c~_p for all p at once, then L_u' x~ = w by block steps from the
     //         bottom (x_p = w_p final; the owners of the slots (p, i) take M_pi' x_p off w_i),
@@ -792,6 +819,7 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       xl[0] = (rl[0] - sacc) * Lv[0];
     }
     __syncthreads();
+    SL_CLK(q4);
     // ---- (5) PAI(:,j) = x; E(:,j) = Y(:,j) - X x
     double* pai = cs.PAI + ((size_t)c * N + j) * KP;
     if (hh == 0)
@@ -835,6 +863,13 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       E[(size_t)j * TP + t] = o;
     }
     __syncthreads();
+    SL_CLK(q5);
+    SL_ACC(0, q0, q1);
+    SL_ACC(1, q1, q2);
+    SL_ACC(2, q2, q3);
+    SL_ACC(3, q3, q4);
+    SL_ACC(4, q4, q5);
+    if (j == 0) SL_ACC(5, 0ull, 1ull);
   }
 }
 
