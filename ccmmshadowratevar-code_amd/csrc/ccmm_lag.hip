@@ -605,7 +605,18 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
         }
         for (; t < t1; ++t) p0 = fma(col[t * ldd], vl[t], p0);
       } else if (a == KL) {
-        for (int t = t0; t < t1; ++t) p0 += vl[t];
+        // the intercept column: one sequential sum of the half's v_t (the order of the plain loop);
+        // sixteen values per LDS round trip, so the chain waits on additions, not on LDS latency
+        // (one read per addition made this thread the phase's straggler: ~40k cycles of ~50k)
+        int t = t0;
+        for (; t + 15 < t1; t += 16) {
+          double vv[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) vv[u] = vl[t + u];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) p0 += vv[u];
+        }
+        for (; t < t1; ++t) p0 += vl[t];
       }
       if (tid < nxv) part[h * 256 + a] = (p0 + p1) + (p2 + p3);
     }
