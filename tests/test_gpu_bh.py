@@ -33,7 +33,7 @@ def _real_bs(bh, oracle, fred):
                        0.25, e0)
 
 
-def _run(pkg, ctx, oracle, bh, bs, B, nsweeps, seed, cta_form="mirror"):
+def _run(pkg, ctx, oracle, bh, bs, B, nsweeps, seed, cta_form="mirror", shadowrate_model=False):
     lin = bs.lin
     sts = []
     for c in range(B):
@@ -42,11 +42,12 @@ def _run(pkg, ctx, oracle, bh, bs, B, nsweeps, seed, cta_form="mirror"):
         sts.append(st)
     rng = np.random.default_rng(seed)
     crns = [[bh.bh_draw_crn(rng, bs) for _ in range(nsweeps)] for _ in range(B)]
-    ch = pkg.Chains(ctx, N=lin.N, p=lin.p, T=lin.T, B=B, crn=True, model=pkg.MODEL_BLOCKHYBRID,
+    model = pkg.MODEL_SHADOWRATE if shadowrate_model else pkg.MODEL_BLOCKHYBRID
+    ch = pkg.Chains(ctx, N=lin.N, p=lin.p, T=lin.T, B=B, crn=True, model=model,
                     Ns=len(bs.ndxS), elbTmax=bs.elbT, elb_gibbsburn=bs.gibbsburn, elb=bs.ELB,
                     store_capacity=nsweeps)
     ch.set_data(0, lin.Y, lin.X, lin.iVdiag, lin.iVb, lin.sPHI, lin.Vol_0mean, lin.Vol_0vcvsqrt)
-    ch.set_elb_model(bs.ndxS, bs.actualrateBlock)
+    ch.set_elb_model(bs.ndxS, None if shadowrate_model else bs.actualrateBlock)
     ch.set_elb_slot(0, bs.elbT0, bs.sNaN)
     ch.set_state(*[np.stack([s[k] for s in sts], -1) for k in ("PAI", "A", "sqrtht", "h",
                                                                "sqrtPHI")])

@@ -97,8 +97,9 @@ def test_ctasys_per_equation_designs(ctx, oracle):
     assert rel_err(got[..., 0], want, sd) < 1e-9
 
 
-def test_astep(ctx, oracle):
-    su = toy_setup(oracle, N=6, p=2, Tobs=90, seed=4)
+@pytest.mark.parametrize("Tobs", [90, 1100])  # 1100: a sample longer than 1024 months
+def test_astep(ctx, oracle, Tobs):
+    su = toy_setup(oracle, N=6, p=2, Tobs=Tobs, seed=4)
     st = random_state(oracle, su, seed=2)
     rng = np.random.default_rng(1)
     RESID = su.Y - su.X @ st["PAI"]

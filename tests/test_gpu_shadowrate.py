@@ -1,7 +1,8 @@
 """mcmcVARshadowrate.m on the device (CCMM_MODEL_SHADOWRATE): CRN parity of the sweep with
 the block-hybrid oracle without an actual-rate block (CTA on the shadow-rate design for
-every equation, YHAT0 = []), and the product wrapper samplers.mcmcVARshadowrate end to end
-(outputs 1-17, the censored recursion flooring ndxOTHERYIELDS only)."""
+every equation, YHAT0 = []) on a toy panel and on the real C3 data (1e-9 against the device-order
+CTA mirror), and the product wrapper samplers.mcmcVARshadowrate end to end (outputs 1-17, the
+censored recursion flooring ndxOTHERYIELDS only)."""
 import numpy as np
 import pytest
 
@@ -53,6 +54,20 @@ def test_shadowrate_sweep_crn(pkg, ctx, oracle):
         e = max(rel_err(got["PAI"][..., c], st["PAI"], 1e-2), rel_err(S[:, :, c], st["shadowrate"], 0.1),
                 rel_err(got["sqrtht"][..., c], st["sqrtht"]))
         assert e < 1e-8, (c, e)
+
+
+def test_shadowrate_sweep_crn_real(pkg, ctx, oracle, fred):
+    """mcmcVARshadowrate.m on the config C3 data (fredblockMD20, ELB 0.25, p = 12; three shadow
+    rates, elbT = 165): CTA on the shadow-rate design for every equation (no actual-rate block),
+    two chained CRN sweeps against the oracle with CTAsys in the device's operation order
+    (oracle/cta_mirror.cta, cta_form="mirror"): the north star's 1e-9 on PAI, A, sqrtht, sqrtPHI, the
+    shadow rates and the rebuilt X / Y, drawTruncNormal branches and KSC indicators bit-exact."""
+    from oracle import ccmm_oracle_bh as bh
+    from test_gpu_bh import _check, _real_bs, _run
+    bs = _real_bs(bh, oracle, fred)
+    bs.actualrateBlock[:] = False                  # mcmcVARshadowrate: no actual-rate block
+    out = _run(pkg, ctx, oracle, bh, bs, B=2, nsweeps=2, seed=70, shadowrate_model=True)
+    _check(oracle, bs, *out, tol_pai=1e-9, tol_s=1e-9)
 
 
 def test_mcmcVARshadowrate_wrapper(pkg, fred):
