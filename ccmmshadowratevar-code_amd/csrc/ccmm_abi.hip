@@ -1459,7 +1459,8 @@ struct ccmm_chains {
 #define CASE_PSW(W)                                                                                   \
   case W:                                                                                             \
     hipLaunchKernelGGL(k_ps_prop<W>, g, dim3(256), 0, ctx->stream, e, ps, ra);                        \
-    hipLaunchKernelGGL(k_ps_apply<W>, dim3(d.B), dim3(1), 0, ctx->stream, e, ps, ra, kept ? 1 : 0); \
+    hipLaunchKernelGGL(k_ps_apply<W>, dim3(d.B), dim3(64), (size_t)ps_nmax * sizeof(double), ctx->stream, e, \
+                       ps, ra, kept ? 1 : 0);                                                           \
     break;
         CASE_PSW(16)
         CASE_PSW(32)

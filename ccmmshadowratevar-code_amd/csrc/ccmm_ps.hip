@@ -278,20 +278,23 @@ __global__ __launch_bounds__(64) void k_ps_chol_w(Dims d, ElbDev e, PsDev ps, Ch
 // out != nullptr writes x into the chain's shadow
 // rates.  Returns whether every cell lies below the ELB (a rejected proposal stops at its first cell
 // at or above it unless out is set).
+//
+// Normals: with CRN, randn(nmiss, Nproposals) column-major (cell i of proposal k: i + n k).  With
+// Philox, cell i of proposal k takes normal i + n2 k, n2 = n rounded up to even, so that every lane
+// of a wave sees the same parity at the same cell and both values of a Box-Muller pair (normals
+// 2P and 2P + 1: one log, one sqrt, one sincospi) serve two consecutive cells; the next pair is
+// formed while the current pair's two cells are substituted (software-pipelined by one pair).
 template <int W>
 __device__ inline bool ps_backsub(const double* __restrict__ Lc, const double* __restrict__ yb, int n,
-                                  const Rng& rng, int k, double elb, double* out, const int* cell) {
+                                  const Rng& rng, int k, double elb, double* out, const int* cell,
+                                  const double* zs = nullptr) {
   double win[W - 1];
 #pragma unroll
   for (int j = 0; j < W - 1; ++j) win[j] = 0.0;
   bool ok = true;
-  // the normal of the next cell is drawn while this cell's substitution runs (the generator does
-  // not depend on it): software-pipelined by one cell
-  double znext = rng.normal(CCMM_RNG_PS, (uint32_t)(n - 1 + n * k));
-  for (int i = n - 1; i >= 0; --i) {
+  // one cell: returns false when the proposal is rejected and nothing more is needed
+  auto step = [&](int i, double z) -> bool {
     const double* li = Lc + (size_t)i * W;
-    const double z = znext;
-    if (i > 0) znext = rng.normal(CCMM_RNG_PS, (uint32_t)(i - 1 + n * k));
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int j = 1; j < W; ++j) acc[j & 3] = fma(li[j], win[j - 1], acc[j & 3]);
@@ -302,11 +305,74 @@ __device__ inline bool ps_backsub(const double* __restrict__ Lc, const double* _
     ok = ok && (v < elb);
     if (out) {
       out[cell[i]] = v;
-    } else if (!ok) {
-      break;  // rejected (a cell at or above the ELB): the rest of this proposal is never read
+      return true;
     }
+    return ok;  // rejected (a cell at or above the ELB): the rest of this proposal is never read
+  };
+  if (zs) {  // the proposal's normals, formed beforehand (ps_normals)
+    for (int i = n - 1; i >= 0; --i)
+      if (!step(i, zs[i])) break;
+    return ok;
+  }
+  if (rng.crn) {
+    for (int i = n - 1; i >= 0; --i)
+      if (!step(i, rng.normal(CCMM_RNG_PS, (uint32_t)(i + n * k)))) break;
+    return ok;
+  }
+  const uint32_t base = (uint32_t)((n + (n & 1)) * k);  // even: the cells' parities are wave-uniform
+  auto pair = [&](uint32_t P, double& lo, double& hi) {  // normals 2P (cos) and 2P + 1 (sin)
+    const u32x4 r = rng.raw(CCMM_RNG_PS, P);
+    const double u1 = u01(r.x, r.y), u2 = u01(r.z, r.w);
+    const double rad = sqrt(-2.0 * log(u1));
+    double sn, cs;
+    sincospi(2.0 * u2, &sn, &cs);
+    lo = rad * cs;
+    hi = rad * sn;
+  };
+  // cell i's normal index base + i; the top cell opens pair (base + n - 1) >> 1
+  int i = n - 1;
+  uint32_t P = (base + (uint32_t)i) >> 1;
+  double lo, hi, nlo = 0.0, nhi = 0.0;
+  pair(P, lo, hi);
+  if (((base + (uint32_t)i) & 1u) == 0u) {  // n odd: the top cell is the even half of its pair
+    if (P > 0 && i > 0) pair(P - 1, nlo, nhi);
+    if (!step(i, lo)) return ok;
+    --i;
+    --P;
+    lo = nlo;
+    hi = nhi;
+  }
+  // now cell i is the odd half (hi) of pair P and cell i - 1 its even half (lo)
+  while (i >= 0) {
+    if (i >= 2) pair(P - 1, nlo, nhi);  // the next pair, formed beside this pair's two cells
+    if (!step(i, hi)) break;
+    if (i >= 1 && !step(i - 1, lo)) break;
+    i -= 2;
+    --P;
+    lo = nlo;
+    hi = nhi;
   }
   return ok;
+}
+
+// The normals of cell i and of cell i - 1 of proposal k, as ps_backsub takes them (i odd: the two
+// halves of one Box-Muller pair under Philox), for a parallel fill: lanes take cells in pairs.
+__device__ inline void ps_normal_pair(const Rng& rng, int n, int k, int i, double& zi, double& zim1) {
+  if (rng.crn) {
+    zi = rng.normal(CCMM_RNG_PS, (uint32_t)(i + n * k));
+    zim1 = (i >= 1) ? rng.normal(CCMM_RNG_PS, (uint32_t)(i - 1 + n * k)) : 0.0;
+    return;
+  }
+  const uint32_t idx = (uint32_t)((n + (n & 1)) * k) + (uint32_t)i;
+  const u32x4 r = rng.raw(CCMM_RNG_PS, idx >> 1);
+  const double u1 = u01(r.x, r.y), u2 = u01(r.z, r.w);
+  const double rad = sqrt(-2.0 * log(u1));
+  double sn, cs;
+  sincospi(2.0 * u2, &sn, &cs);
+  // idx odd: cell i is the pair's sin half and cell i - 1 its cos half; idx even (only the top cell
+  // when n is odd): cell i is the cos half
+  zi = (idx & 1u) ? rad * sn : rad * cs;
+  zim1 = rad * cs;
 }
 
 // proposals k = blockIdx.x * 256 + threadIdx.x of chain blockIdx.y.  The band rows of L are read with
@@ -334,24 +400,49 @@ __global__ __launch_bounds__(256) void k_ps_prop(ElbDev e, PsDev ps, RngArgs ra)
   if (threadIdx.x == 0 && kmin != INT_MAX) atomicMin(ps.acc + c, kmin);
 }
 
+// One wave per chain: the accepted proposal's normals are formed by all lanes (Box-Muller pairs in
+// parallel) into LDS, then lane 0 substitutes it into the chain's shadow rates (the serial chain
+// then waits on the substitution only, not on a log / sqrt / sincos per two cells)
 template <int W>
 __global__ __launch_bounds__(64) void k_ps_apply(ElbDev e, PsDev ps, RngArgs ra, int kept) {
+  extern __shared__ double zl[];  // [nmax]
   const int c = blockIdx.x;
-  if (threadIdx.x != 0) return;
+  const int lane = threadIdx.x;
   const int n = ps.n[c];
   const int kmin = ps.acc[c];
-  ps.acc[c] = INT_MAX;
-  if (n == 0 && ps.first)  // no proposals this sweep (precision not positive definite)
-    for (int q = 0; q < ps.per; ++q) ps.first[(size_t)c * ps.per + q] = __builtin_nan("");
   if (n == 0 || kmin == INT_MAX) {
-    ps.flag[c] = 0;
+    if (lane == 0) {
+      ps.acc[c] = INT_MAX;
+      if (n == 0 && ps.first)  // no proposals this sweep (precision not positive definite)
+        for (int q = 0; q < ps.per; ++q) ps.first[(size_t)c * ps.per + q] = __builtin_nan("");
+      ps.flag[c] = 0;
+    }
     return;
   }
   const Rng rng = ra.make(c);
-  (void)ps_backsub<W>(ps.L + (size_t)c * ps.nmax * W, ps.ybar + (size_t)c * ps.nmax, n, rng, kmin, ps.elb,
-                      e.Scur + (size_t)c * e.elbTmax * e.Ns, ps.cell + (size_t)c * ps.nmax);
-  ps.flag[c] = kmin + 1;
-  ps.count[2 * c + (kept ? 1 : 0)] += 1;
+  // cells in pairs from the top: (n - 1, n - 2), ... (n odd under Philox: the top cell alone first)
+  const bool lone = !rng.crn && (n & 1);
+  if (lone && lane == 0) {
+    double zi, zj;
+    ps_normal_pair(rng, n, kmin, n - 1, zi, zj);
+    zl[n - 1] = zi;
+  }
+  const int top = lone ? n - 2 : n - 1;  // cell top is a pair's upper half
+  for (int q = lane; 2 * q <= top; q += 64) {
+    const int i = top - 2 * q;
+    double zi, zj;
+    ps_normal_pair(rng, n, kmin, i, zi, zj);
+    zl[i] = zi;
+    if (i >= 1) zl[i - 1] = zj;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    ps.acc[c] = INT_MAX;
+    (void)ps_backsub<W>(ps.L + (size_t)c * ps.nmax * W, ps.ybar + (size_t)c * ps.nmax, n, rng, kmin, ps.elb,
+                        e.Scur + (size_t)c * e.elbTmax * e.Ns, ps.cell + (size_t)c * ps.nmax, zl);
+    ps.flag[c] = kmin + 1;
+    ps.count[2 * c + (kept ? 1 : 0)] += 1;
+  }
 }
 
 // missingrate_all(thisMCMCdraw,:,:) = missingrate (mcmcVARshadowrate.m:498): proposal 1 of a PS
