@@ -329,28 +329,35 @@ __device__ inline bool ps_backsub(const double* __restrict__ Lc, const double* _
     lo = rad * cs;
     hi = rad * sn;
   };
-  // cell i's normal index base + i; the top cell opens pair (base + n - 1) >> 1
+  // cell i's normal index base + i; the top cell opens pair (base + n - 1) >> 1.  Pairs run two
+  // ahead of the substitution: the pair of cells i - 4, i - 5 is formed while cells i, i - 1 are
+  // substituted (a pair's log / sqrt / sincos outlasts two cells' substitution)
   int i = n - 1;
   uint32_t P = (base + (uint32_t)i) >> 1;
-  double lo, hi, nlo = 0.0, nhi = 0.0;
+  double lo, hi, lo1 = 0.0, hi1 = 0.0;
   pair(P, lo, hi);
+  if (i >= 1) pair(P - 1, lo1, hi1);
   if (((base + (uint32_t)i) & 1u) == 0u) {  // n odd: the top cell is the even half of its pair
-    if (P > 0 && i > 0) pair(P - 1, nlo, nhi);
     if (!step(i, lo)) return ok;
     --i;
     --P;
-    lo = nlo;
-    hi = nhi;
+    lo = lo1;
+    hi = hi1;
+    if (i >= 3) pair(P - 1, lo1, hi1);
   }
-  // now cell i is the odd half (hi) of pair P and cell i - 1 its even half (lo)
+  // now cell i is the odd half (hi) of pair P and cell i - 1 its even half (lo); pair P - 1 is in
+  // (lo1, hi1) when cells i - 2, i - 3 exist
   while (i >= 0) {
-    if (i >= 2) pair(P - 1, nlo, nhi);  // the next pair, formed beside this pair's two cells
+    double lo2 = 0.0, hi2 = 0.0;
+    if (i >= 5) pair(P - 2, lo2, hi2);
     if (!step(i, hi)) break;
-    if (i >= 1 && !step(i - 1, lo)) break;
+    if (!step(i - 1, lo)) break;
     i -= 2;
     --P;
-    lo = nlo;
-    hi = nhi;
+    lo = lo1;
+    hi = hi1;
+    lo1 = lo2;
+    hi1 = hi2;
   }
   return ok;
 }
