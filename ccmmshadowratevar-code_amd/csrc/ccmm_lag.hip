@@ -756,11 +756,17 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       const bool b8 = lr & 8, b4 = lr & 4;
       auto fold = [&](const dbl4& t, double cv) {
         const double v0 = t[0] * cv, v1 = t[1] * cv, v2 = t[2] * cv, v3 = t[3] * cv;
+        // lane exchanges inside the 16-lane row by DPP (VALU, ~10 clocks) instead of ds_bpermute
+        // (an LDS round trip each): xor 8 = row_ror:8; xor 4 = row_shl:4 (lanes with bit 2 clear take
+        // lane + 4) / row_shr:4 (the others take lane - 4)
         double a = b8 ? v2 : v0, b = b8 ? v3 : v1;
-        a += __shfl_xor(b8 ? v0 : v2, 8);
-        b += __shfl_xor(b8 ? v1 : v3, 8);
+        a += dpp_d<0x128>(b8 ? v0 : v2);
+        b += dpp_d<0x128>(b8 ? v1 : v3);
         double q = b4 ? b : a;
-        q += __shfl_xor(b4 ? a : b, 4);
+        const double x4 = b4 ? a : b;
+        // both moves on every lane first (a DPP read of a lane masked off by a branch returns 0)
+        const double s4l = dpp_d<0x104>(x4), s4r = dpp_d<0x114>(x4);
+        q += b4 ? s4r : s4l;
         q += dpp_d<0x4E>(q);  // xor 2 (quad_perm, no LDS round trip)
         q += dpp_d<0xB1>(q);  // xor 1
         return q;
