@@ -1510,8 +1510,12 @@ struct ccmm_chains {
       hipLaunchKernelGGL(k_elb_prep, dim3(d.B, prep_wg), dim3(kElbPrepThreads), lds_prep, ctx->stream, d, e, xsel(),
                          cs, phi_lds, prep_rows);
     });
-    size_t lds_cond =
-        (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns + N * Ns + N * p * Ns) * sizeof(double);
+    // W_k of kb lags at once (all p + 1 when they fit beside the rest; k_elb_cond)
+    const size_t lds_cond0 =
+        (size_t)((p + 1) * Ns * N + (1 + 2 * p * Ns) * Ns + 2 * Ns * Ns + N * p * Ns) * sizeof(double);
+    int kb_cond = p + 1;
+    while (kb_cond > 1 && lds_cond0 + (size_t)kb_cond * N * Ns * sizeof(double) > 96 * 1024) --kb_cond;
+    size_t lds_cond = lds_cond0 + (size_t)kb_cond * N * Ns * sizeof(double);
     const int a_lds = (lds_cond + (size_t)N * N * sizeof(double) <= 64 * 1024) ? 1 : 0;
     if (a_lds) lds_cond += (size_t)N * N * sizeof(double);
     // two waves per censored month (BH N = 20: k_elb_cond 1.30 -> 1.13 ms at B = 256); four when the
@@ -1523,7 +1527,8 @@ struct ccmm_chains {
   case NS:                                                                                           \
     HIPCHECK(hipFuncSetAttribute((const void*)k_elb_cond<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                  (int)lds_cond));                                                    \
-    hipLaunchKernelGGL(k_elb_cond<NS>, dim3(e.elbTmax, d.B), dim3(nth_cond), lds_cond, ctx->stream, d, e, cs, a_lds); \
+    hipLaunchKernelGGL(k_elb_cond<NS>, dim3(e.elbTmax, d.B), dim3(nth_cond), lds_cond, ctx->stream, d, e, cs, a_lds, \
+                       kb_cond);                                                                        \
     break;
         CASE_NSC(1)
         CASE_NSC(2)

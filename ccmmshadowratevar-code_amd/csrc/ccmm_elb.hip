@@ -232,7 +232,7 @@ __device__ inline void elb_small_inverse(const double* M, double* Minv, int n) {
 }
 
 template <int NS>  // = e.Ns: compile-time, so the per-shadow-rate arrays below stay in registers
-__global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState cs, int a_lds) {
+__global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState cs, int a_lds, int kb) {
   extern __shared__ double sm[];
   __shared__ double red[4 * kElbNsMax];  // per-wave partial sums (blockDim.x = 64 or 256)
   const int c = blockIdx.y;
@@ -255,8 +255,8 @@ __global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState c
   double* gS = Q + (p + 1) * Ns * N;           // (1 + ncol) x Ns
   double* Pm = gS + (1 + ncol) * Ns;           // Ns x Ns
   double* Om = Pm + Ns * Ns;                   // Ns x Ns
-  double* Wl = Om + Ns * Ns;                   // N x Ns: W = diag(1/SVol^2) (A or A Φ_k)[:, S]
-  double* PS = Wl + N * Ns;                    // N x p x Ns: Φ's shadow-rate columns
+  double* Wl = Om + Ns * Ns;                   // kb x N x Ns: W_k = diag(1/SVol^2) (A or A Φ_k)[:, S]
+  double* PS = Wl + kb * N * Ns;               // N x p x Ns: Φ's shadow-rate columns
                                                //   PS[(j p + l) Ns + b] = Φ_{l+1}(j, S_b)
   int S[kElbNsMax];
   for (int a = 0; a < kElbNsMax; ++a) S[a] = a < Ns ? e.ndxS[a] : 0;
@@ -271,35 +271,44 @@ __global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState c
     for (int q = tid; q < N * N; q += nth) Al[q] = Ag[q];
   __syncthreads();
   const double* A = a_lds ? Al : Ag;
-  // ---- Q_0 = Λ_t[S, :], Q_k = B_k' Λ_{t+k};  Λ = A' diag(1/SVol^2) A (B3: A of month t + k)
-  for (int k = 0; k <= kmax; ++k) {
-    if (e.Amon) A = e.Amon + ((size_t)c * e.elbTmax + t + k) * N * N;
-    for (int i = tid; i < N; i += nth) {
+  // ---- Q_0 = Λ_t[S, :], Q_k = B_k' Λ_{t+k};  Λ = A' diag(1/SVol^2) A (B3: A of month t + k).
+  //      kb lags at a time (all kmax + 1 when the LDS holds their W): one pass over (k, i) for the
+  //      W_k, one over (k, a, j) for the Q_k, two barriers per batch instead of two per lag (the
+  //      per-lag passes kept 20-60 of the workgroup's threads busy between barriers).  Every
+  //      entry's sum is the per-lag form's, in the same order.
+  auto A_of = [&](int k) -> const double* {
+    return e.Amon ? e.Amon + ((size_t)c * e.elbTmax + t + k) * N * N : A;
+  };
+  for (int k0 = 0; k0 <= kmax; k0 += kb) {
+    const int k1 = min(kmax + 1, k0 + kb);
+    for (int q = tid; q < (k1 - k0) * N; q += nth) {
+      const int kl = q / N, i = q - kl * N, k = k0 + kl;
+      const double* Ak = A_of(k);
       double w[kElbNsMax] = {0.0, 0.0, 0.0, 0.0};
       const double sv = cs.sqrtht[((size_t)c * N + i) * d.TP + T0 + t + k];
       const double iv = 1.0 / (sv * sv);
       for (int a = 0; a < Ns; ++a) {
         double v = 0.0;
         if (k == 0) {
-          v = A[i + S[a] * N];
+          v = Ak[i + S[a] * N];
         } else {
-          for (int j = 0; j <= i; ++j) v = fma(A[i + j * N], PS[(j * p + k - 1) * Ns + a], v);
+          for (int j = 0; j <= i; ++j) v = fma(Ak[i + j * N], PS[(j * p + k - 1) * Ns + a], v);
         }
         w[a] = v * iv;
       }
-      for (int a = 0; a < Ns; ++a) Wl[i * Ns + a] = w[a];
+      for (int a = 0; a < Ns; ++a) Wl[((size_t)kl * N + i) * Ns + a] = w[a];
     }
     __syncthreads();
-    // Q_k[a][j] = Σ_{i >= j} W[i][a] A(i,j)
-    for (int q = tid; q < Ns * N; q += nth) {
-      const int a = q / N, j = q - a * N;
+    // Q_k[a][j] = Σ_{i >= j} W_k[i][a] A(i,j)
+    for (int q = tid; q < (k1 - k0) * Ns * N; q += nth) {
+      const int kl = q / (Ns * N), r = q - kl * Ns * N, a = r / N, j = r - a * N, k = k0 + kl;
+      const double* Ak = A_of(k);
       double v = 0.0;
-      for (int i = j; i < N; ++i) v = fma(Wl[i * Ns + a], A[i + j * N], v);
+      for (int i = j; i < N; ++i) v = fma(Wl[((size_t)kl * N + i) * Ns + a], Ak[i + j * N], v);
       Q[((size_t)k * Ns + a) * N + j] = v;
     }
     __syncthreads();
   }
-  __syncthreads();
   // ---- P = Λ_t,SS + Σ_k Q_k B_k
   if (tid < Ns * Ns) {
     const int a = tid / Ns, b = tid % Ns;
