@@ -225,14 +225,23 @@ static PhaseLock& phase_lock(int device, int id) {
 // the predictive-density kernels of one kept draw per chain (ccmm_fcst.hip): the paths (one
 // single-wave workgroup per (draw, chain); job Nd = the linear model's mean path) then the scores
 static void launch_fcst(hipStream_t st, FcstArgs& a, double* sv1) {
-  a.hc = fcst_chunk(a.N, a.Kx, a.p, a.H);
+  const bool reg = fcst_reg_path(a.N, a.p, a.bh) && env_select("CCMM_FCST_REG", 1) != 0;
+  a.hc = fcst_chunk(a.N, a.Kx, a.p, a.H, reg);
   a.sv1 = sv1;
-  const size_t lp = fcst_paths_lds_doubles(a.N, a.Kx, a.p, a.hc) * sizeof(double);
+  const size_t lp = fcst_paths_lds_doubles(a.N, a.Kx, a.p, a.hc, reg) * sizeof(double);
   const size_t ls = fcst_scores_lds_doubles(a.N) * sizeof(double);
   if (lp > 160 * 1024) throw std::runtime_error("forecast state does not fit LDS");
   const int njobs = a.bh ? a.Nd : a.Nd + 1;
-  HIPCHECK(hipFuncSetAttribute((const void*)k_fcst, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lp));
-  hipLaunchKernelGGL(k_fcst, dim3(njobs, a.B), dim3(64), lp, st, a);
+  const bool even = reg && a.N % 2 == 0 && a.N < kFcstRegN;
+  const void* kf = even ? (const void*)k_fcst<kFcstRegN - 1>
+                        : reg ? (const void*)k_fcst<kFcstRegN> : (const void*)k_fcst<0>;
+  HIPCHECK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lp));
+  if (even)
+    hipLaunchKernelGGL(k_fcst<kFcstRegN - 1>, dim3(njobs, a.B), dim3(64), lp, st, a);
+  else if (reg)
+    hipLaunchKernelGGL(k_fcst<kFcstRegN>, dim3(njobs, a.B), dim3(64), lp, st, a);
+  else
+    hipLaunchKernelGGL(k_fcst<0>, dim3(njobs, a.B), dim3(64), lp, st, a);
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipFuncSetAttribute((const void*)k_fcst_scores, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ls));
   hipLaunchKernelGGL(k_fcst_scores, dim3(a.Nd, a.B), dim3(64), ls, st, a);

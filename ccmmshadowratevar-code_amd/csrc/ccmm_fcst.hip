@@ -350,11 +350,23 @@ __device__ double score_censored(const double* invA, const double* sv, const dou
 // fcstA * state, its 2 N p lag products spread over G lane groups (lane = i + N g takes the lags
 // l = g mod G) whose partials lane i adds by shuffles.  The draw's SV at horizon 1 goes to
 // a.sv1 for k_fcst_scores.
-__host__ __device__ inline size_t fcst_paths_lds_doubles(int N, int Kx, int p, int hc) {
-  return (size_t)Kx * N + 2 * (size_t)N * N + 2 * (size_t)p * N + 3 * (size_t)hc * N;
+//
+// k_fcst<kFcstRegN> (N <= 21, p <= 3 kFcstRegLags, not hybrid) holds each lane's PAI column
+// entries for its lags in registers instead of staging PAI in LDS: the lag sums then read only
+// the ring from LDS, and the workgroup's LDS drops from ~52 KB to ~18 KB (hc <= 16) so that
+// eight waves share a CU instead of three.  Same fma order, same sums.
+constexpr int kFcstRegN = 21, kFcstRegLags = 4;  // k_fcst<20>: the same for even N <= 20
+
+__host__ __device__ inline bool fcst_reg_path(int N, int p, int bh) {
+  return N <= kFcstRegN && p <= 3 * kFcstRegLags && bh != 2;
 }
 
-__global__ __launch_bounds__(64) void k_fcst(FcstArgs a) {
+__host__ __device__ inline size_t fcst_paths_lds_doubles(int N, int Kx, int p, int hc, bool reg = false) {
+  return (reg ? 0 : (size_t)Kx * N) + 2 * (size_t)N * N + 2 * (size_t)p * N + 3 * (size_t)hc * N;
+}
+
+template <int RN>
+__global__ __launch_bounds__(64, 2) void k_fcst(FcstArgs a) {
   extern __shared__ double sm[];
   const int job = blockIdx.x, c = blockIdx.y;
   const int N = a.N, K = a.K, p = a.p, H = a.H, Nd = a.Nd, Kx = a.Kx, hc = a.hc;
@@ -362,8 +374,9 @@ __global__ __launch_bounds__(64) void k_fcst(FcstArgs a) {
   const int njobs = a.bh ? Nd : Nd + 1;
   if (job >= njobs) return;
   const bool mean_path = job == Nd;
-  double* sPAI = sm;                          // Kx x N (column i = equation i)
-  double* sSq = sPAI + (size_t)Kx * N;        // sqrtPHI, N x N column-major
+  constexpr bool REG = RN > 0;
+  double* sPAI = sm;                          // Kx x N (column i = equation i); none when REG
+  double* sSq = sPAI + (REG ? 0 : (size_t)Kx * N);  // sqrtPHI, N x N column-major
   double* sinvA = sSq + N * N;                // invA, N x N column-major
   double* ringl = sinvA + N * N;              // p x N
   double* ringc = ringl + p * N;              // p x N
@@ -373,10 +386,11 @@ __global__ __launch_bounds__(64) void k_fcst(FcstArgs a) {
   const int sl = a.slot ? a.slot[c] : 0;
   const bool hy = a.bh == 2;
   const double* PAIc = a.PAI + (size_t)c * a.ldPAI * N;
-  for (int e = lane; e < Kx * N; e += 64) {
-    const int j = e / Kx, k = e - j * Kx;
-    sPAI[e] = PAIc[(size_t)j * a.ldPAI + k];
-  }
+  if (!REG)
+    for (int e = lane; e < Kx * N; e += 64) {
+      const int j = e / Kx, k = e - j * Kx;
+      sPAI[e] = PAIc[(size_t)j * a.ldPAI + k];
+    }
   const double* Xj = a.Xj + (size_t)c * a.ldXj;
   for (int e = lane; e < N * N; e += 64) {
     sinvA[e] = a.invA[(size_t)c * N * N + e];
@@ -415,6 +429,20 @@ __global__ __launch_bounds__(64) void k_fcst(FcstArgs a) {
   const int G = N <= 21 ? 3 : (N <= 32 ? 2 : 1);  // lane groups of the lag sums (G N <= 64)
   const int g = lane / N, gi = lane - g * N;
   const double* pcol = sPAI + (size_t)(g < G ? gi : 0) * Kx;
+  // REG: lane (gi, g) holds PAI(1 + l N + j, gi) for its lags l = g + G m, and the intercept
+  double cf[REG ? kFcstRegLags : 1][REG ? RN : 1];
+  double c0 = 0.0;
+  if (REG) {
+    const double* pg = PAIc + (size_t)(g < G ? gi : 0) * a.ldPAI;
+    c0 = pg[0];
+#pragma unroll
+    for (int m = 0; m < (REG ? kFcstRegLags : 1); ++m) {
+      const int l = g + G * m;
+#pragma unroll
+      for (int j = 0; j < (REG ? RN : 1); ++j)
+        cf[m][j] = (g < G && l < p && j < N) ? pg[1 + l * N + j] : 0.0;
+    }
+  }
   int head = 0;
   __syncthreads();
   for (int h0 = 0; h0 < ((a.mode & 2) ? 0 : H); h0 += hc) {
@@ -459,7 +487,40 @@ __global__ __launch_bounds__(64) void k_fcst(FcstArgs a) {
       const int hh = h0 + hq;
       // fcstA * state on the lane groups
       double sl2 = 0.0, sc = 0.0;
-      if (g < G) {
+      if (REG) {
+        if (g < G) {
+          if (g == 0) sl2 = sc = Xj[0] * c0;
+#pragma unroll
+          for (int m = 0; m < (REG ? kFcstRegLags : 1); ++m) {
+            const int l = g + G * m;
+            if (l < p) {
+              int slot = head - l;
+              slot += (slot < 0) ? p : 0;
+              const double* rl = ringl + slot * N;
+              const double* rc = ringc + slot * N;
+              if (RN % 2 == 0) {  // N even: the ring rows are 16-byte aligned, two lags' entries a read
+#pragma unroll
+                for (int j = 0; j < (REG ? RN : 1); j += 2)
+                  if (j < N) {
+                    const double2 vl = *reinterpret_cast<const double2*>(rl + j);
+                    const double2 vc = *reinterpret_cast<const double2*>(rc + j);
+                    sl2 = fma(cf[m][j], vl.x, sl2);
+                    sc = fma(cf[m][j], vc.x, sc);
+                    sl2 = fma(cf[m][j + 1], vl.y, sl2);
+                    sc = fma(cf[m][j + 1], vc.y, sc);
+                  }
+              } else {
+#pragma unroll
+                for (int j = 0; j < (REG ? RN : 1); ++j)
+                  if (j < N) {
+                    sl2 = fma(cf[m][j], rl[j], sl2);
+                    sc = fma(cf[m][j], rc[j], sc);
+                  }
+              }
+            }
+          }
+        }
+      } else if (g < G) {
         if (g == 0) sl2 = sc = Xj[0] * pcol[0];  // constant state stays 1 (fcstA(1,1) = 1)
         for (int l = g; l < p; l += G) {
           int slot = head - l;
@@ -706,9 +767,10 @@ __global__ void k_fcst_accum(int N, int H, int Nd, int cap, int m, const double*
 }
 
 // horizons per shock chunk so that k_fcst's LDS fits one CU (at most H; at least 1)
-inline int fcst_chunk(int N, int Kx, int p, int H) {
-  int hc = H;
-  while (hc > 1 && fcst_paths_lds_doubles(N, Kx, p, hc) * sizeof(double) > 160 * 1024) hc = (hc + 1) / 2;
+// (the register path: at most 16 horizons, so that eight workgroups share a CU)
+inline int fcst_chunk(int N, int Kx, int p, int H, bool reg = false) {
+  int hc = reg ? std::min(H, 16) : H;
+  while (hc > 1 && fcst_paths_lds_doubles(N, Kx, p, hc, reg) * sizeof(double) > 160 * 1024) hc = (hc + 1) / 2;
   return hc;
 }
 

@@ -1,15 +1,17 @@
 """Schedules of the block-hybrid sweep that must not change a bit: the PHI block on the auxiliary
 stream beside the ELB step (the default) against plain stream order (CCMM_PHI_OVERLAP=0) -- the two
 blocks touch disjoint state -- and the lag-structured CTA solve on two workgroups per chain (the
-default at small B) against one (CCMM_SOLVE_SPLIT=0) -- every sum in the same order.  Every draw, the
-shadow rates, the forecasts and the status words are identical."""
+default at small B) against one (CCMM_SOLVE_SPLIT=0), and the forecast paths with the coefficients in
+registers (the default for N <= 21) against PAI staged in LDS (CCMM_FCST_REG=0) -- every sum in the
+same order.  Every draw, the shadow rates, the forecasts and the status words are identical."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("var,B", [("CCMM_PHI_OVERLAP", 8), ("CCMM_SOLVE_SPLIT", 8), ("CCMM_SOLVE_SPLIT", 1)])
+@pytest.mark.parametrize("var,B", [("CCMM_PHI_OVERLAP", 8), ("CCMM_SOLVE_SPLIT", 8), ("CCMM_SOLVE_SPLIT", 1),
+                                        ("CCMM_FCST_REG", 8)])
 def test_schedule_bit_identical(pkg, ctx, fred, monkeypatch, var, B):
     d = fred
     p = 12
