@@ -48,34 +48,48 @@ __global__ __launch_bounds__(256) void k_gram_big(Dims d, const int* __restrict_
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mymat = mats[wave];
   const int lcol = tid & 63, lt0 = (tid >> 6) * 8;
+  // 16 x 16 sub-tiles (x: b rows, y: a columns) that hold no lower-triangle entry of a real
+  // coefficient -- the diagonal tile's upper half and the padded rows / columns >= K, whose X rows
+  // are zero -- are not multiplied: they stay +0 (what the zero products sum to; the Cholesky and
+  // the solve read only the lower triangle)
+  unsigned need = 0;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+      if (b0 + 16 * x < d.K && a0 + 16 * y < d.K && !(ti == tj && y < x)) need |= 1u << (4 * x + y);
+  need = __builtin_amdgcn_readfirstlane(need);
   dbl4 acc[4][4];
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
     for (int y = 0; y < 4; ++y) acc[x][y] = dbl4{0.0, 0.0, 0.0, 0.0};
   const int nchunks = (T + kBC - 1) / kBC;
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const int t0 = ch * kBC;
-    {
-      const double* xa = X + (size_t)(a0 + lcol) * d.TP + t0 + lt0;
-      const double* xb = X + (size_t)(b0 + lcol) * d.TP + t0 + lt0;
-      double va[8], vb[8];
+  // chunk ch + 1's panel rows and weights are loaded into registers while chunk ch multiplies
+  double va[8], vb[8], wn = 0.0;
+  auto load_chunk = [&](int t0) __attribute__((always_inline)) {
+    const double* xa = X + (size_t)(a0 + lcol) * d.TP + t0 + lt0;
+    const double* xb = X + (size_t)(b0 + lcol) * d.TP + t0 + lt0;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        va[q] = xa[q];
-        vb[q] = xb[q];
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        Pa[lt0 + q][lcol] = va[q];
-        Pb[lt0 + q][lcol] = vb[q];
-      }
-      if (tid < 4 * kBC) {
-        const int e = tid >> 5, t = tid & 31;
-        Wl[e][t] = mats[e] >= 0 ? cs.W[(size_t)mats[e] * d.TP + t0 + t] : 0.0;
-      }
+    for (int q = 0; q < 8; ++q) {
+      va[q] = xa[q];
+      vb[q] = xb[q];
     }
+    if (tid < 4 * kBC) {
+      const int e = tid >> 5, t = tid & 31;
+      wn = mats[e] >= 0 ? cs.W[(size_t)mats[e] * d.TP + t0 + t] : 0.0;
+    }
+  };
+  load_chunk(0);
+  for (int ch = 0; ch < nchunks; ++ch) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      Pa[lt0 + q][lcol] = va[q];
+      Pb[lt0 + q][lcol] = vb[q];
+    }
+    if (tid < 4 * kBC) Wl[tid >> 5][tid & 31] = wn;
     __syncthreads();
+    if (ch + 1 < nchunks) load_chunk((ch + 1) * kBC);
 #pragma unroll
     for (int kk = 0; kk < kBC / 4; ++kk) {
       const int kr = kk * 4 + (lane >> 4);
@@ -90,7 +104,8 @@ __global__ __launch_bounds__(256) void k_gram_big(Dims d, const int* __restrict_
       for (int x = 0; x < 4; ++x)
 #pragma unroll
         for (int y = 0; y < 4; ++y)
-          acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[x], fa[y], acc[x][y], 0, 0, 0);
+          if (need & (1u << (4 * x + y)))
+            acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[x], fa[y], acc[x][y], 0, 0, 0);
     }
     __syncthreads();
   }
@@ -115,7 +130,7 @@ __global__ __launch_bounds__(256) void k_gram_big(Dims d, const int* __restrict_
 // HBM into registers one 16-column chunk ahead of use, the shared L(kb, k) chunk is
 // double-buffered in LDS (one barrier per chunk).  Factor phase: the LDS holds the
 // diagonal block and its inverse instead (a union: 66.5 KB, two systems per CU).
-constexpr int kCK = 16;  // k columns per pipelined chunk of the update
+constexpr int kCK = 8;  // k columns per pipelined chunk of the update
 constexpr int kLiLd = 65;
 __global__ __launch_bounds__(256, 2) void k_chol_big(Dims d, const int* __restrict__ slotIV,
                                                      const double* __restrict__ iVdiag, ChainState cs,
@@ -146,8 +161,9 @@ __global__ __launch_bounds__(256, 2) void k_chol_big(Dims d, const int* __restri
     const int lane = tid & 63, lr = lane & 15, lk = lane >> 4;
     const int kcol = kb * kBT;
     const int nch = kcol / kCK;
-    // ---- 1. update of block column kb, four row blocks at a time (one per wave)
-    for (int ib0 = kb; ib0 < nb && !(skip & 1); ib0 += 4) {
+    // ---- 1. update of block column kb, four row blocks at a time (one per wave); block column 0
+    //         has no update (its pass would store back the values it loaded)
+    for (int ib0 = kb; ib0 < nb && kb > 0 && !(skip & 1); ib0 += 4) {
       const int ib = min(ib0 + wave, nb - 1);  // idle waves shadow the last block, store nothing
       const bool act = ib0 + wave < nb;
       const int irow = ib * kBT;
@@ -161,58 +177,64 @@ __global__ __launch_bounds__(256, 2) void k_chol_big(Dims d, const int* __restri
             acc[x][y][r] = -A[(size_t)(kcol + y * 16 + lr) * KP + irow + x * 16 + lk + 4 * r];  // -C: the
       // products add into the negated block (no negated copy of the A fragments), negated back on store
       if (nch > 0) {
-        // the shared L(kb, k) chunk is double-buffered in LDS; each wave's own A fragments are
-        // loaded per chunk (a register prefetch of them would exceed the 256 registers that two
-        // systems per CU leave a wave: one system's serial tile factorisation then runs beside
-        // the other's MFMA update)
-        double bv[4];
+        // the shared L(kb, k) chunk is double-buffered in LDS and each wave's own A fragments are
+        // register double-buffered: chunk ch + 1's loads are in flight while chunk ch multiplies.
+        // A wave without a row block (act false) stages its share of the chunk but multiplies
+        // nothing, and the diagonal block's strictly upper 16 x 16 sub-tiles (never read) are
+        // skipped: the SIMD's MFMA pipe goes to the co-resident system's waves instead.
+        const bool diag = ib == kb;
+        double bv[kCK * kBT / 256];
+        auto load_b = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int e = tid + 256 * q;
-          bv[q] = A[(size_t)(e >> 6) * KP + kcol + (e & 63)];
-        }
+          for (int q = 0; q < kCK * kBT / 256; ++q) {
+            const int e = tid + 256 * q;
+            bv[q] = A[(size_t)(k0 + (e >> 6)) * KP + kcol + (e & 63)];
+          }
+        };
+        auto store_b = [&](double* Bn) __attribute__((always_inline)) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int e = tid + 256 * q;
-          smu[(e >> 6) * kBLd + (e & 63)] = bv[q];
-        }
+          for (int q = 0; q < kCK * kBT / 256; ++q) {
+            const int e = tid + 256 * q;
+            Bn[(e >> 6) * kBLd + (e & 63)] = bv[q];
+          }
+        };
+        double ac[kCK], an[kCK];
+        auto load_a = [&](double (&dst)[kCK], int kc) __attribute__((always_inline)) {
+          if (act) {
+#pragma unroll
+            for (int q = 0; q < kCK; ++q)
+              dst[q] = A[(size_t)(kc + (q >> 2) * 4 + lk) * KP + irow + (q & 3) * 16 + lr];
+          }
+        };
+        load_b(0);
+        load_a(ac, 0);
+        store_b(smu);
         __syncthreads();
         for (int ch = 0; ch < nch; ++ch) {
-          const int kc = ch * kCK;
-          double ac[16];
-#pragma unroll
-          for (int q = 0; q < 16; ++q)
-            ac[q] = A[(size_t)(kc + (q >> 2) * 4 + lk) * KP + irow + (q & 3) * 16 + lr];
           const bool more = ch + 1 < nch;
           if (more) {
-            const int k0 = (ch + 1) * kCK;
+            load_b((ch + 1) * kCK);
+            load_a(an, (ch + 1) * kCK);
+          }
+          if (act) {
+            const double* Bs = smu + (ch & 1) * kCK * kBLd;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int e = tid + 256 * q;
-              bv[q] = A[(size_t)(k0 + (e >> 6)) * KP + kcol + (e & 63)];
+            for (int ks = 0; ks < kCK / 4; ++ks) {
+              double fb[4];
+#pragma unroll
+              for (int y = 0; y < 4; ++y) fb[y] = Bs[(ks * 4 + lk) * kBLd + y * 16 + lr];
+#pragma unroll
+              for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y)
+                  if (!(diag && y > x))
+                    acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[ks * 4 + x], fb[y], acc[x][y], 0, 0, 0);
             }
           }
-          const double* Bs = smu + (ch & 1) * kCK * kBLd;
-#pragma unroll
-          for (int ks = 0; ks < kCK / 4; ++ks) {
-            double fb[4];
-#pragma unroll
-            for (int y = 0; y < 4; ++y) fb[y] = Bs[(ks * 4 + lk) * kBLd + y * 16 + lr];
-#pragma unroll
-            for (int x = 0; x < 4; ++x)
-#pragma unroll
-              for (int y = 0; y < 4; ++y)
-                acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[ks * 4 + x], fb[y], acc[x][y], 0, 0, 0);
-          }
-          if (more) {
-            double* Bn = smu + ((ch + 1) & 1) * kCK * kBLd;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int e = tid + 256 * q;
-              Bn[(e >> 6) * kBLd + (e & 63)] = bv[q];
-            }
-          }
+          if (more) store_b(smu + ((ch + 1) & 1) * kCK * kBLd);
           __syncthreads();
+#pragma unroll
+          for (int q = 0; q < kCK; ++q) ac[q] = an[q];
         }
       }
       if (act) {

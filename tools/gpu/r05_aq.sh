@@ -1,0 +1,14 @@
+#!/bin/bash
+# large path: k_gram_big sub-tile skipping + chunk prefetch, k_chol_big without the empty block-column-0
+# update -- large-path tests (bit-exact hybrid mirror), then the hybrid line's kernel stats
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${TAG:-r05aq}
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
+  tests/test_gpu_big.py tests/test_gpu_hybrid.py tests/test_gpu_bign.py tests/test_gpu_s120.py \
+  tests/test_gpu_fcst_hybrid.py > gpurun_out/${TAG}_tests.log 2>&1 &&
+rm -rf gpurun_out/prof_hy_$TAG &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_hy_$TAG" -o run --output-format csv -- \
+  python "$R/bench.py" --no-cpu --steps 1 --warmup 0 --no-fcst --bh-steps 0 --hy-steps 3 --hy-chains 256 \
+  --oos-steps 0 --oos-full-draws 0 --s120-steps 0 --girf-draws 0 \
+  > gpurun_out/prof_hy_$TAG.json 2> gpurun_out/prof_hy_$TAG.err
