@@ -40,8 +40,34 @@ __host__ __device__ inline int sv_nseg(int T) {
 // block index of separator i (0-based, i < P - 1)
 __host__ __device__ inline int sv_sep(int i, int T, int P) { return ((i + 1) * (T + 1)) / P - 1; }
 
-// per-wave LDS doubles: C (NN x NN+1), X (NN x 2NN+1), w (NN), fill columns, separator rows
-__host__ __device__ constexpr int sv_wave_lds(int NN) { return NN * (NN + 1) + NN * (2 * NN + 1) + NN + 2 * NN * NN; }
+// per-wave LDS doubles: C (NN x NN+2), X (NN x 2NN+2), w (NN), fill columns, separator rows.  The
+// row strides are even (NN is a multiple of 4), so every row starts 16-byte aligned and the
+// substitutions and product passes read two entries per ds_read_b128
+__host__ __device__ constexpr int sv_wave_lds(int NN) { return NN * (NN + 2) + NN * (2 * NN + 2) + NN + 2 * NN * NN; }
+typedef double sv_d2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) sv_d2 lds_d2;
+__device__ __forceinline__ sv_d2 sv_ld2(const lds_f64* p) { return *(const lds_d2*)p; }
+
+// v -= sum_{m<k} C(k, m) x_m in order m = 0..k-1 (row k of C at ro, 16-byte aligned), then
+// x_k = v * C(k, k) (the stored reciprocal); entries read in pairs
+template <int NN>
+__device__ __forceinline__ double sv_row_solve(const lds_f64* myC, int ro, int k, const double (&x)[NN], double v) {
+#pragma unroll
+  for (int m = 0; m + 1 < k; m += 2) {
+    const sv_d2 c2 = sv_ld2(myC + ro + m);
+    v = fma(-c2.x, x[m], v);
+    v = fma(-c2.y, x[m + 1], v);
+  }
+  double dk;
+  if (k & 1) {
+    const sv_d2 c2 = sv_ld2(myC + ro + k - 1);
+    v = fma(-c2.x, x[k - 1], v);
+    dk = c2.y;
+  } else {
+    dk = myC[ro + k];
+  }
+  return v * dk;
+}
 
 template <int NN>
 struct SvRec {
@@ -140,7 +166,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
                                                       const double* __restrict__ V0invm, ChainState cs,
                                                       RngArgs ra, double* __restrict__ sepbuf,
                                                       double* __restrict__ gbuf, int mode, int nwg) {
-  constexpr int CLD = NN + 1, XLD = 2 * NN + 1, NN2 = NN * NN;
+  constexpr int CLD = NN + 2, XLD = 2 * NN + 2, NN2 = NN * NN;
   constexpr bool G3 = 3 * NN <= 64;
   using R = SvRec<NN>;
   extern __shared__ double sm[];
@@ -317,10 +343,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
           // row k's factor entries are read once x[k - 2] is known, i.e. while row k - 1 is being
           // solved (one row in flight ahead: the LDS latency leaves the serial chain)
           const int ro = sv_after(k * CLD, x[k > 1 ? k - 2 : 0], k > 1);
-          double v = sgn * rhs[k * NN + rcol];
-#pragma unroll
-          for (int m = 0; m < k; ++m) v = fma(-myC[ro + m], x[m], v);
-          x[k] = v * myC[ro + k];
+          x[k] = sv_row_solve<NN>(myC, ro, k, x, sgn * rhs[k * NN + rcol]);
         }
         if (lane < 2 * NN) {
 #pragma unroll
@@ -341,7 +364,11 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
         const lds_f64* xr = myX + k * XLD;
         const double ak = xr[acol];
 #pragma unroll
-        for (int m = 0; m < NN; ++m) pr[m] = fma(ak, xr[boff + m], pr[m]);
+        for (int m = 0; m < NN; m += 2) {
+          const sv_d2 b2 = sv_ld2(xr + boff + m);
+          pr[m] = fma(ak, b2.x, pr[m]);
+          pr[m + 1] = fma(ak, b2.y, pr[m + 1]);
+        }
         wd = fma(ak, myw[k], wd);
       }
       // epilogue, uniform over the lanes (each lane group keeps only its own values):
@@ -372,7 +399,11 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
             const lds_f64* xr = myX + k * XLD;
             const double ak = xr[acol];
 #pragma unroll
-            for (int m = 0; m < NN; ++m) pr[m] = fma(ak, xr[NN + m], pr[m]);
+            for (int m = 0; m < NN; m += 2) {
+              const sv_d2 b2 = sv_ld2(xr + NN + m);
+              pr[m] = fma(ak, b2.x, pr[m]);
+              pr[m + 1] = fma(ak, b2.y, pr[m + 1]);
+            }
           }
           if (inD) {
 #pragma unroll
@@ -434,10 +465,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
 #pragma unroll
         for (int k = 0; k < NN; ++k) {
           const int ro = sv_after(k * CLD, x[k > 0 ? k - 1 : 0], k > 0);
-          double v = (lane < NN) ? r[R::M + ln * NN + k] : 0.0;
-#pragma unroll
-          for (int m = 0; m < k; ++m) v = fma(-myC[ro + m], x[m], v);
-          x[k] = v * myC[ro + k];
+          x[k] = sv_row_solve<NN>(myC, ro, k, x, (lane < NN) ? r[R::M + ln * NN + k] : 0.0);
         }
         if (lane < NN) {
 #pragma unroll
@@ -452,7 +480,11 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
           const lds_f64* xr = myX + k * XLD;
           const double ak = xr[ln];
 #pragma unroll
-          for (int m = 0; m < NN; ++m) cg[m] = fma(ak, xr[m], cg[m]);
+          for (int m = 0; m < NN; m += 2) {
+            const sv_d2 b2 = sv_ld2(xr + m);
+            cg[m] = fma(ak, b2.x, cg[m]);
+            cg[m + 1] = fma(ak, b2.y, cg[m + 1]);
+          }
           cb = fma(ak, myw[k], cb);
         }
       }
@@ -632,7 +664,6 @@ template <int NN, int NW, bool PACK>
 static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
                                 const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
                                 int mode, int nwg) {
-  constexpr int CLD = NN + 1, XLD = 2 * NN + 1;
   const size_t lds = (size_t)(2 * NN * NN + kSvMaxSeg * NN + NW * sv_wave_lds(NN)) * sizeof(double);
   hipError_t e = hipFuncSetAttribute((const void*)k_sv_part<NN, NW, PACK>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -695,7 +726,7 @@ hipError_t sv_launch_part(int N, hipStream_t st, Dims d, const int* Tslot, const
     case 20: return sv_launch_one<20, 8>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
     case 24: return sv_launch_one<24, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
     case 28: return sv_launch_one<28, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
-    default: return sv_launch_one<32, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
+    default: return sv_launch_one<32, 2>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);  // LDS
   }
 }
 

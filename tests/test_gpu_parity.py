@@ -110,8 +110,9 @@ def test_astep(ctx, oracle, Tobs):
     assert rel_err(ginvA[..., 0], invA, 1e-3) < 1e-10
 
 
-def test_sv_ksc(ctx, oracle):
-    su = toy_setup(oracle, N=5, p=2, Tobs=120, seed=6)
+@pytest.mark.parametrize("N", [5, 20, 30])  # k_sv_part buckets 8, 20 and 32 (two waves, LDS)
+def test_sv_ksc(ctx, oracle, N):
+    su = toy_setup(oracle, N=N, p=2, Tobs=120, seed=6)
     st = random_state(oracle, su, seed=3)
     rng = np.random.default_rng(2)
     RESID = su.Y - su.X @ st["PAI"]
