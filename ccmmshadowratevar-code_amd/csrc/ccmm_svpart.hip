@@ -160,6 +160,32 @@ __device__ __forceinline__ double sv_bwd(double r, const double (&lc)[NN], const
   return r;
 }
 
+// The same two substitutions with the reciprocal diagonal held per lane (rd = 1 / C_ii on lane i):
+// lane k's entry is scaled before the broadcast instead of after it (the same product), so the
+// phase-C block loads need no uniform copy of the diagonal
+template <int NN>
+__device__ __forceinline__ double sv_fwd_d(double b, const double (&s)[NN], double rd, int lane0) {
+  const int lane = sv_lane(lane0);
+#pragma unroll
+  for (int k = 0; k < NN; ++k) {
+    const double yk = readlane_d(b * rd, k);
+    b = (lane == k) ? yk : ((lane > k) ? fma(-s[k], yk, b) : b);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return b;
+}
+template <int NN>
+__device__ __forceinline__ double sv_bwd_d(double r, const double (&lc)[NN], double rd, int lane0) {
+  const int lane = sv_lane(lane0);
+#pragma unroll
+  for (int k = NN - 1; k >= 0; --k) {
+    const double xk = readlane_d(r * rd, k);
+    r = (lane == k) ? xk : ((lane < k) ? fma(-lc[k], xk, r) : r);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return r;
+}
+
 template <int NN, int NW, bool PACK>
 __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restrict__ Tslot,
                                                       const double* __restrict__ V0inv,
@@ -499,17 +525,23 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
 #pragma unroll
   for (int m = 0; m < NN; ++m) qrow[m] = Ql[ln * NN + m];
   // C_t -> LDS (whole wave), then row / column / reciprocal diagonal per lane
-  auto load_factor = [&](int t, double (&lr)[NN], double (&lc)[NN], double (&rps)[NN])
-                         __attribute__((always_inline)) {
+  // row ln (entry pairs), column ln and the lane's own reciprocal diagonal of the block in LDS
+  auto read_factor = [&](double (&lr)[NN], double (&lc)[NN], double& rd) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < NN; m += 2) {
+      const sv_d2 r2 = sv_ld2(myC + ln * CLD + m);
+      lr[m] = r2.x;
+      lr[m + 1] = r2.y;
+    }
+#pragma unroll
+    for (int m = 0; m < NN; ++m) lc[m] = myC[m * CLD + ln];
+    rd = myC[ln * CLD + ln];
+  };
+  auto load_factor = [&](int t, double (&lr)[NN], double (&lc)[NN], double& rd) __attribute__((always_inline)) {
     const double* Ct = Cg + (size_t)t * NN2;
     for (int e = lane; e < NP; e += 64) myC[unpack_at(e)] = Ct[e];
     sv_wave_sync();
-#pragma unroll
-    for (int m = 0; m < NN; ++m) {
-      lr[m] = myC[ln * CLD + m];
-      lc[m] = myC[m * CLD + ln];
-      rps[m] = myC[m * CLD + m];
-    }
+    read_factor(lr, lc, rd);
     sv_wave_sync();
   };
   // software-pipelined form (NN <= 20): the next block's factor is fetched into registers
@@ -528,34 +560,29 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
       pf[i] = (e < NP) ? __builtin_nontemporal_load(Ct + e) : 0.0;
     }
   };
-  auto commit_factor = [&](const double (&pf)[kPF], double (&lr)[NN], double (&lc)[NN], double (&rps)[NN])
+  auto commit_factor = [&](const double (&pf)[kPF], double (&lr)[NN], double (&lc)[NN], double& rd)
                            __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < kPF; ++i)
       if (lane + 64 * i < NP) myC[upk[i]] = pf[i];
     sv_wave_sync();
-#pragma unroll
-    for (int m = 0; m < NN; ++m) {
-      lr[m] = myC[ln * CLD + m];
-      lc[m] = myC[m * CLD + ln];
-      rps[m] = myC[m * CLD + m];
-    }
+    read_factor(lr, lc, rd);
     sv_wave_sync();
   };
   if (wave == 0 && P > 1 && !(mode & 4)) {
     for (int i = P - 2; i >= 0; --i) {
       const int sb = sv_sep(i, T, P);
-      double lr[NN], lc[NN], rps[NN];
-      load_factor(sb, lr, lc, rps);
+      double lr[NN], lc[NN], rd;
+      load_factor(sb, lr, lc, rd);
       double rv = (lane < NN) ? Wg[(size_t)sb * NN + ln] + zdraw(sb) : 0.0;
       if (i + 1 < P - 1) {
         const double* Mr = rec + (size_t)i * R::LEN + R::M;  // row ln of M: Mr[m*NN + ln]
         double acc = 0.0;
 #pragma unroll
         for (int m = 0; m < NN; ++m) acc = fma(Mr[m * NN + ln], xsep[(i + 1) * NN + m], acc);
-        rv -= sv_fwd<NN>(acc, lr, rps, lane);
+        rv -= sv_fwd_d<NN>(acc, lr, rd, lane);
       }
-      const double x = sv_bwd<NN>(rv, lc, rps, lane);
+      const double x = sv_bwd_d<NN>(rv, lc, rd, lane);
       if (lane < NN) xsep[i * NN + lane] = x;
       if (real) {
         hout[(size_t)ln * TP + sb - 1] = x;
@@ -578,20 +605,24 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
       for (int t = first; t <= last; ++t) {
         if (lane < NN) Gb[(size_t)t * NN + lane] = g;
         if (t < last) {
-          double lr[NN], lc[NN], rps[NN];
+          double lr[NN], lc[NN], rd;
           if constexpr (kPipe) {
-            commit_factor(pf, lr, lc, rps);
+            commit_factor(pf, lr, lc, rd);
             if (t + 1 < last) fetch_factor(t + 1, pf);
           } else {
-            load_factor(t, lr, lc, rps);
+            load_factor(t, lr, lc, rd);
           }
-          double v = sv_fwd<NN>(g, lr, rps, lane);
-          v = sv_bwd<NN>(v, lc, rps, lane);
+          double v = sv_fwd_d<NN>(g, lr, rd, lane);
+          v = sv_bwd_d<NN>(v, lc, rd, lane);
           if (lane < NN) myw[lane] = v;
           sv_wave_sync();
           g = 0.0;
 #pragma unroll
-          for (int m = 0; m < NN; ++m) g = fma(qrow[m], myw[m], g);
+          for (int m = 0; m < NN; m += 2) {
+            const sv_d2 w2 = sv_ld2(myw + m);
+            g = fma(qrow[m], w2.x, g);
+            g = fma(qrow[m + 1], w2.y, g);
+          }
           sv_wave_sync();
         }
       }
@@ -602,17 +633,21 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
     double pfb[kPF];
     if (kPipe) fetch_factor(last, pfb);
     for (int t = last; t >= first; --t) {
-      double lr[NN], lc[NN], rps[NN];
+      double lr[NN], lc[NN], rd;
       if constexpr (kPipe) {
-        commit_factor(pfb, lr, lc, rps);
+        commit_factor(pfb, lr, lc, rd);
         if (t > first) fetch_factor(t - 1, pfb);
       } else {
-        load_factor(t, lr, lc, rps);
+        load_factor(t, lr, lc, rd);
       }
       double acc = 0.0, xn = 0.0;
       if (t < T) {
 #pragma unroll
-        for (int m = 0; m < NN; ++m) acc = fma(-qrow[m], myw[m], acc);
+        for (int m = 0; m < NN; m += 2) {
+          const sv_d2 w2 = sv_ld2(myw + m);
+          acc = fma(-qrow[m], w2.x, acc);
+          acc = fma(-qrow[m + 1], w2.y, acc);
+        }
         xn = myw[ln];
       }
       if (hasL && lane < NN) acc += Gb[(size_t)t * NN + ln];
@@ -621,8 +656,8 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
       if (mode & 64) {  // timing ablation only
         x = rv - acc;
       } else {
-        rv -= sv_fwd<NN>(acc, lr, rps, lane);
-        x = sv_bwd<NN>(rv, lc, rps, lane);
+        rv -= sv_fwd_d<NN>(acc, lr, rd, lane);
+        x = sv_bwd_d<NN>(rv, lc, rd, lane);
       }
       if (real) {
         if (t >= 1) {
