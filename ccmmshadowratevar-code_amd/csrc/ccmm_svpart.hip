@@ -186,13 +186,15 @@ __device__ __forceinline__ double sv_bwd_d(double r, const double (&lc)[NN], dou
   return r;
 }
 
-template <int NN, int NW, bool PACK>
+template <int NN, int NW, bool PACK, bool SVMFMA>
 __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restrict__ Tslot,
                                                       const double* __restrict__ V0inv,
                                                       const double* __restrict__ V0invm, ChainState cs,
                                                       RngArgs ra, double* __restrict__ sepbuf,
                                                       double* __restrict__ gbuf, int mode, int nwg) {
   constexpr int CLD = NN + 2, XLD = 2 * NN + 2, NN2 = NN * NN;
+  // phase A's block products on MFMA (NN = 20; CCMM_SV_MFMA=0 keeps the VALU pass)
+  constexpr bool kSvMfma = NN == 20 && SVMFMA;
   constexpr bool G3 = 3 * NN <= 64;
   using R = SvRec<NN>;
   extern __shared__ double sm[];
@@ -377,25 +379,93 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
         }
       }
       sv_wave_sync();
-      // one uniform product pass: pr[m] = sum_k a[k] X[k][m + boff], a = own column
-      // (lanes < 2NN) or the X2 column of lane - NN (lanes 2NN..3NN-1)
-      const int boff = (lane < 2 * NN) ? 0 : NN;
-      const int acol = (lane < 2 * NN) ? lane : ((lane < 3 * NN) ? lane - NN : NN);
       double pr[NN];
-#pragma unroll
-      for (int m = 0; m < NN; ++m) pr[m] = 0.0;
       double wd = 0.0;
-#pragma unroll 1
-      for (int k = 0; k < NN; ++k) {
-        const lds_f64* xr = myX + k * XLD;
-        const double ak = xr[acol];
+      if constexpr (kSvMfma) {
+        // NN = 20: the three 20 x 20 blocks X1'X1, X2'X1, X2'X2 are blocks of the Gram X'X of the
+        // 20 x 40 block [X1 X2]: six lower 16 x 16 tiles of it on v_mfma_f64_16x16x4_f64 (fragment
+        // F(I, s) = X[4s + l/16][16I + l%16], columns >= 40 zero), written as the row blocks the lane
+        // groups read -- P1 = G(:, 0:20) (40 x 20) and P2 = G(20:40, 20:40) -- over the wave's C and
+        // X area (both dead until the next block).  w'X: each column's own sum (k in order), lanes
+        // 2NN.. take column lane - NN's.
+        {
+          double wo = 0.0;
+#pragma unroll
+          for (int k = 0; k < NN; k += 2) {
+            const sv_d2 w2 = sv_ld2(myw + k);
+            wo = fma(myX[k * XLD + (lane < 2 * NN ? lane : 0)], w2.x, wo);
+            wo = fma(myX[(k + 1) * XLD + (lane < 2 * NN ? lane : 0)], w2.y, wo);
+          }
+          const double wsh = __shfl(wo, (lane >= 2 * NN && lane < 3 * NN) ? lane - NN : lane, 64);
+          wd = (lane >= 2 * NN && lane < 3 * NN) ? wsh : wo;
+        }
+        const int lr = lane & 15, lk = lane >> 4;
+        double F[3][5];
+#pragma unroll
+        for (int I = 0; I < 3; ++I)
+#pragma unroll
+          for (int s5 = 0; s5 < 5; ++s5) {
+            const int col = 16 * I + lr;
+            F[I][s5] = (col < 2 * NN) ? myX[(4 * s5 + lk) * XLD + col] : 0.0;
+          }
+        dbl4 g[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) g[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s5 = 0; s5 < 5; ++s5) {
+          g[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(F[0][s5], F[0][s5], g[0], 0, 0, 0);
+          g[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(F[1][s5], F[0][s5], g[1], 0, 0, 0);
+          g[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(F[1][s5], F[1][s5], g[2], 0, 0, 0);
+          g[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(F[2][s5], F[0][s5], g[3], 0, 0, 0);
+          g[4] = __builtin_amdgcn_mfma_f64_16x16x4f64(F[2][s5], F[1][s5], g[4], 0, 0, 0);
+          g[5] = __builtin_amdgcn_mfma_f64_16x16x4f64(F[2][s5], F[2][s5], g[5], 0, 0, 0);
+        }
+        sv_wave_sync();  // every fragment read before the C / X area is overwritten
+        lds_f64* P1 = myC;                   // 40 x 20
+        lds_f64* P2 = myC + 2 * NN * NN;     // 20 x 20
+        constexpr int TI[6] = {0, 1, 1, 2, 2, 2}, TJ[6] = {0, 0, 1, 0, 1, 2};
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int a = 16 * TI[q] + lk + 4 * r, b = 16 * TJ[q] + lr;  // D(row a, col b)
+            const double v = g[q][r];
+            if (a < 2 * NN && b < 2 * NN) {
+              if (b < NN) P1[a * NN + b] = v;
+              else if (a >= NN) P2[(a - NN) * NN + (b - NN)] = v;
+              if (TI[q] != TJ[q]) {  // the transposed entry (b, a), a > b
+                if (a < NN) P1[b * NN + a] = v;
+                else if (b >= NN) P2[(b - NN) * NN + (a - NN)] = v;
+              }
+            }
+          }
+        sv_wave_sync();
+        const lds_f64* prow = (lane < 2 * NN) ? P1 + lane * NN : P2 + (lane < 3 * NN ? lane - 2 * NN : 0) * NN;
 #pragma unroll
         for (int m = 0; m < NN; m += 2) {
-          const sv_d2 b2 = sv_ld2(xr + boff + m);
-          pr[m] = fma(ak, b2.x, pr[m]);
-          pr[m + 1] = fma(ak, b2.y, pr[m + 1]);
+          const sv_d2 p2 = sv_ld2(prow + m);
+          pr[m] = p2.x;
+          pr[m + 1] = p2.y;
         }
-        wd = fma(ak, myw[k], wd);
+      } else {
+        // one uniform product pass: pr[m] = sum_k a[k] X[k][m + boff], a = own column
+        // (lanes < 2NN) or the X2 column of lane - NN (lanes 2NN..3NN-1)
+        const int boff = (lane < 2 * NN) ? 0 : NN;
+        const int acol = (lane < 2 * NN) ? lane : ((lane < 3 * NN) ? lane - NN : NN);
+#pragma unroll
+        for (int m = 0; m < NN; ++m) pr[m] = 0.0;
+#pragma unroll 1
+        for (int k = 0; k < NN; ++k) {
+          const lds_f64* xr = myX + k * XLD;
+          const double ak = xr[acol];
+#pragma unroll
+          for (int m = 0; m < NN; m += 2) {
+            const sv_d2 b2 = sv_ld2(xr + boff + m);
+            pr[m] = fma(ak, b2.x, pr[m]);
+            pr[m + 1] = fma(ak, b2.y, pr[m + 1]);
+          }
+          wd = fma(ak, myw[k], wd);
+        }
       }
       // epilogue, uniform over the lanes (each lane group keeps only its own values):
       //   lanes 0..NN-1:    successor's D~ row / b~ entry (after the last block of a
@@ -423,7 +493,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
 #pragma unroll 1
           for (int k = 0; k < NN; ++k) {
             const lds_f64* xr = myX + k * XLD;
-            const double ak = xr[acol];
+            const double ak = xr[(lane < 2 * NN) ? lane : NN];  // own column (lanes < 2NN)
 #pragma unroll
             for (int m = 0; m < NN; m += 2) {
               const sv_d2 b2 = sv_ld2(xr + NN + m);
@@ -695,12 +765,12 @@ __global__ void k_sv_normals(Dims d, const int* __restrict__ Tslot, ChainState c
   gbuf[(size_t)(d.B + c) * (d.TP + 1) * NN + (size_t)t * NN + i] = rng.normal(CCMM_RNG_SVZ, (uint32_t)(i + n * t));
 }
 
-template <int NN, int NW, bool PACK>
-static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
-                                const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
-                                int mode, int nwg) {
+template <int NN, int NW, bool PACK, bool MF>
+static hipError_t sv_launch_k(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
+                              const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
+                              int mode, int nwg) {
   const size_t lds = (size_t)(2 * NN * NN + kSvMaxSeg * NN + NW * sv_wave_lds(NN)) * sizeof(double);
-  hipError_t e = hipFuncSetAttribute((const void*)k_sv_part<NN, NW, PACK>,
+  hipError_t e = hipFuncSetAttribute((const void*)k_sv_part<NN, NW, PACK, MF>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_sv_normals, dim3(((d.TP + 1) * d.N + 255) / 256, d.B), dim3(256), 0, st, d, Tslot, cs, ra,
@@ -710,15 +780,28 @@ static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const
   // launches: phase A, then phases B + C, in which every workgroup of the chain redoes the serial
   // separator pass (identical values and stores) instead of a third launch; same draws
   if (nwg == 1) {
-    hipLaunchKernelGGL((k_sv_part<NN, NW, PACK>), dim3(d.B), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm, cs,
-                       ra, sep, gbuf, mode, 1);
+    hipLaunchKernelGGL((k_sv_part<NN, NW, PACK, MF>), dim3(d.B), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm,
+                       cs, ra, sep, gbuf, mode, 1);
   } else {
-    hipLaunchKernelGGL((k_sv_part<NN, NW, PACK>), dim3(d.B, nwg), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm,
-                       cs, ra, sep, gbuf, mode | 2 | 4 | 8, nwg);
-    hipLaunchKernelGGL((k_sv_part<NN, NW, PACK>), dim3(d.B, nwg), dim3(64 * NW), lds, st, d, Tslot, V0inv, V0invm,
-                       cs, ra, sep, gbuf, mode | 1, nwg);
+    hipLaunchKernelGGL((k_sv_part<NN, NW, PACK, MF>), dim3(d.B, nwg), dim3(64 * NW), lds, st, d, Tslot, V0inv,
+                       V0invm, cs, ra, sep, gbuf, mode | 2 | 4 | 8, nwg);
+    hipLaunchKernelGGL((k_sv_part<NN, NW, PACK, MF>), dim3(d.B, nwg), dim3(64 * NW), lds, st, d, Tslot, V0inv,
+                       V0invm, cs, ra, sep, gbuf, mode | 1, nwg);
   }
   return hipGetLastError();
+}
+
+// NN = 20: phase A's block products on MFMA unless CCMM_SV_MFMA=0
+template <int NN, int NW, bool PACK>
+static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
+                                const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
+                                int mode, int nwg) {
+  if constexpr (NN == 20) {
+    const char* ev = std::getenv("CCMM_SV_MFMA");
+    if (ev && std::atoi(ev) == 0)
+      return sv_launch_k<NN, NW, PACK, false>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
+  }
+  return sv_launch_k<NN, NW, PACK, true>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
 }
 
 // block factors stored as packed lower triangles (default: 0.55x the factor traffic of full rows,
