@@ -241,11 +241,8 @@ def main():
             # fused weighted SYRK + Cholesky: N*[T*K(K+1) + K^3/3] flop per chain
             kname = "k_gram_chol"
             flop = B * N * (T * K * (K + 1) + K ** 3 / 3)
-        elif ktimes.get("k_gram_big", (0, 0))[1]:
-            kname = "k_gram_big"  # multi-equation Gram (large-system path): T K (K+1) per system
-            flop = B * N * T * K * (K + 1)
         else:
-            kname = "k_syrk"
+            kname = "k_gram_big"  # multi-equation Gram (large-system path): T K (K+1) per system
             flop = B * N * T * K * (K + 1)
         kms = ktimes[kname][0] / max(ktimes[kname][1], 1)
         ach = flop / (kms * 1e-3) / 1e12

@@ -18,8 +18,10 @@ import numpy as np
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("CCMM_LIB", _HERE / "csrc" / "libccmm.so"))
 
+ABI_VERSION = 4  # include/ccmm.h CCMM_ABI_VERSION this binding's structures follow
 CCMM_OK = 0
 CCMM_ERR_NOTSPD = -4
+STATUS_INFO = 1 | 64  # informational status bits: QR fallback used, PS precision fell back to Gibbs
 MODEL_LINEAR = 0
 MODEL_BLOCKHYBRID = 1
 MODEL_HYBRID = 2  # mcmcVARhybridGibbs.m: K = N*p + 1 + Ns*p
@@ -77,6 +79,13 @@ _SIGS = {
     "ccmm_last_error": (C.c_char_p, []),
     "ccmm_ablation_build": (C.c_int, []),
     "ccmm_env_ignored": (C.c_int, [C.c_char_p, C.c_int]),
+    "ccmm_option_count": (C.c_int, []),
+    "ccmm_option_name": (C.c_char_p, [C.c_int]),
+    "ccmm_option_default": (C.c_int, [C.c_char_p, _ip]),
+    "ccmm_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
+    "ccmm_get_option": (C.c_int, [C.c_void_p, C.c_char_p, _ip]),
+    "ccmm_chains_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
+    "ccmm_chains_get_option": (C.c_int, [C.c_void_p, C.c_char_p, _ip]),
     "ccmm_device_count": (C.c_int, []),
     "ccmm_create": (C.c_void_p, [C.c_int]),
     "ccmm_destroy": (None, [C.c_void_p]),
@@ -179,6 +188,9 @@ def load_library(path: str | os.PathLike | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    v = lib.ccmm_abi_version()
+    if v != ABI_VERSION:  # the ctypes structures (ChainConfig, BatchConfig, BatchOut) follow one header
+        raise RuntimeError(f"{p}: ABI version {v}, this binding expects {ABI_VERSION}; rebuild the library")
     if path is None:
         _lib = lib
     return lib
@@ -203,6 +215,19 @@ def env_ignored() -> tuple[int, list[str]]:
 
 def ablation_build() -> bool:
     return bool(load_library().ccmm_ablation_build())
+
+
+def option_names() -> list[str]:
+    """Names of the kernel options (ccmm_set_option; host only, no GPU needed)."""
+    lib = load_library()
+    return [lib.ccmm_option_name(i).decode() for i in range(lib.ccmm_option_count())]
+
+
+def option_default(name: str) -> int:
+    """ccmm_option_default: the value a new context starts from (host only)."""
+    v = C.c_int(0)
+    _check(load_library().ccmm_option_default(name.encode(), C.byref(v)), f"ccmm_option_default({name})")
+    return int(v.value)
 
 
 def _check(rc, what):
@@ -279,6 +304,32 @@ class Context:
 
     def synchronize(self):
         _check(self.lib.ccmm_synchronize(self.handle), "ccmm_synchronize")
+
+    def set_option(self, name: str, value: int):
+        """ccmm_set_option: a kernel form / schedule for the block-level calls and the chain sets
+        created on this context afterwards."""
+        _check(self.lib.ccmm_set_option(self.handle, name.encode(), int(value)), f"ccmm_set_option({name})")
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int(0)
+        _check(self.lib.ccmm_get_option(self.handle, name.encode(), C.byref(v)), f"ccmm_get_option({name})")
+        return int(v.value)
+
+    def options(self, **opts):
+        """Context manager: set options for the block, restore the previous values after."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old = {k: self.get_option(k) for k in opts}
+            try:
+                for k, v in opts.items():
+                    self.set_option(k, v)
+                yield self
+            finally:
+                for k, v in old.items():
+                    self.set_option(k, v)
+        return cm()
 
     # ------------------------------------------------------------ block-level
     def cta(self, Y, X, A, sqrtht, iVdiag, iVb, PAI, z=None, y_per_chain=False, x_per_chain=False):
@@ -613,7 +664,7 @@ def draw_trunc_normal(mu, sig, elb, u):
 class Chains:
     """Device-resident chain set (ccmm_chains_*): B chains of one model."""
 
-    KERNELS = ("k_resid", "k_cta_weights", "k_syrk", "k_chol", "k_cta_solve", "k_astep",
+    KERNELS = ("k_resid", "k_cta_weights", "k_cta_solve", "k_astep",
                "k_sv_mix", "k_sv_part", "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
                "k_elb_prep", "k_elb_cond", "k_elb_gibbs", "k_elb_rebuild", "k_gram_chol_lag",
                "k_cta_solve_lag", "k_fcst", "k_gram_big", "k_chol_big", "k_cta_solve_big",
@@ -621,7 +672,7 @@ class Chains:
 
     def __init__(self, ctx: Context, *, N, p, T, B, ndata=1, model=MODEL_LINEAR, crn=False,
                  store_capacity=0, logy2offset=1e-3, seed=1012023, dPHI=None, Ns=0, elbTmax=0,
-                 elb_gibbsburn=100, elb=0.25):
+                 elb_gibbsburn=100, elb=0.25, options=None):
         self.ctx = ctx
         self.lib = ctx.lib
         K = N * p + 1 + (Ns * p if model == MODEL_HYBRID else 0)
@@ -634,6 +685,19 @@ class Chains:
             raise RuntimeError(f"ccmm_chains_create failed: {last_error()}")
         self.handle = h
         self.N, self.p, self.K, self.T, self.B = N, p, K, T, B
+        for k, v in (options or {}).items():
+            self.set_option(k, v)
+
+    def set_option(self, name: str, value: int):
+        """ccmm_chains_set_option: a kernel form / schedule of this chain set (include/ccmm.h)."""
+        _check(self.lib.ccmm_chains_set_option(self.handle, name.encode(), int(value)),
+               f"ccmm_chains_set_option({name})")
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int(0)
+        _check(self.lib.ccmm_chains_get_option(self.handle, name.encode(), C.byref(v)),
+               f"ccmm_chains_get_option({name})")
+        return int(v.value)
 
     def close(self):
         if getattr(self, "handle", None):

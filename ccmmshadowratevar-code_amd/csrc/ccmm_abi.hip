@@ -83,8 +83,10 @@ struct DBuf {
     n = count;
     // debug: CCMM_POISON=1 fills new allocations with 0xFF bytes (NaN doubles) to expose
     // reads of never-written device memory
+#ifdef CCMM_ABLATION
     static const bool poison = std::getenv("CCMM_POISON") != nullptr;
     if (poison) HIPCHECK(hipMemset(p, 0xFF, count * sizeof(T)));
+#endif
   }
   ~DBuf() {
     if (p) (void)hipFree(p);
@@ -162,13 +164,12 @@ static GLNodes make_gl_nodes() {
 struct ccmm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  Options opt;  // inherited by the chain sets created on it and used by the block-level drop-ins
 };
 
 enum KernelId {
   KID_RESID,
   KID_WEIGHTS,
-  KID_SYRK,
-  KID_CHOL,
   KID_SOLVE,
   KID_ASTEP,
   KID_SVMIX,
@@ -194,7 +195,7 @@ enum KernelId {
   KID_PSPROP,
   KID_COUNT
 };
-static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights", "k_syrk", "k_chol",
+static const char* kKernelNames[KID_COUNT] = {"k_resid", "k_cta_weights",
                                               "k_cta_solve", "k_astep", "k_sv_mix", "k_sv_part",
                                               "k_phi_gen", "k_phi", "k_store", "k_gram_chol",
                                               "k_elb_prep", "k_elb_cond", "k_elb_gibbs",
@@ -224,8 +225,8 @@ static PhaseLock& phase_lock(int device, int id) {
 
 // the predictive-density kernels of one kept draw per chain (ccmm_fcst.hip): the paths (one
 // single-wave workgroup per (draw, chain); job Nd = the linear model's mean path) then the scores
-static void launch_fcst(hipStream_t st, FcstArgs& a, double* sv1) {
-  const bool reg = fcst_reg_path(a.N, a.p, a.bh) && env_select("CCMM_FCST_REG", 1) != 0;
+static void launch_fcst(hipStream_t st, FcstArgs& a, double* sv1, bool reg_opt) {
+  const bool reg = fcst_reg_path(a.N, a.p, a.bh) && reg_opt;
   a.hc = fcst_chunk(a.N, a.Kx, a.p, a.H, reg);
   a.sv1 = sv1;
   const size_t lp = fcst_paths_lds_doubles(a.N, a.Kx, a.p, a.hc, reg) * sizeof(double);
@@ -265,11 +266,9 @@ struct ccmm_chains {
   // storage of kept draws
   DBuf<double> sPAI, sPHI_, sInvA, sSqrtht, sShadow;
   DBuf<double> solveXch;  // k_cta_solve_lag split: X'v half partials (SolveXch)
-  DBuf<unsigned> solveFlag;
-  unsigned solve_epoch = 0;
-  // two workgroups per chain in k_cta_solve_lag at B <= kSolveSplitMaxB (bit-identical);
-  // CCMM_SOLVE_SPLIT=0 keeps one, 1 splits at any B
-  int solve_split = env_select("CCMM_SOLVE_SPLIT", -1);
+  DBuf<uint64_t> solveFlag;
+  uint64_t solve_epoch = 0;
+  Options opt;  // kernel forms and schedules (ccmm_chains_set_option), from the context at create
   DBuf<double> paiMom;  // running PAI sums | sums of squares (ccmm_chains_pai_moments)
   int mom_done = 0;     // stored draws already added to paiMom
   // block-hybrid ELB model (mcmcVARshadowrateBlockHybrid.m): X/Y slabs 0..ndata-1 hold
@@ -309,21 +308,16 @@ struct ccmm_chains {
   DBuf<uint32_t> rngIds;
   bool resid_valid = false;
   bool have_state = false;
-  // kernel variants (A/B): CCMM_OLD_SOLVE=1 selects the first-generation solve kernel
-  bool use_solve2 = std::getenv("CCMM_OLD_SOLVE") == nullptr;
-  bool use_fused = std::getenv("CCMM_OLD_CHOL") == nullptr;
-  bool gc18 = std::getenv("CCMM_GC18") != nullptr;
   // timing-only ablation of k_gram_chol (results invalid): 1 = no SYRK, 2 = no Cholesky
   int gc_mode = env_ablation("CCMM_GC_MODE", 0);
   std::vector<bool> have_slot;
   // lag-structured design (ccmm_lag.hip): D slabs parallel to the X slabs
   bool lag_capable = false;
-  bool use_lag = std::getenv("CCMM_NO_LAG") == nullptr;
   int lagNT = 0, ldd = 0, drows = 0;
   std::vector<bool> slot_lag;
   DBuf<double> Dpool;
   DBuf<int> dColmap, astepTab;
-  // large-system CTA (ccmm_big.hip): K > 512 or N > 32, or CCMM_FORCE_BIG=1
+  // large-system CTA (ccmm_big.hip): K > 256 or N > 32, or option large_path
   bool big = false;
   int nGroups = 0;
   DBuf<int4> bigGroups;
@@ -455,6 +449,7 @@ struct ccmm_chains {
   void init(ccmm_ctx* c, const ccmm_chain_config& cf, int nX, int nY) {
     ctx = c;
     cfg = cf;
+    opt = c->opt;
     bh = cf.model == CCMM_MODEL_BLOCKHYBRID || cf.model == CCMM_MODEL_HYBRID || cf.model == CCMM_MODEL_SHADOWRATE;
     // mcmcVARshadowrate.m: the ELB step of the block hybrid, one shadow-rate design for every
     // equation (no actual-rate block), the linear model's predictive density (:536-641)
@@ -484,11 +479,8 @@ struct ccmm_chains {
     d.nmat = cf.B * cf.N;
     require(d.KP <= kBigMaxKP, "this build supports K <= 1536");
     // KP > 256: the register-tiled fused Gram + Cholesky (k_gram_chol) stops at 16 tiles; the
-    // large path beats the generic SYRK + Cholesky there (hybrid model K = 277: 32 vs 41 ms)
-    // 256 < K <= 288 (the hybrid model, K = 277): the fused kernel with 18 tiles (k_gram_chol<18>)
-    // (experimental, CCMM_GC18=1: k_gram_chol<18> spills at 8 waves; the large path is the default)
-    big = (d.KP > 256 && (cf.K > 288 || !use_fused || !gc18)) || cf.N > kMaxNSmall ||
-          std::getenv("CCMM_FORCE_BIG") != nullptr;
+    // large path takes every larger system (the hybrid model, K = 277, included)
+    big = d.KP > 256 || cf.N > kMaxNSmall || opt[OPT_LARGE_PATH] != 0;
     nslabX = nX;
     nslabY = nY;
     const size_t B = cf.B, N = cf.N, KP = d.KP, TP = d.TP;
@@ -599,26 +591,14 @@ struct ccmm_chains {
     HIPCHECK(hipMemcpy(dColmap.p, cm.data(), cm.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   bool lag_active() const {
-    if (!lag_capable || !use_lag) return false;
+    if (!lag_capable || !opt[OPT_LAG]) return false;
     for (int s = 0; s < cfg.ndata; ++s)
       if (!slot_lag[s]) return false;
     return true;
   }
   int lag_mode = env_ablation("CCMM_LAG_MODE", 0);
-  // bit 128 (full-row block factors, same draws) is a selector; the other bits are ablations
-  int sv_mode = env_ablation("CCMM_SV_MODE", 0, 128);
-  // k_elb_gibbs_oct (eight passes in flight in one wave) from B >= kElbOctMinB; CCMM_ELB_OCT=0 never,
-  // 2 always
-  int elb_oct = std::getenv("CCMM_ELB_OCT") ? std::atoi(std::getenv("CCMM_ELB_OCT")) : 1;
-  // k_elb_gibbs_wf with per-wave LDS progress flags instead of a barrier per step (CCMM_ELB_ASYNC=0:
-  // the lock-step form)
-  int elb_async = std::getenv("CCMM_ELB_ASYNC") ? std::atoi(std::getenv("CCMM_ELB_ASYNC")) : 1;
-  // passes of the ELB step in flight (k_elb_gibbs_wf): 1 (sequential k_elb_gibbs), 4 or 8
-  int elb_waves = [] {
-    const char* v = std::getenv("CCMM_ELB_WAVES");
-    const int w = v ? std::atoi(v) : 8;
-    return (w == 1 || w == 4) ? w : 8;
-  }();
+  // phase skips (timing only) and bit 128 (full-row block factors, same draws): ablation build only
+  int sv_mode = env_ablation("CCMM_SV_MODE", 0);
   // timing-only ablation of k_elb_gibbs (results invalid): 1 no truncnorm, 2 no uniforms
   int elb_mode = env_ablation("CCMM_ELB_MODE", 0);
   LagSel lagsel() const { return LagSel{Dpool.p, xidx.p, dColmap.p, ldd, drows, cfg.p, lag_mode}; }
@@ -926,14 +906,6 @@ struct ccmm_chains {
     }
     rdiag.alloc((size_t)d.nmat * d.KP);
   }
-  // fused register-tiled Gram + Cholesky: KP <= 256 (16 tiles), or 256 < K <= 288 (18 tiles)
-  int fused_nt() const {
-    if (!use_fused) return 0;
-    if (d.KP <= 256) return d.KP / 16;
-    if (d.K <= 288 && gc18) return 18;
-    return 0;
-  }
-
   void run_resid() {
     ChainState cs = view();
     const int nb = d.N <= 8 ? 8 : (d.N <= 20 ? 20 : 32);
@@ -964,16 +936,15 @@ struct ccmm_chains {
       run_cta_lag(ra, cs);
       return;
     }
-    const int fnt = fused_nt();
-    const bool fused = fnt > 0;
+    // generic design (KP <= 256): the register-tiled fused Gram + Cholesky, then the per-chain solve
+    const int fnt = d.KP / 16;
     launch(KID_WEIGHTS, [&] {
       hipLaunchKernelGGL(k_cta_weights, dim3((d.TP + 255) / 256, d.N, d.B), dim3(256), 0,
-                         ctx->stream, d, Tslot.p, cs, fused ? 1 : 0);
+                         ctx->stream, d, Tslot.p, cs, 1);
     });
-    if (fused) {
-      const size_t lds = (size_t)std::max(2 * kGcTC * gc_ldz(fnt), (fnt + 1) * 16 * kGcLdp) * sizeof(double);
-      launch(KID_GRAMCHOL, [&] {
-        switch (fnt) {
+    const size_t lds = (size_t)std::max(2 * kGcTC * gc_ldz(fnt), (fnt + 1) * 16 * kGcLdp) * sizeof(double);
+    launch(KID_GRAMCHOL, [&] {
+      switch (fnt) {
 #define CASE_GC(NT)                                                                           \
   case NT:                                                                                    \
     HIPCHECK(hipFuncSetAttribute((const void*)k_gram_chol<NT>,                                \
@@ -981,66 +952,27 @@ struct ccmm_chains {
     hipLaunchKernelGGL(k_gram_chol<NT>, dim3(d.nmat), dim3(512), lds, ctx->stream, d, Tslot.p, \
                        xsel(), cs, iVdiag.p, rdiag.p, gc_mode);                               \
     break;
-          CASE_GC(4)
-          CASE_GC(8)
-          CASE_GC(12)
-          CASE_GC(16)
-          CASE_GC(18)
+        CASE_GC(4)
+        CASE_GC(8)
+        CASE_GC(12)
+        CASE_GC(16)
 #undef CASE_GC
-          default:
-            throw ArgError("k_gram_chol: unsupported KP");
-        }
-      });
-    }
-    const int nt = d.KP / kTile;
-    if (!fused) {
-    launch(KID_SYRK, [&] {
-      hipLaunchKernelGGL(k_syrk, dim3(nt * (nt + 1) / 2, d.nmat), dim3(256), 0, ctx->stream, d,
-                         Tslot.p, xsel(), cs);
+        default:
+          throw ArgError("k_gram_chol: unsupported KP");
+      }
     });
-    const size_t lds_chol = (size_t)(kCholNB * (kCholNB + 1) + d.KP * (kCholNB + 1)) * sizeof(double);
-    launch(KID_CHOL, [&] {
-      HIPCHECK(hipFuncSetAttribute((const void*)k_chol, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds_chol));
-      hipLaunchKernelGGL(k_chol, dim3(d.nmat), dim3(256), lds_chol, ctx->stream, d, slot.p,
-                         iVdiag.p, cs, rdiag.p);
-    });
-    }
-    const size_t lds_solve = (size_t)(d.TP + d.KP) * sizeof(double);
     const size_t lds_solve2 =
         (size_t)(d.TP + 2 * d.KP + 64 * kSolveLd + 2 * d.N * d.N) * sizeof(double);
     launch(KID_SOLVE, [&] {
-      if (use_solve2) {
-        if (d.N <= 8)
-          hipLaunchKernelGGL(k_cta_solve2<8>, dim3(d.B), dim3(256), lds_solve2, ctx->stream, d,
-                             Tslot.p, iVb.p, xsel(), cs, rdiag.p, ra);
-        else if (d.N <= 20)
-          hipLaunchKernelGGL(k_cta_solve2<20>, dim3(d.B), dim3(256), lds_solve2, ctx->stream, d,
-                             Tslot.p, iVb.p, xsel(), cs, rdiag.p, ra);
-        else
-          hipLaunchKernelGGL(k_cta_solve2<32>, dim3(d.B), dim3(256), lds_solve2, ctx->stream, d,
-                             Tslot.p, iVb.p, xsel(), cs, rdiag.p, ra);
-        return;
-      }
-      const int rpl = d.KP / 64;
-      switch (rpl) {
-#define CASE_RPL(R)                                                                              \
-  case R:                                                                                        \
-    hipLaunchKernelGGL(k_cta_solve<R>, dim3(d.B), dim3(256), lds_solve, ctx->stream, d, Tslot.p, \
-                       iVb.p, xsel(), cs, rdiag.p, ra);                                          \
-    break;
-        CASE_RPL(1)
-        CASE_RPL(2)
-        CASE_RPL(3)
-        CASE_RPL(4)
-        CASE_RPL(5)
-        CASE_RPL(6)
-        CASE_RPL(7)
-        CASE_RPL(8)
-#undef CASE_RPL
-        default:
-          throw ArgError("unsupported KP");
-      }
+      if (d.N <= 8)
+        hipLaunchKernelGGL(k_cta_solve2<8>, dim3(d.B), dim3(256), lds_solve2, ctx->stream, d,
+                           Tslot.p, iVb.p, xsel(), cs, rdiag.p, ra);
+      else if (d.N <= 20)
+        hipLaunchKernelGGL(k_cta_solve2<20>, dim3(d.B), dim3(256), lds_solve2, ctx->stream, d,
+                           Tslot.p, iVb.p, xsel(), cs, rdiag.p, ra);
+      else
+        hipLaunchKernelGGL(k_cta_solve2<32>, dim3(d.B), dim3(256), lds_solve2, ctx->stream, d,
+                           Tslot.p, iVb.p, xsel(), cs, rdiag.p, ra);
     });
   }
 
@@ -1171,6 +1103,20 @@ struct ccmm_chains {
                          hipMemcpyDeviceToHost));
   }
 
+  // k_cta_solve_lag on two workgroups per chain (bit-identical draws; the halves spin on each other's
+  // X'v partials): only when all 2B workgroups can be resident at once, so no half waits on a partner
+  // that cannot start (auto: also B <= kSolveSplitMaxB, where the split pays)
+  int split_resident = -1;
+  bool solve_split_ok() {
+    const int o = opt[OPT_SOLVE_SPLIT];
+    if (o == 0 || (o < 0 && d.B > kSolveSplitMaxB)) return false;
+    if (split_resident < 0) {
+      const int nmax = d.N <= 8 ? 8 : (d.N <= 20 ? 20 : 32);
+      split_resident = lag_solve_resident(lagNT, nmax, sl_lds_bytes(lagNT, drows, ldd, d.TP, nmax), opt[OPT_SOLVE_ASYNC]);
+    }
+    return 2 * d.B <= split_resident;
+  }
+
   // CTA on the lag structure: sqrt weights -> Gram + Cholesky + inverse -> sequential solve
   void run_cta_lag(const RngArgs& ra, const ChainState& cs) {
     launch(KID_WEIGHTS, [&] {
@@ -1198,16 +1144,17 @@ struct ccmm_chains {
       lk.unlock();
     }
     SolveXch xc{nullptr, nullptr, 0};
-    if (solve_split > 0 || (solve_split < 0 && d.B <= kSolveSplitMaxB)) {
+    if (solve_split_ok()) {
       if (!solveFlag.p) {
         solveXch.alloc((size_t)d.B * 2 * 2 * 256);
         solveFlag.alloc((size_t)d.B * 2);
-        HIPCHECK(hipMemsetAsync(solveFlag.p, 0, (size_t)d.B * 2 * sizeof(unsigned), ctx->stream));
+        HIPCHECK(hipMemsetAsync(solveFlag.p, 0, (size_t)d.B * 2 * sizeof(uint64_t), ctx->stream));
       }
-      xc = SolveXch{solveXch.p, solveFlag.p, ++solve_epoch};
+      xc = SolveXch{solveXch.p, (unsigned long long*)solveFlag.p, ++solve_epoch};
     }
     launch(KID_SOLVELAG, [&] {
-      HIPCHECK(lag_launch_solve(lagNT, nmax, ctx->stream, lds_s, d, Tslot.p, iVb.p, xsel(), ls, cs, ra, xc));
+      HIPCHECK(lag_launch_solve(lagNT, nmax, opt[OPT_SOLVE_ASYNC], ctx->stream, lds_s, d, Tslot.p, iVb.p, xsel(), ls,
+                                cs, ra, xc));
     });
   }
 
@@ -1228,9 +1175,9 @@ struct ccmm_chains {
       lds = staged;
     }
     // k_astep_w (wave-parallel factorisations, the default) or the one-thread-per-regression
-    // k_astep (CCMM_ASTEP_V1=1, kept for A/B timing); same draws up to summation order inside
-    // the factorisation (identical update order, fma placement as written)
-    const bool v1 = env_select("CCMM_ASTEP_V1", 0) != 0;
+    // k_astep (option astep_serial); same draws up to summation order inside the factorisation
+    // (identical update order, fma placement as written)
+    const bool v1 = opt[OPT_ASTEP_SERIAL] != 0;
     const void* fn = v1 ? (const void*)k_astep : (N <= 20 ? (const void*)k_astep_w<20> : (const void*)k_astep_w<32>);
     if (lds > 64 * 1024) HIPCHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (!astepTab.p) {  // the 4 x 4 Gram tiles (ii, A, B) of astep_gram_tiles, largest ii first
@@ -1277,7 +1224,8 @@ struct ccmm_chains {
                          d, Tslot.p, cs, ra);
     });
     launch(KID_SVSAMPLE, [&] {
-      HIPCHECK(sv_launch_part(d.N, ctx->stream, d, Tslot.p, V0inv.p, V0invm.p, cs, ra, svSep.p, svG.p, sv_mode));
+      HIPCHECK(sv_launch_part(d.N, ctx->stream, d, Tslot.p, V0inv.p, V0invm.p, cs, ra, svSep.p, svG.p, sv_mode,
+                                opt[OPT_SV_NWG], opt[OPT_SV_MFMA] != 0));
     });
   }
 
@@ -1423,15 +1371,14 @@ struct ccmm_chains {
   // every PS sweep in the draw store (ccmm_chains_keep_missingrate)
   bool keep_first = false;
   DBuf<double> psFirst, sMissing;
-  // CCMM_PS_CHOL_V1=1: the first-generation k_ps_chol (LDS window) for every band width (A/B; same factor)
-  int ps_chol_v1 = env_select("CCMM_PS_CHOL_V1", 0);
   int last_ps = 0;  // whether the last ELB step ran the PS branch (draw store bookkeeping)
 
   void run_ps(const RngArgs& ra, ElbDev& e, bool kept) {
     ChainState cs = view();
     if (keep_first) psFirst.alloc((size_t)d.B * cfg.Ns * std::max(cfg.elbTmax, 1));
     const PsDev ps = ps_view();
-    if (psW <= 64 && !ps_chol_v1) {  // register-window factorisation, one wave per chain (k_ps_chol_w)
+    // option ps_chol_lds: the first-generation k_ps_chol (LDS window) for every band width (same factor)
+    if (psW <= 64 && !opt[OPT_PS_CHOL_LDS]) {  // register-window factorisation, one wave per chain (k_ps_chol_w)
       const size_t lds = ps_chol_w_lds_bytes(psW, std::max(cfg.elbTmax, 1), ps_nmax);
       require(lds <= 160 * 1024, "PS branch: cell list does not fit LDS");
       launch(KID_PSCHOL, [&] {
@@ -1551,20 +1498,21 @@ struct ccmm_chains {
     });
     if (ps) run_ps(ra, e, kept);
     // Gibbs passes: elb_waves passes in flight (k_elb_gibbs_wf, bit-identical draws), or the
-    // one-wave sequential kernel (CCMM_ELB_WAVES=1)
+    // one-wave sequential kernel (option elb_waves = 1)
     auto gibbs_lds = [&](int w) {  // shadow rates | per pass: uniforms and their elb_ppnd16 | month tables
       return w == 1 ? (size_t)3 * e.elbTmax * Ns * sizeof(double) + (size_t)e.elbTmax * sizeof(int)
                     : (size_t)(1 + 2 * w) * e.elbTmax * Ns * sizeof(double) + (size_t)2 * e.elbTmax * sizeof(int) +
                           (size_t)2 * w * sizeof(int);
     };
-    int W = elb_waves;
+    int W = opt[OPT_ELB_WAVES] <= 1 ? 1 : (opt[OPT_ELB_WAVES] < 8 ? 4 : 8);
     while (W > 1 && gibbs_lds(W) > 160 * 1024) W = (W == 8) ? 4 : 1;  // long ELB windows
     const size_t lds_gibbs = gibbs_lds(W);
     // eight passes in flight inside one wave (k_elb_gibbs_oct, bit-identical draws): the default;
-    // CCMM_ELB_OCT=0 selects the wave kernels
+    // option elb_oct = 0 selects the wave kernels
     const size_t lds_oct = (size_t)e.elbTmax * Ns * sizeof(double) + (size_t)2 * e.elbTmax * sizeof(int);
     // (the per-chain wave kernels keep shorter months at B < kElbOctMinB: one wave per chain cannot
     // fill the chip there, and a month costs the octet kernel more latency)
+    const int elb_oct = opt[OPT_ELB_OCT];
     if (elb_oct && lds_oct <= 160 * 1024 && (elb_oct == 2 || d.B >= kElbOctMinB)) {
       launch(KID_ELBGIBBS, [&] {
         switch (Ns) {
@@ -1584,6 +1532,44 @@ struct ccmm_chains {
             throw ArgError("Ns must be in [1, 5]");
         }
       });
+    } else if (elb_parts(W) > 1) {
+      // the wavefront over 2 or 4 CUs per chain (k_elb_gibbs_mp, bit-identical draws)
+      const int parts = elb_parts(W), wpc = 8 / parts;
+      elbXch.alloc((size_t)d.B * parts * e.elbTmax * Ns * 2);
+      if (elbXchZeroed != elbXch.p) {  // tags start at zero (tags of a launch are >= 2^16)
+        HIPCHECK(hipMemsetAsync(elbXch.p, 0, elbXch.n * sizeof(double), ctx->stream));
+        elbXchZeroed = elbXch.p;
+      }
+      const ElbXch xc{elbXch.p, ++elb_epoch};
+      const size_t lds_mp = (size_t)(1 + 2 * wpc) * e.elbTmax * Ns * sizeof(double) +
+                            (size_t)2 * e.elbTmax * sizeof(int) + (size_t)(wpc + 1) * sizeof(int);
+      launch(KID_ELBGIBBS, [&] {
+#define GIBBS_MP(NS, WPC_, PT)                                                                                  \
+  do {                                                                                                        \
+    HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs_mp<NS, WPC_, PT>,                                   \
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_mp));                   \
+    hipLaunchKernelGGL((k_elb_gibbs_mp<NS, WPC_, PT>), dim3(d.B, PT), dim3(64 * (WPC_ + 1)), lds_mp, ctx->stream, \
+                       d, e, cs, ra, xc);                                                                     \
+  } while (0)
+#define CASE_MP(NS)                    \
+  case NS:                             \
+    if (parts == 2)                    \
+      GIBBS_MP(NS, 4, 2);              \
+    else                               \
+      GIBBS_MP(NS, 2, 4);              \
+    break;
+        switch (Ns) {
+          CASE_MP(1)
+          CASE_MP(2)
+          CASE_MP(3)
+          CASE_MP(4)
+          CASE_MP(5)
+          default:
+            throw ArgError("Ns must be in [1, 5]");
+        }
+#undef CASE_MP
+#undef GIBBS_MP
+      });
     } else
     launch(KID_ELBGIBBS, [&] {
 #define GIBBS_KA(NS, WW, AS)                                                                                \
@@ -1595,7 +1581,7 @@ struct ccmm_chains {
   } while (0)
 #define GIBBS_K(NS, WW)            \
   do {                             \
-    if (elb_async)                 \
+    if (opt[OPT_ELB_ASYNC])        \
       GIBBS_KA(NS, WW, true);      \
     else                           \
       GIBBS_KA(NS, WW, false);     \
@@ -1631,6 +1617,23 @@ struct ccmm_chains {
                          xsel(), cs, cfg.ndata, lag_capable ? Dpool.p : nullptr, ldd, drows);
     });
     resid_valid = false;  // X, Y changed: RESID is recomputed before the next CTA
+  }
+
+  // workgroups (CUs) per chain of the ELB wavefront: k_elb_gibbs_mp spreads the W = 8 passes in flight
+  // over 2 (or 4) CUs at small B, one drawing wave per SIMD, when every chain's parts can be resident
+  // together (option elb_parts; auto: 2 for B <= kElbMpMaxB)
+  DBuf<double> elbXch;
+  const double* elbXchZeroed = nullptr;
+  unsigned long long elb_epoch = 0;
+  int elb_parts(int W) {
+    const int o = opt[OPT_ELB_PARTS];
+    if (W != 8 || !opt[OPT_ELB_ASYNC] || o == 1 || cfg.elb_gibbsburn + 1 >= 65535) return 1;
+    const int parts = o == 0 ? (d.B <= kElbMpMaxB ? 2 : 1) : (o >= 4 ? 4 : 2);
+    if (parts == 1) return 1;
+    int cus = 0;
+    HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    // one workgroup of <= 320 threads per part, <= 110 KB of LDS: at least one per CU is resident
+    return (d.B * parts <= cus) ? parts : 1;
   }
 
   void set_fcst(int H, int Nd, const uint8_t* ndxYields, int keep) {
@@ -1806,7 +1809,7 @@ struct ccmm_chains {
       hipLaunchKernelGGL(k_fcst_jumpoff, dim3(B), dim3(256), 0, ctx->stream, N, cfg.p, N * cfg.p + 1, d.TP,
                          Tslot.p, slot.p, xs.ypool, xs.yidx, fldXj, fXj.p, hybrid ? cfg.Ns : 0,
                          hybrid ? dNdxS.p : nullptr, cfg.elb);
-      launch_fcst(ctx->stream, a, fSv1.p);
+      launch_fcst(ctx->stream, a, fSv1.p, opt[OPT_FCST_REG] != 0);
       hipLaunchKernelGGL(k_fcst_accum, dim3(B), dim3(256), 0, ctx->stream, N, H, Nd,
                          cfg.store_capacity, fstored, fY.p, fYc.p, (fcst_bh || hybrid) ? nullptr : fYhat.p, fSc.p,
                          fYsum.p, fYcsum.p, fYhatsum.p, fScStore.p, fKeep ? fPaths.p : nullptr,
@@ -1820,24 +1823,21 @@ struct ccmm_chains {
   // CTA.m:80-92: a chain whose coefficient block met a non-positive Cholesky pivot
   // (status bit 2) is redrawn on the host (host_cta_chain: Cholesky, or the Householder QR
   // of Kailath's array where it fails) from the same previous draw and normals; status
-  // bit 2 is then replaced by bit 1 ("QR fallback used", informational).  CCMM_FORCE_QR=1
-  // routes every chain through the host QR branch (tests); CCMM_NO_QR_FALLBACK=1 disables.
-  // CCMM_PHI_OVERLAP=0: the PHI block in stream order before the ELB step (A/B; same draws)
-  bool phi_overlap = env_select("CCMM_PHI_OVERLAP", 1) != 0;
-  bool qr_fallback = std::getenv("CCMM_NO_QR_FALLBACK") == nullptr;
-  bool force_qr = std::getenv("CCMM_FORCE_QR") != nullptr;
+  // bit 2 is then replaced by bit 1 ("QR fallback used", informational).  Option force_qr routes
+  // every chain through the host QR branch (tests); qr_fallback = 0 disables the check.
   DBuf<double> paiPrev, zHost;
   int64_t qr_count = 0;
 
   void snapshot_pai() {
-    if (!qr_fallback) return;
+    if (!opt[OPT_QR_FALLBACK]) return;
     paiPrev.alloc(PAI.n);
     HIPCHECK(hipMemcpyAsync(paiPrev.p, PAI.p, PAI.n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
   }
 
   // returns the chains redrawn
   int cta_fallback(const RngArgs& ra) {
-    if (!qr_fallback) return 0;
+    if (!opt[OPT_QR_FALLBACK]) return 0;
+    const bool force_qr = opt[OPT_FORCE_QR] != 0;
     const int B = d.B, N = d.N, K = d.K, KP = d.KP, TP = d.TP;
     std::vector<int> st(B);
     HIPCHECK(hipMemcpyAsync(st.data(), status.p, B * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
@@ -1942,7 +1942,7 @@ struct ccmm_chains {
     run_sv(ra);
     // block hybrid, N <= 32: the PHI block on the auxiliary stream beside the ELB step (the ELB kernels
     // read PAI, A, invA, sqrtht and the chain's data; PHI reads eta and writes sqrtPHI / PHI / Zphi)
-    const bool fork = bh && cfg.elbTmax > 0 && d.N <= kMaxNSmall && phi_overlap;
+    const bool fork = bh && cfg.elbTmax > 0 && d.N <= kMaxNSmall && opt[OPT_PHI_OVERLAP];
     if (fork) {
       ensure_aux();
       HIPCHECK(hipEventRecord(evFork, ctx->stream));
@@ -1964,7 +1964,7 @@ struct ccmm_chains {
     std::vector<int> st(d.B);
     HIPCHECK(hipMemcpy(st.data(), status.p, d.B * sizeof(int), hipMemcpyDeviceToHost));
     int any = 0;
-    for (int v : st) any |= v & ~1;  // bit 1: QR fallback used (not an error)
+    for (int v : st) any |= v & ~CCMM_STATUS_INFO;  // bits 1, 64: informational (valid draws)
     if (any) {
       HIPCHECK(hipMemset(status.p, 0, d.B * sizeof(int)));
       g_err = "non positive-definite matrix in a Gibbs block (status bits " + std::to_string(any) + ")";
@@ -1989,8 +1989,8 @@ struct AblationVar {
 };
 const AblationVar kAblationVars[] = {
     {"CCMM_CHOL_SKIP", 0},  {"CCMM_SOLVE_SKIP", 0}, {"CCMM_SV_SKIP", 0},  {"CCMM_GC_MODE", 0},
-    {"CCMM_LAG_MODE", 0},   {"CCMM_BIG_MASK", 0},   {"CCMM_ELB_MODE", 0}, {"CCMM_SV_MODE", 128},
-    {"CCMM_FCST_MODE", 0},
+    {"CCMM_LAG_MODE", 0},   {"CCMM_BIG_MASK", 0},   {"CCMM_ELB_MODE", 0}, {"CCMM_SV_MODE", 0},
+    {"CCMM_FCST_MODE", 0},  {"CCMM_POISON", 0},
 };
 // an ablation variable is "ignored" when it is set and a bit outside its keep_mask is non-zero
 bool ablation_ignored(const AblationVar& v) {
@@ -2002,17 +2002,64 @@ bool ablation_ignored(const AblationVar& v) {
   return e && (std::atoi(e) & ~v.keep_mask) != 0;
 #endif
 }
+// an option's variable is "ignored" by a default build whenever it is set
+bool option_env_ignored(int i) {
+#ifdef CCMM_ABLATION
+  (void)i;
+  return false;
+#else
+  return std::getenv(kOptDesc[i].env) != nullptr;
+#endif
+}
+// switches of kernels that no longer exist (round 5 and before): read by no build
+const char* const kRetiredVars[] = {"CCMM_OLD_SOLVE", "CCMM_OLD_CHOL", "CCMM_GC18", "CCMM_NO_LAG",
+                                    "CCMM_NO_QR_FALLBACK", "CCMM_SOLVE_WAVES"};
 std::string ignored_list() {
   std::string out;
   for (const auto& v : kAblationVars)
     if (ablation_ignored(v)) out += (out.empty() ? "" : ",") + std::string(v.name);
+  for (const char* r : kRetiredVars)
+    if (std::getenv(r)) out += (out.empty() ? "" : ",") + std::string(r);
+  for (int i = 0; i < kOptCount; ++i)
+    if (option_env_ignored(i)) out += (out.empty() ? "" : ",") + std::string(kOptDesc[i].env);
   return out;
 }
 }  // namespace
 
-int ccmm::env_select(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
+const ccmm::OptDesc ccmm::kOptDesc[ccmm::kOptCount] = {
+    {"solve_split", "CCMM_SOLVE_SPLIT", -1, -1, 1},
+    {"solve_async", "CCMM_SOLVE_ASYNC", 1, 0, 1},
+    {"sv_nwg", "CCMM_SV_NWG", 0, 0, 4},
+    {"elb_waves", "CCMM_ELB_WAVES", 8, 1, 8},
+    {"elb_oct", "CCMM_ELB_OCT", 1, 0, 2},
+    {"elb_async", "CCMM_ELB_ASYNC", 1, 0, 1},
+    {"elb_parts", "CCMM_ELB_PARTS", 0, 0, 4},
+    {"fcst_reg", "CCMM_FCST_REG", 1, 0, 1},
+    {"phi_overlap", "CCMM_PHI_OVERLAP", 1, 0, 1},
+    {"qr_fallback", "CCMM_QR_FALLBACK", 1, 0, 1},
+    {"lag", "CCMM_LAG", 1, 0, 1},
+    {"large_path", "CCMM_FORCE_BIG", 0, 0, 1},
+    {"astep_serial", "CCMM_ASTEP_V1", 0, 0, 1},
+    {"ps_chol_lds", "CCMM_PS_CHOL_V1", 0, 0, 1},
+    {"sv_mfma", "CCMM_SV_MFMA", 1, 0, 1},
+    {"force_qr", "CCMM_FORCE_QR", 0, 0, 1},
+    {"girf_generic", "CCMM_GIRF_GENERIC", 0, 0, 1},
+};
+
+ccmm::Options::Options() {
+  for (int i = 0; i < kOptCount; ++i) {
+    v[i] = kOptDesc[i].dflt;
+#ifdef CCMM_ABLATION
+    if (const char* e = std::getenv(kOptDesc[i].env)) v[i] = std::max(kOptDesc[i].lo, std::min(kOptDesc[i].hi, std::atoi(e)));
+#endif
+  }
+}
+
+int ccmm::option_id(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < kOptCount; ++i)
+    if (std::strcmp(name, kOptDesc[i].name) == 0) return i;
+  return -1;
 }
 
 int ccmm::env_ablation(const char* name, int off, int keep_mask) {
@@ -2046,9 +2093,44 @@ int ccmm_env_ignored(char* buf, int len) {
     std::memcpy(buf, l.data(), n);
     buf[n] = 0;
   }
-  int count = 0;
-  for (const auto& v : kAblationVars) count += ablation_ignored(v) ? 1 : 0;
+  int count = l.empty() ? 0 : 1;
+  for (char ch : l) count += ch == ',' ? 1 : 0;
   return count;
+}
+
+int ccmm_option_count(void) { return kOptCount; }
+
+
+const char* ccmm_option_name(int i) { return (i >= 0 && i < kOptCount) ? kOptDesc[i].name : nullptr; }
+
+static int set_opt(Options& o, const char* name, int value) {
+  const int i = option_id(name);
+  if (i < 0) {
+    g_err = std::string("unknown option '") + (name ? name : "(null)") + "'";
+    return CCMM_ERR_ARG;
+  }
+  if (value < kOptDesc[i].lo || value > kOptDesc[i].hi) {
+    g_err = std::string("option '") + name + "' out of range [" + std::to_string(kOptDesc[i].lo) + ", " +
+            std::to_string(kOptDesc[i].hi) + "]";
+    return CCMM_ERR_ARG;
+  }
+  o.v[i] = value;
+  return CCMM_OK;
+}
+
+static int get_opt(const Options& o, const char* name, int* value) {
+  const int i = option_id(name);
+  if (i < 0 || !value) {
+    g_err = std::string("unknown option '") + (name ? name : "(null)") + "'";
+    return CCMM_ERR_ARG;
+  }
+  *value = o.v[i];
+  return CCMM_OK;
+}
+
+int ccmm_option_default(const char* name, int* value) {
+  const Options o;  // what a new context starts from (a default build: the built-in values)
+  return get_opt(o, name, value);
 }
 
 int ccmm_device_count(void) {
@@ -2084,6 +2166,22 @@ void ccmm_destroy(ccmm_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+}
+
+int ccmm_set_option(ccmm_ctx* ctx, const char* name, int value) {
+  if (!ctx) {
+    g_err = "null context";
+    return CCMM_ERR_ARG;
+  }
+  return set_opt(ctx->opt, name, value);
+}
+
+int ccmm_get_option(ccmm_ctx* ctx, const char* name, int* value) {
+  if (!ctx) {
+    g_err = "null context";
+    return CCMM_ERR_ARG;
+  }
+  return get_opt(ctx->opt, name, value);
 }
 
 int ccmm_synchronize(ccmm_ctx* ctx) {
@@ -2127,7 +2225,7 @@ static int cta_impl(ccmm_ctx* ctx, int B, int T, int N, int K, const double* Y, 
     const int nX = nx * (x_per_chain ? B : 1), nY = y_per_chain ? B : 1;
     ch.init(ctx, cf, nX, nY);
     if (Aelb) {
-      require(!ch.big && ch.use_solve2, "CTAsysAswitching: supported for K <= 256 and N <= 32");
+      require(!ch.big, "CTAsysAswitching: supported for K <= 256 and N <= 32");
       ch.aswitch = true;
       ch.AelbD.alloc((size_t)B * N * N);
       HIPCHECK(hipMemcpy(ch.AelbD.p, Aelb, (size_t)B * N * N * sizeof(double), hipMemcpyHostToDevice));
@@ -2668,6 +2766,34 @@ ccmm_chains* ccmm_chains_create(ccmm_ctx* ctx, const ccmm_chain_config* cfg) {
   return ch;
 }
 
+int ccmm_chains_set_option(ccmm_chains* ch, const char* name, int value) {
+  return guarded([&] {
+    require(ch != nullptr, "null argument");
+    const int i = option_id(name);
+    const int old = i >= 0 ? ch->opt[i] : 0;
+    const int rc = set_opt(ch->opt, name, value);
+    if (rc != CCMM_OK) return rc;
+    if (i == OPT_LARGE_PATH && value != old) {  // the path's grouping of systems follows the choice
+      require(!ch->have_state, "option large_path: set it before ccmm_chains_set_data / set_state");
+      HIPCHECK(hipSetDevice(ch->ctx->device));
+      ch->big = ch->d.KP > 256 || ch->cfg.N > kMaxNSmall || value != 0;
+      std::vector<int> sl(ch->cfg.B);
+      HIPCHECK(hipMemcpy(sl.data(), ch->slot.p, ch->cfg.B * sizeof(int), hipMemcpyDeviceToHost));
+      ch->set_slots(sl.data());
+    }
+    if (i == OPT_SOLVE_SPLIT || i == OPT_SOLVE_ASYNC) ch->split_resident = -1;
+    return CCMM_OK;
+  });
+}
+
+int ccmm_chains_get_option(ccmm_chains* ch, const char* name, int* value) {
+  if (!ch) {
+    g_err = "null argument";
+    return CCMM_ERR_ARG;
+  }
+  return get_opt(ch->opt, name, value);
+}
+
 void ccmm_chains_destroy(ccmm_chains* ch) {
   if (!ch) return;
   (void)hipSetDevice(ch->ctx->device);
@@ -2779,7 +2905,7 @@ int ccmm_chains_get_status(ccmm_chains* ch, int* status) {
     HIPCHECK(hipStreamSynchronize(ch->ctx->stream));
     HIPCHECK(hipMemcpy(status, ch->status.p, ch->cfg.B * sizeof(int), hipMemcpyDeviceToHost));
     int any = 0;
-    for (int c = 0; c < ch->cfg.B; ++c) any |= status[c] & ~1;  // bit 1: QR fallback used
+    for (int c = 0; c < ch->cfg.B; ++c) any |= status[c] & ~CCMM_STATUS_INFO;  // bits 1, 64: informational
     return any ? 1 : 0;
   });
 }
@@ -2810,6 +2936,7 @@ int ccmm_chains_set_state(ccmm_chains* ch, const double* PAI, const double* A,
     }
     ch->sweep = 0;
     ch->stored = 0;
+    ch->mom_done = 0;  // the store restarts: the running PAI sums are re-based on reset (pai_moments)
     HIPCHECK(hipMemset(ch->status.p, 0, ch->cfg.B * sizeof(int)));
     if (ch->psCount.p) HIPCHECK(hipMemset(ch->psCount.p, 0, 2 * (size_t)ch->cfg.B * sizeof(int)));
     if (ch->have_fcst) ch->reset_fcst();
@@ -2919,6 +3046,7 @@ int ccmm_chains_pai_moments(ccmm_chains* ch, int reset, double* sum, double* sum
       HIPCHECK(hipMemsetAsync(ch->paiMom.p, 0, 2 * B * per * sizeof(double), ch->ctx->stream));
       ch->mom_done = 0;
     }
+    require(ch->stored >= ch->mom_done, "ccmm_chains_pai_moments: the store was reset; call with reset != 0");
     if (ch->stored > ch->mom_done && ch->sPAI.p) {
       hipLaunchKernelGGL(k_pai_moments, dim3((unsigned)((B * per + 255) / 256)), dim3(256), 0, ch->ctx->stream,
                          ch->sPAI.p, ch->cfg.store_capacity, ch->mom_done, ch->stored, (int)per, (int)B,
@@ -3279,7 +3407,7 @@ static int girf_impl(ccmm_ctx* ctx, int M, int N, int p, int H, int nsim, const 
     a.elb = elb; a.shock11 = shock11;
     a.z = z ? dZ.p : nullptr; a.svz = z ? dSZ.p : nullptr; a.seed = seed;
     a.cumcode = cumcode ? dCum.p : nullptr; a.np_ = np_; a.part = dPart.p; a.out = dOut.p;
-    a.force_generic = std::getenv("CCMM_GIRF_GENERIC") != nullptr ? 1 : 0;  // A/B of the specialised kernel
+    a.force_generic = ctx->opt[OPT_GIRF_GENERIC];  // A/B of the specialised kernel
     HIPCHECK(girf_launch(ctx->stream, a));
     HIPCHECK(hipStreamSynchronize(ctx->stream));
     HIPCHECK(hipMemcpy(yhat, dOut.p, dOut.n * sizeof(double), hipMemcpyDeviceToHost));
@@ -3457,7 +3585,7 @@ int ccmm_fcst(ccmm_ctx* ctx, int B, int N, int p, int H, int Nd, const double* P
     a.fY = dfY.p; a.fYc = dfYc.p; a.yhat = dyhat.p; a.scores = dsc.p; a.status = dst.p;
     a.gl = gl;
     dsv1.alloc((size_t)B * Nd * N);
-    launch_fcst(ctx->stream, a, dsv1.p);
+    launch_fcst(ctx->stream, a, dsv1.p, ctx->opt[OPT_FCST_REG] != 0);
     HIPCHECK(hipStreamSynchronize(ctx->stream));
     HIPCHECK(hipMemcpy(fcstY, dfY.p, nout * sizeof(double), hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(fcstYcensor, dfYc.p, nout * sizeof(double), hipMemcpyDeviceToHost));

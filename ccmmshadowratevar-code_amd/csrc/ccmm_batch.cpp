@@ -256,7 +256,7 @@ struct Runner {
     std::vector<char> ok(nv, 1);
     for (int s = 0; s < nv; ++s)
       for (int c = 0; c < C; ++c)
-        if (status[size_t(s) * C + c] & ~1) ok[s] = 0;  // bit 1: QR fallback used (valid draws)
+        if (status[size_t(s) * C + c] & ~CCMM_STATUS_INFO) ok[s] = 0;  // bits 1, 64: informational (valid draws)
 
     const size_t nq = size_t(cf.nq);
     if (cf.postprocess) {

@@ -1020,6 +1020,257 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
   for (int q = tid; q < T * NS; q += 64 * W) Sc[q] = Sl[q];
 }
 
+// ---------------------------------------------------------------- Gibbs passes, wavefront over CUs
+// k_elb_gibbs_wf's asynchronous wavefront with its W = WPC * PARTS passes in flight spread over PARTS
+// workgroups (CUs) per chain, WPC drawing waves each: one drawing wave per SIMD instead of two, so a
+// month's draw is no longer issue-bound on a shared SIMD (the one-chain-per-vintage floor of the OOS
+// run, goVARshadowrateBlockHybrid.m:258-303, runs 8 waves on one CU otherwise).  Pass n runs on global
+// wave n mod W (part = gw / WPC).  Every part keeps its own copy of the shadow rates in LDS.
+//   within a part: the waves hand off through LDS progress words exactly as k_elb_gibbs_wf;
+//   across parts: the last drawing wave of part j publishes every cell it draws as a 16-byte granule
+//   {value, tag = epoch 2^16 + pass + 1} with one write-through (sc1) store (the data is the flag; no
+//   fence), and an importer wave of part j + 1 (wave WPC) reads the granules of the censored months in
+//   order with sc1 loads, up to eight months per round trip, copies them into its part's LDS copy and
+//   publishes its progress in the predecessor's encoding, so wave 0 of part j + 1 waits on it as on a
+//   local predecessor.
+// Why a copy can be refreshed late: in the one-copy kernel pass n overwrites month m only once every
+// earlier pass is done with it, and pass n + 1 reads it only after pass n has drawn past reach(m); the
+// import of pass n's value for m happens between those two events in the consumer part, so every read
+// sees the value the sequential order gives it: draws, flags and states are bit-identical to
+// k_elb_gibbs.  All PARTS workgroups of a chain must be resident together (the host checks occupancy);
+// every spin is bounded (status bit 32, then the wave publishes "done" so its successors drain).
+constexpr int kElbMpMaxB = 64;  // auto: the multi-CU wavefront for B <= 64 chains
+struct ElbXch {
+  double* gran;                // [B][PARTS][elbTmax][NS] granules of 2 doubles {value, tag bits}
+  unsigned long long epoch;    // launch counter (host): tags of older launches never match
+};
+template <int NS, int WPC, int PARTS>
+__global__ __launch_bounds__(64 * (WPC + 1)) void k_elb_gibbs_mp(Dims d, ElbDev e, ChainState cs, RngArgs ra,
+                                                                 ElbXch xc) {
+  constexpr int W = WPC * PARTS;
+  extern __shared__ double sm[];
+  const int c = blockIdx.x, part = blockIdx.y;
+  const int s = cs.slot[c];
+  const int p = e.p;
+  const int T = e.elbT[s], nc = e.ncens[s];
+  if (nc == 0) return;
+  if (e.psFlag && e.psFlag[c] > 0) return;  // a PS proposal was accepted (:453-454)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // WPC = the importer
+  const int gw = part * WPC + wave;
+  const Rng rng = ra.make(c);
+  const int ncol = 2 * p * NS;
+  const int head = elb_cond_head(NS);
+  const int pg = e.elbTmax * NS;
+  double* Sl = sm;                                            // T x NS (t-major): this part's copy
+  double* Ul = sm + (size_t)pg * (1 + min(wave, WPC - 1));    // this wave's pass uniforms
+  double* Zl = sm + (size_t)pg * (1 + WPC + min(wave, WPC - 1));
+  int* Tm = (int*)(sm + (size_t)pg * (1 + 2 * WPC));          // censored months: t | (mask << 16)
+  int* reach = Tm + e.elbTmax;
+  int* prog = reach + e.elbTmax;                              // [WPC + 1]: drawing waves, importer
+  double* Sc = e.Scur + (size_t)c * e.elbTmax * NS;
+  const uint8_t* sN = e.sNaN + (size_t)s * e.elbTmax * NS;
+  const int* cl = e.cens + (size_t)s * e.elbTmax;
+  const double* recs = e.cond + (size_t)c * e.elbTmax * e.condStride;
+  const int P = e.passes;
+  const int done_all = P * nc;
+  const unsigned long long tag0 = xc.epoch << 16;
+  // granule buffers of this chain: the one this part publishes into, the one its importer reads
+  const size_t gstride = (size_t)e.elbTmax * NS * 16;  // bytes per part
+  char* gbase = (char*)(xc.gran) + (size_t)c * PARTS * gstride;
+  const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(gbase, 0, (int)(PARTS * gstride), 0x00020000);
+  const int gout = part * (int)gstride, gin = ((part + PARTS - 1) % PARTS) * (int)gstride;
+  for (int q = tid; q < T * NS; q += 64 * (WPC + 1)) Sl[q] = Sc[q];
+  for (int q = tid; q < nc; q += 64 * (WPC + 1)) {
+    const int t = cl[q];
+    int m = 0;
+    for (int a = 0; a < NS; ++a) m |= sN[t * NS + a] ? (1 << a) : 0;
+    Tm[q] = t | (m << 16);
+    int j = q;
+    while (j + 1 < nc && cl[j + 1] <= t + p) ++j;
+    reach[q] = j;
+  }
+  if (tid <= WPC) {
+    const int g = part * WPC + tid;  // the importer's predecessor pass is gw - 1 of the part before
+    prog[tid] = tid < WPC ? ((g < P) ? g * nc : done_all) : ((part * WPC - 1 + W) % W) * nc;
+  }
+  __syncthreads();
+  if (wave == WPC) {
+    // ---- importer: passes n' = gw - 1 (mod W) of the previous part's last wave, whose successor pass
+    //      n' + 1 runs here; month by month in order, up to 8 months per round trip
+    constexpr int KM = 8;
+    const int k = lane / NS, a = lane - (lane / NS) * NS;
+    const bool act = lane < KM * NS;
+    bool stuck = false;
+    for (int np = (part * WPC - 1 + W) % W; np + 1 < P && !stuck; np += W) {
+      const unsigned long long want = tag0 + (unsigned long long)(np + 1);
+      int it = 0;
+      for (int m = 0; m < nc;) {
+        const int mk = m + k;
+        bool ok = true;
+        double v = 0.0;
+        int t = 0;
+        if (act && mk < nc) {
+          t = Tm[mk] & 0xffff;
+          const auto x = __builtin_amdgcn_raw_buffer_load_b128(grs, gin + (t * NS + a) * 16, 0, 16);  // sc1
+          v = __hiloint2double((int)x[1], (int)x[0]);
+          ok = ((unsigned long long)x[3] << 32 | x[2]) == want;
+        }
+        // months m .. m + cnt - 1 are complete (every cell tagged for pass np)
+        const unsigned long long bad = __ballot(!ok);
+        int cnt = KM;
+#pragma unroll
+        for (int kk = 0; kk < KM; ++kk)
+          if (cnt == KM && ((bad >> (kk * NS)) & ((1ull << NS) - 1))) cnt = kk;
+        cnt = min(cnt, nc - m);
+        if (cnt == 0) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++it > (1 << 24)) {
+            stuck = true;
+            break;
+          }
+          continue;
+        }
+        it = 0;
+        if (act && k < cnt) Sl[t * NS + a] = v;
+        wave_lds_sync();
+        m += cnt;
+        if (lane == 0)
+          __hip_atomic_store(&prog[WPC], np * nc + m, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    if (lane == 0) __hip_atomic_store(&prog[WPC], done_all, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (stuck && lane == 0) atomicOr(&cs.status[c], CCMM_STATUS_HANDOFF);
+    __syncthreads();
+    return;
+  }
+  const int c0 = lane, c1 = lane + 64;
+  const bool h0 = c0 < ncol, h1 = c1 < ncol;
+  const int kk0 = c0 / NS, sp0 = c0 % NS, kk1 = c1 / NS, sp1 = c1 % NS;
+  const int off0 = (kk0 < p) ? -(kk0 + 1) : (kk0 - p + 1);
+  const int off1 = (kk1 < p) ? -(kk1 + 1) : (kk1 - p + 1);
+  constexpr int kHd = NS + NS * (NS - 1) + NS;
+  struct Rec {
+    double hd[kHd], g0[NS], g1[NS];
+  };
+  const int c0l = h0 ? c0 : 0, c1l = h1 ? c1 : 0;
+  auto load_rec = [&](int ci, Rec& r_) {
+    const double* r = recs + (size_t)ci * e.condStride;
+    for (int q = 0; q < kHd; ++q) r_.hd[q] = r[q];
+    for (int a = 0; a < NS; ++a) {
+      r_.g0[a] = r[head + c0l * NS + a];
+      r_.g1[a] = r[head + c1l * NS + a];
+    }
+  };
+  auto uniforms = [&](int n) {  // pass n's rand(Ns, elbT) (gibbsdrawShadowrates.m:173, page n)
+    if (rng.crn) {
+      for (int q = lane; q < T * NS; q += 64) {
+        const double uu = rng.uniform(CCMM_RNG_ELB, (uint32_t)(q + T * NS * n));
+        Ul[q] = uu;
+        Zl[q] = elb_ppnd16(uu);
+      }
+    } else {
+      const uint32_t base = (uint32_t)(T * NS * n);
+      for (int q = 2 * lane; q < T * NS + 1; q += 128) {
+        const uint32_t i0 = base + (uint32_t)q - ((base + (uint32_t)q) & 1u);
+        const u32x4 r = rng.raw(CCMM_RNG_ELB, i0 >> 1);
+        const int q0 = (int)(i0 - base), q1 = q0 + 1;
+        const double u0 = u01(r.x, r.y), u1 = u01(r.z, r.w);
+        if (q0 >= 0 && q0 < T * NS) {
+          Ul[q0] = u0;
+          Zl[q0] = elb_ppnd16(u0);
+        }
+        if (q1 >= 0 && q1 < T * NS) {
+          Ul[q1] = u1;
+          Zl[q1] = elb_ppnd16(u1);
+        }
+      }
+    }
+    wave_lds_sync();
+  };
+  int* pprog = &prog[wave == 0 ? WPC : wave - 1];  // the predecessor: local wave or the importer
+  const bool publish = wave == WPC - 1;                  // the last wave feeds the next part
+  int n = gw;
+  Rec rc, rn;
+  load_rec(0, rc);
+  int tm = Tm[0];
+  bool stuck = false;
+  int tmn = Tm[nc > 1 ? 1 : 0];
+  for (; n < P && !stuck; n += W) {
+    uniforms(n);
+    const unsigned long long tag = tag0 + (unsigned long long)(n + 1);
+    for (int i = 0; i < nc; ++i) {
+      const int ni = (i + 1 < nc) ? i + 1 : 0;
+      const int nni = (ni + 1 < nc) ? ni + 1 : 0;
+      const int tmnn = Tm[nni];
+      load_rec(ni, rn);  // next month of this wave (month 0 of its next pass after the last)
+      if (n > 0) {
+        const int need = (n - 1) * nc + reach[i] + 1;
+        int it = 0;
+        while (__hip_atomic_load(pprog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++it > (1 << 24)) {
+            stuck = true;
+            break;
+          }
+        }
+        if (stuck) break;
+      }
+      const int t = __builtin_amdgcn_readfirstlane(tm) & 0xffff, msk = __builtin_amdgcn_readfirstlane(tm) >> 16;
+      double u[NS], zu[NS];
+      for (int a = 0; a < NS; ++a) {
+        u[a] = Ul[t * NS + a];
+        zu[a] = Zl[t * NS + a];
+      }
+      const int tn0 = t + off0, tn1 = t + off1;
+      const double v0 = (h0 && tn0 >= 0 && tn0 < T) ? Sl[tn0 * NS + sp0] : 0.0;
+      const double v1 = (h1 && tn1 >= 0 && tn1 < T) ? Sl[tn1 * NS + sp1] : 0.0;
+      double cur[NS];
+      for (int a = 0; a < NS; ++a) cur[a] = Sl[t * NS + a];
+      double sp[NS];
+      for (int a = 0; a < NS; ++a) sp[a] = fma(h0 ? rc.g0[a] : 0.0, v0, (h1 ? rc.g1[a] : 0.0) * v1);
+      wave_sum_dpp_n(sp);
+      for (int a = 0; a < NS; ++a) sp[a] = rc.hd[a] + sp[a];
+      const double* beta = rc.hd + NS;
+      const double* so = beta + NS * (NS - 1);
+      for (int a = 0; a < NS; ++a) {
+        if (!((msk >> a) & 1)) continue;
+        double mu = sp[a];
+        int y = 0;
+        for (int b = 0; b < NS; ++b) {
+          if (b == a) continue;
+          mu = fma(beta[a * (NS - 1) + y], cur[b] - sp[b], mu);
+          ++y;
+        }
+        uint8_t fl = 0;
+        cur[a] = elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
+        if (e.flags && lane == 0) e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
+      }
+      for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
+      if (publish && n + 1 < P && lane < NS) {  // the month's cells for the next part, write-through
+        double v = cur[0];
+#pragma unroll
+        for (int a = 1; a < NS; ++a) v = lane == a ? cur[a] : v;
+        const unsigned long long vb = (unsigned long long)__double_as_longlong(v);
+        const __attribute__((ext_vector_type(4))) unsigned g = {(unsigned)vb, (unsigned)(vb >> 32), (unsigned)tag,
+                                                                 (unsigned)(tag >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b128(g, grs, gout + (t * NS + lane) * 16, 0, 16);  // sc1
+      }
+      rc = rn;
+      tm = tmn;
+      tmn = tmnn;
+      if (lane == 0)
+        __hip_atomic_store(&prog[wave], n * nc + i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  if (lane == 0) __hip_atomic_store(&prog[wave], done_all, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (stuck && lane == 0) atomicOr(&cs.status[c], CCMM_STATUS_HANDOFF);
+  __syncthreads();
+  // the part that ran the last pass holds the final draw of every censored cell
+  if (((P - 1) % W) / WPC == part)
+    for (int q = tid; q < T * NS; q += 64 * WPC) Sc[q] = Sl[q];
+}
+
 // ---------------------------------------------------------------- Gibbs passes, eight per wave
 // The wavefront of k_elb_gibbs_wf inside ONE wave: eight lanes per pass in flight ("octets": lane
 // 8 w + j, pass slot w = 0..7 runs passes w, w + 8, ...), so the passes synchronise by cross-lane

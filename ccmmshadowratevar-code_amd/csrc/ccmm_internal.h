@@ -270,15 +270,49 @@ __device__ __forceinline__ void wave_sum_dpp_n(double (&v)[K]) {
   for (int k = 0; k < K; ++k) v[k] = readlane_d(v[k], 63);
 }
 
-// ---------------------------------------------------------------- environment switches (host)
-// Selectors choose between kernels or schedules whose draws are the same (bit-identical, or one
-// algorithm in another summation order) and are read in every build (CCMM_ELB_OCT, CCMM_SV_NWG, ...).
-// Timing-only ablations skip or truncate work and leave the draws invalid (CCMM_CHOL_SKIP,
-// CCMM_GC_MODE, ...): only a build with -DCCMM_ABLATION (make ablation -> libccmm_ablation.so) reads
-// them.  A default build returns `off` (the bits of keep_mask excepted: selector bits that share a
-// variable with ablation bits) and reports the variables it ignored through ccmm_env_ignored() and, on
-// ccmm_chains_create, ccmm_last_error().
-int env_select(const char* name, int dflt);
+// ---------------------------------------------------------------- kernel options (host)
+// Choices between kernel forms and schedules are explicit options of a context or a chain set
+// (ccmm_set_option / ccmm_chains_set_option, include/ccmm.h), never environment variables: a stray
+// variable cannot change a run's draws or speed.  Schedules (kOptSchedule) give bit-identical draws;
+// forms (kOptForm) the same algorithm in another summation order (or the QR branch of CTA.m:80-92).
+// The ablation build (-DCCMM_ABLATION, libccmm_ablation.so) also takes each option's default from
+// its CCMM_* variable for the timing tools; a default build reads none of them and names the ones set
+// through ccmm_env_ignored().
+enum OptId {
+  OPT_SOLVE_SPLIT,  // k_cta_solve_lag on two workgroups per chain: -1 auto (B <= kSolveSplitMaxB and resident), 0, 1
+  OPT_SOLVE_ASYNC,  // k_cta_solve_lag row-owned substitutions with LDS flags (1) or barrier-stepped (0)
+  OPT_SV_NWG,       // k_sv_part workgroups per chain: 0 auto, 1, 2, 4
+  OPT_ELB_WAVES,    // passes in flight per chain in k_elb_gibbs_wf: 1 (sequential k_elb_gibbs), 4, 8
+  OPT_ELB_OCT,      // k_elb_gibbs_oct: 0 never, 1 from B >= kElbOctMinB, 2 always
+  OPT_ELB_ASYNC,    // k_elb_gibbs_wf with per-wave progress flags (1) or lock-step barriers (0)
+  OPT_ELB_PARTS,    // workgroups (CUs) per chain of the ELB wavefront: 0 auto, 1, 2, 4
+  OPT_FCST_REG,     // k_fcst with the lag coefficients in registers (1) or PAI in LDS (0)
+  OPT_PHI_OVERLAP,  // PHI block on the auxiliary stream beside the ELB step (1) or in stream order (0)
+  OPT_QR_FALLBACK,  // host QR branch for a failed CTA Cholesky (CTA.m:80-92): 1 on, 0 off
+  kOptSchedule,     // ---- forms below: same algorithm, other summation order / branch
+  OPT_LAG = kOptSchedule,  // lag-structured CTA kernels when the design allows (1) or the generic path (0)
+  OPT_LARGE_PATH,   // 1: the large-system CTA path for every shape (set before ccmm_chains_set_data)
+  OPT_ASTEP_SERIAL, // 1: k_astep (one thread per regression) instead of k_astep_w
+  OPT_PS_CHOL_LDS,  // 1: k_ps_chol (LDS window) instead of k_ps_chol_w
+  OPT_SV_MFMA,      // k_sv_part phase-A products on MFMA (N <= 20 buckets): 1, or the FMA pass 0
+  OPT_FORCE_QR,     // 1: every chain through the host QR branch of CTA.m:80-92
+  OPT_GIRF_GENERIC, // 1: the table-driven GIRF kernel for the reference shape too
+  kOptCount
+};
+struct OptDesc {
+  const char* name;  // ccmm_set_option name
+  const char* env;   // variable the ablation build reads as the default
+  int dflt, lo, hi;
+};
+extern const OptDesc kOptDesc[kOptCount];
+struct Options {
+  int v[kOptCount];
+  Options();  // defaults (ablation build: from the environment)
+  int operator[](int i) const { return v[i]; }
+};
+int option_id(const char* name);  // -1 when unknown
+// timing-only ablation variables (results invalid): read by the ablation build only; a default build
+// returns `off` (the bits of keep_mask excepted) and reports the variable through ccmm_env_ignored()
 int env_ablation(const char* name, int off, int keep_mask = 0);
 
 // host CTA draw of one chain with the QR branch of CTA.m:80-92 (ccmm_host_cta.cpp)

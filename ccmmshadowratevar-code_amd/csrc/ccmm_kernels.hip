@@ -4,11 +4,11 @@
 // (CTA.m:60-98).  The per-sweep pipeline for B chains is
 //
 //   k_cta_weights   w_t^(j) = sum_{i>=j} A(i,j)^2 / sqrtht(t,i)^2        (elementwise)
-//   k_syrk          G_cj = X' diag(w^(j)) X   on v_mfma_f64_16x16x4_f64    (FP64 MFMA)
-//   k_chol          L_cj = chol(G_cj + diag(iV_j)), writes L (lower), L' (upper), 1/diag
-//   k_cta_solve     per chain, j = 1..N in order: rhs = iVb_j + X' v^(j) (needs the
+//   k_gram_chol     G_cj = X' diag(w^(j)) X + diag(iV_j) and its Cholesky factor on
+//                   v_mfma_f64_16x16x4_f64 (ccmm_gram_chol.hip; ccmm_lag.hip for lag designs)
+//   k_cta_solve2    per chain, j = 1..N in order: rhs = iVb_j + X' v^(j) (needs the
 //                   draws of equations < j), L L' x = rhs, PAI(:,j) = L'^-1 (L^-1 rhs + z_j),
-//                   residual update.                                    (latency bound)
+//                   residual update (ccmm_cta_solve.hip)               (latency bound)
 //   k_astep         A-matrix rows (mcmcVAR.m:236-254), invA, logy2 (mcmcVAR.m:259)
 //   k_sv_mix        KSC mixture indicators (elementwise)
 //   k_sv_part       partitioned block-tridiagonal sampler of h_0..h_T (ccmm_svpart.hip)
@@ -118,314 +118,6 @@ __global__ void k_cta_weights(Dims d, const int* __restrict__ Tslot, ChainState 
     ihv = 1.0 / (shv * shv);
   }
   cs.ih2[((size_t)c * d.N + j) * d.TP + t] = ihv;
-}
-
-// ============================================================== weighted SYRK (FP64 MFMA)
-// G_cj[a][b] = sum_t X[t][a] w[t] X[t][b] for the lower 64x64 tiles (ti >= tj).
-// 256 threads = 4 waves, each a 32x32 sub-tile as 2x2 v_mfma_f64_16x16x4_f64 blocks.
-// The MFMA is issued with the b-panel as the A operand so that a lane's 16
-// consecutive accumulator columns are 16 consecutive rows a of column-major G.
-constexpr int kLdP = kTile + 16;  // 80 doubles: conflict-free ds_read_b64 fragment reads
-
-__global__ __launch_bounds__(256) void k_syrk(Dims d, const int* __restrict__ Tslot, XSel xs,
-                                              ChainState cs) {
-  __shared__ double Pa[kTChunk][kLdP];  // weighted a-panel  (t, a)
-  __shared__ double Pb[kTChunk][kLdP];  // b-panel           (t, b)
-  const int mat = blockIdx.y;
-  const int c = mat / d.N;
-  const int T = Tslot[cs.slot[c]];
-  // lower-tile index -> (ti, tj)
-  int tile = blockIdx.x, ti = 0;
-  while (tile > ti) {
-    tile -= ti + 1;
-    ++ti;
-  }
-  const int tj = tile;
-  const int a0 = ti * kTile, b0 = tj * kTile;
-  const double* X = xs.pool + (size_t)xs.idx[mat] * d.KP * d.TP;
-  const double* w = cs.W + (size_t)mat * d.TP;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int lcol = tid & 63, lt0 = (tid >> 6) * 8;  // loader: column, 8 consecutive t
-
-  dbl4 acc[2][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = dbl4{0.0, 0.0, 0.0, 0.0};
-
-  const int nchunks = (T + kTChunk - 1) / kTChunk;
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const int t0 = ch * kTChunk;
-    {
-      const double* xa = X + (size_t)(a0 + lcol) * d.TP + t0 + lt0;
-      const double* xb = X + (size_t)(b0 + lcol) * d.TP + t0 + lt0;
-      double va[8], vb[8], ww[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        va[q] = xa[q];
-        vb[q] = xb[q];
-        ww[q] = w[t0 + lt0 + q];
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        Pa[lt0 + q][lcol] = va[q] * ww[q];
-        Pb[lt0 + q][lcol] = vb[q];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < kTChunk / 4; ++kk) {
-      const int kr = kk * 4 + (lane >> 4);
-      double fa[2], fb[2];
-#pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        fb[x] = Pb[kr][wn * 32 + x * 16 + (lane & 15)];  // MFMA A operand: rows = b
-        fa[x] = Pa[kr][wm * 32 + x * 16 + (lane & 15)];  // MFMA B operand: cols = a
-      }
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-          acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[x], fa[y], acc[x][y], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  // D[row = b][col = a]: lane holds rows (lane>>4) + 4r, column lane & 15
-  double* G = cs.G + (size_t)mat * d.KP * d.KP;
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = b0 + wn * 32 + x * 16 + (lane >> 4) + 4 * r;
-        const int a = a0 + wm * 32 + y * 16 + (lane & 15);
-        G[(size_t)b * d.KP + a] = acc[x][y][r];
-      }
-}
-
-// ============================================================== batched Cholesky
-// In place on G_cj + diag(iV_j) (CTA.m:73-74).  One workgroup per system,
-// right-looking blocked with 32-wide panels; the diagonal block is factored in
-// registers by one wave (lane i = row i), the panel solve is one row per
-// thread, the trailing update reads the panel from LDS.  Writes L (lower),
-// L' (upper triangle, for the row-oriented back substitution), 1/L_kk.
-__global__ __launch_bounds__(256) void k_chol(Dims d, const int* __restrict__ slotIV,
-                                              const double* __restrict__ iVdiag, ChainState cs,
-                                              double* __restrict__ rdiag) {
-  extern __shared__ double sm[];
-  double* Dg = sm;                    // 32 x 33
-  double* P = sm + kCholNB * (kCholNB + 1);  // (KP) x 33 panel rows
-  const int mat = blockIdx.x;
-  const int c = mat / d.N, j = mat % d.N;
-  const int KP = d.KP;
-  double* A = cs.G + (size_t)mat * KP * KP;
-  const double* iv = iVdiag + ((size_t)slotIV[c] * d.N + j) * KP;
-  double* rd = rdiag + (size_t)mat * KP;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int a = tid; a < KP; a += blockDim.x) A[(size_t)a * KP + a] += iv[a];
-  __syncthreads();
-  int bad = 0;
-  for (int k0 = 0; k0 < KP; k0 += kCholNB) {
-    // ---- factor the diagonal block: wave 0, lane i holds row i
-    if (wave == 0) {
-      double row[kCholNB];
-      double mydiag = 1.0;
-#pragma unroll
-      for (int m = 0; m < kCholNB; ++m)
-        row[m] = (lane < kCholNB && m <= lane) ? A[(size_t)(k0 + m) * KP + k0 + lane] : 0.0;
-#pragma unroll
-      for (int kk = 0; kk < kCholNB; ++kk) {
-        double dkk = readlane_d(row[kk], kk);
-        if (!(dkk > 0.0)) {
-          bad = 1;
-          dkk = 1.0;
-        }
-        const double piv = sqrt(dkk);
-        const double rp = 1.0 / piv;
-        if (lane == kk) {
-          row[kk] = piv;
-          mydiag = piv;
-        }
-        if (lane > kk) row[kk] *= rp;
-        const double lik = row[kk];
-#pragma unroll
-        for (int m = kk + 1; m < kCholNB; ++m) {
-          const double lmk = readlane_d(lik, m);
-          if (lane >= m) row[m] = fma(-lik, lmk, row[m]);
-        }
-      }
-      if (lane < kCholNB) {
-#pragma unroll
-        for (int m = 0; m < kCholNB; ++m) {
-          const double v = (m <= lane) ? row[m] : 0.0;
-          Dg[lane * (kCholNB + 1) + m] = v;  // Dg[row][col]
-          if (m <= lane) {
-            A[(size_t)(k0 + m) * KP + k0 + lane] = v;  // L(k0+lane, k0+m)
-            A[(size_t)(k0 + lane) * KP + k0 + m] = v;  // L' (upper)
-          }
-        }
-        rd[k0 + lane] = 1.0 / mydiag;
-      }
-    }
-    __syncthreads();
-    // ---- panel: rows i >= k0+32 solve x * L_kk' = A(i, k0:k0+32)
-    const int r0 = k0 + kCholNB;
-    const int nrow = KP - r0;
-    for (int ii = tid; ii < nrow; ii += blockDim.x) {
-      const int i = r0 + ii;
-      double x[kCholNB];
-#pragma unroll
-      for (int m = 0; m < kCholNB; ++m) x[m] = A[(size_t)(k0 + m) * KP + i];
-#pragma unroll
-      for (int m = 0; m < kCholNB; ++m) {
-        double s = x[m];
-#pragma unroll
-        for (int q = 0; q < m; ++q) s = fma(-x[q], Dg[m * (kCholNB + 1) + q], s);
-        x[m] = s / Dg[m * (kCholNB + 1) + m];
-      }
-#pragma unroll
-      for (int m = 0; m < kCholNB; ++m) {
-        P[ii * (kCholNB + 1) + m] = x[m];
-        A[(size_t)(k0 + m) * KP + i] = x[m];  // L(i, k0+m)
-        A[(size_t)i * KP + k0 + m] = x[m];    // L' (upper)
-      }
-    }
-    __syncthreads();
-    // ---- trailing update of the lower triangle: A(i,jj) -= P(i,:) . P(jj,:)
-    for (int jj = 0; jj < nrow; ++jj) {
-      for (int ii = jj + tid; ii < nrow; ii += blockDim.x) {
-        double s = 0.0;
-#pragma unroll
-        for (int m = 0; m < kCholNB; ++m)
-          s = fma(P[ii * (kCholNB + 1) + m], P[jj * (kCholNB + 1) + m], s);
-        A[(size_t)(r0 + jj) * KP + r0 + ii] -= s;
-      }
-    }
-    __syncthreads();
-  }
-  if (bad && lane == 0) atomicOr(&cs.status[c], 2);
-}
-
-// ============================================================== CTA sequential part
-// One workgroup per chain, equations in order (CTA.m:60-97).  RPL = KP/64 rows
-// of the K-vector per lane in the wave-0 triangular solves.
-template <int RPL>
-__global__ __launch_bounds__(256) void k_cta_solve(Dims d, const int* __restrict__ Tslot,
-                                                   const double* __restrict__ iVb, XSel xs,
-                                                   ChainState cs, const double* __restrict__ rdiag,
-                                                   RngArgs ra) {
-  extern __shared__ double sm[];
-  double* v = sm;           // TP
-  double* yv = sm + d.TP;   // KP
-  const int c = blockIdx.x;
-  const int s = cs.slot[c];
-  const int T = Tslot[s];
-  const int N = d.N, KP = d.KP, TP = d.TP, K = d.K;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const Rng rng = ra.make(c);
-  const double* A = cs.A + (size_t)c * N * N;
-  const double* sh = cs.sqrtht + (size_t)c * N * TP;
-  const double* Y = xs.ypool + (size_t)xs.yidx[c] * N * TP;
-  double* E = cs.E + (size_t)c * N * TP;
-
-  for (int j = 0; j < N; ++j) {
-    const int mat = c * N + j;
-    const double* X = xs.pool + (size_t)xs.idx[mat] * KP * TP;
-    // 1. PAI(:,j) = 0  ->  E(:,j) = Y(:,j)
-    for (int t = tid; t < TP; t += blockDim.x) E[(size_t)j * TP + t] = (t < T) ? Y[(size_t)j * TP + t] : 0.0;
-    __syncthreads();
-    // 2. v_t = sum_{i>=j} A(i,j)/sqrtht(t,i)^2 * [E_t A(i,:)']   (X_j'Y_j = X' v, CTA.m:67)
-    for (int t = tid; t < TP; t += blockDim.x) {
-      double acc = 0.0;
-      if (t < T) {
-        for (int i = j; i < N; ++i) {
-          double ea = 0.0;
-          for (int k = 0; k <= i; ++k) ea = fma(E[(size_t)k * TP + t], A[i + k * N], ea);
-          const double hi = sh[(size_t)i * TP + t];
-          acc += A[i + j * N] * (ea / hi) / hi;
-        }
-      }
-      v[t] = acc;
-    }
-    __syncthreads();
-    // 3. rhs = iVb_j + X' v   (one wave per column)
-    const double* ivb = iVb + ((size_t)s * N + j) * KP;
-    for (int a = wave; a < KP; a += 4) {
-      double p = 0.0;
-      if (a < K) {
-        const double* xa = X + (size_t)a * TP;
-        for (int t = lane; t < T; t += 64) p = fma(xa[t], v[t], p);
-      }
-      p = wave_sum(p);
-      if (lane == 0) yv[a] = ivb[a] + p;
-    }
-    __syncthreads();
-    // 4./5. solves on wave 0:  L y = rhs ; L' x = y + z   (x = b_post + Vchol_post z, CTA.m:95-96)
-    if (wave == 0) {
-      const double* L = cs.G + (size_t)mat * KP * KP;
-      const double* rd = rdiag + (size_t)mat * KP;
-      double y[RPL];
-#pragma unroll
-      for (int r = 0; r < RPL; ++r) y[r] = yv[r * 64 + lane];
-      // forward substitution, column oriented
-#pragma unroll
-      for (int r = 0; r < RPL; ++r) {
-        for (int kk = 0; kk < 64; ++kk) {
-          const int k = r * 64 + kk;
-          if (k >= K) break;
-          const double yk = readlane_d(y[r], kk) * rd[k];
-          if (lane == kk) y[r] = yk;
-          const double* Lk = L + (size_t)k * KP;
-#pragma unroll
-          for (int r2 = r; r2 < RPL; ++r2) {
-            const int i = r2 * 64 + lane;
-            if (i > k) y[r2] = fma(-Lk[i], yk, y[r2]);
-          }
-        }
-      }
-      // add z_j (randn(K,N) of CTA.m:58, column j)
-#pragma unroll
-      for (int r = 0; r < RPL; ++r) {
-        const int a = r * 64 + lane;
-        if (a < K) y[r] += rng.normal(CCMM_RNG_PAI, (uint32_t)(a + K * j));
-      }
-      // back substitution with L' (upper storage: U(i,k) = L(k,i) at column k)
-#pragma unroll
-      for (int r = RPL - 1; r >= 0; --r) {
-        for (int kk = 63; kk >= 0; --kk) {
-          const int k = r * 64 + kk;
-          if (k >= K) continue;
-          const double xk = readlane_d(y[r], kk) * rd[k];
-          if (lane == kk) y[r] = xk;
-          const double* Uk = L + (size_t)k * KP;
-#pragma unroll
-          for (int r2 = 0; r2 <= r; ++r2) {
-            const int i = r2 * 64 + lane;
-            if (i < k) y[r2] = fma(-Uk[i], xk, y[r2]);
-          }
-        }
-      }
-      double* pai = cs.PAI + ((size_t)c * N + j) * KP;
-#pragma unroll
-      for (int r = 0; r < RPL; ++r) {
-        const int a = r * 64 + lane;
-        const double val = (a < K) ? y[r] : 0.0;
-        yv[a] = val;
-        pai[a] = val;
-      }
-    }
-    __syncthreads();
-    // 6. E(:,j) = Y(:,j) - X PAI(:,j)
-    for (int t = tid; t < T; t += blockDim.x) {
-      double acc = 0.0;
-      for (int a = 0; a < K; ++a) acc = fma(X[(size_t)a * TP + t], yv[a], acc);
-      E[(size_t)j * TP + t] = Y[(size_t)j * TP + t] - acc;
-    }
-    __syncthreads();
-  }
 }
 
 // ============================================================== A-step

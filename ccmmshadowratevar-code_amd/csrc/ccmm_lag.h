@@ -22,8 +22,8 @@ struct LagSel {
 // [2 equation parities][256], and one progress flag per workgroup; part == nullptr: one workgroup
 struct SolveXch {
   double* part;
-  unsigned* flag;
-  unsigned epoch;  // launch counter: equation j of this launch posts epoch * 64 + j + 1
+  unsigned long long* flag;
+  unsigned long long epoch;  // launch counter: equation j of this launch posts epoch * 64 + j + 1 (64 bits: no wrap)
 };
 constexpr int kSolveSplitMaxB = 64;
 
@@ -72,7 +72,9 @@ inline size_t sl_lds_bytes(int NT, int rows, int ldd, int TP, int nmax) {
 bool lag_supported_nt(int nt);
 hipError_t lag_launch_gram(int NT, hipStream_t st, size_t lds, Dims d, const int* Tslot, LagSel ls,
                            ChainState cs, const double* iVdiag);
-hipError_t lag_launch_solve(int NT, int nmax, hipStream_t st, size_t lds, Dims d, const int* Tslot,
+// workgroups of the solve kernel that can be resident at once on the device (occupancy x CUs)
+int lag_solve_resident(int NT, int nmax, size_t lds, int async);
+hipError_t lag_launch_solve(int NT, int nmax, int async, hipStream_t st, size_t lds, Dims d, const int* Tslot,
                             const double* iVb, XSel xs, LagSel ls, ChainState cs, RngArgs ra, SolveXch xc);
 
 }  // namespace ccmm

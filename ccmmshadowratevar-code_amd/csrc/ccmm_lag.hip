@@ -630,7 +630,7 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
       if (tid <= KL) mine[tid] = part[hh * 256 + tid];
       __threadfence();
       __syncthreads();
-      const unsigned seq = xc.epoch * 64u + (unsigned)j + 1u;
+      const unsigned long long seq = xc.epoch * 64ull + (unsigned long long)j + 1ull;
       if (tid == 0) {
         __hip_atomic_store(&xc.flag[c * 2 + hh], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         for (int it = 0;; ++it) {
@@ -911,36 +911,46 @@ hipError_t lag_launch_gram(int NT, hipStream_t st, size_t lds, Dims d, const int
   return hipGetLastError();
 }
 
-// SW = 8 waves (default) or 16 (CCMM_SOLVE_WAVES=16: half the factor tiles per wave and four waves
-// per SIMD, but 128 registers per lane, which the kernel overflows).  Same arithmetic either way
-// (per-thread v_t and residual rows, per-tile substitution products, the X'v t-halves on threads
-// 0..511).
-template <int NT, int NM, int SW, bool RO>
-static hipError_t solve_sw(hipStream_t st, size_t lds, Dims d, const int* Tslot, const double* iVb, XSel xs,
+// row-owned substitutions with LDS flag hand-offs (RO, option solve_async = 1) or the barrier-stepped
+// form (solve_async = 0).  Same arithmetic either way (per-thread v_t and residual rows, per-tile
+// substitution products, the X'v t-halves on threads 0..511).
+template <int NT, int NM, bool RO>
+static hipError_t solve_ro(hipStream_t st, size_t lds, Dims d, const int* Tslot, const double* iVb, XSel xs,
                            LagSel ls, ChainState cs, RngArgs ra, SolveXch xc) {
-  hipError_t e = hipFuncSetAttribute((const void*)k_cta_solve_lag<NT, NM, SW, RO>,
+  hipError_t e = hipFuncSetAttribute((const void*)k_cta_solve_lag<NT, NM, 8, RO>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_cta_solve_lag<NT, NM, SW, RO>), dim3(d.B, xc.part ? 2 : 1), dim3(64 * SW), lds, st, d,
+  hipLaunchKernelGGL((k_cta_solve_lag<NT, NM, 8, RO>), dim3(d.B, xc.part ? 2 : 1), dim3(64 * 8), lds, st, d,
                      Tslot, iVb, xs, ls, cs, ra, xc);
   return hipGetLastError();
 }
-template <int NT, int NM>
-static hipError_t solve_one(hipStream_t st, size_t lds, Dims d, const int* Tslot, const double* iVb, XSel xs,
-                            LagSel ls, ChainState cs, RngArgs ra, SolveXch xc) {
-  // row-owned substitutions with LDS flag hand-offs (default) or the barrier-stepped form
-  // (CCMM_SOLVE_ASYNC=0); CCMM_SOLVE_WAVES=16: the stepped form on sixteen waves
-  const char* v = std::getenv("CCMM_SOLVE_WAVES");
-  const char* a = std::getenv("CCMM_SOLVE_ASYNC");
-  if (v && std::atoi(v) == 16) return solve_sw<NT, NM, 16, false>(st, lds, d, Tslot, iVb, xs, ls, cs, ra, xc);
-  if (a && std::atoi(a) == 0) return solve_sw<NT, NM, 8, false>(st, lds, d, Tslot, iVb, xs, ls, cs, ra, xc);
-  return solve_sw<NT, NM, 8, true>(st, lds, d, Tslot, iVb, xs, ls, cs, ra, xc);
+
+template <int NT, int NM, bool RO>
+static int solve_resident(size_t lds) {
+  const void* fn = (const void*)k_cta_solve_lag<NT, NM, 8, RO>;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return 0;
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * 8, lds) != hipSuccess) return 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return per_cu * cus;
 }
 
-hipError_t lag_launch_solve(int NT, int nmax, hipStream_t st, size_t lds, Dims d, const int* Tslot,
+int lag_solve_resident(int NT, int nmax, size_t lds, int async) {
+#define SR_CASE(NT_, NM_)                                                                              \
+  if (NT == NT_ && nmax == NM_) return async ? solve_resident<NT_, NM_, true>(lds) : solve_resident<NT_, NM_, false>(lds);
+  SR_CASE(1, 8) SR_CASE(1, 20) SR_CASE(1, 32) SR_CASE(15, 8) SR_CASE(15, 20) SR_CASE(15, 32)
+#undef SR_CASE
+  return 0;
+}
+
+hipError_t lag_launch_solve(int NT, int nmax, int async, hipStream_t st, size_t lds, Dims d, const int* Tslot,
                             const double* iVb, XSel xs, LagSel ls, ChainState cs, RngArgs ra, SolveXch xc) {
-#define SL_CASE(NT_, NM_) \
-  if (NT == NT_ && nmax == NM_) return solve_one<NT_, NM_>(st, lds, d, Tslot, iVb, xs, ls, cs, ra, xc);
+#define SL_CASE(NT_, NM_)                                                                           \
+  if (NT == NT_ && nmax == NM_)                                                                     \
+    return async ? solve_ro<NT_, NM_, true>(st, lds, d, Tslot, iVb, xs, ls, cs, ra, xc)            \
+                 : solve_ro<NT_, NM_, false>(st, lds, d, Tslot, iVb, xs, ls, cs, ra, xc);
   SL_CASE(1, 8) SL_CASE(1, 20) SL_CASE(1, 32) SL_CASE(15, 8) SL_CASE(15, 20) SL_CASE(15, 32)
 #undef SL_CASE
   return hipErrorInvalidValue;

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(128) void k_ps_chol(Dims d, ElbDev e, PsDev ps, Cha
   if (fail) {  // not positive definite: no proposals, the Gibbs draw serves the sweep
     if (lane == 0) {
       ps.n[c] = 0;
-      cs.status[c] |= 32;
+      atomicOr(&cs.status[c], CCMM_STATUS_PS_GIBBS);  // informational (k_phi sets bit 16 concurrently)
     }
   }
 }
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(64) void k_ps_chol_w(Dims d, ElbDev e, PsDev ps, Ch
   }
   if (fail && lane == 0) {  // not positive definite: no proposals, the Gibbs draw serves the sweep
     ps.n[c] = 0;
-    cs.status[c] |= 32;
+    atomicOr(&cs.status[c], CCMM_STATUS_PS_GIBBS);  // informational (k_phi sets bit 16 concurrently)
   }
 }
 

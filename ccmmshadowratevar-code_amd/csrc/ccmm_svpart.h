@@ -17,6 +17,6 @@ inline size_t sv_sep_len(int N) {
 // per-chain block factors C_t: (TP + 1) x NN x NN; w_t and the fill vectors g_t: (TP + 1) x NN
 hipError_t sv_launch_part(int N, hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
                           const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
-                          int mode = 0);  // mode: timing-only phase skips (CCMM_SV_MODE)
+                          int mode, int nwg_opt, bool mfma);  // mode: timing-only phase skips (CCMM_SV_MODE)
 
 }  // namespace ccmm

@@ -791,15 +791,15 @@ static hipError_t sv_launch_k(hipStream_t st, Dims d, const int* Tslot, const do
   return hipGetLastError();
 }
 
-// NN = 20: phase A's block products on MFMA unless CCMM_SV_MFMA=0
+// NN = 20: phase A's block products on MFMA unless option sv_mfma = 0 (mode bit 256 here): a different
+// accumulation order than the FMA pass, so the two forms agree to rounding, not bit for bit
 template <int NN, int NW, bool PACK>
 static hipError_t sv_launch_one_(hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
                                 const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf,
                                 int mode, int nwg) {
   if constexpr (NN == 20) {
-    const char* ev = std::getenv("CCMM_SV_MFMA");
-    if (ev && std::atoi(ev) == 0)
-      return sv_launch_k<NN, NW, PACK, false>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
+    if (mode & 256)
+      return sv_launch_k<NN, NW, PACK, false>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode & ~256, nwg);
   }
   return sv_launch_k<NN, NW, PACK, true>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, nwg);
 }
@@ -817,16 +817,15 @@ static hipError_t sv_launch_one(hipStream_t st, Dims d, const int* Tslot, const 
 
 // Workgroups per chain: 1 from B = 129 (the chip is full), 2 of 8 waves down to B = 33, and at
 // B <= 32 (NN <= 20) 4 of 4 waves -- one wave per SIMD on 4 CUs, so that the serial block chains of
-// phases A and C no longer share a SIMD's issue (the OOS floor runs one chain).  CCMM_SV_NWG=1|2|4
+// phases A and C no longer share a SIMD's issue (the OOS floor runs one chain).  Option sv_nwg = 1|2|4
 // overrides.  The segments, their order of operations and the draws are the same in every layout.
 hipError_t sv_launch_part(int N, hipStream_t st, Dims d, const int* Tslot, const double* V0inv,
-                          const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf, int mode) {
+                          const double* V0invm, ChainState cs, RngArgs ra, double* sep, double* gbuf, int mode,
+                          int nwg_opt, bool mfma) {
   const int nb = sv_bucket(N);
   int nwg = d.B <= 32 && nb <= 20 ? 4 : (d.B <= 128 ? 2 : 1);
-  if (const char* ev = std::getenv("CCMM_SV_NWG")) {
-    const int v = std::atoi(ev);
-    nwg = v >= 4 && nb <= 20 ? 4 : std::max(1, std::min(2, v));
-  }
+  if (nwg_opt > 0) nwg = nwg_opt >= 4 && nb <= 20 ? 4 : std::max(1, std::min(2, nwg_opt));
+  if (!mfma) mode |= 256;
   if (nwg == 4) {
     switch (nb) {
       case 4: return sv_launch_one<4, 4>(st, d, Tslot, V0inv, V0invm, cs, ra, sep, gbuf, mode, 4);

@@ -908,7 +908,7 @@ def goVARshadowrateBlockHybrid_batch(data0, ydates0, ndxSHADOWRATE, ndxOTHERYIEL
         Ny = int(np.count_nonzero(yields))
         for k, i in enumerate(vidx):
             cs = slice(k * C, (k + 1) * C)
-            if np.any(status[cs] & ~1):  # bit 1: CTA QR fallback used (valid draws)
+            if np.any(status[cs] & ~_abi.STATUS_INFO):  # bits 1, 64: informational (valid draws)
                 failed.append(i)
                 continue
             thisT, bm, yr = units[i]

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define CCMM_ABI_VERSION 3
+#define CCMM_ABI_VERSION 4  /* 4: ccmm_batch_out.shadowratePSRFchains, kernel options, status bit 64 */
 
 /* return codes */
 #define CCMM_OK 0
@@ -48,6 +48,17 @@ extern "C" {
 #define CCMM_ERR_HIP (-3)          /* HIP runtime failure */
 #define CCMM_ERR_NOTSPD (-4)       /* Cholesky failure in a block without fallback */
 #define CCMM_ERR_STATE (-5)        /* call order violated (e.g. sweep before set_data) */
+
+/* per-chain status bits (ccmm_chains_get_status) */
+#define CCMM_STATUS_QR 1            /* CTA Cholesky failed, the host QR branch of CTA.m:80-92 redrew the chain (valid) */
+#define CCMM_STATUS_CTA 2           /* CTA Cholesky pivot <= 0 without the QR repair (invalid draws) */
+#define CCMM_STATUS_ASTEP 4         /* A-step Cholesky pivot <= 0 (invalid draws) */
+#define CCMM_STATUS_SV 8            /* SV sampler pivot <= 0 (invalid draws) */
+#define CCMM_STATUS_PHI 16          /* PHI Cholesky pivot <= 0 (invalid draws) */
+#define CCMM_STATUS_HANDOFF 32      /* a device hand-off between workgroups / waves reached its spin cap (invalid) */
+#define CCMM_STATUS_PS_GIBBS 64     /* the PS precision was not positive definite: the Gibbs draw served the
+                                       sweep, as the reference's fallback (:462-463) does (valid) */
+#define CCMM_STATUS_INFO (CCMM_STATUS_QR | CCMM_STATUS_PS_GIBBS)  /* informational bits */
 
 /* model ids for the sweep-level API */
 #define CCMM_MODEL_LINEAR 0        /* mcmcVAR.m */
@@ -72,20 +83,36 @@ typedef struct ccmm_chains ccmm_chains;
 /* ---------------------------------------------------------------- context */
 int ccmm_abi_version(void);
 const char* ccmm_last_error(void);
-/* Environment switches (host only, no GPU needed).  Timing-only ablation variables (CCMM_CHOL_SKIP,
- * CCMM_SOLVE_SKIP, CCMM_SV_SKIP, CCMM_GC_MODE, CCMM_LAG_MODE, CCMM_BIG_MASK, CCMM_ELB_MODE, the
- * ablation bits of CCMM_SV_MODE, CCMM_FCST_MODE) leave the draws invalid and are read only by a build
- * with -DCCMM_ABLATION (`make ablation`: libccmm_ablation.so); ccmm_ablation_build() returns 1 there.
- * A default build ignores them: ccmm_env_ignored() returns how many are set in the environment and
- * ignored (their names comma-separated in buf, len bytes with the terminator; buf may be NULL), and
+/* Environment.  A default build reads NO environment variable: kernel forms and schedules are the
+ * explicit options below.  Timing-only ablation variables (CCMM_CHOL_SKIP, CCMM_SOLVE_SKIP, CCMM_SV_SKIP,
+ * CCMM_GC_MODE, CCMM_LAG_MODE, CCMM_BIG_MASK, CCMM_ELB_MODE, the ablation bits of CCMM_SV_MODE,
+ * CCMM_FCST_MODE, CCMM_POISON) leave the draws invalid and, like the options' CCMM_* defaults, are read
+ * only by a build with -DCCMM_ABLATION (`make ablation`: libccmm_ablation.so); ccmm_ablation_build()
+ * returns 1 there.  ccmm_env_ignored() returns how many CCMM_* variables the library knows are set and
+ * ignored (names comma-separated in buf, len bytes with the terminator; buf may be NULL), and
  * ccmm_chains_create() leaves the same list in ccmm_last_error() as a warning. */
 int ccmm_ablation_build(void);
 int ccmm_env_ignored(char* buf, int len);
+/* Kernel options: choices between kernel forms and schedules, set explicitly per context (inherited by
+ * the chain sets created on it afterwards and used by the block-level drop-ins) or per chain set.
+ * Schedules give bit-identical draws: solve_split (-1 auto, 0, 1), solve_async (0/1), sv_nwg (0 auto,
+ * 1, 2, 4), elb_waves (1, 4, 8), elb_oct (0, 1 auto, 2), elb_async (0/1), elb_parts (0 auto, 1, 2, 4:
+ * workgroups per chain of the ELB wavefront), fcst_reg (0/1), phi_overlap (0/1), qr_fallback (0/1).
+ * Forms run the same algorithm in another summation order (or the QR branch): lag (0/1), large_path
+ * (0/1; set before ccmm_chains_set_data), astep_serial, ps_chol_lds, sv_mfma (0/1), force_qr,
+ * girf_generic.  CCMM_ERR_ARG for an unknown name or a value out of range. */
+int ccmm_option_count(void);
+const char* ccmm_option_name(int i);
+/* The value a new context starts from (host only): the built-in default in a default build, whatever the
+ * environment holds; the ablation build's CCMM_* override. */
+int ccmm_option_default(const char* name, int* value);
 int ccmm_device_count(void);
 /* Create a context bound to HIP device `device`.  Returns NULL on failure. */
 ccmm_ctx* ccmm_create(int device);
 void ccmm_destroy(ccmm_ctx* ctx);
 int ccmm_synchronize(ccmm_ctx* ctx);
+int ccmm_set_option(ccmm_ctx* ctx, const char* name, int value);
+int ccmm_get_option(ccmm_ctx* ctx, const char* name, int* value);
 
 /* --------------------------------------------------- block-level drop-ins */
 
@@ -223,6 +250,9 @@ typedef struct {
 
 ccmm_chains* ccmm_chains_create(ccmm_ctx* ctx, const ccmm_chain_config* cfg);
 void ccmm_chains_destroy(ccmm_chains* ch);
+/* Kernel options of one chain set (see ccmm_set_option; initialised from its context at create). */
+int ccmm_chains_set_option(ccmm_chains* ch, const char* name, int value);
+int ccmm_chains_get_option(ccmm_chains* ch, const char* name, int* value);
 
 /* Data slot `slot`: one vintage's design (mcmcVAR.m:62-72, 186; 164-169).
  *   Y T x N, X T x K, iVdiag K x N, iVb K x N, sPHI N x N, h0mean N, h0vcvsqrt N x N */
@@ -253,13 +283,14 @@ int ccmm_chains_get_kai(ccmm_chains* ch, int8_t* kai);
  * Ns x elbTmax x (gibbsburn + 1) x B uint8 (0 for uncensored cells). */
 int ccmm_chains_record_elb_flags(ccmm_chains* ch, int enable);
 int ccmm_chains_get_elb_flags(ccmm_chains* ch, uint8_t* flags);
-/* Per-chain status word since set_state (B ints, OR of: 2 CTA Cholesky, 4 A-step
+/* Per-chain status word since set_state (B ints, OR of CCMM_STATUS_*: 2 CTA Cholesky, 4 A-step
  * Cholesky, 8 SV sampler, 16 PHI Cholesky found a non-positive pivot; the block
  * then continued with a unit pivot, so the chain's draws are invalid; 32: a device hand-off
- * between waves reached its spin cap, never expected).  A CTA Cholesky
+ * between workgroups or waves reached its spin cap, never expected).  A CTA Cholesky
  * failure is repaired within the sweep by the host QR branch of CTA.m:80-92, which
- * replaces bit 2 by bit 1 ("QR fallback used", informational: the draws are valid).
- * Returns 1 if any chain carries a bit other than 1, 0 otherwise; the batch driver re-runs
+ * replaces bit 2 by bit 1 ("QR fallback used", informational: the draws are valid); bit 64
+ * (informational) marks a sweep whose PS precision failed and whose Gibbs draw served instead.
+ * Returns 1 if any chain carries a bit outside CCMM_STATUS_INFO, 0 otherwise; the batch driver re-runs
  * flagged units (goVARshadowrateBlockHybrid.m:287-310). */
 int ccmm_chains_get_status(ccmm_chains* ch, int* status);
 /* Any output pointer may be NULL.  invA, PHI, RESID are those of the last sweep. */

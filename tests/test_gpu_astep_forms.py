@@ -5,7 +5,6 @@ shared logy2 form), so A, invA and the whole chain state agree bit for bit after
 real data (fredblockMD20-2022-09, N = 20, p = 12, T = 750; k_astep_w<20>), a synthetic 24-series
 panel (k_astep_w<32>, N in 21..32) and a synthetic sample longer than 1024 months (the Gram tiles
 have no sample-length limit).  Philox draws, same seed."""
-import os
 
 import numpy as np
 import pytest
@@ -31,20 +30,16 @@ def _model(pkg, fred, case):
 
 
 def _run(pkg, m, p, v1, B=6, sweeps=3):
-    os.environ["CCMM_ASTEP_V1"] = "1" if v1 else "0"
-    try:
-        ctx = pkg.Context(0)
-        ch = pkg.Chains(ctx, N=m.N, p=p, T=m.T, B=B, crn=False, seed=99)
-        ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
-        st = pkg.model.initial_state(m, B)
-        ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
-        ch.sweep(sweeps)
-        out = dict(ch.get_state())
-        out["status"] = ch.get_status()
-        ch.close()
-        return out
-    finally:
-        os.environ.pop("CCMM_ASTEP_V1", None)
+    ctx = pkg.Context(0)
+    ch = pkg.Chains(ctx, N=m.N, p=p, T=m.T, B=B, crn=False, seed=99, options={"astep_serial": int(v1)})
+    ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+    st = pkg.model.initial_state(m, B)
+    ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+    ch.sweep(sweeps)
+    out = dict(ch.get_state())
+    out["status"] = ch.get_status()
+    ch.close()
+    return out
 
 
 @pytest.mark.parametrize("case", ["real", "n24", "t1100"])

@@ -7,7 +7,6 @@ Against the oracle as written (oracle.cta_sys_aswitching: the kron-materialised 
 stacked over the away rows, explicit inverse), Cholesky branch and the QR branch of :82-93
 (CCMM_FORCE_QR=1: host Householder QR of Kailath's array with the same two-matrix map).
 Tolerance: |delta| / max(|x|, sd_post) < 1e-9."""
-import os
 
 import numpy as np
 import pytest
@@ -56,11 +55,8 @@ def test_cta_aswitching(ctx, oracle):
 
 
 def test_cta_aswitching_qr_branch(ctx, oracle):
-    os.environ["CCMM_FORCE_QR"] = "1"
-    try:
+    with ctx.options(force_qr=1):
         _check(ctx, oracle, True)
-    finally:
-        del os.environ["CCMM_FORCE_QR"]
 
 
 def test_cta_aswitching_all_away_equals_ctasys(ctx, oracle):

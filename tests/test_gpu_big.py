@@ -2,10 +2,9 @@
 Gram, per-system blocked Cholesky, per-chain sequential solve; CTA.m:57-98 /
 CTAsys.m:57-108) against the oracle (as written: kron-materialised X_j, explicit inverse).
 
-The large path serves K > 512 or N > 32 (the S120 configuration); CCMM_FORCE_BIG=1 routes
+The large path serves K > 512 or N > 32 (the S120 configuration); option large_path = 1 routes
 the N = 20 / K = 241 shapes through it too, so it is checked on the same cases as the
 lag-structured path.  Tolerance: |Δ| / max(|x|, sd_post) as tests/test_gpu_parity.py."""
-import os
 
 import numpy as np
 import pytest
@@ -17,10 +16,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture
-def force_big():
-    os.environ["CCMM_FORCE_BIG"] = "1"
-    yield
-    del os.environ["CCMM_FORCE_BIG"]
+def force_big(ctx):
+    with ctx.options(large_path=1):  # the block-level calls and the chain sets created in the test
+        yield
 
 
 def _cta(oracle, ctx, su, sts, rng, XX=None):

@@ -2,8 +2,7 @@
 explicit inverse factor as CTA.m:77) against the generic-X path (ccmm_gram_chol.hip +
 ccmm_cta_solve.hip) and against the oracle, on the same common random numbers.
 
-The generic path is selected with CCMM_NO_LAG=1 (read when a chain set is created)."""
-import os
+The generic path is selected with the chain set's option lag = 0."""
 
 import numpy as np
 import pytest
@@ -19,12 +18,7 @@ def _run_linear(pkg, ctx, oracle, su, m, B, nsweeps, no_lag, seed=21):
     rng = np.random.default_rng(seed)
     crns = [[oracle.draw_crn(rng, su.N, su.K, su.T, su.dPHI) for _ in range(nsweeps)]
             for _ in range(B)]
-    if no_lag:
-        os.environ["CCMM_NO_LAG"] = "1"
-    try:
-        ch = pkg.Chains(ctx, N=su.N, p=su.p, T=su.T, B=B, crn=True)
-    finally:
-        os.environ.pop("CCMM_NO_LAG", None)
+    ch = pkg.Chains(ctx, N=su.N, p=su.p, T=su.T, B=B, crn=True, options={"lag": 0 if no_lag else 1})
     ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
     ch.set_state(*[np.stack([s[k] for s in sts], -1) for k in ("PAI", "A", "sqrtht", "h",
                                                                "sqrtPHI")])

@@ -97,7 +97,7 @@ def _run(pkg, ctx, oracle, fred, g, kind, B=128, burn=1000, keep=2000, chunk=50,
         ps = ch.get_ps()
         acc = float((ps["countAccept"].sum() + ps["countAcceptBurnin"].sum()) / (B * (burn + keep - burn // 2)))
     ch.close()
-    assert not np.any(status & ~1), status
+    assert not np.any(status & ~65), status
     return sums / keep, acc                                                # nq x B chain means
 
 

@@ -266,17 +266,16 @@ def test_ps_hybrid_toy(pkg, ctx, oracle, bh):
 @pytest.mark.parametrize("window", ["real", "toy"])
 def test_ps_chol_register_window_matches_lds_kernel(pkg, ctx, oracle, bh, fred, monkeypatch, window):
     """k_ps_chol_w (register window, one wave, W <= 64) against the first-generation k_ps_chol
-    (CCMM_PS_CHOL_V1=1): the same band factor and forward solve in the same per-entry order, so the
+    (option ps_chol_lds = 1): the same band factor and forward solve in the same per-entry order, so the
     PS centre, the accepted proposals and the shadow rates of a Philox run are identical."""
     bs = _real_bs(bh, oracle, fred) if window == "real" else _toy_bs(bh, (80, 120))
     lin = bs.lin
     B, nsw = 4, 3
     outs = []
-    for v1 in ("1", "0"):
-        monkeypatch.setenv("CCMM_PS_CHOL_V1", v1)
+    for v1 in (1, 0):
         ch = pkg.Chains(ctx, N=lin.N, p=lin.p, T=lin.T, B=B, crn=False, model=pkg.MODEL_BLOCKHYBRID,
                         Ns=len(bs.ndxS), elbTmax=bs.elbT, elb_gibbsburn=bs.gibbsburn, elb=bs.ELB,
-                        store_capacity=nsw, seed=1234)
+                        store_capacity=nsw, seed=1234, options={"ps_chol_lds": v1})
         ch.set_data(0, lin.Y, lin.X, lin.iVdiag, lin.iVb, lin.sPHI, lin.Vol_0mean, lin.Vol_0vcvsqrt)
         ch.set_elb_model(bs.ndxS, bs.actualrateBlock)
         ch.set_elb_slot(0, bs.elbT0, bs.sNaN)

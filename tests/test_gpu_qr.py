@@ -6,7 +6,6 @@ CCMM_FORCE_QR=1 sends every chain through that branch, so the test compares it w
 oracle's QR branch (oracle.cta(..., force_qr=True): numpy/LAPACK QR of the kron-stacked
 matrix, exactly as CTA.m:87).  Tolerance: |delta| / max(|x|, sd_post) < 1e-9.  A system
 whose QR factor is itself singular returns CCMM_ERR_NOTSPD."""
-import os
 
 import numpy as np
 import pytest
@@ -18,10 +17,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture
-def force_qr():
-    os.environ["CCMM_FORCE_QR"] = "1"
-    yield
-    del os.environ["CCMM_FORCE_QR"]
+def force_qr(ctx):
+    with ctx.options(force_qr=1):  # every chain through the host QR branch (chain sets inherit it)
+        yield
 
 
 def test_cta_qr_branch(ctx, oracle, force_qr):

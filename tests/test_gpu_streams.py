@@ -1,8 +1,8 @@
 """Schedules of the block-hybrid sweep that must not change a bit: the PHI block on the auxiliary
-stream beside the ELB step (the default) against plain stream order (CCMM_PHI_OVERLAP=0) -- the two
+stream beside the ELB step (the default) against plain stream order (option phi_overlap = 0) -- the two
 blocks touch disjoint state -- and the lag-structured CTA solve on two workgroups per chain (the
-default at small B) against one (CCMM_SOLVE_SPLIT=0), and the forecast paths with the coefficients in
-registers (the default for N <= 21) against PAI staged in LDS (CCMM_FCST_REG=0) -- every sum in the
+default at small B) against one (option solve_split = 0), and the forecast paths with the coefficients in
+registers (the default for N <= 21) against PAI staged in LDS (option fcst_reg = 0) -- every sum in the
 same order.  Every draw, the shadow rates, the forecasts and the status words are identical."""
 import numpy as np
 import pytest
@@ -10,9 +10,9 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("var,B", [("CCMM_PHI_OVERLAP", 8), ("CCMM_SOLVE_SPLIT", 8), ("CCMM_SOLVE_SPLIT", 1),
-                                        ("CCMM_FCST_REG", 8)])
-def test_schedule_bit_identical(pkg, ctx, fred, monkeypatch, var, B):
+@pytest.mark.parametrize("var,B", [("phi_overlap", 8), ("solve_split", 8), ("solve_split", 1),
+                                   ("fcst_reg", 8)])
+def test_schedule_bit_identical(pkg, ctx, fred, var, B):
     d = fred
     p = 12
     mpm = pkg.model.setMinnesotaMean(d["ncode"])
@@ -25,10 +25,10 @@ def test_schedule_bit_identical(pkg, ctx, fred, monkeypatch, var, B):
     yreal = pkg.samplers.realized_values(d["data"], len(d["ydates"]) - 1, 12, ndxS, 0.25)
     nsw = 4
     outs = []
-    for ov in ("0", "1"):
-        monkeypatch.setenv(var, ov)
+    for ov in (0, 1):
         ch = pkg.Chains(ctx, N=m.N, p=p, T=m.T, B=B, crn=False, store_capacity=nsw, seed=77,
-                        model=pkg.MODEL_BLOCKHYBRID, Ns=len(bm.ndxS), elbTmax=bm.elbT, elb_gibbsburn=20, elb=0.25)
+                        model=pkg.MODEL_BLOCKHYBRID, Ns=len(bm.ndxS), elbTmax=bm.elbT, elb_gibbsburn=20, elb=0.25,
+                        options={var: ov})
         ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
         ch.set_elb_model(bm.ndxS, bm.actual_block)
         ch.set_elb_slot(0, bm.elbT0, bm.sNaN)

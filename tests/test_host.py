@@ -1,6 +1,7 @@
 """CPU tests of the host side: the C-ABI library loads and exports every symbol
 include/ccmm.h declares; host-only entry points behave; the host model setup
 (ccmm_amd.model, mirror of mcmcVAR.m:28-206) equals the oracle's restatement."""
+import os
 import re
 from pathlib import Path
 
@@ -27,7 +28,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_host_entry_points(pkg):
     lib = pkg.load_library()
-    assert lib.ccmm_abi_version() == 3
+    assert lib.ccmm_abi_version() == 4 == pkg._abi.ABI_VERSION
     # the ChainConfig ctypes mirror has the header's fields in order
     src = (ROOT / "include" / "ccmm.h").read_text()
     start = src.index("typedef struct {", src.index("sweep-level")) + len("typedef struct {")
@@ -183,7 +184,40 @@ def test_psrf_entry_points_match_oracle(pkg):
 
 
 ABLATION_VARS = ("CCMM_CHOL_SKIP", "CCMM_SOLVE_SKIP", "CCMM_SV_SKIP", "CCMM_GC_MODE", "CCMM_LAG_MODE",
-                 "CCMM_BIG_MASK", "CCMM_ELB_MODE", "CCMM_SV_MODE", "CCMM_FCST_MODE")
+                 "CCMM_BIG_MASK", "CCMM_ELB_MODE", "CCMM_SV_MODE", "CCMM_FCST_MODE", "CCMM_POISON")
+# the kernel A/B switches of round 5 and every schedule selector: a default build
+# reads none of them (kernel forms and schedules are explicit options, ccmm_set_option)
+SELECTOR_VARS = {"CCMM_OLD_SOLVE": None, "CCMM_OLD_CHOL": None, "CCMM_GC18": None, "CCMM_NO_LAG": None,
+                 "CCMM_NO_QR_FALLBACK": None, "CCMM_SOLVE_WAVES": None,
+                 "CCMM_ASTEP_V1": ("astep_serial", 0), "CCMM_PS_CHOL_V1": ("ps_chol_lds", 0),
+                 "CCMM_FORCE_BIG": ("large_path", 0), "CCMM_SV_MFMA": ("sv_mfma", 1),
+                 "CCMM_SOLVE_SPLIT": ("solve_split", -1), "CCMM_SOLVE_ASYNC": ("solve_async", 1),
+                 "CCMM_SV_NWG": ("sv_nwg", 0), "CCMM_ELB_WAVES": ("elb_waves", 8), "CCMM_ELB_OCT": ("elb_oct", 1),
+                 "CCMM_ELB_ASYNC": ("elb_async", 1), "CCMM_ELB_PARTS": ("elb_parts", 0),
+                 "CCMM_FCST_REG": ("fcst_reg", 1), "CCMM_PHI_OVERLAP": ("phi_overlap", 1),
+                 "CCMM_QR_FALLBACK": ("qr_fallback", 1), "CCMM_LAG": ("lag", 1), "CCMM_FORCE_QR": ("force_qr", 0),
+                 "CCMM_GIRF_GENERIC": ("girf_generic", 0)}
+
+
+def test_default_build_ignores_every_selector(pkg, monkeypatch):
+    """No CCMM_* variable changes what the default library runs: with every A/B switch and schedule
+    selector set (to a non-default value), each option still starts from its built-in default, and
+    ccmm_env_ignored names every variable."""
+    lib = pkg.load_library()
+    assert lib.ccmm_ablation_build() == 0
+    for v in list(SELECTOR_VARS) + list(ABLATION_VARS):
+        monkeypatch.delenv(v, raising=False)
+    assert pkg._abi.env_ignored() == (0, [])
+    for v, o in SELECTOR_VARS.items():
+        monkeypatch.setenv(v, "0" if o is not None and o[1] == 1 else "1")
+    n, names = pkg._abi.env_ignored()
+    assert n == len(SELECTOR_VARS) and sorted(names) == sorted(SELECTOR_VARS), names
+    opts = set(pkg._abi.option_names())
+    for v, o in SELECTOR_VARS.items():
+        if o is not None:
+            assert o[0] in opts
+            assert pkg._abi.option_default(o[0]) == o[1], (v, o)
+    assert opts == {o[0] for o in SELECTOR_VARS.values() if o is not None}
 
 
 def test_default_build_ignores_timing_ablations(pkg, monkeypatch):
@@ -198,19 +232,25 @@ def test_default_build_ignores_timing_ablations(pkg, monkeypatch):
         monkeypatch.setenv(v, "1")
     n, names = pkg._abi.env_ignored()
     assert n == len(ABLATION_VARS) and sorted(names) == sorted(ABLATION_VARS)
-    # CCMM_SV_MODE bit 128 is a selector (full-row SV block factors, same draws): honoured, not reported
+    # CCMM_SV_MODE bit 128 (full-row SV block factors) is read by the ablation build only, like the rest
     monkeypatch.setenv("CCMM_SV_MODE", "128")
     n, names = pkg._abi.env_ignored()
-    assert "CCMM_SV_MODE" not in names and n == len(ABLATION_VARS) - 1
+    assert "CCMM_SV_MODE" in names and n == len(ABLATION_VARS)
 
 
-def test_ablation_build_honours_switches(monkeypatch):
-    """libccmm_ablation.so (make ablation), when built, reports ablation mode and ignores nothing."""
-    import ctypes
+def test_ablation_build_honours_switches():
+    """libccmm_ablation.so (make ablation), when built, reports ablation mode, ignores nothing and takes
+    an option's default from its CCMM_* variable (checked in a child process: the timing build is never
+    loaded beside the product library)."""
+    import subprocess
+    import sys
     p = ROOT / "ccmmshadowratevar-code_amd" / "csrc" / "libccmm_ablation.so"
     if not p.exists():
         pytest.skip("libccmm_ablation.so not built")
-    lib = ctypes.CDLL(str(p))
-    monkeypatch.setenv("CCMM_CHOL_SKIP", "1")
-    assert lib.ccmm_ablation_build() == 1
-    assert lib.ccmm_env_ignored(None, 0) == 0
+    code = ("import ctypes, sys; lib = ctypes.CDLL(sys.argv[1]); v = ctypes.c_int(0); "
+            "lib.ccmm_option_default(b'elb_waves', ctypes.byref(v)); "
+            "print(lib.ccmm_ablation_build(), lib.ccmm_env_ignored(None, 0), v.value)")
+    env = dict(os.environ, CCMM_CHOL_SKIP="1", CCMM_ELB_WAVES="4")
+    out = subprocess.run([sys.executable, "-c", code, str(p)], env=env, capture_output=True, text=True,
+                         check=True, timeout=120).stdout.split()
+    assert out == ["1", "0", "4"], out

@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Kernel times of the OOS per-rank floor (bench.py bench_oos floor=True: the longest vintage,
 thisT = 762, 1 chain) for each ELB phase (Gibbs burn-in, PS burn-in, kept sweeps):
-python tools/probe_floor.py [steps].  Timing-only; CCMM_* switches are read from the env."""
+python tools/probe_floor.py [steps] [option=value ...] (kernel options, ccmm_set_option).  Timing-only.
+Without wall-clock profiling events ("noprof" as an option) the sweep time is the event-free wall time."""
 import json
 import sys
 import time
@@ -26,6 +27,13 @@ def main():
     e0 = pkg.model.elbT0_of(d["data"], ndxS, 0.25, p)
     u1 = S._bh_units(d["data"], d["ydates"], [Tj[-1]], p, 12, ndxS, ndxO, mpm, 0.25, e0, True, 48)
     ctx = pkg.Context(0)
+    noprof = False
+    for kv in sys.argv[2:]:
+        if kv == "noprof":
+            noprof = True
+            continue
+        k, v = kv.split("=")
+        ctx.set_option(k, int(v))
     ch, _, _ = S._bh_chain_set(ctx, u1, 1, seed=1012023, ids=np.array([0], np.uint32),
                                store_capacity=steps + 1, gibbsburn=100, ELBbound=0.25, ndxYIELDS=ndxY,
                                fcstNhorizons=48, Nd=10)
@@ -35,7 +43,7 @@ def main():
     ch.get_draws()
     out = {}
     for name, store in (("gibbs", False), ("ps", False), ("kept", True)):
-        ch.profile(True)
+        ch.profile(not noprof)
         ctx.synchronize()
         t0 = time.perf_counter()
         ch.sweep(steps, store=store)
