@@ -929,7 +929,7 @@ def _physical_cores():
     return len(phys) or None
 
 
-def _cpp_line(budget_s, workers, model="linear"):
+def _cpp_line(budget_s, workers, model="linear", form="kron"):
     """The compiled restatement (oracle/cpu_sweep.cpp), `workers` single-thread processes at once, one chain
     each (parfor), real data T = 750, the reference initialisation: model "linear" = the sweep of
     mcmcVAR.m:211-274 as written (kron-materialised CTA, explicit inverse); "blockhybrid" = the sweep of
@@ -956,7 +956,10 @@ def _cpp_line(budget_s, workers, model="linear"):
             su = O.var_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], mpm, True)
             CB.write_state(sp, su, O.init_state(su))
             what = "the linear sweep as written (CTA.m kron form, explicit inverse)"
-        procs = [CB.bench_process(sp, budget_s, 1000 + w) for w in range(workers)]
+        if form == "syrk":
+            what = what.replace("kron form", "algorithmic weighted-SYRK form").replace(
+                "as written", "in the algorithmic form").replace(", explicit inverse", ", Cholesky + triangular solves")
+        procs = [CB.bench_process(sp, budget_s, 1000 + w, form=form) for w in range(workers)]
         res = [CB.bench_result(p_, budget_s * 20 + 300) for p_ in procs]
     value = sum(n / el for n, el in res)
     nsw = sum(n for n, _ in res)
@@ -966,6 +969,97 @@ def _cpp_line(budget_s, workers, model="linear"):
             "sample": f"{nsw} sweeps: {workers} single-thread processes (parfor-style, one chain each) x "
                       f"~{budget_s:.0f} s of oracle/cpu_sweep.cpp, {what}, in C++ on OpenBLAS "
                       f"{CB.blas_path().rsplit('/', 1)[-1]}"}
+
+
+def _cpp_oos_line(budget_s, workers, nsample=4):
+    """configs[3] on the host: the 164 single-chain vintage units of the OOS run
+    (goVARshadowrateBlockHybrid.m:258-303, one chain per vintage, 1000 + 1000 sweeps) as the compiled
+    block-hybrid restatement as written (oracle/cpu_sweep.cpp, kron CTAsys, QR gibbsdrawShadowrates with 101
+    Gibbs passes every sweep).  Measured: the per-sweep time of `nsample` vintages spread over the jump-offs
+    (T = 587..750, 2..109 censored months), `workers` processes at once; projected: the per-sweep cost
+    a T + e n_cens fitted to them (non-negative least squares), 2000 sweeps per vintage, the 164 units
+    LPT-packed on `workers` single-thread workers (parfor).  The PS branch and the forecasts of the
+    reference schedule are not restated on the host (every sweep runs the Gibbs ELB step, no forecast
+    block), so this is the CPU time of the sweeps only."""
+    import sys as _s
+    import tempfile
+    _s.path.insert(0, str(ROOT))
+    from scipy.optimize import nnls
+
+    from oracle import ccmm_oracle as O
+    from oracle import ccmm_oracle_bh as BH
+    from oracle import cpu_baseline as CB
+    fred = O.load_fred_csv(ROOT / "tests/golden/data/fredblockMD20-2022-09.csv")
+    mpm = O.set_minnesota_mean(fred["ncode"])
+    ndxS, ndxO, _ = O.set_shadow_yields(fred["ncode"], 0.25)
+    e0 = O.elb_t0(fred["data"], ndxS, 0.25, 12)
+    yd = np.asarray(fred["ydates"], float)
+    dec2008 = 733743.0  # datenum(2008, 12, 1)
+    Tj = [int(t) for t in (np.flatnonzero(yd > dec2008) + 1)]
+    feats = []
+    for thisT in Tj:  # (T, censored months) of every vintage
+        bs = BH.bh_setup(thisT, 12, 12, fred["data"], fred["ydates"], ndxS, ndxO, mpm, 0.25, e0)
+        feats.append((bs.lin.T, int(np.count_nonzero(np.any(bs.sNaN, axis=0)))))
+    pick = sorted({int(round(x)) for x in np.linspace(0, len(Tj) - 1, nsample)})
+    per = max(1, workers // len(pick))
+    costs = []
+    with tempfile.TemporaryDirectory() as td:
+        procs = []
+        for q in pick:
+            bs = BH.bh_setup(Tj[q], 12, 12, fred["data"], fred["ydates"], ndxS, ndxO, mpm, 0.25, e0)
+            sp = Path(td) / f"state{q}.bin"
+            CB.write_state(sp, bs.lin, BH.bh_init_state(bs), bs)
+            procs.append([CB.bench_process(sp, budget_s, 2000 + 10 * q + w) for w in range(per)])
+        for q, ps in zip(pick, procs):
+            res = [CB.bench_result(p_, budget_s * 20 + 300) for p_ in ps]
+            costs.append(sum(el for _, el in res) / sum(n for n, _ in res))
+    F = np.array([feats[q] for q in pick], float)
+    coef, _ = nnls(F, np.array(costs))
+    unit = np.array(feats, float) @ coef * 2000.0  # seconds per vintage unit (2000 sweeps)
+    loads = np.zeros(workers)
+    for u in sorted(unit, reverse=True):  # LPT over the parfor workers
+        loads[np.argmin(loads)] += u
+    wall = float(loads.max())
+    return {"value": round(len(Tj) * 2000 / wall, 4), "unit": "sweeps/s", "cores": workers, "kind": "port",
+            "workload": f"configs[3]: {len(Tj)} vintages x 1 chain x 2000 sweeps (Gibbs ELB step every sweep)",
+            "projected_full_run_s": round(wall, 1), "projected": True,
+            "per_sweep_s_measured": {f"thisT={Tj[q]} (T={feats[q][0]}, n_cens={feats[q][1]})": round(c, 5)
+                                     for q, c in zip(pick, costs)},
+            "fit_s_per_sweep": {"per_month_of_data": float(coef[0]), "per_censored_month": float(coef[1])},
+            "sample": f"{len(pick)} vintages x {per} single-thread processes x ~{budget_s:.0f} s of "
+                      f"oracle/cpu_sweep.cpp (block-hybrid sweep as written), the rest projected by the fit; "
+                      f"the 164 units LPT-packed on {workers} workers; no PS branch, no forecast block"}
+
+
+def _cpp_s120_line(budget_s, workers):
+    """configs[4] (S120: N = 120, p = 12, K = 1441, T = 750, Ns = 4) on the host: oracle/cpu_sweep.cpp's
+    block-hybrid sweep with CTAsys in the algorithmic weighted-SYRK form (the kron form would materialise
+    T (N - j + 1) x K = up to 1 GB per equation and ~11 TFLOP of CTA per sweep), `workers` processes of one
+    chain each, at least one sweep each; gibbsdrawShadowrates as written (QR smoothing weights)."""
+    import sys as _s
+    import tempfile
+    _s.path.insert(0, str(ROOT))
+    from oracle import ccmm_oracle as O
+    from oracle import ccmm_oracle_bh as BH
+    from oracle import cpu_baseline as CB
+    import __graft_entry__ as ge
+    d = ge.load_package().synthetic.s120()
+    ndxS, ndxO, _ = O.set_shadow_yields(d["ncode"], 0.25)
+    e0 = O.elb_t0(d["data"], ndxS, 0.25, 12)
+    bs = BH.bh_setup(len(d["ydates"]), 12, 12, d["data"], d["ydates"], ndxS, ndxO, np.ones(d["data"].shape[1]),
+                     0.25, e0)
+    with tempfile.TemporaryDirectory() as td:
+        sp = Path(td) / "s120.bin"
+        CB.write_state(sp, bs.lin, BH.bh_init_state(bs), bs)
+        procs = [CB.bench_process(sp, budget_s, 3000 + w, form="syrk") for w in range(workers)]
+        res = [CB.bench_result(p_, budget_s * 40 + 900) for p_ in procs]
+    value = sum(n / el for n, el in res)
+    nsw = sum(n for n, _ in res)
+    return {"value": round(value, 5), "unit": "sweeps/s", "cores": workers, "kind": "port",
+            "workload": "configs[4] S120 block hybrid, N = 120, K = 1441, T = 750, Ns = 4, elbT = 114",
+            "s_per_sweep_per_process": round(sum(el for _, el in res) / nsw, 2),
+            "sample": f"{nsw} sweeps: {workers} single-thread processes x >= 1 sweep of oracle/cpu_sweep.cpp "
+                      f"(CTAsys in the weighted-SYRK form, gibbsdrawShadowrates as written), OpenBLAS"}
 
 
 def cpu_baseline(budget_s, workers=0):
@@ -1017,8 +1111,13 @@ def cpu_baseline(budget_s, workers=0):
     if ncore:
         bh["all_host_cores"] = {"value": round(bh["per_core"] * ncore, 3), "unit": "sweeps/s", "cores": ncore,
                                 "projected": True, "method": "measured per-core rate x physical cores"}
+    bh_syrk = _cpp_line(budget_s, workers, model="blockhybrid", form="syrk")
+    bh_syrk["sample"] += f", CPU {cpu}"
     lin["lines"] = {
         "blockhybrid_cpp": bh,
+        "blockhybrid_cpp_syrk": bh_syrk,
+        "oos_configs3_cpp": _cpp_oos_line(max(3.0, budget_s / 2), workers),
+        "s120_cpp_syrk": _cpp_s120_line(1.0, workers),
         "linear_numpy": _cpu_line("linear-syrk", max(2.0, budget_s / 3), workers,
                                   "linear sweep, algorithmic CTA (weighted SYRK + Cholesky + "
                                   "triangular solves) in numpy, " + env),

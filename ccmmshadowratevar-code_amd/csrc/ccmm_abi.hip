@@ -655,6 +655,7 @@ struct ccmm_chains {
   const double* elb_yhat = nullptr;  // ccmm_gibbs_shadowrates: explicit YHAT0
   int elb_b3 = 0;                    // ccmm_gibbs_shadowrates_b3: no Y0 path, intercept in the state
   const double* elb_Amon = nullptr;  // ccmm_gibbs_shadowrates_b3: per-month structural matrices
+  int elb_Afull = 0;                 // ccmm_gibbs_shadowrates*: A = inverse of a general impact matrix
   uint8_t* elb_flags = nullptr;      // drawTruncNormal branch flags of the last ELB step (or nullptr)
   DBuf<uint8_t> dElbFlags;
   ElbDev elb_view() const {
@@ -689,6 +690,7 @@ struct ccmm_chains {
     e.psFlag = nullptr;
     e.b3 = elb_b3;
     e.Amon = elb_Amon;
+    e.Afull = elb_Afull;
     return e;
   }
 
@@ -2640,28 +2642,68 @@ static int gibbs_shadowrates_impl(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns
     // state: PAI = C(2:Ny+1, :)' (elb.A rows, :404-407), A = Psi(2:Ny+1, :) \ I, sqrtht = SVol'
     std::vector<double> PAI((size_t)K * Ny * B), A((size_t)Ny * Ny * B, 0.0), sh((size_t)T * Ny * B),
         hh((size_t)T * Ny * B), sq((size_t)Ny * Ny * B, 0.0);
-    // A = Psi(2:Ny+1, :) \ I by forward substitution with the lower triangle (B3 with a 3-D B: per month)
-    auto inv_lower = [&](const double* Pc, double* Ac) {
-      for (int col = 0; col < Ny; ++col)
-        for (int r = col; r < Ny; ++r) {
-          double v = (r == col) ? 1.0 : 0.0;
-          for (int q = col; q < r; ++q) v -= Pc[(1 + r) + (size_t)q * K] * Ac[q + (size_t)col * Ny];
-          Ac[r + (size_t)col * Ny] = v / Pc[(1 + r) + (size_t)r * K];
-        }
-    };
+    // A = Psi(2:Ny+1, :) \ I: forward substitution when the impact matrix is lower triangular (every
+    // reference caller passes invA, mcmcVARshadowrateBlockHybrid.m:418); otherwise Gauss-Jordan with
+    // partial pivoting, and the ELB kernels take the full structural matrix (gibbsdrawShadowrates.m:49-58,
+    // 74-95 QR-factor M = Cpowerp Psi diag(SVol) for any Psi: the same conditionals)
     const int nPsi = psi3d ? T : 1;
-    for (int c = 0; c < B; ++c)  // the structural form needs a lower-triangular impact matrix
-      for (int m = 0; m < nPsi; ++m) {
+    bool lower = true;
+    for (int c = 0; c < B && lower; ++c)
+      for (int m = 0; m < nPsi && lower; ++m) {
         const double* Pc = Psi + ((size_t)c * nPsi + m) * K * Ny;
-        for (int col = 1; col < Ny; ++col)
+        for (int col = 1; col < Ny && lower; ++col)
           for (int r = 0; r < col; ++r)
             if (Pc[(1 + r) + (size_t)col * K] != 0.0) {
-              g_err = std::string(b3 ? "ccmm_gibbs_shadowrates_b3: B" : "ccmm_gibbs_shadowrates: Psi") +
-                      "(2:Ny+1, :) must be lower triangular (the device evaluates the structural form A = its "
-                      "inverse; every reference caller passes invA)";
-              return CCMM_ERR_ARG;
+              lower = false;
+              break;
             }
       }
+    bool singular = false;
+    auto inv_struct = [&](const double* Pc, double* Ac) {
+      if (lower) {
+        for (int col = 0; col < Ny; ++col)
+          for (int r = col; r < Ny; ++r) {
+            double v = (r == col) ? 1.0 : 0.0;
+            for (int q = col; q < r; ++q) v -= Pc[(1 + r) + (size_t)q * K] * Ac[q + (size_t)col * Ny];
+            Ac[r + (size_t)col * Ny] = v / Pc[(1 + r) + (size_t)r * K];
+          }
+        return;
+      }
+      std::vector<double> M((size_t)Ny * Ny), I((size_t)Ny * Ny, 0.0);
+      for (int col = 0; col < Ny; ++col) {
+        I[col + (size_t)col * Ny] = 1.0;
+        for (int r = 0; r < Ny; ++r) M[r + (size_t)col * Ny] = Pc[(1 + r) + (size_t)col * K];
+      }
+      for (int col = 0; col < Ny; ++col) {
+        int piv = col;
+        for (int r = col + 1; r < Ny; ++r)
+          if (std::fabs(M[r + (size_t)col * Ny]) > std::fabs(M[piv + (size_t)col * Ny])) piv = r;
+        if (!(std::fabs(M[piv + (size_t)col * Ny]) > 0.0)) {
+          singular = true;
+          return;
+        }
+        if (piv != col)
+          for (int q = 0; q < Ny; ++q) {
+            std::swap(M[col + (size_t)q * Ny], M[piv + (size_t)q * Ny]);
+            std::swap(I[col + (size_t)q * Ny], I[piv + (size_t)q * Ny]);
+          }
+        const double ip = 1.0 / M[col + (size_t)col * Ny];
+        for (int q = 0; q < Ny; ++q) {
+          M[col + (size_t)q * Ny] *= ip;
+          I[col + (size_t)q * Ny] *= ip;
+        }
+        for (int r = 0; r < Ny; ++r) {
+          if (r == col) continue;
+          const double f = M[r + (size_t)col * Ny];
+          if (f == 0.0) continue;
+          for (int q = 0; q < Ny; ++q) {
+            M[r + (size_t)q * Ny] -= f * M[col + (size_t)q * Ny];
+            I[r + (size_t)q * Ny] -= f * I[col + (size_t)q * Ny];
+          }
+        }
+      }
+      std::copy(I.begin(), I.end(), Ac);
+    };
     std::vector<double> Am(psi3d ? (size_t)B * T * Ny * Ny : 0, 0.0);
     for (int c = 0; c < B; ++c) {
       const double* Cc = C + (size_t)c * KK;
@@ -2669,9 +2711,9 @@ static int gibbs_shadowrates_impl(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns
       for (int i = 0; i < Ny; ++i)
         for (int k = 0; k < K; ++k) PAI[((size_t)c * Ny + i) * K + k] = Cc[(1 + i) + (size_t)k * K];
       double* Ac = A.data() + (size_t)c * Ny * Ny;
-      inv_lower(Pc, Ac);
+      inv_struct(Pc, Ac);
       for (int m = 0; m < (psi3d ? T : 0); ++m)
-        inv_lower(Pc + (size_t)m * K * Ny, Am.data() + ((size_t)c * T + m) * Ny * Ny);
+        inv_struct(Pc + (size_t)m * K * Ny, Am.data() + ((size_t)c * T + m) * Ny * Ny);
       for (int i = 0; i < Ny; ++i) {
         sq[(size_t)c * Ny * Ny + i + (size_t)i * Ny] = 1.0;
         for (int t = 0; t < T; ++t) {
@@ -2681,6 +2723,12 @@ static int gibbs_shadowrates_impl(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns
         }
       }
     }
+    if (singular) {
+      g_err = std::string(b3 ? "ccmm_gibbs_shadowrates_b3: B" : "ccmm_gibbs_shadowrates: Psi") +
+              "(2:Ny+1, :) is singular";
+      return CCMM_ERR_ARG;
+    }
+    ch.elb_Afull = lower ? 0 : 1;
     ch.upload_KN(ch.PAI.p, B, PAI.data(), 0.0);
     HIPCHECK(hipMemcpy(ch.A.p, A.data(), A.size() * sizeof(double), hipMemcpyHostToDevice));
     ch.upload_TN(ch.sqrtht.p, B, T, sh.data(), 1.0);

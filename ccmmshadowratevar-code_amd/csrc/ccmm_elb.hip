@@ -60,6 +60,9 @@ struct ElbDev {
   // per window month, A_tau = B(2:Ny+1, :, tau)^-1 ([B][elbTmax][N][N], lower)
   int b3;
   const double* Amon;
+  // 1: the structural matrices A (cs.A / Amon) are full -- the inverse of a general impact matrix
+  // Psi(2:Ny+1, :) (ccmm_gibbs_shadowrates); 0: unit lower triangular (every sweep; invA's inverse)
+  int Afull;
 };
 
 // condition record per censored month (doubles):
@@ -292,19 +295,20 @@ __global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState c
         if (k == 0) {
           v = Ak[i + S[a] * N];
         } else {
-          for (int j = 0; j <= i; ++j) v = fma(Ak[i + j * N], PS[(j * p + k - 1) * Ns + a], v);
+          const int jend = e.Afull ? N - 1 : i;
+          for (int j = 0; j <= jend; ++j) v = fma(Ak[i + j * N], PS[(j * p + k - 1) * Ns + a], v);
         }
         w[a] = v * iv;
       }
       for (int a = 0; a < Ns; ++a) Wl[((size_t)kl * N + i) * Ns + a] = w[a];
     }
     __syncthreads();
-    // Q_k[a][j] = Σ_{i >= j} W_k[i][a] A(i,j)
+    // Q_k[a][j] = Σ_{i >= j} W_k[i][a] A(i,j)   (Σ over every i when A is full)
     for (int q = tid; q < (k1 - k0) * Ns * N; q += nth) {
       const int kl = q / (Ns * N), r = q - kl * Ns * N, a = r / N, j = r - a * N, k = k0 + kl;
       const double* Ak = A_of(k);
       double v = 0.0;
-      for (int i = j; i < N; ++i) v = fma(Wl[((size_t)kl * N + i) * Ns + a], Ak[i + j * N], v);
+      for (int i = e.Afull ? 0 : j; i < N; ++i) v = fma(Wl[((size_t)kl * N + i) * Ns + a], Ak[i + j * N], v);
       Q[((size_t)k * Ns + a) * N + j] = v;
     }
     __syncthreads();

@@ -191,11 +191,11 @@ int ccmm_phi_iw(ccmm_ctx* ctx, int B, int T, int N, const double* eta, const dou
  *                                        branches, as ccmm_draw_trunc_normal) or NULL
  * Ndraws must be 1 (the reference's only use).  Evaluated in the stable residual form of the
  * device ELB step (ccmm_elb.hip): the same conditional moments as the QR formulation of
- * gibbsdrawShadowrates.m:74-145 in exact arithmetic.  That form needs the structural matrix
- * A = Psi(2:Ny+1, :)^-1, so Psi(2:Ny+1, :) must be lower triangular (every reference caller passes
- * invA, mcmcVARshadowrateBlockHybrid.m:418; the QR form of the reference also takes a general
- * impact matrix): CCMM_ERR_ARG otherwise.  CCMM_ERR_DIM: sum(ndxS) != Ns
- * (gibbsdrawShadowrates.m:50-52). */
+ * gibbsdrawShadowrates.m:74-145 in exact arithmetic, on the structural matrix A = Psi(2:Ny+1, :)^-1.
+ * Any invertible impact matrix: a lower-triangular one (every reference caller passes invA,
+ * mcmcVARshadowrateBlockHybrid.m:418) by forward substitution, a general one by Gauss-Jordan with
+ * partial pivoting and the conditionals on the full A.  CCMM_ERR_ARG when Psi(2:Ny+1, :) is
+ * singular; CCMM_ERR_DIM: sum(ndxS) != Ns (gibbsdrawShadowrates.m:50-52). */
 int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p, const uint8_t* ndxS,
                            const uint8_t* sNaN, const double* Y, const double* STATE0,
                            const double* YHAT0, const double* C, const double* Psi, const double* SVol,
@@ -208,7 +208,7 @@ int ccmm_gibbs_shadowrates(ccmm_ctx* ctx, int B, int Ny, int elbT, int Ns, int p
  * STATE0, no deterministic Y0 path: :171-185) and an impact matrix that may vary by month.
  *   A      K x K x B (the companion with intercept)
  *   Bmat   K x Ny x elbT x B when B3d != 0 (B(:,:,t), :49-62), else K x Ny x B (repeated over t);
- *          rows 2..Ny+1 must be lower triangular (every caller's B = invA); CCMM_ERR_ARG otherwise
+ *          rows 2..Ny+1 any invertible matrix (as ccmm_gibbs_shadowrates' Psi; every caller's B = invA)
  * The other arguments as ccmm_gibbs_shadowrates (no YHAT0).  The reference's only caller
  * (mcmcVARshadowrateBlockHybridAelb.m:451-452, 469-470) passes 13 arguments to this 12-parameter
  * function and cannot run as shipped; this entry serves the function itself. */

@@ -61,7 +61,7 @@ def _env():
     return env
 
 
-def crn_sweep(su, st, crn, workdir, bs=None):
+def crn_sweep(su, st, crn, workdir, bs=None, form="kron"):
     """One sweep on the injected common random numbers (oracle.crn_sizes order; block hybrid: + uELB);
     returns the new PAI, A, sqrtht, h, sqrtPHI, the KSC indicators and (bs) the shadow rates."""
     ensure_built()
@@ -71,7 +71,8 @@ def crn_sweep(su, st, crn, workdir, bs=None):
     with open(cp, "wb") as fh:
         for k in ("zPAI", "zA", "uSV", "zSV", "zPHI") + (("uELB",) if bs is not None else ()):
             np.asfortranarray(crn[k], dtype=np.float64).ravel(order="F").tofile(fh)
-    subprocess.run([str(BIN), "crn", str(sp), str(cp), str(op)], check=True, env=_env(), capture_output=True)
+    mode = "crn" if form == "kron" else "crn-syrk"
+    subprocess.run([str(BIN), mode, str(sp), str(cp), str(op)], check=True, env=_env(), capture_output=True)
     v = np.fromfile(op, np.float64)
     N, K, T = su.N, su.K, su.T
     out, o = {}, 0
@@ -87,10 +88,12 @@ def crn_sweep(su, st, crn, workdir, bs=None):
     return out
 
 
-def bench_process(state_path, seconds, seed):
-    """Start one single-threaded worker process (the caller runs several at once); returns the Popen."""
+def bench_process(state_path, seconds, seed, form="kron"):
+    """Start one single-threaded worker process (the caller runs several at once); returns the Popen.
+    form: "kron" (CTA / CTAsys as written) or "syrk" (the algorithmic weighted-SYRK form)."""
     ensure_built()
-    return subprocess.Popen([str(BIN), "bench", str(state_path), f"{seconds:.3f}", str(int(seed))],
+    mode = "bench" if form == "kron" else "bench-syrk"
+    return subprocess.Popen([str(BIN), mode, str(state_path), f"{seconds:.3f}", str(int(seed))],
                             env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
 
 

@@ -23,9 +23,16 @@
 // Gibbs passes with drawTruncNormal.m's inverse CDF -- AS241 for -sqrt(2) erfcinv(2 u PHIbar)), and the
 // rebuild of X, Y from the shadow draws (:501-509).  Selected by the BH block of state.bin.
 //
+// Algorithmic form (modes bench-syrk / crn-syrk; BASELINE.md §2's second CPU line, SURVEY §8d "a second CPU
+// line with the algorithmic (SYRK) form keeps the comparison honest"): the CTA / CTAsys draw by the identity
+// X_j'X_j = X' diag(w) X, X_j'Y_j = X' v (w_t = sum_{i>=j} A(i,j)^2 / sqrtht(t,i)^2) -- one dsyrk of the
+// T x K design scaled by sqrt(w), dpotrf, and PAI(:,j) = L' \ (L \ rhs + z) by two dtrsv -- instead of the
+// kron-materialised T(N-j+1) x K array and the explicit inverse; every other block as above.
+//
 // Usage:
-//   cpu_sweep bench <state.bin> <seconds> <seed>      sweeps of one chain for `seconds`, JSON line out
-//   cpu_sweep crn <state.bin> <crn.bin> <out.bin>     one sweep on injected common random numbers
+//   cpu_sweep bench[-syrk] <state.bin> <seconds> <seed>   sweeps of one chain for `seconds` (at least one),
+//                                                          JSON line out
+//   cpu_sweep crn[-syrk] <state.bin> <crn.bin> <out.bin>  one sweep on injected common random numbers
 // state.bin: int32 N, K, T, dPHI, then doubles Y (T x N), X (T x K), iVdiag, iVb (K x N), sPHI (N x N),
 // h0mean (N), h0vcvsqrt (N x N), logy2offset, PAI (K x N), A (N x N), sqrtht (T x N), h (T x N),
 // sqrtPHI (N x N); all column-major; then optionally the BH block: int32 magic 0x31304842 ("BH01"), p,
@@ -212,6 +219,51 @@ void cta(const Model& m, State& s, const double* z, const std::vector<const doub
   }
 }
 
+// ---------------------------------------------------------------- the same draw, algorithmic form
+// L L' = iV + X' diag(w) X, rhs = iVb + X' v, PAI(:,j) = L' \ (L \ rhs + z): the draw of CTA.m:95-96 with
+// V = (L L')^-1 and Vchol = L^-T, without forming either
+void cta_syrk(const Model& m, State& s, const double* z, const std::vector<const double*>& Xs) {
+  const int N = m.N, K = m.K, T = m.T;
+  const double one = 1.0, zero = 0.0, mone = -1.0;
+  const int i1 = 1;
+  std::vector<double> E((size_t)T * N), Xw((size_t)T * K), G((size_t)K * K), w(T), v(T), rhs(K);
+  for (int j = 0; j < N; ++j) {
+    for (int k = 0; k < K; ++k) M2(s.PAI.data(), K, k, j) = 0.0;  // PAI(:,j) = 0 (:63)
+    E = m.Y;
+    for (int jj = 0; jj < N; ++jj)
+      dgemv("N", &T, &K, &mone, Xs[jj], &T, &M2(s.PAI.data(), K, 0, jj), &i1, &one, &E[(size_t)jj * T], &i1);
+    // w_t = sum_{i>=j} A(i,j)^2 / sqrtht(t,i)^2;  v_t = sum_{i>=j} A(i,j) (E A(i,:)')_t / sqrtht(t,i)^2
+    for (int t = 0; t < T; ++t) {
+      double wt = 0.0, vt = 0.0;
+      for (int i = j; i < N; ++i) {
+        const double a = M2(s.A.data(), N, i, j), h = M2(s.sqrtht.data(), T, t, i);
+        double ea = 0.0;
+        for (int q = 0; q <= i; ++q) ea += M2(E.data(), T, t, q) * M2(s.A.data(), N, i, q);
+        const double ih2 = 1.0 / (h * h);
+        wt += a * a * ih2;
+        vt += a * ea * ih2;
+      }
+      w[t] = wt;
+      v[t] = vt;
+    }
+    const double* X = Xs[j];
+    for (int k = 0; k < K; ++k)
+      for (int t = 0; t < T; ++t) Xw[(size_t)k * T + t] = X[(size_t)k * T + t] * std::sqrt(w[t]);
+    dsyrk("L", "T", &K, &T, &one, Xw.data(), &T, &zero, G.data(), &K);  // X' diag(w) X
+    for (int k = 0; k < K; ++k) M2(G.data(), K, k, k) += M2(m.iVdiag.data(), K, k, j);
+    int info = 0;
+    dpotrf("L", &K, G.data(), &K, &info);
+    if (info) throw std::runtime_error("CTA chol (the QR branch of CTA.m:80-92 is not restated here)");
+    for (int k = 0; k < K; ++k) rhs[k] = M2(m.iVb.data(), K, k, j);
+    dgemv("T", &T, &K, &one, X, &T, v.data(), &i1, &one, rhs.data(), &i1);  // iVb + X' v
+    dtrsv("L", "N", "N", &K, G.data(), &K, rhs.data(), &i1);                // L \ rhs
+    for (int k = 0; k < K; ++k) rhs[k] += z[(size_t)j * K + k];
+    dtrsv("L", "T", "N", &K, G.data(), &K, rhs.data(), &i1);                // L' \ (. + z)
+    for (int k = 0; k < K; ++k) M2(s.PAI.data(), K, k, j) = rhs[k];
+  }
+}
+bool g_syrk = false;  // modes bench-syrk / crn-syrk
+
 // ---------------------------------------------------------------- one sweep (mcmcVAR.m:228-274)
 void elb_step(Model& m, State& s, const Crn& r, const std::vector<double>& invA);
 void sweep(Model& m, State& s, const Crn& r, std::vector<double>* kai_out) {
@@ -223,7 +275,10 @@ void sweep(Model& m, State& s, const Crn& r, std::vector<double>* kai_out) {
   if (m.bh)
     for (int j = 0; j < N; ++j)
       if (m.actual[j]) Xs[j] = m.Xactual.data();
-  cta(m, s, r.zPAI.data(), Xs);
+  if (g_syrk)
+    cta_syrk(m, s, r.zPAI.data(), Xs);
+  else
+    cta(m, s, r.zPAI.data(), Xs);
   // RESID = Y - X*PAI (:233; block hybrid per equation, :350)
   std::vector<double> RESID = m.Y;
   for (int jj = 0; jj < N; ++jj)
@@ -757,14 +812,18 @@ void draw(const Model& m, std::mt19937_64& g, Crn& r) {
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    std::fprintf(stderr, "usage: cpu_sweep bench <state.bin> <seconds> <seed> | crn <state.bin> <crn.bin> <out.bin>\n");
+    std::fprintf(stderr, "usage: cpu_sweep bench[-syrk] <state.bin> <seconds> <seed> | crn[-syrk] <state.bin> <crn.bin> <out.bin>\n");
     return 2;
   }
   load_blas();
   Model m;
   State s;
   read_state(argv[2], m, s);
-  const std::string mode = argv[1];
+  std::string mode = argv[1];
+  if (mode.size() > 5 && mode.compare(mode.size() - 5, 5, "-syrk") == 0) {
+    g_syrk = true;
+    mode.resize(mode.size() - 5);
+  }
   try {
     if (mode == "bench") {
       const double budget = std::atof(argv[3]);

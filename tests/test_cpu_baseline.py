@@ -26,8 +26,10 @@ def _oracle_sweep(O, st, su, crn):
     return dict(PAI=PAI, A=A, h=h, sqrtht=np.exp(h / 2), sqrtPHI=sqrtPHI, kai=kai), sd
 
 
+@pytest.mark.parametrize("form", ["kron", "syrk"])
 @pytest.mark.parametrize("shape", ["toy", "real"])
-def test_cpu_sweep_matches_oracle(oracle, fred, tmp_path, shape):
+def test_cpu_sweep_matches_oracle(oracle, fred, tmp_path, shape, form):
+    """Both CPU lines: CTA as written (kron) and the algorithmic weighted-SYRK form (bench-syrk)."""
     from helpers import random_state
     from oracle import cpu_baseline as CB
     O = oracle
@@ -39,12 +41,12 @@ def test_cpu_sweep_matches_oracle(oracle, fred, tmp_path, shape):
         su = O.var_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], mpm, True)
     st = random_state(O, su, seed=5)
     crn = O.draw_crn(np.random.default_rng(6), su.N, su.K, su.T, su.dPHI)
-    got = CB.crn_sweep(su, st, crn, tmp_path)
+    got = CB.crn_sweep(su, st, crn, tmp_path, form=form)
     want, sd = _oracle_sweep(O, st, su, crn)
     np.testing.assert_array_equal(got["kai"], want["kai"])
     e = {"PAI": rel_err(got["PAI"], want["PAI"], sd), "A": rel_err(got["A"], want["A"], 1.0),
          "sqrtht": rel_err(got["sqrtht"], want["sqrtht"]), "sqrtPHI": rel_err(got["sqrtPHI"], want["sqrtPHI"], 1e-3)}
-    print(shape, e)
+    print(shape, form, e)
     assert max(e.values()) < 1e-7, e
 
 
@@ -87,8 +89,9 @@ def _oracle_bh_sweep(O, BH, st, bs, crn):
     return dict(PAI=PAI, A=A, h=h, sqrtht=sqrtht, sqrtPHI=sqrtPHI, kai=kai, shadowrate=sr), sd
 
 
+@pytest.mark.parametrize("form", ["kron", "syrk"])
 @pytest.mark.parametrize("shape", ["toy", "real"])
-def test_cpu_sweep_blockhybrid_matches_oracle(oracle, fred, tmp_path, shape):
+def test_cpu_sweep_blockhybrid_matches_oracle(oracle, fred, tmp_path, shape, form):
     """The compiled block-hybrid sweep (kron CTAsys, gibbsdrawShadowrates as written with dgeqrf, 101
     Gibbs passes) against the numpy oracle on the same common random numbers."""
     from helpers import random_state, synth_bh_data
@@ -112,13 +115,13 @@ def test_cpu_sweep_blockhybrid_matches_oracle(oracle, fred, tmp_path, shape):
         st = random_state(O, bs.lin, seed=9)   # (the reference initialisation's CTA sits at cond ~1e13)
     st["X"], st["Y"] = bs.lin.X.copy(), bs.lin.Y.copy()
     crn = BH.bh_draw_crn(np.random.default_rng(7), bs)
-    got = CB.crn_sweep(bs.lin, st, crn, tmp_path, bs)
+    got = CB.crn_sweep(bs.lin, st, crn, tmp_path, bs, form=form)
     want, sd = _oracle_bh_sweep(O, BH, st, bs, crn)
     np.testing.assert_array_equal(got["kai"], want["kai"])
     e = {"PAI": rel_err(got["PAI"], want["PAI"], sd), "A": rel_err(got["A"], want["A"], 1.0),
          "sqrtht": rel_err(got["sqrtht"], want["sqrtht"]), "sqrtPHI": rel_err(got["sqrtPHI"], want["sqrtPHI"], 1e-3),
          "shadowrate": rel_err(got["shadowrate"], want["shadowrate"], 0.1)}
-    print(shape, e)
+    print(shape, form, e)
     assert max(e.values()) < 1e-7, e
 
 
@@ -132,5 +135,6 @@ def test_cpu_sweep_blockhybrid_bench_mode(oracle, fred, tmp_path):
     bs = BH.bh_setup(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"], ndxS, ndxO, mpm, 0.25, e0)
     st = BH.bh_init_state(bs)
     CB.write_state(tmp_path / "s.bin", bs.lin, st, bs)
-    n, el = CB.bench_result(CB.bench_process(tmp_path / "s.bin", 0.5, 1), 120)
-    assert n >= 1 and el >= 0.5
+    for form in ("kron", "syrk"):
+        n, el = CB.bench_result(CB.bench_process(tmp_path / "s.bin", 0.5, 1, form=form), 120)
+        assert n >= 1 and el >= 0.5

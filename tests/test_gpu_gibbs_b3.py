@@ -60,9 +60,17 @@ def test_b3_matches_oracle(pkg, ctx, oracle, month_varying):
     np.testing.assert_array_equal(again, got[..., 0])
 
 
-def test_b3_rejects_non_triangular_B(ctx):
+def test_b3_dense_B_matches_oracle(ctx, oracle):
+    """A B(2:Ny+1, :) with an upper triangle (the function takes any impact matrix; its QR form factors
+    M = Cpowerp B diag(SVol), gibbsdrawShadowratesB3.m:49-62): the device inverts it by Gauss-Jordan and
+    runs the conditionals on the full structural matrix.  Flags bit-exact, draws within 1e-9."""
     Y, STATE0, ndxS, sNaN, p, A, Bm, SVol, u = _case(6, month_varying=False)
-    Bm[1, 2] = 0.1  # upper triangle of B(2:Ny+1, :)
-    with pytest.raises(RuntimeError, match="lower triangular"):
-        ctx.gibbs_shadowrates_b3(Y[..., None], STATE0[:, None], ndxS, sNaN, p, A[..., None], Bm[..., None],
-                                 SVol[..., None], 0.25, burnin=2, u=u[:, :, :3, None])
+    Bm[1:5, :] += np.triu(0.25 * np.random.default_rng(1).standard_normal((4, 4)), 1)
+    want, wfl = oracle.gibbsdraw_shadowrates_b3(Y, STATE0, ndxS, sNaN, p, A, Bm, SVol, 0.25, 1, 100, u,
+                                                return_flags=True)
+    got, fl = ctx.gibbs_shadowrates_b3(Y[..., None], STATE0[:, None], ndxS, sNaN, p, A[..., None], Bm[..., None],
+                                       SVol[..., None], 0.25, burnin=100, u=u[..., None], flags=True)
+    np.testing.assert_array_equal(fl[..., 0][sNaN[:, :, None].repeat(101, 2)], wfl[sNaN[:, :, None].repeat(101, 2)])
+    err = np.max(np.abs(got[:, :, 0, 0][sNaN] - want[:, :, 0][sNaN]))
+    print(f"dense B: max |draw - oracle| {err:.2e}")
+    assert err < 1e-9
