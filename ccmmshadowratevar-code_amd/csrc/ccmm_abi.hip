@@ -908,12 +908,16 @@ struct ccmm_chains {
     }
     rdiag.alloc((size_t)d.nmat * d.KP);
   }
+  static constexpr int kResidMultiMinB = 16;
   void run_resid() {
     ChainState cs = view();
     const int nb = d.N <= 8 ? 8 : (d.N <= 20 ? 20 : 32);
     const size_t lds = (size_t)d.K * nb * sizeof(double);
     launch(KID_RESID, [&] {
-      if (d.N <= 32 && lds <= 64 * 1024) {  // one pass per design slab (k_resid_multi)
+      // one pass per design slab (k_resid_multi) once the chains fill the chip; at small B the per-equation
+      // kernel's B N TP / 256 workgroups keep the slab loads in flight (0.12 -> ~0.01 ms at B = 1): the same
+      // fma order per equation, so E is bit-identical either way
+      if (d.N <= 32 && lds <= 64 * 1024 && d.B > kResidMultiMinB) {
         const dim3 g((d.TP + 255) / 256, d.B);
         if (nb == 8) hipLaunchKernelGGL(k_resid_multi<8>, g, dim3(256), lds, ctx->stream, d, Tslot.p, xsel(), cs);
         else if (nb == 20) hipLaunchKernelGGL(k_resid_multi<20>, g, dim3(256), lds, ctx->stream, d, Tslot.p, xsel(), cs);
@@ -1550,7 +1554,7 @@ struct ccmm_chains {
   do {                                                                                                        \
     HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs_mp<NS, WPC_, PT>,                                   \
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_mp));                   \
-    hipLaunchKernelGGL((k_elb_gibbs_mp<NS, WPC_, PT>), dim3(d.B, PT), dim3(64 * (WPC_ + 1)), lds_mp, ctx->stream, \
+    hipLaunchKernelGGL((k_elb_gibbs_mp<NS, WPC_, PT>), dim3(d.B, PT), dim3(64 * (WPC_ + 2)), lds_mp, ctx->stream, \
                        d, e, cs, ra, xc);                                                                     \
   } while (0)
 #define CASE_MP(NS)                    \
@@ -1634,7 +1638,7 @@ struct ccmm_chains {
     if (parts == 1) return 1;
     int cus = 0;
     HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    // one workgroup of <= 320 threads per part, <= 110 KB of LDS: at least one per CU is resident
+    // one workgroup of <= 384 threads per part, <= 110 KB of LDS: at least one per CU is resident
     return (d.B * parts <= cus) ? parts : 1;
   }
 

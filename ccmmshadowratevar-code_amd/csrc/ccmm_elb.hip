@@ -66,13 +66,14 @@ struct ElbDev {
 };
 
 // condition record per censored month (doubles):
-//   a_t [Ns] | beta1 [Ns][Ns-1] | sqrtOmega1 [Ns] | Ω [Ns][Ns] | G [2p Ns][Ns]
+//   a_t [Ns] | beta1 [Ns][Ns-1] | sqrtOmega1 [Ns] | 1 / sqrtOmega1 [Ns] | Ω [Ns][Ns] | G [2p Ns][Ns]
+// (1 / sqrtOmega1: the Gibbs kernels form ub = (elb - mu) / sig as a product, off the division's latency)
 // G column col = kk*Ns + s': kk < p past lag kk+1, kk >= p future lead kk-p+1.
 // With the PS branch (e.ps) the record continues (elb_cond_ps_off):
 //   P [Ns][Ns] (the month's precision, Ω^-1) | b_PS [Ns] | gP [p Ns][Ns]
 // b_PS = the PS model's linear term with every censored cell at 0; gP = the raw unit
 // responses of the past neighbours (-gP = the off-diagonal precision blocks).
-__host__ __device__ inline int elb_cond_head(int Ns) { return Ns + Ns * (Ns - 1) + Ns + Ns * Ns; }
+__host__ __device__ inline int elb_cond_head(int Ns) { return Ns + Ns * (Ns - 1) + 2 * Ns + Ns * Ns; }
 __host__ __device__ inline int elb_cond_ps_off(int Ns, int p) {
   return elb_cond_head(Ns) + 2 * p * Ns * Ns;
 }
@@ -386,7 +387,8 @@ __global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState c
   double* rec = e.cond + ((size_t)c * e.elbTmax + ci) * e.condStride;
   double* beta = rec + Ns;
   double* so = beta + Ns * (Ns - 1);
-  double* Orec = so + Ns;
+  double* iso = so + Ns;
+  double* Orec = iso + Ns;
   double* G = Orec + Ns * Ns;
   if (tid == 0) {
     double Pl[kElbNsMax * kElbNsMax], Oi[kElbNsMax * kElbNsMax];
@@ -424,6 +426,7 @@ __global__ __launch_bounds__(256) void k_elb_cond(Dims d, ElbDev e, ChainState c
       }
       so[a] = sqrt(var);
     }
+    for (int a = 0; a < Ns; ++a) iso[a] = 1.0 / so[a];
   }
   __syncthreads();
   // G = Ω g(unit); zero for uncensored or out-of-window neighbours
@@ -570,21 +573,42 @@ __device__ __forceinline__ double elb_trunc_normal(double mu, double sig, double
   return mu;
 }
 
+// The Gibbs kernels' draw: drawTruncNormal.m as elb_trunc_normal, with ub = (elb - mu) * isig from the
+// record's 1 / sig (k_elb_cond) instead of the division (a product: ~80 fewer clocks of dependent latency
+// per draw; ub may differ from the quotient in its last bit, the draws by rounding only).  Every Gibbs
+// kernel evaluates this same function, so their draws stay bit-identical to each other; the drop-in
+// drawTruncNormal (k_truncnorm, ccmm_draw_trunc_normal) keeps the quotient.
+__device__ __forceinline__ double elb_gibbs_trunc_normal(double mu, double sig, double isig, double elb, double u,
+                                                         uint8_t& fl) {
+#pragma clang fp contract(off)
+  const double tol = 1e-10;
+  const double eps = 2.220446049250313080847e-16;
+  fl = 0;
+  if (fabs(sig) > tol) {
+    const double ub = (elb - mu) * fabs(isig);
+    const double PHIbar = 0.5 * erfc(-0.70710678118654752440 * ub);
+    fl = (PHIbar > eps) ? 3 : 1;
+    const double z = (PHIbar > eps) ? elb_ppnd16(u * PHIbar) : ub;
+    return fma(fabs(sig), z, mu);
+  }
+  return mu;
+}
+
 // The same draw with zu = elb_ppnd16(u) computed beforehand (off the month-to-month path).  When
 // ub = (elb - mu) / sig >= 9, erfc(-ub / sqrt 2) = 2 - erfc(ub / sqrt 2) with erfc(6.36) ~ 1e-19, below
 // half an ulp of 2: PHIbar is exactly 1, u PHIbar = u, and the full evaluation returns mu + sig zu.  So
 // the draw is bit-identical without erfc and AS241 on the path (on the real window about half of the
 // draws: the conditional means sit far below the ELB, ub median 8.9).
 constexpr double kElbFastUb = 9.0;
-__device__ __forceinline__ double elb_trunc_normal_pz(double mu, double sig, double elb, double u, double zu,
-                                                      uint8_t& fl) {
+__device__ __forceinline__ double elb_trunc_normal_pz(double mu, double sig, double isig, double elb, double u,
+                                                      double zu, uint8_t& fl) {
 #pragma clang fp contract(off)
   const double as = fabs(sig);
-  if (as > 1e-10 && (elb - mu) / as >= kElbFastUb) {
+  if (as > 1e-10 && (elb - mu) * fabs(isig) >= kElbFastUb) {
     fl = 3;
     return fma(as, zu, mu);
   }
-  return elb_trunc_normal(mu, sig, elb, u, fl);
+  return elb_gibbs_trunc_normal(mu, sig, isig, elb, u, fl);
 }
 
 // timing-only ablation bits of ElbDev::mode (CCMM_ELB_MODE, read by the ablation build only; a
@@ -641,7 +665,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
   const int kk0 = c0 / NS, sp0 = c0 % NS, kk1 = c1 / NS, sp1 = c1 % NS;
   const int off0 = (kk0 < p) ? -(kk0 + 1) : (kk0 - p + 1);
   const int off1 = (kk1 < p) ? -(kk1 + 1) : (kk1 - p + 1);
-  constexpr int kHd = NS + NS * (NS - 1) + NS;
+  constexpr int kHd = NS + NS * (NS - 1) + 2 * NS;
   struct Rec {
     double hd[kHd], g0[NS], g1[NS];
   };
@@ -724,7 +748,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
         ++y;
       }
       uint8_t fl = 0;
-      cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
+      cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], so[NS + a], e.elb, u[a], zu[a], fl);
       if (e.flags && lane == 0)  // drawTruncNormal.m branch taken (oracle.draw_trunc_normal flags)
         e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
     }
@@ -820,7 +844,7 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
   const int kk0 = c0 / NS, sp0 = c0 % NS, kk1 = c1 / NS, sp1 = c1 % NS;
   const int off0 = (kk0 < p) ? -(kk0 + 1) : (kk0 - p + 1);
   const int off1 = (kk1 < p) ? -(kk1 + 1) : (kk1 - p + 1);
-  constexpr int kHd = NS + NS * (NS - 1) + NS;
+  constexpr int kHd = NS + NS * (NS - 1) + 2 * NS;
   struct Rec {
     double hd[kHd], g0[NS], g1[NS];
   };
@@ -924,7 +948,7 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
             ++y;
           }
           uint8_t fl = 0;
-          cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
+          cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], so[NS + a], e.elb, u[a], zu[a], fl);
           if (e.flags && lane == 0)
             e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
         }
@@ -1008,7 +1032,7 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
           ++y;
         }
         uint8_t fl = 0;
-        cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
+        cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_trunc_normal_pz(mu, so[a], so[NS + a], e.elb, u[a], zu[a], fl);
         if (e.flags && lane == 0)
           e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
       }
@@ -1031,12 +1055,14 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
 // run, goVARshadowrateBlockHybrid.m:258-303, runs 8 waves on one CU otherwise).  Pass n runs on global
 // wave n mod W (part = gw / WPC).  Every part keeps its own copy of the shadow rates in LDS.
 //   within a part: the waves hand off through LDS progress words exactly as k_elb_gibbs_wf;
-//   across parts: the last drawing wave of part j publishes every cell it draws as a 16-byte granule
-//   {value, tag = epoch 2^16 + pass + 1} with one write-through (sc1) store (the data is the flag; no
-//   fence), and an importer wave of part j + 1 (wave WPC) reads the granules of the censored months in
-//   order with sc1 loads, up to eight months per round trip, copies them into its part's LDS copy and
-//   publishes its progress in the predecessor's encoding, so wave 0 of part j + 1 waits on it as on a
-//   local predecessor.
+//   across parts: an exporter wave of part j (wave WPC + 1) follows the LDS progress of the part's last
+//   drawing wave and publishes every cell it has drawn as a 16-byte granule {value, tag = epoch 2^16 +
+//   pass + 1}, one write-through (sc1) store each (the data is the flag; no fence), up to eight months at
+//   a time; an importer wave of part j + 1 (wave WPC) reads the granules of the censored months in order
+//   with sc1 loads, up to eight months per round trip, copies them into its part's LDS copy and publishes
+//   its progress in the predecessor's encoding, so wave 0 of part j + 1 waits on it as on a local
+//   predecessor.  The drawing waves issue no global store: a write-through store's completion would
+//   hold the next month's record loads behind it (vmcnt counts both in order).
 // Why a copy can be refreshed late: in the one-copy kernel pass n overwrites month m only once every
 // earlier pass is done with it, and pass n + 1 reads it only after pass n has drawn past reach(m); the
 // import of pass n's value for m happens between those two events in the consumer part, so every read
@@ -1049,7 +1075,7 @@ struct ElbXch {
   unsigned long long epoch;    // launch counter (host): tags of older launches never match
 };
 template <int NS, int WPC, int PARTS>
-__global__ __launch_bounds__(64 * (WPC + 1)) void k_elb_gibbs_mp(Dims d, ElbDev e, ChainState cs, RngArgs ra,
+__global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev e, ChainState cs, RngArgs ra,
                                                                  ElbXch xc) {
   constexpr int W = WPC * PARTS;
   extern __shared__ double sm[];
@@ -1060,7 +1086,7 @@ __global__ __launch_bounds__(64 * (WPC + 1)) void k_elb_gibbs_mp(Dims d, ElbDev 
   if (nc == 0) return;
   if (e.psFlag && e.psFlag[c] > 0) return;  // a PS proposal was accepted (:453-454)
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // WPC = the importer
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // WPC: the importer, WPC + 1: the exporter
   const int gw = part * WPC + wave;
   const Rng rng = ra.make(c);
   const int ncol = 2 * p * NS;
@@ -1084,8 +1110,8 @@ __global__ __launch_bounds__(64 * (WPC + 1)) void k_elb_gibbs_mp(Dims d, ElbDev 
   char* gbase = (char*)(xc.gran) + (size_t)c * PARTS * gstride;
   const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(gbase, 0, (int)(PARTS * gstride), 0x00020000);
   const int gout = part * (int)gstride, gin = ((part + PARTS - 1) % PARTS) * (int)gstride;
-  for (int q = tid; q < T * NS; q += 64 * (WPC + 1)) Sl[q] = Sc[q];
-  for (int q = tid; q < nc; q += 64 * (WPC + 1)) {
+  for (int q = tid; q < T * NS; q += 64 * (WPC + 2)) Sl[q] = Sc[q];
+  for (int q = tid; q < nc; q += 64 * (WPC + 2)) {
     const int t = cl[q];
     int m = 0;
     for (int a = 0; a < NS; ++a) m |= sN[t * NS + a] ? (1 << a) : 0;
@@ -1099,6 +1125,43 @@ __global__ __launch_bounds__(64 * (WPC + 1)) void k_elb_gibbs_mp(Dims d, ElbDev 
     prog[tid] = tid < WPC ? ((g < P) ? g * nc : done_all) : ((part * WPC - 1 + W) % W) * nc;
   }
   __syncthreads();
+  if (wave == WPC + 1) {
+    // ---- exporter: the cells of every month the last drawing wave (global wave gw_last) has drawn in a
+    //      pass whose successor runs on the next part, in month order, up to 8 months per batch
+    constexpr int KM = 8;
+    const int k = lane / NS, a = lane - (lane / NS) * NS;
+    const bool act = lane < KM * NS;
+    bool stuck = false;
+    for (int ne = part * WPC + WPC - 1; ne + 1 < P && !stuck; ne += W) {
+      const unsigned long long tag = tag0 + (unsigned long long)(ne + 1);
+      int it = 0;
+      for (int m = 0; m < nc;) {
+        const int pl = __hip_atomic_load(&prog[WPC - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int avail = pl >= done_all ? nc : min(nc, max(0, pl - ne * nc));
+        const int cnt = min(avail - m, KM);
+        if (cnt <= 0) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++it > (1 << 24)) {
+            stuck = true;
+            break;
+          }
+          continue;
+        }
+        it = 0;
+        if (act && k < cnt) {
+          const int t = Tm[m + k] & 0xffff;
+          const unsigned long long vb = (unsigned long long)__double_as_longlong(Sl[t * NS + a]);
+          const __attribute__((ext_vector_type(4))) unsigned g = {(unsigned)vb, (unsigned)(vb >> 32), (unsigned)tag,
+                                                                   (unsigned)(tag >> 32)};
+          __builtin_amdgcn_raw_buffer_store_b128(g, grs, gout + (t * NS + a) * 16, 0, 16);  // sc1
+        }
+        m += cnt;
+      }
+    }
+    if (stuck && lane == 0) atomicOr(&cs.status[c], CCMM_STATUS_HANDOFF);
+    __syncthreads();
+    return;
+  }
   if (wave == WPC) {
     // ---- importer: passes n' = gw - 1 (mod W) of the previous part's last wave, whose successor pass
     //      n' + 1 runs here; month by month in order, up to 8 months per round trip
@@ -1153,7 +1216,7 @@ __global__ __launch_bounds__(64 * (WPC + 1)) void k_elb_gibbs_mp(Dims d, ElbDev 
   const int kk0 = c0 / NS, sp0 = c0 % NS, kk1 = c1 / NS, sp1 = c1 % NS;
   const int off0 = (kk0 < p) ? -(kk0 + 1) : (kk0 - p + 1);
   const int off1 = (kk1 < p) ? -(kk1 + 1) : (kk1 - p + 1);
-  constexpr int kHd = NS + NS * (NS - 1) + NS;
+  constexpr int kHd = NS + NS * (NS - 1) + 2 * NS;
   struct Rec {
     double hd[kHd], g0[NS], g1[NS];
   };
@@ -1193,7 +1256,6 @@ __global__ __launch_bounds__(64 * (WPC + 1)) void k_elb_gibbs_mp(Dims d, ElbDev 
     wave_lds_sync();
   };
   int* pprog = &prog[wave == 0 ? WPC : wave - 1];  // the predecessor: local wave or the importer
-  const bool publish = wave == WPC - 1;                  // the last wave feeds the next part
   int n = gw;
   Rec rc, rn;
   load_rec(0, rc);
@@ -1202,7 +1264,6 @@ __global__ __launch_bounds__(64 * (WPC + 1)) void k_elb_gibbs_mp(Dims d, ElbDev 
   int tmn = Tm[nc > 1 ? 1 : 0];
   for (; n < P && !stuck; n += W) {
     uniforms(n);
-    const unsigned long long tag = tag0 + (unsigned long long)(n + 1);
     for (int i = 0; i < nc; ++i) {
       const int ni = (i + 1 < nc) ? i + 1 : 0;
       const int nni = (ni + 1 < nc) ? ni + 1 : 0;
@@ -1247,19 +1308,10 @@ __global__ __launch_bounds__(64 * (WPC + 1)) void k_elb_gibbs_mp(Dims d, ElbDev 
           ++y;
         }
         uint8_t fl = 0;
-        cur[a] = elb_trunc_normal_pz(mu, so[a], e.elb, u[a], zu[a], fl);
+        cur[a] = elb_trunc_normal_pz(mu, so[a], so[NS + a], e.elb, u[a], zu[a], fl);
         if (e.flags && lane == 0) e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
       }
       for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
-      if (publish && n + 1 < P && lane < NS) {  // the month's cells for the next part, write-through
-        double v = cur[0];
-#pragma unroll
-        for (int a = 1; a < NS; ++a) v = lane == a ? cur[a] : v;
-        const unsigned long long vb = (unsigned long long)__double_as_longlong(v);
-        const __attribute__((ext_vector_type(4))) unsigned g = {(unsigned)vb, (unsigned)(vb >> 32), (unsigned)tag,
-                                                                 (unsigned)(tag >> 32)};
-        __builtin_amdgcn_raw_buffer_store_b128(g, grs, gout + (t * NS + lane) * 16, 0, 16);  // sc1
-      }
       rc = rn;
       tm = tmn;
       tmn = tmnn;
@@ -1371,9 +1423,9 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
       }
       double unext[NS];
       if (nn < P) draw_u(nn, ni, unext);
-      double hd[NS + NS * (NS - 1) + NS];
+      double hd[NS + NS * (NS - 1) + 2 * NS];
 #pragma unroll
-      for (int q = 0; q < NS + NS * (NS - 1) + NS; ++q) hd[q] = r[q];
+      for (int q = 0; q < NS + NS * (NS - 1) + 2 * NS; ++q) hd[q] = r[q];
       double x[8][NS];
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
@@ -1415,7 +1467,7 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
           ++y;
         }
         uint8_t fl = 0;
-        cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_trunc_normal(mu, so[a], e.elb, ucur[a], fl);
+        cur[a] = ELB_ABL(1) ? fmin(mu, e.elb) : elb_gibbs_trunc_normal(mu, so[a], so[NS + a], e.elb, ucur[a], fl);
         if (e.flags && j == 0) e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
       }
       if (j == 0) {
