@@ -337,6 +337,16 @@ struct ccmm_chains {
   hipEvent_t mfma_ev = nullptr;
 
   ~ccmm_chains() {
+    if (evFcstFork) {
+      (void)hipEventDestroy(evFcstFork);
+      (void)hipEventDestroy(evFcstDone);
+    }
+    if (aux2) {
+      (void)hipStreamSynchronize(aux2);
+      (void)hipEventDestroy(evSpec);
+      (void)hipEventDestroy(evSpecJoin);
+      (void)hipStreamDestroy(aux2);
+    }
     if (aux) {
       (void)hipStreamSynchronize(aux);
       (void)hipEventDestroy(evFork);
@@ -691,6 +701,10 @@ struct ccmm_chains {
     e.b3 = elb_b3;
     e.Amon = elb_Amon;
     e.Afull = elb_Afull;
+    e.spec = 0;
+    e.psState = nullptr;
+    e.psEpoch = 0;
+    e.ScurSpec = nullptr;
     return e;
   }
 
@@ -969,6 +983,7 @@ struct ccmm_chains {
     });
     const size_t lds_solve2 =
         (size_t)(d.TP + 2 * d.KP + 64 * kSolveLd + 2 * d.N * d.N) * sizeof(double);
+    join_fcst();  // the previous kept sweep's predictive density reads PAI
     launch(KID_SOLVE, [&] {
       if (d.N <= 8)
         hipLaunchKernelGGL(k_cta_solve2<8>, dim3(d.B), dim3(256), lds_solve2, ctx->stream, d,
@@ -1046,6 +1061,7 @@ struct ccmm_chains {
       L->last = mfma_ev;
       lk.unlock();
     }
+    join_fcst();  // the previous kept sweep's predictive density reads PAI
     launch(KID_SOLVEBIG, [&] {
       HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
                               nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 4 & big_mask));
@@ -1158,6 +1174,7 @@ struct ccmm_chains {
       }
       xc = SolveXch{solveXch.p, (unsigned long long*)solveFlag.p, ++solve_epoch};
     }
+    join_fcst();  // the previous kept sweep's predictive density reads PAI
     launch(KID_SOLVELAG, [&] {
       HIPCHECK(lag_launch_solve(lagNT, nmax, opt[OPT_SOLVE_ASYNC], ctx->stream, lds_s, d, Tslot.p, iVb.p, xsel(), ls,
                                 cs, ra, xc));
@@ -1371,6 +1388,8 @@ struct ccmm_chains {
     ps.count = psCount.p;
     ps.per = cfg.Ns * std::max(cfg.elbTmax, 1);
     ps.first = keep_first ? psFirst.p : nullptr;
+    ps.state = psState.p;
+    ps.epoch = ps_epoch;
     return ps;
   }
   // missingrate_all (mcmcVARshadowrate.m:435, 498; mcmcVARhybridGibbs.m:486): keep proposal 1 of
@@ -1502,13 +1521,12 @@ struct ccmm_chains {
           throw ArgError("Ns must be in [1, 5]");
       }
     });
-    if (ps) run_ps(ra, e, kept);
     // Gibbs passes: elb_waves passes in flight (k_elb_gibbs_wf, bit-identical draws), or the
     // one-wave sequential kernel (option elb_waves = 1)
     auto gibbs_lds = [&](int w) {  // shadow rates | per pass: uniforms and their elb_ppnd16 | month tables
       return w == 1 ? (size_t)3 * e.elbTmax * Ns * sizeof(double) + (size_t)e.elbTmax * sizeof(int)
                     : (size_t)(1 + 2 * w) * e.elbTmax * Ns * sizeof(double) + (size_t)2 * e.elbTmax * sizeof(int) +
-                          (size_t)2 * w * sizeof(int);
+                          (size_t)(2 * w + 1) * sizeof(int);
     };
     int W = opt[OPT_ELB_WAVES] <= 1 ? 1 : (opt[OPT_ELB_WAVES] < 8 ? 4 : 8);
     while (W > 1 && gibbs_lds(W) > 160 * 1024) W = (W == 8) ? 4 : 1;  // long ELB windows
@@ -1519,14 +1537,42 @@ struct ccmm_chains {
     // (the per-chain wave kernels keep shorter months at B < kElbOctMinB: one wave per chain cannot
     // fill the chip there, and a month costs the octet kernel more latency)
     const int elb_oct = opt[OPT_ELB_OCT];
-    if (elb_oct && lds_oct <= 160 * 1024 && (elb_oct == 2 || d.B >= kElbOctMinB)) {
+    const bool use_oct = elb_oct && lds_oct <= 160 * 1024 && (elb_oct == 2 || d.B >= kElbOctMinB);
+    // speculative Gibbs step (option elb_spec, small B): the asynchronous wave kernels start beside the PS
+    // branch on a stream of their own and stop once it accepts; the draw is kept only for a rejected PS
+    // (the reference's order and draws: PS first, the Gibbs draw the fallback, :438-466)
+    const bool spec = ps && opt[OPT_ELB_SPEC] && d.B <= kElbMpMaxB && !use_oct && W > 1 && opt[OPT_ELB_ASYNC] &&
+                      elb_flags == nullptr;
+    hipStream_t gst = ctx->stream;
+    if (spec) {
+      if (!aux2) {
+        HIPCHECK(hipStreamCreateWithFlags(&aux2, hipStreamNonBlocking));
+        HIPCHECK(hipEventCreateWithFlags(&evSpec, hipEventDisableTiming));
+        HIPCHECK(hipEventCreateWithFlags(&evSpecJoin, hipEventDisableTiming));
+      }
+      if (!psState.p) {
+        psState.alloc(d.B);
+        HIPCHECK(hipMemsetAsync(psState.p, 0, d.B * sizeof(unsigned long long), ctx->stream));
+      }
+      HIPCHECK(hipEventRecord(evSpec, ctx->stream));
+      HIPCHECK(hipStreamWaitEvent(aux2, evSpec, 0));
+      gst = aux2;
+      eScurSpec.alloc(eScur.n);
+      e.spec = 1;
+      e.psState = psState.p;
+      e.psEpoch = ++ps_epoch;
+      e.ScurSpec = eScurSpec.p;
+    } else if (ps) {
+      run_ps(ra, e, kept);
+    }
+    if (use_oct) {
       launch(KID_ELBGIBBS, [&] {
         switch (Ns) {
 #define CASE_NSO(NS)                                                                                           \
   case NS:                                                                                                     \
     HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs_oct<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                  (int)lds_oct));                                                               \
-    hipLaunchKernelGGL(k_elb_gibbs_oct<NS>, dim3(d.B), dim3(64), lds_oct, ctx->stream, d, e, cs, ra);           \
+    hipLaunchKernelGGL(k_elb_gibbs_oct<NS>, dim3(d.B), dim3(64), lds_oct, gst, d, e, cs, ra);                   \
     break;
           CASE_NSO(1)
           CASE_NSO(2)
@@ -1537,7 +1583,7 @@ struct ccmm_chains {
           default:
             throw ArgError("Ns must be in [1, 5]");
         }
-      });
+      }, gst);
     } else if (elb_parts(W) > 1) {
       // the wavefront over 2 or 4 CUs per chain (k_elb_gibbs_mp, bit-identical draws)
       const int parts = elb_parts(W), wpc = 8 / parts;
@@ -1548,13 +1594,13 @@ struct ccmm_chains {
       }
       const ElbXch xc{elbXch.p, ++elb_epoch};
       const size_t lds_mp = (size_t)(1 + 2 * wpc) * e.elbTmax * Ns * sizeof(double) +
-                            (size_t)2 * e.elbTmax * sizeof(int) + (size_t)(wpc + 1) * sizeof(int);
+                            (size_t)2 * e.elbTmax * sizeof(int) + (size_t)(wpc + 2) * sizeof(int);
       launch(KID_ELBGIBBS, [&] {
 #define GIBBS_MP(NS, WPC_, PT)                                                                                  \
   do {                                                                                                        \
     HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs_mp<NS, WPC_, PT>,                                   \
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_mp));                   \
-    hipLaunchKernelGGL((k_elb_gibbs_mp<NS, WPC_, PT>), dim3(d.B, PT), dim3(64 * (WPC_ + 2)), lds_mp, ctx->stream, \
+    hipLaunchKernelGGL((k_elb_gibbs_mp<NS, WPC_, PT>), dim3(d.B, PT), dim3(64 * (WPC_ + 2)), lds_mp, gst,       \
                        d, e, cs, ra, xc);                                                                     \
   } while (0)
 #define CASE_MP(NS)                    \
@@ -1575,14 +1621,14 @@ struct ccmm_chains {
         }
 #undef CASE_MP
 #undef GIBBS_MP
-      });
+      }, gst);
     } else
     launch(KID_ELBGIBBS, [&] {
 #define GIBBS_KA(NS, WW, AS)                                                                                \
   do {                                                                                                      \
     HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs_wf<NS, WW, AS>,                                   \
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gibbs));              \
-    hipLaunchKernelGGL((k_elb_gibbs_wf<NS, WW, AS>), dim3(d.B), dim3(64 * WW), lds_gibbs, ctx->stream, d, e, \
+    hipLaunchKernelGGL((k_elb_gibbs_wf<NS, WW, AS>), dim3(d.B), dim3(64 * WW), lds_gibbs, gst, d, e,         \
                        cs, ra);                                                                             \
   } while (0)
 #define GIBBS_K(NS, WW)            \
@@ -1597,7 +1643,7 @@ struct ccmm_chains {
     if (W == 1) {                                                                              \
       HIPCHECK(hipFuncSetAttribute((const void*)k_elb_gibbs<NS>,                               \
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gibbs)); \
-      hipLaunchKernelGGL(k_elb_gibbs<NS>, dim3(d.B), dim3(64), lds_gibbs, ctx->stream, d, e, cs, ra); \
+      hipLaunchKernelGGL(k_elb_gibbs<NS>, dim3(d.B), dim3(64), lds_gibbs, gst, d, e, cs, ra);         \
     } else if (W == 4) {                                                                       \
       GIBBS_K(NS, 4);                                                                          \
     } else {                                                                                   \
@@ -1616,7 +1662,17 @@ struct ccmm_chains {
 #undef CASE_NS
 #undef GIBBS_K
 #undef GIBBS_KA
-    });
+    }, gst);
+    if (spec) {  // the PS branch beside the Gibbs passes; k_ps_apply posts the decision they wait on
+      ElbDev ep = e;
+      ep.spec = 0;
+      run_ps(ra, ep, kept);
+      HIPCHECK(hipEventRecord(evSpecJoin, aux2));
+      HIPCHECK(hipStreamWaitEvent(ctx->stream, evSpecJoin, 0));
+      ep.spec = 1;  // (ep.psFlag: set by run_ps)
+      hipLaunchKernelGGL(k_elb_spec_select, dim3(d.B), dim3(256), 0, ctx->stream, ep, slot.p, d.B);
+      HIPCHECK(hipGetLastError());
+    }
     const int nrb = e.elbTmax * Ns * (p + 1);
     launch(KID_ELBREBUILD, [&] {
       hipLaunchKernelGGL(k_elb_rebuild, dim3((nrb + 255) / 256, d.B), dim3(256), 0, ctx->stream, d, e,
@@ -1629,6 +1685,11 @@ struct ccmm_chains {
   // over 2 (or 4) CUs at small B, one drawing wave per SIMD, when every chain's parts can be resident
   // together (option elb_parts; auto: 2 for B <= kElbMpMaxB)
   DBuf<double> elbXch;
+  hipStream_t aux2 = nullptr;  // the speculative Gibbs step's stream
+  hipEvent_t evSpec = nullptr, evSpecJoin = nullptr;
+  DBuf<unsigned long long> psState;  // PS decision per chain: ps_epoch << 1 | accepted (k_ps_apply)
+  DBuf<double> eScurSpec;            // the speculative Gibbs draw (k_elb_spec_select)
+  unsigned long long ps_epoch = 0;
   const double* elbXchZeroed = nullptr;
   unsigned long long elb_epoch = 0;
   int elb_parts(int W) {
@@ -1784,8 +1845,32 @@ struct ccmm_chains {
     get(quant, dq, (size_t)S * nq);
   }
 
+  // the predictive density of a kept sweep on the auxiliary stream (option fcst_overlap, N <= 32): it reads
+  // the sweep's PAI, invA, h, sqrtPHI and the chain's Y, which the next sweep first rewrites in its CTA
+  // solve (PAI), so it runs beside the next sweep's residual, weights and Gram + Cholesky; join_fcst()
+  // orders the solve (and the end of every ccmm_chains_sweep call) after it.  Same kernels, same inputs.
+  bool fcst_pending = false;
+  hipEvent_t evFcstFork = nullptr, evFcstDone = nullptr;
+  void join_fcst() {
+    if (!fcst_pending) return;
+    HIPCHECK(hipStreamWaitEvent(ctx->stream, evFcstDone, 0));
+    fcst_pending = false;
+  }
+
   void run_fcst(const RngArgs& ra) {
     if (fstored >= cfg.store_capacity) throw ArgError("forecast store full: call ccmm_chains_get_fcst");
+    hipStream_t fst = ctx->stream;
+    const bool overlap = opt[OPT_FCST_OVERLAP] != 0 && d.N <= kMaxNSmall;
+    if (overlap) {
+      ensure_aux();
+      if (!evFcstFork) {
+        HIPCHECK(hipEventCreateWithFlags(&evFcstFork, hipEventDisableTiming));
+        HIPCHECK(hipEventCreateWithFlags(&evFcstDone, hipEventDisableTiming));
+      }
+      HIPCHECK(hipEventRecord(evFcstFork, ctx->stream));
+      HIPCHECK(hipStreamWaitEvent(aux, evFcstFork, 0));
+      fst = aux;
+    }
     static const GLNodes gl = make_gl_nodes();
     const int N = d.N, B = d.B, H = fH, Nd = fNd;
     ChainState cs = view();
@@ -1812,17 +1897,21 @@ struct ccmm_chains {
     a.mode = env_ablation("CCMM_FCST_MODE", 0);  // timing-only: 1 no scores, 2 no horizons
     const XSel xs = xsel();
     launch(KID_FCST, [&] {
-      hipLaunchKernelGGL(k_fcst_jumpoff, dim3(B), dim3(256), 0, ctx->stream, N, cfg.p, N * cfg.p + 1, d.TP,
+      hipLaunchKernelGGL(k_fcst_jumpoff, dim3(B), dim3(256), 0, fst, N, cfg.p, N * cfg.p + 1, d.TP,
                          Tslot.p, slot.p, xs.ypool, xs.yidx, fldXj, fXj.p, hybrid ? cfg.Ns : 0,
                          hybrid ? dNdxS.p : nullptr, cfg.elb);
-      launch_fcst(ctx->stream, a, fSv1.p, opt[OPT_FCST_REG] != 0);
-      hipLaunchKernelGGL(k_fcst_accum, dim3(B), dim3(256), 0, ctx->stream, N, H, Nd,
+      launch_fcst(fst, a, fSv1.p, opt[OPT_FCST_REG] != 0);
+      hipLaunchKernelGGL(k_fcst_accum, dim3(B), dim3(256), 0, fst, N, H, Nd,
                          cfg.store_capacity, fstored, fY.p, fYc.p, (fcst_bh || hybrid) ? nullptr : fYhat.p, fSc.p,
                          fYsum.p, fYcsum.p, fYhatsum.p, fScStore.p, fKeep ? fPaths.p : nullptr,
                          fKeep ? fPathsC.p : nullptr);
-    });
+    }, fst);
     (void)cs;
     ++fstored;
+    if (overlap) {
+      HIPCHECK(hipEventRecord(evFcstDone, aux));
+      fcst_pending = true;
+    }
   }
 
   // ---------------------------------------------------------------- QR fallback
@@ -2040,7 +2129,9 @@ const ccmm::OptDesc ccmm::kOptDesc[ccmm::kOptCount] = {
     {"elb_oct", "CCMM_ELB_OCT", 1, 0, 2},
     {"elb_async", "CCMM_ELB_ASYNC", 1, 0, 1},
     {"elb_parts", "CCMM_ELB_PARTS", 0, 0, 4},
+    {"elb_spec", "CCMM_ELB_SPEC", 0, 0, 1},
     {"fcst_reg", "CCMM_FCST_REG", 1, 0, 1},
+    {"fcst_overlap", "CCMM_FCST_OVERLAP", 1, 0, 1},
     {"phi_overlap", "CCMM_PHI_OVERLAP", 1, 0, 1},
     {"qr_fallback", "CCMM_QR_FALLBACK", 1, 0, 1},
     {"lag", "CCMM_LAG", 1, 0, 1},
@@ -3049,6 +3140,7 @@ int ccmm_chains_sweep(ccmm_chains* ch, int nsweeps, const double* crn, int store
       const double* base = crn ? ch->crn.p + (size_t)m * ch->crn_len : nullptr;
       ch->sweep_once(base, (int64_t)nsweeps * ch->crn_len, store != 0);
     }
+    ch->join_fcst();
     if (ch->profiling) ch->collect_profile();
     if (crn) {
       HIPCHECK(hipStreamSynchronize(ch->ctx->stream));

@@ -63,7 +63,22 @@ struct ElbDev {
   // 1: the structural matrices A (cs.A / Amon) are full -- the inverse of a general impact matrix
   // Psi(2:Ny+1, :) (ccmm_gibbs_shadowrates); 0: unit lower triangular (every sweep; invA's inverse)
   int Afull;
+  // speculative Gibbs step (k_elb_gibbs_wf ASYNC / k_elb_gibbs_mp, small B): the passes start beside the PS
+  // branch (ccmm_ps.hip) on another stream; k_ps_apply posts psState[c] = psEpoch << 1 | accepted, the
+  // waves stop early once they see an accepted proposal (a poll, never a wait: the streams need not run
+  // concurrently), the draw goes to ScurSpec, and k_elb_spec_select keeps it only where the PS branch
+  // rejected -- the reference's order (PS first, the Gibbs draw as the fallback, :438-466), same draws
+  int spec;
+  const unsigned long long* psState;
+  unsigned long long psEpoch;
+  double* ScurSpec;  // [B][elbTmax][Ns]
 };
+
+// spec mode: the PS decision of this sweep for chain c: 0 undecided, 1 accepted, 2 rejected (sc1 load)
+__device__ __forceinline__ int elb_ps_decision(const ElbDev& e, int c) {
+  const unsigned long long v = __hip_atomic_load(&e.psState[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (v >> 1) != e.psEpoch ? 0 : ((v & 1) ? 1 : 2);
+}
 
 // condition record per censored month (doubles):
 //   a_t [Ns] | beta1 [Ns][Ns-1] | sqrtOmega1 [Ns] | 1 / sqrtOmega1 [Ns] | Ω [Ns][Ns] | G [2p Ns][Ns]
@@ -805,7 +820,7 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
   const int p = e.p;
   const int T = e.elbT[s], nc = e.ncens[s];
   if (nc == 0) return;
-  if (e.psFlag && e.psFlag[c] > 0) return;  // a PS proposal was accepted (:453-454)
+  if (!e.spec && e.psFlag && e.psFlag[c] > 0) return;  // a PS proposal was accepted (:453-454)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Rng rng = ra.make(c);
@@ -895,7 +910,9 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
     bool stuck = false;
     unsigned long long acc_w = 0, acc_s = 0, acc_d = 0, acc_t = 0, months = 0;
     int tmn = Tm[nc > 1 ? 1 : 0];
-    for (; n < P && !stuck; n += W) {
+    bool aborted = false;  // spec mode: the PS branch accepted a proposal
+    int dec = 0;           // spec mode: the decision loaded one month ago (checked one month later)
+    for (; n < P && !stuck && !aborted; n += W) {
       uniforms(n);
       for (i = 0; i < nc; ++i) {
         ELB_CLK(t0);
@@ -906,6 +923,13 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
           load_rec(ni, rn);  // next month of this wave (month 0 of its next pass after the last)
         else
           rn = rc;  // (128: timing only, no record loads)
+        if (e.spec && (i & 3) == 0) {  // the PS decision, loaded after the record (in-order completion) and
+          if (dec == 1) {              // read four months later, so the poll never holds a month up
+            aborted = true;
+            break;
+          }
+          dec = elb_ps_decision(e, c);
+        }
         if (n > 0 && !ELB_ABL(256)) {  // (256: timing only, no predecessor wait)
           const int need = (n - 1) * nc + reach[i] + 1;
           int it = 0;
@@ -984,7 +1008,8 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
     if (lane == 0) __hip_atomic_store(&prog[wave], done_all, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (stuck && lane == 0) atomicOr(&cs.status[c], 32);
     __syncthreads();
-    for (int q = tid; q < T * NS; q += 64 * W) Sc[q] = Sl[q];
+    double* dst = e.spec ? e.ScurSpec + (size_t)c * e.elbTmax * NS : Sc;  // (spec: k_elb_spec_select picks)
+    for (int q = tid; q < T * NS; q += 64 * W) dst[q] = Sl[q];
     return;
   }
   for (int step = 0;; ++step) {
@@ -1084,7 +1109,7 @@ __global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev 
   const int p = e.p;
   const int T = e.elbT[s], nc = e.ncens[s];
   if (nc == 0) return;
-  if (e.psFlag && e.psFlag[c] > 0) return;  // a PS proposal was accepted (:453-454)
+  if (!e.spec && e.psFlag && e.psFlag[c] > 0) return;  // a PS proposal was accepted (:453-454)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // WPC: the importer, WPC + 1: the exporter
   const int gw = part * WPC + wave;
@@ -1140,6 +1165,10 @@ __global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev 
         const int avail = pl >= done_all ? nc : min(nc, max(0, pl - ne * nc));
         const int cnt = min(avail - m, KM);
         if (cnt <= 0) {
+          if (e.spec && (it & 63) == 63 && elb_ps_decision(e, c) == 1) {  // the PS branch accepted
+            ne = P;
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
           if (++it > (1 << 24)) {
             stuck = true;
@@ -1191,6 +1220,10 @@ __global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev 
           if (cnt == KM && ((bad >> (kk * NS)) & ((1ull << NS) - 1))) cnt = kk;
         cnt = min(cnt, nc - m);
         if (cnt == 0) {
+          if (e.spec && (it & 63) == 63 && elb_ps_decision(e, c) == 1) {  // the PS branch accepted
+            np = P;
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
           if (++it > (1 << 24)) {
             stuck = true;
@@ -1262,13 +1295,22 @@ __global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev 
   int tm = Tm[0];
   bool stuck = false;
   int tmn = Tm[nc > 1 ? 1 : 0];
-  for (; n < P && !stuck; n += W) {
+  bool aborted = false;  // spec mode: the PS branch accepted a proposal
+  int dec = 0;           // spec mode: the decision loaded one month ago
+  for (; n < P && !stuck && !aborted; n += W) {
     uniforms(n);
     for (int i = 0; i < nc; ++i) {
       const int ni = (i + 1 < nc) ? i + 1 : 0;
       const int nni = (ni + 1 < nc) ? ni + 1 : 0;
       const int tmnn = Tm[nni];
       load_rec(ni, rn);  // next month of this wave (month 0 of its next pass after the last)
+      if (e.spec && (i & 3) == 0) {  // the PS decision, loaded after the record, read four months later
+        if (dec == 1) {
+          aborted = true;
+          break;
+        }
+        dec = elb_ps_decision(e, c);
+      }
       if (n > 0) {
         const int need = (n - 1) * nc + reach[i] + 1;
         int it = 0;
@@ -1323,8 +1365,9 @@ __global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev 
   if (stuck && lane == 0) atomicOr(&cs.status[c], CCMM_STATUS_HANDOFF);
   __syncthreads();
   // the part that ran the last pass holds the final draw of every censored cell
+  double* dst = e.spec ? e.ScurSpec + (size_t)c * e.elbTmax * NS : Sc;  // (spec: k_elb_spec_select picks)
   if (((P - 1) % W) / WPC == part)
-    for (int q = tid; q < T * NS; q += 64 * WPC) Sc[q] = Sl[q];
+    for (int q = tid; q < T * NS; q += 64 * WPC) dst[q] = Sl[q];
 }
 
 // ---------------------------------------------------------------- Gibbs passes, eight per wave
@@ -1484,6 +1527,19 @@ __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainSta
   if (prog < done_all && lane == 0) atomicOr(&cs.status[c], 32);  // hand-off step cap reached (ccmm.h bit 32; never expected)
   __syncthreads();
   for (int q = lane; q < T * NS; q += 64) Sc[q] = Sl[q];
+}
+
+// ---------------------------------------------------------------- speculative step: the sweep's draw
+// after the PS branch and the speculative Gibbs passes: the accepted proposal (already in Scur, k_ps_apply)
+// or, where the PS branch rejected (or had no proposals), the Gibbs draw
+__global__ void k_elb_spec_select(ElbDev e, const int* slot, int B) {
+  const int c = blockIdx.x;
+  if (c >= B) return;
+  const int s = slot[c];
+  if (e.ncens[s] == 0 || e.psFlag[c] > 0) return;
+  const size_t n = (size_t)e.elbT[s] * e.Ns;
+  for (size_t q = threadIdx.x; q < n; q += blockDim.x)
+    e.Scur[(size_t)c * e.elbTmax * e.Ns + q] = e.ScurSpec[(size_t)c * e.elbTmax * e.Ns + q];
 }
 
 // ---------------------------------------------------------------- rebuild X, Y (per chain)

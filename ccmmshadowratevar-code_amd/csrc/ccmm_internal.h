@@ -286,7 +286,9 @@ enum OptId {
   OPT_ELB_OCT,      // k_elb_gibbs_oct: 0 never, 1 from B >= kElbOctMinB, 2 always
   OPT_ELB_ASYNC,    // k_elb_gibbs_wf with per-wave progress flags (1) or lock-step barriers (0)
   OPT_ELB_PARTS,    // workgroups (CUs) per chain of the ELB wavefront: 0 auto, 1, 2, 4
+  OPT_ELB_SPEC,     // speculative Gibbs step beside the PS branch at small B (1; measured neutral, off) or PS first (0)
   OPT_FCST_REG,     // k_fcst with the lag coefficients in registers (1) or PAI in LDS (0)
+  OPT_FCST_OVERLAP, // kept sweeps' predictive density on the auxiliary stream beside the next sweep's CTA (1)
   OPT_PHI_OVERLAP,  // PHI block on the auxiliary stream beside the ELB step (1) or in stream order (0)
   OPT_QR_FALLBACK,  // host QR branch for a failed CTA Cholesky (CTA.m:80-92): 1 on, 0 off
   kOptSchedule,     // ---- forms below: same algorithm, other summation order / branch

@@ -40,6 +40,8 @@ struct PsDev {
   double* first;    // [B][Ns elbTmax] proposal 1 over the window (shadowrateProposals(:,:,1), kept as
                     //               missingrate, mcmcVARshadowrate.m:435); nullptr: not kept
   int per;          // Ns elbTmax
+  unsigned long long* state;  // [B] speculative Gibbs step: epoch << 1 | accepted, posted by k_ps_apply
+  unsigned long long epoch;   //     (nullptr / 0: no Gibbs step waits on the decision)
 };
 
 // ---------------------------------------------------------------- banded Cholesky
@@ -423,6 +425,7 @@ __global__ __launch_bounds__(64) void k_ps_apply(ElbDev e, PsDev ps, RngArgs ra,
       if (n == 0 && ps.first)  // no proposals this sweep (precision not positive definite)
         for (int q = 0; q < ps.per; ++q) ps.first[(size_t)c * ps.per + q] = __builtin_nan("");
       ps.flag[c] = 0;
+      if (ps.state) __hip_atomic_store(&ps.state[c], ps.epoch << 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
   }
@@ -449,6 +452,7 @@ __global__ __launch_bounds__(64) void k_ps_apply(ElbDev e, PsDev ps, RngArgs ra,
                         e.Scur + (size_t)c * e.elbTmax * e.Ns, ps.cell + (size_t)c * ps.nmax, zl);
     ps.flag[c] = kmin + 1;
     ps.count[2 * c + (kept ? 1 : 0)] += 1;
+    if (ps.state) __hip_atomic_store(&ps.state[c], ps.epoch << 1 | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

@@ -1,4 +1,6 @@
-"""Schedules of the block-hybrid sweep that must not change a bit: the PHI block on the auxiliary
+"""Schedules of the block-hybrid sweep that must not change a bit: the speculative Gibbs step beside the
+PS branch (option elb_spec, the default at small B) against PS first, then Gibbs; the ELB wavefront over two
+CUs per chain (elb_parts) against one; the PHI block on the auxiliary
 stream beside the ELB step (the default) against plain stream order (option phi_overlap = 0) -- the two
 blocks touch disjoint state -- and the lag-structured CTA solve on two workgroups per chain (the
 default at small B) against one (option solve_split = 0), and the forecast paths with the coefficients in
@@ -11,7 +13,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("var,B", [("phi_overlap", 8), ("solve_split", 8), ("solve_split", 1),
-                                   ("fcst_reg", 8)])
+                                   ("fcst_reg", 8), ("elb_spec", 8), ("elb_spec", 1), ("elb_parts", 8),
+                                   ("fcst_overlap", 8), ("fcst_overlap", 1)])
 def test_schedule_bit_identical(pkg, ctx, fred, var, B):
     d = fred
     p = 12

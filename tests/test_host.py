@@ -194,7 +194,8 @@ SELECTOR_VARS = {"CCMM_OLD_SOLVE": None, "CCMM_OLD_CHOL": None, "CCMM_GC18": Non
                  "CCMM_SOLVE_SPLIT": ("solve_split", -1), "CCMM_SOLVE_ASYNC": ("solve_async", 1),
                  "CCMM_SV_NWG": ("sv_nwg", 0), "CCMM_ELB_WAVES": ("elb_waves", 8), "CCMM_ELB_OCT": ("elb_oct", 1),
                  "CCMM_ELB_ASYNC": ("elb_async", 1), "CCMM_ELB_PARTS": ("elb_parts", 0),
-                 "CCMM_FCST_REG": ("fcst_reg", 1), "CCMM_PHI_OVERLAP": ("phi_overlap", 1),
+                 "CCMM_ELB_SPEC": ("elb_spec", 0),
+                 "CCMM_FCST_REG": ("fcst_reg", 1), "CCMM_FCST_OVERLAP": ("fcst_overlap", 1), "CCMM_PHI_OVERLAP": ("phi_overlap", 1),
                  "CCMM_QR_FALLBACK": ("qr_fallback", 1), "CCMM_LAG": ("lag", 1), "CCMM_FORCE_QR": ("force_qr", 0),
                  "CCMM_GIRF_GENERIC": ("girf_generic", 0)}
 
