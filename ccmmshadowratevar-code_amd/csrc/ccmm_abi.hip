@@ -1860,7 +1860,8 @@ struct ccmm_chains {
   void run_fcst(const RngArgs& ra) {
     if (fstored >= cfg.store_capacity) throw ArgError("forecast store full: call ccmm_chains_get_fcst");
     hipStream_t fst = ctx->stream;
-    const bool overlap = opt[OPT_FCST_OVERLAP] != 0 && d.N <= kMaxNSmall;
+    // (small B only: with the chip full of the next sweep's Gram + Cholesky the overlap buys nothing)
+    const bool overlap = opt[OPT_FCST_OVERLAP] != 0 && d.N <= kMaxNSmall && d.B <= kElbMpMaxB;
     if (overlap) {
       ensure_aux();
       if (!evFcstFork) {
