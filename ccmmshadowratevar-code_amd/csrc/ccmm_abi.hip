@@ -1,6 +1,7 @@
 // C-ABI implementation of libccmm (include/ccmm.h): contexts, device-resident
-// chain sets and the block-level drop-ins.  Host code only; kernels live in
-// ccmm_kernels.hip (included here so the whole library is one translation unit).
+// chain sets and the block-level drop-ins.  Host code only: the kernels are defined in their own
+// translation units (ccmm_kernels / ccmm_gram_chol / ccmm_cta_solve / ccmm_elb / ccmm_ps / ccmm_fcst /
+// ccmm_lag / ccmm_svpart / ccmm_big / ccmm_bign / ccmm_post / ccmm_girf) and declared in their headers.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -14,12 +15,9 @@
 #include <string>
 #include <vector>
 
-#include "ccmm_kernels.hip"
-#include "ccmm_cta_solve.hip"
-#include "ccmm_gram_chol.hip"
-#include "ccmm_elb.hip"
-#include "ccmm_ps.hip"
-#include "ccmm_fcst.hip"
+#include "ccmm_sweep.h"
+#include "ccmm_elb.h"
+#include "ccmm_fcst.h"
 #include "ccmm_lag.h"
 #include "ccmm_svpart.h"
 #include "ccmm_big.h"

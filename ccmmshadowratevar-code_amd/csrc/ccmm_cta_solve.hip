@@ -10,12 +10,10 @@
 //   PAI(:,j) = x ; E(:,j) = Y(:,j) - X x                     thread per t
 // L (lower) and L' (upper) both live in the system's KP x KP buffer written by
 // k_chol; rdiag holds 1/L_kk.
-#pragma once
-#include "ccmm_internal.h"
+#include "ccmm_sweep.h"
 
 namespace ccmm {
 
-constexpr int kSolveLd = 65;  // LDS row stride of the staged 64x64 diagonal block
 
 template <int NMAX>
 __global__ __launch_bounds__(256) void k_cta_solve2(Dims d, const int* __restrict__ Tslot,
@@ -181,5 +179,10 @@ __global__ __launch_bounds__(256) void k_cta_solve2(Dims d, const int* __restric
     __syncthreads();
   }
 }
+
+// ---------------------------------------------------------------- instantiations launched by ccmm_abi.hip
+template __global__ void k_cta_solve2<8>(Dims, const int*, const double*, XSel, ChainState, const double*, RngArgs);
+template __global__ void k_cta_solve2<20>(Dims, const int*, const double*, XSel, ChainState, const double*, RngArgs);
+template __global__ void k_cta_solve2<32>(Dims, const int*, const double*, XSel, ChainState, const double*, RngArgs);
 
 }  // namespace ccmm

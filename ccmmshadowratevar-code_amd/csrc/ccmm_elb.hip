@@ -20,59 +20,11 @@
 //   k_elb_cond    per (chain, censored month): Ω_t, a_t, G_t, conditional betas
 //   k_elb_gibbs   per chain: burnin + 1 sequential passes, inverse-CDF truncated normals
 //   k_elb_rebuild per chain: splice the shadow rates into the chain's Y and X (:501-509)
-#pragma once
-#include "ccmm_internal.h"
+#include "ccmm_elb.h"
 
 namespace ccmm {
 
-constexpr int kElbNsMax = 5;  // Ns = 5: the Krippner / Wu-Xia datasets at ELB > 0.25 (setShadowYields.m:1-5)
-constexpr int kElbColMax = 128;  // 2 p Ns neighbour columns, two per lane
 
-struct ElbDev {
-  int Ns, p, elbTmax, passes;    // passes = gibbsburn + 1
-  double elb;
-  const int* ndxS;               // [Ns]
-  const uint8_t* actual;         // [N] actualrateBlock
-  const int* elbT0;              // [ndata]
-  const int* elbT;               // [ndata]
-  const uint8_t* sNaN;           // [ndata][elbTmax][Ns]  (t-major)
-  const int* ncens;              // [ndata]
-  const int* cens;               // [ndata][elbTmax] censored months in increasing order
-  const double* Xactual;         // X pool (slot slabs first)
-  // per chain scratch
-  double* Phi;    // [B][N][N*p]   Phi[i][(l-1)N + q] = PAIshadow(1+(l-1)N+q, i)
-  double* Y0;     // [B][elbTmax][N]  scratch: Yb - Yhatactual
-  double* Yt;     // [B][elbTmax][N]  Yb: the chain's Y, censored shadow-rate cells at 0
-  double* Et;     // [B][elbTmax][N]  ε_τ (stable residual form, see k_elb_prep)
-  double* cond;   // [B][elbTmax][condStride]
-  double* Scur;   // [B][elbTmax][Ns] shadow rates (in/out)
-  int condStride;
-  int kshadow, K;  // hybrid model: PAI rows kshadow..K-1 load the actual-rate lags (K > kshadow)
-  int mode;        // CCMM_ELB_MODE timing ablation (0 in production)
-  const double* yhat;  // [B][elbTmax][N] explicit YHAT0 (ccmm_gibbs_shadowrates) or nullptr
-  uint8_t* flags;      // [B][passes][elbTmax][Ns] truncated-normal branch flags or nullptr
-  // acceptance-sampling branch (mcmcVARshadowrateBlockHybrid.m:438-466, ccmm_ps.hip)
-  int ps;              // 1: k_elb_prep / k_elb_cond also build the PS precision records
-  double* EtPS;        // [B][elbTmax][N] residuals of the PS model (Yhatactual as intercept)
-  const int* psFlag;   // [B] PS outcome of this sweep: > 0 accepted (k_elb_gibbs skips the chain)
-  // gibbsdrawShadowratesB3 (ccmm_gibbs_shadowrates_b3): the VAR on Y itself with the intercept in the
-  // state (base residuals in the PS model's form, yhat = 0) and, when Amon is set, a structural matrix
-  // per window month, A_tau = B(2:Ny+1, :, tau)^-1 ([B][elbTmax][N][N], lower)
-  int b3;
-  const double* Amon;
-  // 1: the structural matrices A (cs.A / Amon) are full -- the inverse of a general impact matrix
-  // Psi(2:Ny+1, :) (ccmm_gibbs_shadowrates); 0: unit lower triangular (every sweep; invA's inverse)
-  int Afull;
-  // speculative Gibbs step (k_elb_gibbs_wf ASYNC / k_elb_gibbs_mp, small B): the passes start beside the PS
-  // branch (ccmm_ps.hip) on another stream; k_ps_apply posts psState[c] = psEpoch << 1 | accepted, the
-  // waves stop early once they see an accepted proposal (a poll, never a wait: the streams need not run
-  // concurrently), the draw goes to ScurSpec, and k_elb_spec_select keeps it only where the PS branch
-  // rejected -- the reference's order (PS first, the Gibbs draw as the fallback, :438-466), same draws
-  int spec;
-  const unsigned long long* psState;
-  unsigned long long psEpoch;
-  double* ScurSpec;  // [B][elbTmax][Ns]
-};
 
 // spec mode: the PS decision of this sweep for chain c: 0 undecided, 1 accepted, 2 rejected (sc1 load)
 __device__ __forceinline__ int elb_ps_decision(const ElbDev& e, int c) {
@@ -80,21 +32,6 @@ __device__ __forceinline__ int elb_ps_decision(const ElbDev& e, int c) {
   return (v >> 1) != e.psEpoch ? 0 : ((v & 1) ? 1 : 2);
 }
 
-// condition record per censored month (doubles):
-//   a_t [Ns] | beta1 [Ns][Ns-1] | sqrtOmega1 [Ns] | 1 / sqrtOmega1 [Ns] | Ω [Ns][Ns] | G [2p Ns][Ns]
-// (1 / sqrtOmega1: the Gibbs kernels form ub = (elb - mu) / sig as a product, off the division's latency)
-// G column col = kk*Ns + s': kk < p past lag kk+1, kk >= p future lead kk-p+1.
-// With the PS branch (e.ps) the record continues (elb_cond_ps_off):
-//   P [Ns][Ns] (the month's precision, Ω^-1) | b_PS [Ns] | gP [p Ns][Ns]
-// b_PS = the PS model's linear term with every censored cell at 0; gP = the raw unit
-// responses of the past neighbours (-gP = the off-diagonal precision blocks).
-__host__ __device__ inline int elb_cond_head(int Ns) { return Ns + Ns * (Ns - 1) + 2 * Ns + Ns * Ns; }
-__host__ __device__ inline int elb_cond_ps_off(int Ns, int p) {
-  return elb_cond_head(Ns) + 2 * p * Ns * Ns;
-}
-__host__ __device__ inline int elb_cond_stride(int Ns, int p, int ps = 0) {
-  return elb_cond_ps_off(Ns, p) + (ps ? Ns * Ns + Ns + p * Ns * Ns : 0);
-}
 
 // ---------------------------------------------------------------- prep (per chain)
 // Stable residual form (oracle/elb_fast.py, gibbsdraw_shadowrates_stable): the
@@ -109,7 +46,6 @@ __host__ __device__ inline int elb_cond_stride(int Ns, int p, int ps = 0) {
 // rows > 0 (small batches, phi_lds & 2): workgroup blockIdx.y forms the residual rows
 // [rows y, rows (y + 1)) of the window only, from the Yb / Z rows p months before them (the lag sums);
 // the same values and operation order per row as one workgroup per chain
-constexpr int kElbPrepThreads = 512;
 __global__ __launch_bounds__(kElbPrepThreads) void k_elb_prep(Dims d, ElbDev e, XSel xs, ChainState cs, int phi_lds,
                                                               int rows) {
   extern __shared__ double sm[];
@@ -1094,11 +1030,6 @@ __global__ __launch_bounds__(64 * W) void k_elb_gibbs_wf(Dims d, ElbDev e, Chain
 // sees the value the sequential order gives it: draws, flags and states are bit-identical to
 // k_elb_gibbs.  All PARTS workgroups of a chain must be resident together (the host checks occupancy);
 // every spin is bounded (status bit 32, then the wave publishes "done" so its successors drain).
-constexpr int kElbMpMaxB = 64;  // auto: the multi-CU wavefront for B <= 64 chains
-struct ElbXch {
-  double* gran;                // [B][PARTS][elbTmax][NS] granules of 2 doubles {value, tag bits}
-  unsigned long long epoch;    // launch counter (host): tags of older launches never match
-};
 template <int NS, int WPC, int PARTS>
 __global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev e, ChainState cs, RngArgs ra,
                                                                  ElbXch xc) {
@@ -1311,7 +1242,7 @@ __global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev 
         }
         dec = elb_ps_decision(e, c);
       }
-      if (n > 0) {
+      if (n > 0 && !ELB_ABL(256)) {  // (256: timing only, no predecessor wait)
         const int need = (n - 1) * nc + reach[i] + 1;
         int it = 0;
         while (__hip_atomic_load(pprog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
@@ -1336,6 +1267,12 @@ __global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev 
       for (int a = 0; a < NS; ++a) cur[a] = Sl[t * NS + a];
       double sp[NS];
       for (int a = 0; a < NS; ++a) sp[a] = fma(h0 ? rc.g0[a] : 0.0, v0, (h1 ? rc.g1[a] : 0.0) * v1);
+      if (ELB_ABL(1024)) {  // timing only: a second, discarded copy of the month sums on the path
+        double sq[NS];
+        for (int a = 0; a < NS; ++a) sq[a] = sp[a] * 1.0000001;
+        wave_sum_dpp_n(sq);
+        for (int a = 0; a < NS; ++a) asm volatile("" ::"v"(sq[a]));
+      }
       wave_sum_dpp_n(sp);
       for (int a = 0; a < NS; ++a) sp[a] = rc.hd[a] + sp[a];
       const double* beta = rc.hd + NS;
@@ -1351,6 +1288,11 @@ __global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev 
         }
         uint8_t fl = 0;
         cur[a] = elb_trunc_normal_pz(mu, so[a], so[NS + a], e.elb, u[a], zu[a], fl);
+        if (ELB_ABL(2048)) {  // timing only: a second, discarded draw on the path
+          uint8_t f2 = 0;
+          const double d2 = elb_trunc_normal_pz(mu * 1.0000001, so[a], so[NS + a], e.elb, u[a], zu[a], f2);
+          asm volatile("" ::"v"(d2));
+        }
         if (e.flags && lane == 0) e.flags[(((size_t)c * e.passes + n) * e.elbTmax + t) * NS + a] = fl;
       }
       for (int a = 0; a < NS; ++a) Sl[t * NS + a] = cur[a];
@@ -1382,7 +1324,6 @@ __global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev 
 // Wavefront rule as there: pass n may draw month i once pass n - 1 has drawn every month up to
 // reach(i) (the predecessor octet's progress, read by one shuffle per step; within a step the eight
 // passes touch disjoint cells of Sl).
-constexpr int kElbOctMinB = 384;
 template <int NS>
 __global__ __launch_bounds__(64) void k_elb_gibbs_oct(Dims d, ElbDev e, ChainState cs, RngArgs ra) {
   constexpr int W = 8;
@@ -1580,5 +1521,23 @@ __global__ void k_elb_store(ElbDev e, ChainState cs, double* out, int cap, int m
   double* o = out + ((size_t)c * cap + m) * per;
   for (int q = threadIdx.x; q < per; q += blockDim.x) o[q] = (q / e.Ns < T) ? Sc[q] : __builtin_nan("");
 }
+
+// ---------------------------------------------------------------- instantiations launched by ccmm_abi.hip
+#define CCMM_ELB_INST(NS)                                                                              \
+  template __global__ void k_elb_cond<NS>(Dims, ElbDev, ChainState, int, int);                         \
+  template __global__ void k_elb_gibbs<NS>(Dims, ElbDev, ChainState, RngArgs);                         \
+  template __global__ void k_elb_gibbs_wf<NS, 4, false>(Dims, ElbDev, ChainState, RngArgs);            \
+  template __global__ void k_elb_gibbs_wf<NS, 4, true>(Dims, ElbDev, ChainState, RngArgs);             \
+  template __global__ void k_elb_gibbs_wf<NS, 8, false>(Dims, ElbDev, ChainState, RngArgs);            \
+  template __global__ void k_elb_gibbs_wf<NS, 8, true>(Dims, ElbDev, ChainState, RngArgs);             \
+  template __global__ void k_elb_gibbs_mp<NS, 4, 2>(Dims, ElbDev, ChainState, RngArgs, ElbXch);        \
+  template __global__ void k_elb_gibbs_mp<NS, 2, 4>(Dims, ElbDev, ChainState, RngArgs, ElbXch);        \
+  template __global__ void k_elb_gibbs_oct<NS>(Dims, ElbDev, ChainState, RngArgs);
+CCMM_ELB_INST(1)
+CCMM_ELB_INST(2)
+CCMM_ELB_INST(3)
+CCMM_ELB_INST(4)
+CCMM_ELB_INST(5)
+#undef CCMM_ELB_INST
 
 }  // namespace ccmm

@@ -24,47 +24,10 @@
 //       (MFMA, operands from the LDS panel; dead tiles in a live group of four
 //       get a zero operand instead of a branch).
 // Output, as k_chol: L (lower) and L' (upper) in the system's KP x KP buffer, 1/L_kk.
-#pragma once
-#include "ccmm_internal.h"
+#include "ccmm_sweep.h"
 
 namespace ccmm {
 
-constexpr int kGcWaves = 8;
-constexpr int kGcTC = 16;     // t rows per SYRK chunk
-constexpr int kGcLdp = 17;    // LDS row stride of a 16 x 16 panel tile
-// LDS row stride (doubles) of a Z chunk: 16 NT + 16, rows 32 banks apart (272 at NT = 16)
-__host__ __device__ constexpr int gc_ldz(int NT) { return 16 * NT + 16; }
-constexpr int kGcLdz = gc_ldz(16);
-
-// column-major enumeration of the lower tiles of an NT x NT tile grid
-__host__ __device__ constexpr int gc_tj(int NT, int g) {
-  int tj = 0;
-  while (tj < NT && g >= NT - tj) {
-    g -= NT - tj;
-    ++tj;
-  }
-  return tj;
-}
-__host__ __device__ constexpr int gc_ti(int NT, int g) {
-  int tj = 0;
-  while (tj < NT && g >= NT - tj) {
-    g -= NT - tj;
-    ++tj;
-  }
-  return tj + g;
-}
-__host__ __device__ constexpr int gc_tpw(int NT) { return (NT * (NT + 1) / 2 + kGcWaves - 1) / kGcWaves; }
-
-struct GcArgs {
-  const double* X;   // system's design, KP x TP column-major (ld TP)
-  const double* w;   // sqrt weights, TP
-  const double* iv;  // prior precision diagonal, KP
-  double* L;         // KP x KP output
-  double* rd;        // KP output
-  int T, TP, KP;
-  int mode;  // timing-only ablation (CCMM_GC_MODE): 1 no SYRK, 2 no Cholesky, 4 no trailing
-             // update, 8 no panel solve, 16 no diagonal factor
-};
 
 template <int NT, int W>
 __device__ __forceinline__ int gram_chol_body(const GcArgs& g, double* sm, int tid) {
@@ -305,5 +268,11 @@ __global__ __launch_bounds__(512, 1) void k_gram_chol(Dims d, const int* __restr
   }
   if (bad && (tid & 63) == 0) atomicOr(&cs.status[c], 2);
 }
+
+// ---------------------------------------------------------------- instantiations launched by ccmm_abi.hip
+template __global__ void k_gram_chol<4>(Dims, const int*, XSel, ChainState, const double*, double*, int);
+template __global__ void k_gram_chol<8>(Dims, const int*, XSel, ChainState, const double*, double*, int);
+template __global__ void k_gram_chol<12>(Dims, const int*, XSel, ChainState, const double*, double*, int);
+template __global__ void k_gram_chol<16>(Dims, const int*, XSel, ChainState, const double*, double*, int);
 
 }  // namespace ccmm

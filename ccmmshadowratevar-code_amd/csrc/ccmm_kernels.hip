@@ -17,7 +17,7 @@
 //
 // The algebraic identity X_j'X_j = X' diag(w) X, X_j'Y_j = X' v
 // removes the kron materialisation of CTA.m:69 (T(N-j+1) x K per equation).
-#include "ccmm_internal.h"
+#include "ccmm_sweep.h"
 
 namespace ccmm {
 
@@ -676,13 +676,6 @@ __global__ __launch_bounds__(256) void k_phi(Dims d, const int* __restrict__ Tsl
 }
 
 // ============================================================== draw storage
-struct Store {
-  double* PAI;     // [B][cap][N][K]
-  double* PHI;     // [B][cap][N(N+1)/2]
-  double* invA;    // [B][cap][N][N]
-  double* sqrtht;  // [B][cap][N][T]
-  int cap, m, Tmax;
-};
 
 __global__ void k_store(Dims d, ChainState cs, Store st) {
   const int c = blockIdx.y;
@@ -799,5 +792,12 @@ __global__ void k_mfma_selftest_acc(const double* A, const double* B, const doub
 #pragma unroll
   for (int r = 0; r < 4; ++r) D[((l >> 4) + 4 * r) + 16 * (l & 15)] = acc[r];
 }
+
+// ---------------------------------------------------------------- instantiations launched by ccmm_abi.hip
+template __global__ void k_resid_multi<8>(Dims, const int*, XSel, ChainState);
+template __global__ void k_resid_multi<20>(Dims, const int*, XSel, ChainState);
+template __global__ void k_resid_multi<32>(Dims, const int*, XSel, ChainState);
+template __global__ void k_astep_w<20>(Dims, const int*, ChainState, RngArgs, double, int, const int*);
+template __global__ void k_astep_w<32>(Dims, const int*, ChainState, RngArgs, double, int, const int*);
 
 }  // namespace ccmm

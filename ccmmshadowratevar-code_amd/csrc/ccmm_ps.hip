@@ -20,29 +20,10 @@
 //              by an LDS then a global atomic min
 //   k_ps_apply per chain: recompute the accepted proposal into the chain's shadow rates
 //              (k_elb_gibbs skips those chains), bookkeeping of :453-460
-#pragma once
-#include "ccmm_elb.hip"
+#include "ccmm_elb.h"
 
 namespace ccmm {
 
-constexpr int kPsWMax = 80;  // band width limit: Ns (p + 1) <= 80 (Ns = 5 with p = 12: 65)
-
-struct PsDev {
-  int nmax, W, NP;  // max censored cells over slots, band width, proposals per sweep
-  double elb;
-  double* L;        // [B][nmax][W]  L(i + j, i) at [i][j], zero beyond n
-  double* ybar;     // [B][nmax]     L^-1 b
-  int* cell;        // [B][nmax]     shadow-rate offset t Ns + a of censored cell i
-  int* n;           // [B]           censored cells (0: PS skipped this sweep)
-  int* acc;         // [B]           smallest accepted proposal (0-based), INT_MAX none
-  int* flag;        // [B]           ndxAccept of this sweep (1-based), 0 none
-  int* count;       // [B][2]        accepted sweeps: [0] burn-in, [1] kept (countELBaccept*)
-  double* first;    // [B][Ns elbTmax] proposal 1 over the window (shadowrateProposals(:,:,1), kept as
-                    //               missingrate, mcmcVARshadowrate.m:435); nullptr: not kept
-  int per;          // Ns elbTmax
-  unsigned long long* state;  // [B] speculative Gibbs step: epoch << 1 | accepted, posted by k_ps_apply
-  unsigned long long epoch;   //     (nullptr / 0: no Gibbs step waits on the decision)
-};
 
 // ---------------------------------------------------------------- banded Cholesky
 // One thread per band row (64 threads, 128 for band widths above 64: Ns = 5 with p = 12)
@@ -148,11 +129,6 @@ __global__ __launch_bounds__(128) void k_ps_chol(Dims d, ElbDev e, PsDev ps, Cha
 // wave-scope syncs, against k_ps_chol's three workgroup barriers and a W x W read-modify-write of
 // the window in LDS (and its serial assembly of the cell list).  Same band storage, same updates
 // (fma(-L(i,k), L(j,k), A(i,j)) and bb -= L(i,k) yk) in the same order per entry.
-constexpr int kPsChunk = 64;  // assembled band rows per LDS chunk
-
-__host__ __device__ inline size_t ps_chol_w_lds_bytes(int W, int elbTmax, int nmax) {
-  return (size_t)(kPsChunk * W + kPsChunk + W) * sizeof(double) + (size_t)(elbTmax + nmax) * sizeof(int);
-}
 
 template <int W>
 __global__ __launch_bounds__(64) void k_ps_chol_w(Dims d, ElbDev e, PsDev ps, ChainState cs) {
@@ -472,5 +448,20 @@ __global__ void k_ps_store(const int* flag, int* out, int B, int cap, int m) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < B) out[(size_t)c * cap + m] = flag ? flag[c] : 0;
 }
+
+// ---------------------------------------------------------------- instantiations launched by ccmm_abi.hip
+template __global__ void k_ps_chol_w<16>(Dims, ElbDev, PsDev, ChainState);
+template __global__ void k_ps_chol_w<32>(Dims, ElbDev, PsDev, ChainState);
+template __global__ void k_ps_chol_w<48>(Dims, ElbDev, PsDev, ChainState);
+template __global__ void k_ps_chol_w<64>(Dims, ElbDev, PsDev, ChainState);
+#define CCMM_PS_INST(W)                                                 \
+  template __global__ void k_ps_prop<W>(ElbDev, PsDev, RngArgs);        \
+  template __global__ void k_ps_apply<W>(ElbDev, PsDev, RngArgs, int);
+CCMM_PS_INST(16)
+CCMM_PS_INST(32)
+CCMM_PS_INST(48)
+CCMM_PS_INST(64)
+CCMM_PS_INST(80)
+#undef CCMM_PS_INST
 
 }  // namespace ccmm
