@@ -1264,9 +1264,11 @@ struct ccmm_chains {
     }, st);
     size_t lds = (size_t)(4 * d.N * (d.N + 1)) * sizeof(double);
     const size_t staged = lds + (size_t)d.N * (d.TP + 1) * sizeof(double);
-    const int stage_eta = staged <= 160 * 1024 ? 1 : 0;
+    // bit 0: eta staged in LDS; bit 1: then Z in the same region (k_phi)
+    const size_t staged_z = lds + (size_t)d.N * std::max(d.TP + 1, d.TP + cfg.dPHI) * sizeof(double);
+    const int stage_eta = staged_z <= 160 * 1024 ? 3 : (staged <= 160 * 1024 ? 1 : 0);
     if (stage_eta) {
-      lds = staged;
+      lds = (stage_eta & 2) ? staged_z : staged;
       if (lds > 64 * 1024)
         HIPCHECK(hipFuncSetAttribute((const void*)k_phi, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds));

@@ -625,8 +625,23 @@ __global__ __launch_bounds__(256) void k_phi(Dims d, const int* __restrict__ Tsl
     }
     for (; t < T; ++t) a0 = fma(er[t], ec[t], a0);
     Lpost[r * NS + col] = sP[r + col * N] + ((a0 + a1) + (a2 + a3));
-    const double* zr = Z + r;
-    const double* zc = Z + col;
+  }
+  // stage_eta bit 1: Z (N x TZ, k_phi_gen) follows eta into the same LDS region, one coalesced pass,
+  // so that the ZZ' chains read LDS instead of strided HBM rows (~0.2 ms of global-load latency per
+  // launch at B = 1); the same products in the same order
+  const double* Zw = Z;
+  if (stage_eta & 2) {
+    double* zs = Ph + N * NS;
+    __syncthreads();
+    for (int q = tid; q < N * TZ; q += blockDim.x) zs[q] = Z[q];
+    __syncthreads();
+    Zw = zs;
+  }
+  for (int e = tid; e < N * N; e += blockDim.x) {
+    const int r = e / N, col = e % N;
+    if (col > r) continue;
+    const double* zr = Zw + r;
+    const double* zc = Zw + col;
     double b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
     int q = 0;
     for (; q + 3 < TZ; q += 4) {
