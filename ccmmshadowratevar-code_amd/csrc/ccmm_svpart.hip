@@ -193,7 +193,7 @@ __global__ __launch_bounds__(64 * NW) void k_sv_part(Dims d, const int* __restri
                                                       RngArgs ra, double* __restrict__ sepbuf,
                                                       double* __restrict__ gbuf, int mode, int nwg) {
   constexpr int CLD = NN + 2, XLD = 2 * NN + 2, NN2 = NN * NN;
-  // phase A's block products on MFMA (NN = 20; CCMM_SV_MFMA=0 keeps the VALU pass)
+  // phase A's block products on MFMA (NN = 20; option sv_mfma = 0 keeps the VALU pass)
   constexpr bool kSvMfma = NN == 20 && SVMFMA;
   constexpr bool G3 = 3 * NN <= 64;
   using R = SvRec<NN>;
