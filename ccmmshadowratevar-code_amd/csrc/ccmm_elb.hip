@@ -548,8 +548,11 @@ __device__ __forceinline__ double elb_gibbs_trunc_normal(double mu, double sig, 
 // The same draw with zu = elb_ppnd16(u) computed beforehand (off the month-to-month path).  When
 // ub = (elb - mu) / sig >= 9, erfc(-ub / sqrt 2) = 2 - erfc(ub / sqrt 2) with erfc(6.36) ~ 1e-19, below
 // half an ulp of 2: PHIbar is exactly 1, u PHIbar = u, and the full evaluation returns mu + sig zu.  So
-// the draw is bit-identical without erfc and AS241 on the path (on the real window about half of the
-// draws: the conditional means sit far below the ELB, ub median 8.9).
+// the draw is bit-identical without erfc and AS241 on the path (two thirds of the floor vintage's draws,
+// profiles/r06final_elb_ubhist.json).  A second-order path for 5 <= ub < 9 (a sixth of the draws: z moved
+// from zu by the Taylor series of Phi^-1, the tail Q = Phi(-ub) from exp and a Mills-ratio polynomial)
+// measured no faster at B = 1 and slower in the octet kernel (two exp per draw cost what erfc does): not
+// kept (round 6).
 constexpr double kElbFastUb = 9.0;
 __device__ __forceinline__ double elb_trunc_normal_pz(double mu, double sig, double isig, double elb, double u,
                                                       double zu, uint8_t& fl) {
@@ -739,6 +742,15 @@ __global__ __launch_bounds__(64) void k_elb_gibbs(Dims d, ElbDev e, ChainState c
 // shader-clock cycles spent waiting for the predecessor, in the neighbour sums, in the draws and
 // in the store/publish tail, plus the month count (read by ccmm_elb_prof)
 __device__ unsigned long long g_elb_prof[8 * 6];
+__device__ unsigned long long g_elb_ubhist[8];  // k_elb_gibbs_mp draws by ub = (elb - mu) / sig bin (mode 4096)
+extern "C" int ccmm_elb_ubhist(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_elb_ubhist), sizeof(g_elb_ubhist)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_elb_ubhist), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
 extern "C" int ccmm_elb_prof(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_elb_prof), sizeof(g_elb_prof)) != hipSuccess) return -1;
   if (reset) {
@@ -1287,6 +1299,13 @@ __global__ __launch_bounds__(64 * (WPC + 2)) void k_elb_gibbs_mp(Dims d, ElbDev 
           ++y;
         }
         uint8_t fl = 0;
+#ifdef CCMM_ABLATION
+        if (ELB_ABL(4096) && lane == 0) {  // ub histogram of the draws (ablation build, ccmm_elb_ubhist)
+          const double ub = (e.elb - mu) * fabs(so[NS + a]);
+          const int bin = ub >= 9.0 ? 0 : ub >= 7.0 ? 1 : ub >= 5.0 ? 2 : ub >= 3.0 ? 3 : ub >= 1.0 ? 4 : ub >= -1.0 ? 5 : 6;
+          atomicAdd(&g_elb_ubhist[bin], 1ull);
+        }
+#endif
         cur[a] = elb_trunc_normal_pz(mu, so[a], so[NS + a], e.elb, u[a], zu[a], fl);
         if (ELB_ABL(2048)) {  // timing only: a second, discarded draw on the path
           uint8_t f2 = 0;
