@@ -314,6 +314,14 @@ struct ccmm_chains {
   int lagNT = 0, ldd = 0, drows = 0;
   std::vector<bool> slot_lag;
   DBuf<double> Dpool;
+  // large path: column-major lag twin of every X slab (ccmm_big.h ColX), when each slab's X is
+  // [1, lags 1..p of N (+ Ns) data columns]; k_elb_rebuild keeps the chains' twins current
+  bool colx_capable = false;
+  std::vector<bool> slot_colx;
+  DBuf<double> Dcpool;
+  DBuf<int> dXoff;
+  int dcld = 0, dcext = 0;
+  size_t dcslab = 0;
   DBuf<int> dColmap, astepTab;
   // large-system CTA (ccmm_big.hip): K > 256 or N > 32, or option large_path
   bool big = false;
@@ -504,6 +512,7 @@ struct ccmm_chains {
     HIPCHECK(hipMemsetAsync(Xpool.p, 0, Xpool.n * sizeof(double), ctx->stream));
     HIPCHECK(hipMemsetAsync(Ypool.p, 0, Ypool.n * sizeof(double), ctx->stream));
     init_lag(nX);
+    init_colx();
     iVdiag.alloc((size_t)cf.ndata * N * KP);
     iVb.alloc((size_t)cf.ndata * N * KP);
     sPHI.alloc((size_t)cf.ndata * N * N);
@@ -597,6 +606,63 @@ struct ccmm_chains {
     }
     dColmap.alloc(cm.size());
     HIPCHECK(hipMemcpy(dColmap.p, cm.data(), cm.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  // the lag twin of the large path: columns 0..N-1 the data, N..N+Ns-1 the hybrid's actual-rate
+  // columns (mcmcVARhybridGibbs.m:77-84), then a column of ones (the intercept) and a zero column
+  // (padded coefficients); row p + t = month t, rows 0..p-1 the presample
+  void init_colx() {
+    if (colx_capable || !big || cfg.p < 1) return;
+    slot_colx.assign(cfg.ndata, false);
+    const int N = cfg.N, p = cfg.p, ex = hybrid ? cfg.Ns : 0;
+    if (cfg.K != N * p + 1 + ex * p) return;
+    dcext = ex;
+    dcld = round_up(d.TP + p, 8);
+    dcslab = (size_t)(N + ex + 2) * dcld;
+    Dcpool.alloc((size_t)nslabX * dcslab);
+    HIPCHECK(hipMemsetAsync(Dcpool.p, 0, Dcpool.n * sizeof(double), ctx->stream));
+    std::vector<int> off(d.KP);
+    for (int a = 0; a < d.KP; ++a) {
+      if (a == 0) {
+        off[a] = (N + ex) * dcld;
+      } else if (a >= cfg.K) {
+        off[a] = (N + ex + 1) * dcld;
+      } else if (a - 1 < N * p) {
+        const int b = a - 1, l = b / N + 1, k = b % N;
+        off[a] = k * dcld + p - l;
+      } else {
+        const int b = a - 1 - N * p, l = b / ex + 1, si = b % ex;
+        off[a] = (N + si) * dcld + p - l;
+      }
+    }
+    dXoff.alloc(d.KP);
+    HIPCHECK(hipMemcpy(dXoff.p, off.data(), off.size() * sizeof(int), hipMemcpyHostToDevice));
+    colx_capable = true;
+  }
+  // a slot's twin from its X (T x K): column k's rows from the lag-1 column one month later and the
+  // presample from X's first row; exact check against every entry of X
+  void try_upload_Dc(int slot, int T, const double* X) {
+    if (!colx_capable) return;
+    slot_colx[slot] = false;
+    const int N = cfg.N, p = cfg.p, K = cfg.K, ex = dcext, nc = N + ex;
+    std::vector<double> D(dcslab, 0.0);
+    std::vector<int> off(K);
+    HIPCHECK(hipMemcpy(off.data(), dXoff.p, K * sizeof(int), hipMemcpyDeviceToHost));
+    auto colk = [&](int k, int l) { return k < N ? 1 + (l - 1) * N + k : 1 + N * p + (l - 1) * ex + (k - N); };
+    for (int k = 0; k < nc; ++k) {
+      for (int l = 1; l <= p; ++l) D[(size_t)k * dcld + p - l] = X[(size_t)colk(k, l) * T];  // rows 0..p-1
+      for (int t = 1; t < T; ++t) D[(size_t)k * dcld + p + t - 1] = X[(size_t)colk(k, 1) * T + t];
+    }
+    for (int t = 0; t < d.TP + p; ++t) D[(size_t)nc * dcld + t] = 1.0;
+    for (int a = 0; a < K; ++a)
+      for (int t = 0; t < T; ++t)
+        if (X[(size_t)a * T + t] != D[(size_t)off[a] + t]) return;
+    HIPCHECK(hipMemcpy(Dcpool.p + (size_t)slot * dcslab, D.data(), D.size() * sizeof(double), hipMemcpyHostToDevice));
+    slot_colx[slot] = true;
+  }
+  ColX colx() const {
+    bool on = colx_capable && opt[OPT_BIG_LAGX];
+    for (int s = 0; on && s < cfg.ndata; ++s) on = slot_colx[s];
+    return on ? ColX{Dcpool.p, dXoff.p, (long long)dcslab} : ColX{nullptr, nullptr, 0};
   }
   bool lag_active() const {
     if (!lag_capable || !opt[OPT_LAG]) return false;
@@ -764,6 +830,9 @@ struct ccmm_chains {
                               xs * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
       HIPCHECK(hipMemcpyAsync(Ypool.p + (size_t)(cfg.ndata + c) * ys, Ypool.p + (size_t)sl[c] * ys,
                               ys * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+      if (colx_capable)
+        HIPCHECK(hipMemcpyAsync(Dcpool.p + (size_t)(cfg.ndata + c) * dcslab, Dcpool.p + (size_t)sl[c] * dcslab,
+                                dcslab * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
       if (lag_capable) {
         const size_t ds = (size_t)drows * ldd;
         HIPCHECK(hipMemcpyAsync(Dpool.p + (size_t)(cfg.ndata + c) * ds, Dpool.p + (size_t)sl[c] * ds,
@@ -1048,11 +1117,11 @@ struct ccmm_chains {
     });
     launch(KID_GRAMBIG, [&] {
       HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
-                              nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 1 & big_mask));
+                              nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 1 & big_mask, colx()));
     });
     launch(KID_CHOLBIG, [&] {
       HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
-                              nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 2 & big_mask));
+                              nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 2 & big_mask, colx()));
     });
     if (L) {
       HIPCHECK(hipEventRecord(mfma_ev, ctx->stream));
@@ -1062,7 +1131,7 @@ struct ccmm_chains {
     join_fcst();  // the previous kept sweep's predictive density reads PAI
     launch(KID_SOLVEBIG, [&] {
       HIPCHECK(big_launch_cta(ctx->stream, d, Tslot.p, slot.p, iVdiag.p, iVb.p, xsel(), cs, bigGroups.p,
-                              nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 4 & big_mask));
+                              nGroups, rdiag.p, ra, Ubuf.p, Dinv.p, 4 & big_mask, colx()));
     });
   }
 
@@ -1676,7 +1745,8 @@ struct ccmm_chains {
     const int nrb = e.elbTmax * Ns * (p + 1);
     launch(KID_ELBREBUILD, [&] {
       hipLaunchKernelGGL(k_elb_rebuild, dim3((nrb + 255) / 256, d.B), dim3(256), 0, ctx->stream, d, e,
-                         xsel(), cs, cfg.ndata, lag_capable ? Dpool.p : nullptr, ldd, drows);
+                         xsel(), cs, cfg.ndata, lag_capable ? Dpool.p : nullptr, ldd, drows,
+                         colx_capable ? Dcpool.p : nullptr, dcld, (long long)dcslab);
     });
     resid_valid = false;  // X, Y changed: RESID is recomputed before the next CTA
   }
@@ -2135,6 +2205,7 @@ const ccmm::OptDesc ccmm::kOptDesc[ccmm::kOptCount] = {
     {"fcst_overlap", "CCMM_FCST_OVERLAP", 1, 0, 1},
     {"phi_overlap", "CCMM_PHI_OVERLAP", 1, 0, 1},
     {"qr_fallback", "CCMM_QR_FALLBACK", 1, 0, 1},
+    {"big_lagx", "CCMM_BIG_LAGX", 1, 0, 1},
     {"lag", "CCMM_LAG", 1, 0, 1},
     {"large_path", "CCMM_FORCE_BIG", 0, 0, 1},
     {"astep_serial", "CCMM_ASTEP_V1", 0, 0, 1},
@@ -2921,6 +2992,7 @@ int ccmm_chains_set_option(ccmm_chains* ch, const char* name, int value) {
       require(!ch->have_state, "option large_path: set it before ccmm_chains_set_data / set_state");
       HIPCHECK(hipSetDevice(ch->ctx->device));
       ch->big = ch->d.KP > 256 || ch->cfg.N > kMaxNSmall || value != 0;
+      ch->init_colx();
       std::vector<int> sl(ch->cfg.B);
       HIPCHECK(hipMemcpy(sl.data(), ch->slot.p, ch->cfg.B * sizeof(int), hipMemcpyDeviceToHost));
       ch->set_slots(sl.data());
@@ -2956,6 +3028,7 @@ int ccmm_chains_set_data(ccmm_chains* ch, int slot, int T, const double* Y, cons
     ch->set_T(slot, T);
     ch->upload_X(slot, T, X);
     ch->try_upload_D(slot, T, Y, X);
+    ch->try_upload_Dc(slot, T, X);
     ch->upload_TN(ch->Ypool.p + (size_t)slot * ch->d.N * ch->d.TP, 1, T, Y, 0.0);
     ch->set_slot_prior(slot, iVdiag, iVb, sPHI, h0mean, h0vcvsqrt);
     ch->have_slot[slot] = true;

@@ -29,7 +29,7 @@ constexpr int kBLd = 80;     // LDS row stride of staged panels (conflict-free b
 
 // ============================================================== Gram (FP64 MFMA)
 __global__ __launch_bounds__(256) void k_gram_big(Dims d, const int* __restrict__ Tslot, XSel xs,
-                                                  ChainState cs, const int4* __restrict__ groups) {
+                                                  ChainState cs, const int4* __restrict__ groups, ColX cx) {
   __shared__ double Pa[kBC][kBLd];   // a-panel (t, a)
   __shared__ double Pb[kBC][kBLd];   // b-panel (t, b)
   __shared__ double Wl[4][kBC];      // weights of the group's four systems
@@ -44,10 +44,21 @@ __global__ __launch_bounds__(256) void k_gram_big(Dims d, const int* __restrict_
   }
   const int tj = tile;
   const int a0 = ti * kBT, b0 = tj * kBT;
-  const double* X = xs.pool + (size_t)xs.idx[g.x] * d.KP * d.TP;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mymat = mats[wave];
   const int lcol = tid & 63, lt0 = (tid >> 6) * 8;
+  // this thread's two staged columns a0 + lcol and b0 + lcol (X itself or its lag twin; the twin's
+  // rows t >= T hold data where X holds zeros, but their weights are 0)
+  const double *xa0, *xb0;
+  if (cx.pool) {
+    const double* D = cx.pool + (size_t)xs.idx[g.x] * cx.slab;
+    xa0 = D + cx.off[a0 + lcol];
+    xb0 = D + cx.off[b0 + lcol];
+  } else {
+    const double* X = xs.pool + (size_t)xs.idx[g.x] * d.KP * d.TP;
+    xa0 = X + (size_t)(a0 + lcol) * d.TP;
+    xb0 = X + (size_t)(b0 + lcol) * d.TP;
+  }
   // 16 x 16 sub-tiles (x: b rows, y: a columns) that hold no lower-triangle entry of a real
   // coefficient -- the diagonal tile's upper half and the padded rows / columns >= K, whose X rows
   // are zero -- are not multiplied: they stay +0 (what the zero products sum to; the Cholesky and
@@ -68,8 +79,8 @@ __global__ __launch_bounds__(256) void k_gram_big(Dims d, const int* __restrict_
   // chunk ch + 1's panel rows and weights are loaded into registers while chunk ch multiplies
   double va[8], vb[8], wn = 0.0;
   auto load_chunk = [&](int t0) __attribute__((always_inline)) {
-    const double* xa = X + (size_t)(a0 + lcol) * d.TP + t0 + lt0;
-    const double* xb = X + (size_t)(b0 + lcol) * d.TP + t0 + lt0;
+    const double* xa = xa0 + t0 + lt0;
+    const double* xb = xb0 + t0 + lt0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       va[q] = xa[q];
@@ -446,7 +457,7 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
                                                         const double* __restrict__ iVb, XSel xs,
                                                         ChainState cs, const double* __restrict__ rdiag,
                                                         RngArgs ra, double* __restrict__ Ubuf,
-                                                        const double* __restrict__ Dinv, int skip) {
+                                                        const double* __restrict__ Dinv, int skip, ColX cx) {
   // skip: timing-only phase ablation (CCMM_SOLVE_SKIP; results invalid): 1 v/U, 2 X'v,
   // 4 forward, 8 backward, 16 residual
   extern __shared__ double sm[];
@@ -479,7 +490,12 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
   const int nb = (K + 63) / 64;
   for (int j = 0; j < N; ++j) {
     const int mat = c * N + j;
-    const double* X = xs.pool + (size_t)xs.idx[mat] * KP * TP;
+    // column a of the design: X + a TP, or its lag twin's column (same values for t < T; every
+    // read below at t >= T is multiplied by v_t = 0 or not made)
+    const double* X = cx.pool ? cx.pool + (size_t)xs.idx[mat] * cx.slab : xs.pool + (size_t)xs.idx[mat] * KP * TP;
+    auto xcol = [&](int a) __attribute__((always_inline)) -> const double* {
+      return cx.pool ? X + cx.off[a] : X + (size_t)a * TP;
+    };
     const double* L = cs.G + (size_t)mat * KP * KP;
     // ---- E(:,j) = Y(:,j) (PAI(:,j) = 0, CTA.m:63); U(:,i) += dE A(i,j), i >= j; v_t
     for (int t = tid; t < TP && !(skip & 1); t += NT) {
@@ -522,7 +538,7 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
       double p[4] = {0.0, 0.0, 0.0, 0.0};
       const double* xc[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) xc[q] = X + (size_t)min(a0 + q, K - 1) * TP;
+      for (int q = 0; q < 4; ++q) xc[q] = xcol(min(a0 + q, K - 1));
       int t = lane;
       for (; t + 64 * 3 < TP; t += 64 * 4) {  // 16 loads in flight per lane
         double xv[4][4];
@@ -672,7 +688,7 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
           for (; a + 15 < a_hi; a += 16) {  // 16 loads in flight per lane
             double xv[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) xv[q] = X[(size_t)(a + q) * TP + t];
+            for (int q = 0; q < 16; ++q) xv[q] = xcol(a + q)[t];
 #pragma unroll
             for (int q = 0; q < 16; q += 4) {
               a0 = fma(xv[q], yv[a + q], a0);
@@ -681,7 +697,7 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
               a3 = fma(xv[q + 3], yv[a + q + 3], a3);
             }
           }
-          for (; a < a_hi; ++a) a0 = fma(X[(size_t)a * TP + t], yv[a], a0);
+          for (; a < a_hi; ++a) a0 = fma(xcol(a)[t], yv[a], a0);
         }
         if (t < TP) part[slc * TP + t] = (t < T) ? (a0 + a1) + (a2 + a3) : 0.0;
       }
@@ -706,13 +722,13 @@ size_t big_solve_lds_bytes(const Dims& d) {
 hipError_t big_launch_cta(hipStream_t st, const Dims& d, const int* Tslot, const int* slotIV,
                           const double* iVdiag, const double* iVb, XSel xs, ChainState cs,
                           const int4* groups, int ngroups, double* rdiag, RngArgs ra, double* Ubuf,
-                          double* Dinv, int phase_mask) {
+                          double* Dinv, int phase_mask, ColX cx) {
   static const int skip = env_ablation("CCMM_SOLVE_SKIP", 0);
   static const int cskip = env_ablation("CCMM_CHOL_SKIP", 0);
   const int nt = d.KP / kBT;
   if (phase_mask & 1)
     hipLaunchKernelGGL(k_gram_big, dim3(nt * (nt + 1) / 2, ngroups), dim3(256), 0, st, d, Tslot, xs, cs,
-                       groups);
+                       groups, cx);
   if (phase_mask & 2)
     hipLaunchKernelGGL(k_chol_big, dim3(d.nmat), dim3(256), 0, st, d, slotIV, iVdiag, cs, rdiag, Dinv,
                        cskip);
@@ -722,7 +738,7 @@ hipError_t big_launch_cta(hipStream_t st, const Dims& d, const int* Tslot, const
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_cta_solve_big, dim3(d.B), dim3(1024), lds, st, d, Tslot, iVb, xs, cs, rdiag,
-                       ra, Ubuf, Dinv, skip);
+                       ra, Ubuf, Dinv, skip, cx);
   }
   return hipGetLastError();
 }

@@ -115,7 +115,8 @@ template <int NS, int WPC, int PARTS>
 __global__ void k_elb_gibbs_mp(Dims d, ElbDev e, ChainState cs, RngArgs ra, ElbXch xc);
 template <int NS> __global__ void k_elb_gibbs_oct(Dims d, ElbDev e, ChainState cs, RngArgs ra);
 __global__ void k_elb_spec_select(ElbDev e, const int* slot, int B);
-__global__ void k_elb_rebuild(Dims d, ElbDev e, XSel xs, ChainState cs, int xslab0, double* dpool, int ldd, int drows);
+__global__ void k_elb_rebuild(Dims d, ElbDev e, XSel xs, ChainState cs, int xslab0, double* dpool, int ldd, int drows,
+                              double* dcpool, int dcld, long long dcslab);
 __global__ void k_elb_store(ElbDev e, ChainState cs, double* out, int cap, int m);
 // ---------------------------------------------------------------- kernels (ccmm_ps.hip)
 __global__ void k_ps_chol(Dims d, ElbDev e, PsDev ps, ChainState cs);

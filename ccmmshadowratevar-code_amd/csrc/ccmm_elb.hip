@@ -1505,7 +1505,7 @@ __global__ void k_elb_spec_select(ElbDev e, const int* slot, int B) {
 // ---------------------------------------------------------------- rebuild X, Y (per chain)
 // shadowYdata(p+elbT0+1:end, ndxS) = shadowrate'; X(t, 1+(l-1)N+s) = Y(t-l, s) (:501-509)
 __global__ void k_elb_rebuild(Dims d, ElbDev e, XSel xs, ChainState cs, int xslab0, double* dpool,
-                              int ldd, int drows) {
+                              int ldd, int drows, double* dcpool, int dcld, long long dcslab) {
   const int c = blockIdx.y;
   const int s = cs.slot[c];
   const int N = d.N, TP = d.TP, Ns = e.Ns, p = e.p;
@@ -1524,6 +1524,8 @@ __global__ void k_elb_rebuild(Dims d, ElbDev e, XSel xs, ChainState cs, int xsla
     Y[(size_t)var * TP + T0 + t] = v;
     // lag-structured twin of the chain's X/Y (ccmm_lag.hip): D(p + row, var) = Y(row, var)
     if (dpool) dpool[((size_t)(xslab0 + c) * drows + p + T0 + t) * ldd + var] = v;
+    // column-major twin of the large path (ccmm_big.h ColX): D(p + row, var), column var
+    if (dcpool) dcpool[(size_t)(xslab0 + c) * dcslab + (size_t)var * dcld + p + T0 + t] = v;
   } else {
     const int row = T0 + t + l;  // X(row, lag l of var) = Y(row - l, var)
     if (row < T0 + T) X[(size_t)(1 + (l - 1) * N + var) * TP + row] = v;

@@ -291,6 +291,7 @@ enum OptId {
   OPT_FCST_OVERLAP, // kept sweeps' predictive density on the auxiliary stream beside the next sweep's CTA (1)
   OPT_PHI_OVERLAP,  // PHI block on the auxiliary stream beside the ELB step (1) or in stream order (0)
   OPT_QR_FALLBACK,  // host QR branch for a failed CTA Cholesky (CTA.m:80-92): 1 on, 0 off
+  OPT_BIG_LAGX,     // large path: Gram and solve read the lag twin of a lag-structured X (1) or X itself (0)
   kOptSchedule,     // ---- forms below: same algorithm, other summation order / branch
   OPT_LAG = kOptSchedule,  // lag-structured CTA kernels when the design allows (1) or the generic path (0)
   OPT_LARGE_PATH,   // 1: the large-system CTA path for every shape (set before ccmm_chains_set_data)

@@ -197,7 +197,7 @@ SELECTOR_VARS = {"CCMM_OLD_SOLVE": None, "CCMM_OLD_CHOL": None, "CCMM_GC18": Non
                  "CCMM_ELB_SPEC": ("elb_spec", 0),
                  "CCMM_FCST_REG": ("fcst_reg", 1), "CCMM_FCST_OVERLAP": ("fcst_overlap", 1), "CCMM_PHI_OVERLAP": ("phi_overlap", 1),
                  "CCMM_QR_FALLBACK": ("qr_fallback", 1), "CCMM_LAG": ("lag", 1), "CCMM_FORCE_QR": ("force_qr", 0),
-                 "CCMM_GIRF_GENERIC": ("girf_generic", 0)}
+                 "CCMM_GIRF_GENERIC": ("girf_generic", 0), "CCMM_BIG_LAGX": ("big_lagx", 1)}
 
 
 def test_default_build_ignores_every_selector(pkg, monkeypatch):
