@@ -470,7 +470,7 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
   const int c = blockIdx.x;
   const int s = cs.slot[c];
   const int T = Tslot[s];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid0 = threadIdx.x;
   constexpr int NT = 1024, NW = 16;
   const Rng rng = ra.make(c);
   const double* Ac = cs.A + (size_t)c * N * N;
@@ -479,7 +479,7 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
   double* E = cs.E + (size_t)c * N * TP;
   double* U = Ubuf + (size_t)c * N * TP;
   // U = E A' (E: residuals of the current PAI, k_resid)
-  for (int q = tid; q < N * TP; q += NT) {
+  for (int q = tid0; q < N * TP; q += NT) {
     const int i = q / TP, t = q - i * TP;
     double u = 0.0;
     if (t < T)
@@ -489,6 +489,11 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
   __syncthreads();
   const int nb = (K + 63) / 64;
   for (int j = 0; j < N; ++j) {
+    // per-equation opaque thread id: the lane-derived addresses of the phases below are formed
+    // where they are used instead of being hoisted out of the equation loop (and spilled)
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid0 >> 6);
     const int mat = c * N + j;
     // column a of the design: X + a TP, or its lag twin's column (same values for t < T; every
     // read below at t >= T is multiplied by v_t = 0 or not made)
@@ -676,39 +681,64 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
     }
     __syncthreads();
     {
-      const int nchunk = (T + 63) / 64;
+      // items = (slice, pair of 64-month chunks): each lane forms the slice's sum for months t and
+      // t + 64 with 32 loads in flight (the sum of each month in the same order as one month per item)
+      const int nchunk = (T + 63) / 64, npair = (nchunk + 1) / 2;
       const int per = (K + kResSlices - 1) / kResSlices;
-      for (int item = wave; item < nchunk * kResSlices && !(skip & 16); item += NW) {
-        const int slc = item % kResSlices, tch = item / kResSlices;
-        const int t = tch * 64 + lane;
+      for (int item = wave; item < npair * kResSlices && !(skip & 16); item += NW) {
+        const int slc = item % kResSlices, tpr = item / kResSlices;
+        const int t = tpr * 128 + lane, t2 = t + 64;
         const int a_lo = slc * per, a_hi = min(K, a_lo + per);
+        const int tc = min(t, T - 1), tc2 = min(t2, T - 1);  // clamped reads; results of t >= T unused
         double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-        if (t < T) {
-          int a = a_lo;
-          for (; a + 15 < a_hi; a += 16) {  // 16 loads in flight per lane
-            double xv[16];
+        double b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
+        int a = a_lo;
+        for (; a + 15 < a_hi; a += 16) {
+          double xv[16], xw[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) xv[q] = xcol(a + q)[t];
-#pragma unroll
-            for (int q = 0; q < 16; q += 4) {
-              a0 = fma(xv[q], yv[a + q], a0);
-              a1 = fma(xv[q + 1], yv[a + q + 1], a1);
-              a2 = fma(xv[q + 2], yv[a + q + 2], a2);
-              a3 = fma(xv[q + 3], yv[a + q + 3], a3);
-            }
+          for (int q = 0; q < 16; ++q) {
+            const double* xc = xcol(a + q);
+            xv[q] = xc[tc];
+            xw[q] = xc[tc2];
           }
-          for (; a < a_hi; ++a) a0 = fma(xcol(a)[t], yv[a], a0);
+#pragma unroll
+          for (int q = 0; q < 16; q += 4) {
+            a0 = fma(xv[q], yv[a + q], a0);
+            a1 = fma(xv[q + 1], yv[a + q + 1], a1);
+            a2 = fma(xv[q + 2], yv[a + q + 2], a2);
+            a3 = fma(xv[q + 3], yv[a + q + 3], a3);
+            b0 = fma(xw[q], yv[a + q], b0);
+            b1 = fma(xw[q + 1], yv[a + q + 1], b1);
+            b2 = fma(xw[q + 2], yv[a + q + 2], b2);
+            b3 = fma(xw[q + 3], yv[a + q + 3], b3);
+          }
+        }
+        for (; a < a_hi; ++a) {
+          const double* xc = xcol(a);
+          a0 = fma(xc[tc], yv[a], a0);
+          b0 = fma(xc[tc2], yv[a], b0);
         }
         if (t < TP) part[slc * TP + t] = (t < T) ? (a0 + a1) + (a2 + a3) : 0.0;
+        if (t2 < TP) part[slc * TP + t2] = (t2 < T) ? (b0 + b1) + (b2 + b3) : 0.0;
       }
     }
     __syncthreads();
+    // E(:,j) and the rank-one update of U(:, i >= j), U's entries loaded eight at a time (one round
+    // trip per eight instead of one per entry)
     for (int t = tid; t < T; t += NT) {
       double xp = 0.0;
 #pragma unroll
       for (int q = 0; q < kResSlices; ++q) xp += part[q * TP + t];
       E[(size_t)j * TP + t] = Y[(size_t)j * TP + t] - xp;
-      for (int i = j; i < N; ++i) U[(size_t)i * TP + t] = fma(-xp, Ac[i + j * N], U[(size_t)i * TP + t]);
+      int i = j;
+      for (; i + 7 < N; i += 8) {
+        double u[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) u[q] = U[(size_t)(i + q) * TP + t];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) U[(size_t)(i + q) * TP + t] = fma(-xp, Ac[i + q + j * N], u[q]);
+      }
+      for (; i < N; ++i) U[(size_t)i * TP + t] = fma(-xp, Ac[i + j * N], U[(size_t)i * TP + t]);
     }
     __syncthreads();
   }

@@ -1,7 +1,7 @@
 """Probe: full block-hybrid sweeps at the S120 shape (N = 120, p = 12, K = 1441, T = 750) on
 the synthetic panel, B chains, Philox draws; prints the per-kernel device times.  No result
 checks (phase ablations such as CCMM_SV_SKIP produce meaningless draws).
-Usage: python tools/probe_s120_sweep.py [B] [sweeps]"""
+Usage: python tools/probe_s120_sweep.py [B] [sweeps] [option=value ...]"""
 import sys
 import time
 from pathlib import Path
@@ -14,6 +14,7 @@ import __graft_entry__ as g
 pkg = g.load_package()
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 nsw = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+opts = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in sys.argv[3:])  # kernel options name=value
 p = 12
 d = pkg.synthetic.s120()
 ndxS, ndxO, _ = pkg.model.setShadowYields(d["ncode"], 0.25)
@@ -23,7 +24,7 @@ bm = pkg.model.build_bh(len(d["ydates"]), p, 12, d["data"], d["ydates"], ndxS, n
 m = bm.var
 ctx = pkg.Context(0)
 ch = pkg.Chains(ctx, N=m.N, p=p, T=m.T, B=B, crn=False, model=pkg.MODEL_BLOCKHYBRID,
-                Ns=len(bm.ndxS), elbTmax=bm.elbT, elb_gibbsburn=100, elb=0.25)
+                Ns=len(bm.ndxS), elbTmax=bm.elbT, elb_gibbsburn=100, elb=0.25, options=opts or None)
 ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
 ch.set_elb_model(bm.ndxS, bm.actual_block)
 ch.set_elb_slot(0, bm.elbT0, bm.sNaN)
@@ -37,7 +38,7 @@ ch.sweep(nsw)
 ctx.synchronize()
 el = time.perf_counter() - t0
 kt = ch.kernel_times()
-print(f"B={B}: {1e3 * el / nsw:.1f} ms/sweep")
+print(f"B={B} {opts}: {1e3 * el / nsw:.1f} ms/sweep")
 for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0]):
     if v[1]:
         print(f"  {k:18s} {v[0] / v[1]:9.3f} ms")
