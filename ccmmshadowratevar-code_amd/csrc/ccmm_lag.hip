@@ -364,14 +364,31 @@ __global__ __launch_bounds__(512, 1) void k_gram_chol_lag(Dims d, const int* __r
   const int s = cs.slot[c];
   const int tid = threadIdx.x;
   const int TP = d.TP;
-  // D slab and sqrt weights -> LDS
+  // D slab and sqrt weights -> LDS: every load of a thread's share (up to 32 + 2) issued before the
+  // first LDS store, so the slab arrives in one HBM/L2 round trip instead of one per element
   {
     const double* src = ls.dpool + (size_t)ls.idx[mat] * ls.rows * ls.ldd;
     const int n = ls.rows * ls.ldd;
-    for (int q = tid; q < n; q += 512) sm[q] = src[q];
-    double* swl = sm + n;
     const double* w = cs.W + (size_t)mat * TP;
-    for (int t = tid; t < TP + 4; t += 512) swl[t] = (t < TP) ? w[t] : 0.0;
+    double* swl = sm + n;
+    int q = tid;
+    for (; q < n; q += 32 * 512) {
+      double v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = (q + 512 * u < n) ? src[q + 512 * u] : 0.0;
+      double wv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) wv[u] = (q == tid && tid + 512 * u < TP) ? w[tid + 512 * u] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
+        if (q + 512 * u < n) sm[q + 512 * u] = v[u];
+      if (q == tid) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (tid + 512 * u < TP + 4) swl[tid + 512 * u] = wv[u];
+      }
+    }
+    for (int t = tid + 1024; t < TP + 4; t += 512) swl[t] = (t < TP) ? w[t] : 0.0;
   }
   __syncthreads();
   GlArgs g;
@@ -512,7 +529,15 @@ __global__ __launch_bounds__(64 * SW) void k_cta_solve_lag(Dims d, const int* __
     if (slab != cur) {
       __syncthreads();
       const double* src = ls.dpool + (size_t)slab * rows * ldd;
-      for (int q = tid; q < rows * ldd; q += NTH) Dl[q] = src[q];
+      // every load of a thread's share issued before the first LDS store (one round trip per 16)
+      for (int q = tid; q < rows * ldd; q += 16 * NTH) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = (q + NTH * u < rows * ldd) ? src[q + NTH * u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (q + NTH * u < rows * ldd) Dl[q + NTH * u] = v[u];
+      }
       cur = slab;
     }
     SL_CLK(q0);
