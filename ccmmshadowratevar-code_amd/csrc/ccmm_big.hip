@@ -265,10 +265,19 @@ __global__ __launch_bounds__(256, 2) void k_chol_big(Dims d, const int* __restri
     //         L_qq^-T and the trailing tiles updated on MFMA by all waves; then the inverse's
     //         off-diagonal tiles Li_rq = -L_rr^-1 sum_k L_rk Li_kq by distance r - q on MFMA
     if (!(skip & 2)) {
-      for (int e = tid; e < kBT * kBT; e += 256) {
-        const int i = e & 63, k = e >> 6;
-        Lk[i * kLiLd + k] = (k <= i) ? A[(size_t)(kcol + k) * KP + kcol + i] : 0.0;
-        Li[i * kLiLd + k] = 0.0;
+      {  // the diagonal block's 16 entries per thread loaded before the first LDS store (one round trip)
+        double lv[kBT * kBT / 256];
+#pragma unroll
+        for (int u = 0; u < kBT * kBT / 256; ++u) {
+          const int e = tid + 256 * u, i = e & 63, k = e >> 6;
+          lv[u] = (k <= i) ? A[(size_t)(kcol + k) * KP + kcol + i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kBT * kBT / 256; ++u) {
+          const int e = tid + 256 * u, i = e & 63, k = e >> 6;
+          Lk[i * kLiLd + k] = lv[u];
+          Li[i * kLiLd + k] = 0.0;
+        }
       }
       __syncthreads();
       for (int q = 0; q < 4; ++q) {
