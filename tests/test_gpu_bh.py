@@ -175,3 +175,29 @@ def test_bh_philox_batch(pkg, ctx, oracle, bh, fred):
     assert np.std(sr[-1, 0, 30, :]) > 0
     for k in ("PAI_all", "PHI_all", "invA_all", "sqrtht_all"):
         assert np.all(np.isfinite(d[k]))
+
+
+def test_bh_large_path_lag_twin_bit_identical(pkg, ctx, oracle, bh, fred):
+    """CTAsys on the large path (option large_path = 1) with the Gram and solve reading the lag twins
+    of the vintage's and the chain's X slabs (big_lagx = 1) against the designs themselves (0): the
+    same draws bit for bit over three sweeps (the chain slabs' twins are rebuilt by the ELB step)."""
+    bs = _real_bs(bh, oracle, fred)
+    lin = bs.lin
+    m = pkg.model.build_var(len(fred["ydates"]), 12, 12, fred["data"], fred["ydates"],
+                            oracle.set_minnesota_mean(fred["ncode"]), True)
+    out = {}
+    for lx in (1, 0):
+        ch = pkg.Chains(ctx, N=lin.N, p=lin.p, T=lin.T, B=4, crn=False, seed=9, model=pkg.MODEL_BLOCKHYBRID,
+                        Ns=len(bs.ndxS), elbTmax=bs.elbT, elb=0.25, store_capacity=3,
+                        options={"large_path": 1, "big_lagx": lx})
+        ch.set_data(0, m.Y, m.X, m.iVdiag, m.iVb, m.sPHI, m.Vol_0mean, m.Vol_0vcvsqrt)
+        ch.set_elb_model(bs.ndxS, bs.actualrateBlock)
+        ch.set_elb_slot(0, bs.elbT0, bs.sNaN)
+        st = pkg.model.initial_state(m, 4)
+        ch.set_state(st["PAI"], st["A"], st["sqrtht"], st["h"], st["sqrtPHI"])
+        ch.sweep(3, store=True)
+        out[lx] = (ch.get_state(), ch.get_shadowrate(), ch.get_status())
+    assert np.all(out[1][2] & ~1 == 0) and np.all(out[0][2] & ~1 == 0)
+    for k in out[1][0]:
+        np.testing.assert_array_equal(out[1][0][k], out[0][0][k], err_msg=k)
+    np.testing.assert_array_equal(out[1][1], out[0][1])

@@ -127,3 +127,27 @@ def test_hybrid_philox_batch(pkg, ctx, oracle, hy, fred):
     Yw = np.broadcast_to(lin.Y[hs.elbT0:, hs.ndxS].T[None, :, :, None], sr.shape)
     np.testing.assert_array_equal(sr[~cens], Yw[~cens])
     assert d["PAI_all"].shape == (2, lin.K, lin.N, B) and np.all(np.isfinite(d["PAI_all"]))
+
+
+def test_lag_twin_bit_identical(pkg, ctx, oracle, hy, fred):
+    """The large path's Gram and solve on the column-major lag twin of X (option big_lagx = 1, the
+    default) against X itself (0): the same products in the same order, so the same draws bit for bit
+    -- over three sweeps, so the ELB step's rebuild of the twin (k_elb_rebuild) is exercised."""
+    hs = _real_hs(hy, oracle, fred)
+    lin = hs.lin
+    out = {}
+    for lx in (1, 0):
+        ch = pkg.Chains(ctx, N=lin.N, p=lin.p, T=lin.T, B=4, crn=False, seed=11, model=pkg.MODEL_HYBRID,
+                        Ns=len(hs.ndxS), elbTmax=hs.elbT, elb_gibbsburn=hs.gibbsburn, elb=hs.ELB,
+                        store_capacity=3, options={"big_lagx": lx})
+        ch.set_data(0, lin.Y, lin.X, lin.iVdiag, lin.iVb, lin.sPHI, lin.Vol_0mean, lin.Vol_0vcvsqrt)
+        ch.set_elb_model(hs.ndxS, None)
+        ch.set_elb_slot(0, hs.elbT0, hs.sNaN)
+        sts = [random_state(oracle, lin, seed=40 + c) for c in range(4)]
+        ch.set_state(*[np.stack([s[k] for s in sts], -1) for k in ("PAI", "A", "sqrtht", "h", "sqrtPHI")])
+        ch.sweep(3, store=True)
+        out[lx] = (ch.get_state(), ch.get_shadowrate(), ch.get_status())
+    assert np.all(out[1][2] & ~1 == 0) and np.all(out[0][2] & ~1 == 0)
+    for k in out[1][0]:
+        np.testing.assert_array_equal(out[1][0][k], out[0][0][k], err_msg=k)
+    np.testing.assert_array_equal(out[1][1], out[0][1])
