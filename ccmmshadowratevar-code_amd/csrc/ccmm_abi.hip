@@ -662,7 +662,7 @@ struct ccmm_chains {
   ColX colx() const {
     bool on = colx_capable && opt[OPT_BIG_LAGX];
     for (int s = 0; on && s < cfg.ndata; ++s) on = slot_colx[s];
-    return on ? ColX{Dcpool.p, dXoff.p, (long long)dcslab} : ColX{nullptr, nullptr, 0};
+    return on ? ColX{Dcpool.p, dXoff.p, (long long)dcslab, dcld, (int)(dcslab / dcld)} : ColX{nullptr, nullptr, 0, 0, 0};
   }
   bool lag_active() const {
     if (!lag_capable || !opt[OPT_LAG]) return false;

@@ -20,6 +20,8 @@ struct ColX {
   const double* pool;
   const int* off;
   long long slab;
+  int ld;    // leading dimension of a twin column (off[a] = column * ld + row offset)
+  int ncol;  // columns per twin (data, actual rates, ones, zeros)
 };
 
 // groups: ngroups x int4 systems (c*N + j) sharing one design X slab (-1 padded);

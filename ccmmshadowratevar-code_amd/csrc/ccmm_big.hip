@@ -462,6 +462,14 @@ __global__ __launch_bounds__(256, 2) void k_chol_big(Dims d, const int* __restri
 //   X x        the K columns split in 8 slices x T in 64-row chunks, partial sums in LDS
 constexpr int kBSLd = 65;
 constexpr int kResSlices = 8;
+// staged twin (KP <= kStageMaxKP): the X'v and residual phases read the lag twin from LDS, 256 months
+// (plus the p - 1 presample rows their lags reach) at a time, instead of one L2 load per product
+constexpr int kStageMonths = 256;
+constexpr int kStageMaxKP = 320;
+__host__ __device__ inline int big_stage_rows(int p) { return kStageMonths + p; }
+__host__ inline size_t big_stage_lds_doubles(const Dims& d, const ColX& cx) {
+  return (size_t)cx.ncol * big_stage_rows(d.p) + (d.KP + 1) / 2;  // + the KP int offsets
+}
 __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __restrict__ Tslot,
                                                         const double* __restrict__ iVb, XSel xs,
                                                         ChainState cs, const double* __restrict__ rdiag,
@@ -476,6 +484,11 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
   double* rdl = yv + KP;             // KP
   double* Ls = rdl + KP;             // 64 x kBSLd
   double* part = Ls + 64 * kBSLd;    // kResSlices x TP
+  // staged twin: ncol x SR doubles, then the LDS offset of every design column
+  const bool staged = cx.pool && cx.ncol > 0;
+  const int SR = big_stage_rows(d.p);
+  double* Ds = part + kResSlices * TP;
+  int* loff = reinterpret_cast<int*>(Ds + (staged ? cx.ncol * SR : 0));
   const int c = blockIdx.x;
   const int s = cs.slot[c];
   const int T = Tslot[s];
@@ -495,8 +508,29 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
       for (int k = 0; k <= i; ++k) u = fma(E[(size_t)k * TP + t], Ac[i + k * N], u);
     U[q] = u;
   }
+  if (staged)
+    for (int a = tid0; a < KP; a += NT) {
+      const int o = cx.off[a], col = o / cx.ld;
+      loff[a] = col * SR + (o - col * cx.ld);
+    }
   __syncthreads();
   const int nb = (K + 63) / 64;
+  // months [t0, t0 + 256) of the chain's twin -> Ds (rows t0 .. t0 + SR - 1 of every column); the
+  // thread's loads are all issued before its LDS stores
+  auto stage = [&](const double* Dg, int t0, int tid) __attribute__((always_inline)) {
+    const int n = cx.ncol * SR;
+    for (int e0 = tid; e0 < n; e0 += 8 * NT) {
+      double val[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * NT, col = e / SR, r = e - col * SR;
+        val[u] = (e < n && t0 + r < cx.ld) ? Dg[(size_t)col * cx.ld + t0 + r] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (e0 + u * NT < n) Ds[e0 + u * NT] = val[u];
+    }
+  };
   for (int j = 0; j < N; ++j) {
     // per-equation opaque thread id: the lane-derived addresses of the phases below are formed
     // where they are used instead of being hoisted out of the equation loop (and spilled)
@@ -548,7 +582,48 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
     __syncthreads();
     // ---- rhs = iVb_j + X' v: four columns per wave at a time
     const double* ivb = iVb + ((size_t)s * N + j) * KP;
-    for (int a0 = wave * 4; a0 < KP && !(skip & 2); a0 += NW * 4) {
+    if (staged && !(skip & 2)) {
+      // the twin staged 256 months at a time; wave w keeps the sums of columns w*4 + 64 r + q (r < 5)
+      // across the pieces, each lane adding its months t = lane + 64 u in increasing order: every
+      // column's sum is formed in the order of the unstaged loop below
+      double pr[kStageMaxKP / 64][4];
+#pragma unroll
+      for (int r = 0; r < kStageMaxKP / 64; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pr[r][q] = 0.0;
+      for (int t0 = 0; t0 < TP; t0 += kStageMonths) {
+        __syncthreads();
+        stage(X, t0, tid);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kStageMaxKP / 64; ++r) {
+          const int a0 = wave * 4 + 64 * r;
+          if (a0 < KP) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const double* col = Ds + loff[min(a0 + q, K - 1)] - t0;
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const int t = t0 + lane + 64 * u;
+                if (t < TP) pr[r][q] = fma(col[t], v[t], pr[r][q]);
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kStageMaxKP / 64; ++r) {
+        const int a0 = wave * 4 + 64 * r;
+        if (a0 < KP) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const double tot = wave_sum_dpp(a0 + q < K ? pr[r][q] : 0.0);
+            if (lane == 0 && a0 + q < KP) yv[a0 + q] = ivb[a0 + q] + tot;
+          }
+        }
+      }
+    }
+    for (int a0 = wave * 4; a0 < KP && !(skip & 2) && !staged; a0 += NW * 4) {
       double p[4] = {0.0, 0.0, 0.0, 0.0};
       const double* xc[4];
 #pragma unroll
@@ -689,7 +764,52 @@ __global__ __launch_bounds__(1024) void k_cta_solve_big(Dims d, const int* __res
       yv[a] = val;
     }
     __syncthreads();
-    {
+    if (staged && !(skip & 16)) {
+      // the same items from the staged twin: each 256-month piece holds two chunk pairs, so the
+      // piece's 16 items (8 slices x 2 pairs) are one per wave; each month's sum as below
+      const int per = (K + kResSlices - 1) / kResSlices;
+      for (int t0 = 0; t0 < TP; t0 += kStageMonths) {
+        __syncthreads();
+        stage(X, t0, tid);
+        __syncthreads();
+        const int slc = wave % kResSlices;
+        const int t = t0 + (wave / kResSlices) * 128 + lane, t2 = t + 64;
+        if (t < TP) {
+          const int a_lo = slc * per, a_hi = min(K, a_lo + per);
+          const int tc = max(min(t, T - 1) - t0, 0), tc2 = max(min(t2, T - 1) - t0, 0);  // unused when >= T
+          double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+          double b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
+          int a = a_lo;
+          for (; a + 15 < a_hi; a += 16) {
+            double xv[16], xw[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+              const double* xc = Ds + loff[a + q];
+              xv[q] = xc[tc];
+              xw[q] = xc[tc2];
+            }
+#pragma unroll
+            for (int q = 0; q < 16; q += 4) {
+              a0 = fma(xv[q], yv[a + q], a0);
+              a1 = fma(xv[q + 1], yv[a + q + 1], a1);
+              a2 = fma(xv[q + 2], yv[a + q + 2], a2);
+              a3 = fma(xv[q + 3], yv[a + q + 3], a3);
+              b0 = fma(xw[q], yv[a + q], b0);
+              b1 = fma(xw[q + 1], yv[a + q + 1], b1);
+              b2 = fma(xw[q + 2], yv[a + q + 2], b2);
+              b3 = fma(xw[q + 3], yv[a + q + 3], b3);
+            }
+          }
+          for (; a < a_hi; ++a) {
+            const double* xc = Ds + loff[a];
+            a0 = fma(xc[tc], yv[a], a0);
+            b0 = fma(xc[tc2], yv[a], b0);
+          }
+          part[slc * TP + t] = (t < T) ? (a0 + a1) + (a2 + a3) : 0.0;
+          if (t2 < TP) part[slc * TP + t2] = (t2 < T) ? (b0 + b1) + (b2 + b3) : 0.0;
+        }
+      }
+    } else {
       // items = (slice, pair of 64-month chunks): each lane forms the slice's sum for months t and
       // t + 64 with 32 loads in flight (the sum of each month in the same order as one month per item)
       const int nchunk = (T + 63) / 64, npair = (nchunk + 1) / 2;
@@ -772,12 +892,17 @@ hipError_t big_launch_cta(hipStream_t st, const Dims& d, const int* Tslot, const
     hipLaunchKernelGGL(k_chol_big, dim3(d.nmat), dim3(256), 0, st, d, slotIV, iVdiag, cs, rdiag, Dinv,
                        cskip);
   if (phase_mask & 4) {
-    const size_t lds = big_solve_lds_bytes(d);
+    // the staged twin when the design fits kStageMaxKP and its LDS fits beside the rest
+    ColX cs_x = cx;
+    size_t lds = big_solve_lds_bytes(d);
+    const size_t lds_st = lds + big_stage_lds_doubles(d, cx) * sizeof(double);
+    if (!cx.pool || d.KP > kStageMaxKP || lds_st > 160 * 1024) cs_x.ncol = 0;
+    else lds = lds_st;
     hipError_t e = hipFuncSetAttribute((const void*)k_cta_solve_big,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_cta_solve_big, dim3(d.B), dim3(1024), lds, st, d, Tslot, iVb, xs, cs, rdiag,
-                       ra, Ubuf, Dinv, skip, cx);
+                       ra, Ubuf, Dinv, skip, cs_x);
   }
   return hipGetLastError();
 }
