@@ -97,7 +97,9 @@ int ccmm_env_ignored(char* buf, int len);
  * the chain sets created on it afterwards and used by the block-level drop-ins) or per chain set.
  * Schedules give bit-identical draws: solve_split (-1 auto, 0, 1), solve_async (0/1), sv_nwg (0 auto,
  * 1, 2, 4), elb_waves (1, 4, 8), elb_oct (0, 1 auto, 2), elb_async (0/1), elb_parts (0 auto, 1, 2, 4:
- * workgroups per chain of the ELB wavefront), fcst_reg (0/1), phi_overlap (0/1), qr_fallback (0/1).
+ * workgroups per chain of the ELB wavefront), fcst_reg (0/1), phi_overlap (0/1), qr_fallback (0/1),
+ * big_lagx (0/1: the large path reads the column-major lag twin of a lag-structured X; set before
+ * ccmm_chains_set_data).
  * Forms run the same algorithm in another summation order (or the QR branch): lag (0/1), large_path
  * (0/1; set before ccmm_chains_set_data), astep_serial, ps_chol_lds, sv_mfma (0/1), force_qr,
  * girf_generic.  CCMM_ERR_ARG for an unknown name or a value out of range. */
