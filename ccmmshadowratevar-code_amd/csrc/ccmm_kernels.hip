@@ -21,6 +21,19 @@
 
 namespace ccmm {
 
+// dst[q] = src[q] for q < n (a global -> LDS staging copy): sixteen loads per thread are issued
+// before their stores, one round trip per sixteen elements instead of one per element
+__device__ __forceinline__ void stage_copy16(double* dst, const double* __restrict__ src, int n, int tid, int nth) {
+  for (int q0 = tid; q0 < n; q0 += 16 * nth) {
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = (q0 + u * nth < n) ? src[q0 + u * nth] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (q0 + u * nth < n) dst[q0 + u * nth] = v[u];
+  }
+}
+
 // ============================================================== residual
 // E(:,j) = Y(:,j) - X_j * PAI(:,j)   (mcmcVAR.m:233; CTAsys residual mcmcVARshadowrateBlockHybrid.m:348-351)
 __global__ void k_resid(Dims d, const int* __restrict__ Tslot, XSel xs, ChainState cs) {
@@ -259,7 +272,7 @@ __global__ __launch_bounds__(256) void k_astep(Dims d, const int* __restrict__ T
   }
   // es_off >= 0: this chain's residuals E (N x TP) are staged in LDS at sm + es_off
   if (es_off >= 0)
-    for (int q = tid; q < N * TP; q += blockDim.x) sm[es_off + q] = E[q];
+    stage_copy16(sm + es_off, E, N * TP, tid, blockDim.x);
   __syncthreads();
   const double* Ew = (es_off >= 0) ? sm + es_off : E;
   const int total = boff[N];
@@ -380,7 +393,7 @@ __global__ __launch_bounds__(512) void k_astep_w(Dims d, const int* __restrict__
     boff[N] = o;
   }
   if (es_off >= 0)
-    for (int q = tid; q < N * TP; q += blockDim.x) sm[es_off + q] = E[q];
+    stage_copy16(sm + es_off, E, N * TP, tid, blockDim.x);
   __syncthreads();
   AS_CLK(k1);
   const double* Ew = (es_off >= 0) ? sm + es_off : E;
@@ -601,9 +614,20 @@ __global__ __launch_bounds__(256) void k_phi(Dims d, const int* __restrict__ Tsl
   const double* etaw = eta;
   if (stage_eta) {
     double* es = Ph + N * NS;
-    for (int q = tid; q < N * TP; q += blockDim.x) {
-      const int r = q / TP, t = q - r * TP;
-      es[r * lde + t] = eta[q];
+    // sixteen loads per thread issued before their LDS stores (one round trip per sixteen)
+    const int nth = blockDim.x;
+    for (int q0 = tid; q0 < N * TP; q0 += 16 * nth) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = (q0 + u * nth < N * TP) ? eta[q0 + u * nth] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int q = q0 + u * nth;
+        if (q < N * TP) {
+          const int r = q / TP, t = q - r * TP;
+          es[r * lde + t] = v[u];
+        }
+      }
     }
     __syncthreads();
     etaw = es;
@@ -633,7 +657,14 @@ __global__ __launch_bounds__(256) void k_phi(Dims d, const int* __restrict__ Tsl
   if (stage_eta & 2) {
     double* zs = Ph + N * NS;
     __syncthreads();
-    for (int q = tid; q < N * TZ; q += blockDim.x) zs[q] = Z[q];
+    for (int q0 = tid; q0 < N * TZ; q0 += 16 * (int)blockDim.x) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = (q0 + u * (int)blockDim.x < N * TZ) ? Z[q0 + u * blockDim.x] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (q0 + u * (int)blockDim.x < N * TZ) zs[q0 + u * blockDim.x] = v[u];
+    }
     __syncthreads();
     Zw = zs;
   }
