@@ -194,6 +194,9 @@ __global__ __launch_bounds__(256, 2) void k_chol_big(Dims d, const int* __restri
         // nothing, and the diagonal block's strictly upper 16 x 16 sub-tiles (never read) are
         // skipped: the SIMD's MFMA pipe goes to the co-resident system's waves instead.
         const bool diag = ib == kb;
+        // 16-row sub-blocks wholly in the padding (rows >= K: zero data, identity prior, L rows
+        // e_r) take no products: their update is by zero rows of L (the stored value is the same)
+        const int xr = __builtin_amdgcn_readfirstlane(min(4, max(0, (d.K - irow + 15) / 16)));
         double bv[kCK * kBT / 256];
         auto load_b = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_big(Dims d, const int* __restri
               for (int x = 0; x < 4; ++x)
 #pragma unroll
                 for (int y = 0; y < 4; ++y)
-                  if (!(diag && y > x))
+                  if (x < xr && !(diag && y > x))
                     acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[ks * 4 + x], fb[y], acc[x][y], 0, 0, 0);
             }
           }
@@ -412,6 +415,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_big(Dims d, const int* __restri
     //         the tile's C fragments are loaded in four bursts of 16 per lane
     for (int rt = kb + 1 + wave; rt < nb && !(skip & 4); rt += 4) {
       const int r0 = rt * kBT;
+      const int xr = __builtin_amdgcn_readfirstlane(min(4, max(0, (d.K - r0 + 15) / 16)));  // as in the update
       dbl4 acc[4][4];
 #pragma unroll
       for (int x = 0; x < 4; ++x)
@@ -435,7 +439,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_big(Dims d, const int* __restri
           for (int x = 0; x < 4; ++x)
 #pragma unroll
             for (int y = 0; y < 4; ++y)
-              acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ks * 4 + x], fb[y], acc[x][y], 0, 0, 0);
+              if (x < xr) acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ks * 4 + x], fb[y], acc[x][y], 0, 0, 0);
         }
       }
 #pragma unroll
